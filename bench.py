@@ -1,0 +1,230 @@
+"""Benchmark: proximal-gradient iterations/s on (m,n,l) = (8192,16384,32) fp64 (BASELINE.json).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--method gl_ProxGD_primal] [--dtype f64]
+                    [--m 8192 --n 16384 --l 32] [--no-cpu-baseline] [--variant V]
+
+One step = one recorded iteration of the solver (objective, stop rule, threshold, A^T(Ax-b),
+line search, prox) on one synthetic instance whose A, b, x live in HBM before timing starts.
+N > 1 (launched by torch.distributed.run, one process per GPU): A and b are row-sharded, the
+gradient is summed with RCCL, and the same global problem is solved (strong scaling); the
+reported value is iterations/s of the whole job (max of the per-rank times).
+
+Also reported, for the dominant kernel (A@x, launched every line-search trial):
+  roofline — algorithmic bytes (A streamed once + x, b, r: s*(m n + (m+n) l)) / average launch
+             time from HIP events recorded on the solver's stream over the timed region; peak
+             8 TB/s (MI355X HBM3E); `traffic` = HBM bytes per launch from rocprofv3 PMC
+             (profiles/pmc_traffic.json, 2*FETCH_SIZE + WRITE_SIZE per the gfx950 correction) when
+             that file holds the same config, else null;
+  cpu_baseline — the repo's NumPy oracle (oracle/numpy_ref.py) on the host cores, on a bounded
+             sample of the same instance (rank 0, N = 1 only).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import math
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "convex-optimization_amd"))
+sys.path.insert(0, ROOT)
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+METRIC = "prox-grad iters/sec + MFMA-roofline %, (m,n,l)=(8192,16384,32) fp64"
+HBM_PEAK_GBS = 8000.0
+MFMA_PEAK_TFS = {"f64": 78.6, "f32": 157.3}
+BLOCK_ROWS = 256
+
+
+def log(*a):
+    print(*a, file=sys.stderr, flush=True)
+
+
+def make_instance(m, n, l, r0, r1, dtype, device, seed=97006855):
+    """Synthetic instance (the gen_data recipe of main.py:37-51 at scale): A ~ N(0,1), a 10 %
+    row-sparse ground truth u, b = A u, x0 ~ N(0,1). Generated on the device in 256-row blocks
+    with per-block seeds, so every rank builds exactly its rows of the same global A."""
+    g = torch.Generator(device=device)
+    g.manual_seed(seed)
+    k = round(0.1 * n)
+    u = torch.zeros(n, l, dtype=torch.float64, device=device)
+    support = torch.randperm(n, generator=g, device=device)[:k]
+    u[support] = torch.randn(k, l, generator=g, device=device, dtype=torch.float64)
+    x0 = torch.randn(n, l, generator=g, device=device, dtype=torch.float64)
+    A = torch.empty(r1 - r0, n, dtype=dtype, device=device)
+    for blk in range(r0 // BLOCK_ROWS, (r1 + BLOCK_ROWS - 1) // BLOCK_ROWS):
+        b0, b1 = blk * BLOCK_ROWS, min((blk + 1) * BLOCK_ROWS, m)
+        g.manual_seed(seed * 1000003 + blk)
+        rows = torch.randn(b1 - b0, n, generator=g, device=device, dtype=torch.float64)
+        lo, hi = max(b0, r0), min(b1, r1)
+        A[lo - r0:hi - r0] = rows[lo - b0:hi - b0].to(dtype)
+        del rows
+    b = (A.to(torch.float64) @ u).to(dtype)
+    return A.contiguous(), b.contiguous(), x0.to(dtype).contiguous()
+
+
+def cpu_baseline(method, A, b, x0, mu, opts, budget_s=15.0):
+    """Time the NumPy oracle (test infrastructure) on the host on a bounded sample: the same
+    instance, a fixed number of iterations per continuation phase."""
+    from oracle import numpy_ref
+    try:
+        from threadpoolctl import threadpool_info
+        info = [d for d in threadpool_info() if d.get("user_api") == "blas"]
+        threads = int(info[0]["num_threads"]) if info else os.cpu_count()
+        blas = "%s %s" % (info[0].get("internal_api"), info[0].get("version")) if info else "?"
+    except Exception:
+        threads, blas = os.cpu_count(), "?"
+    An, bn, xn = A.cpu().numpy(), b.cpu().numpy(), x0.cpu().numpy()
+    fn = numpy_ref.SOLVERS[method]
+    # calibrate: one iteration per phase
+    o = dict(opts, maxit=1)
+    t0 = time.perf_counter()
+    _, k1, _ = fn(xn, An, bn, mu, o)
+    t1 = time.perf_counter() - t0
+    per_iter = t1 / max(1, k1)
+    maxit = int(max(1, min(20, budget_s / (3 * per_iter))))
+    o = dict(opts, maxit=maxit)
+    t0 = time.perf_counter()
+    _, k, _ = fn(xn, An, bn, mu, o)
+    dt = time.perf_counter() - t0
+    return {"value": k / dt, "unit": "iters/s", "cores": threads, "kind": "port",
+            "sample": "oracle/numpy_ref.%s on the same instance, %d iterations (maxit=%d per phase), "
+                      "%.1f s; BLAS %s" % (method, k, maxit, dt, blas)}
+
+
+def pmc_traffic(cfg_key):
+    path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    try:
+        with open(path) as fh:
+            d = json.load(fh)
+        e = d.get(cfg_key)
+        return None if e is None else float(e["bytes_per_launch"])
+    except Exception:
+        return None
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=200)
+    ap.add_argument("--warmup", type=int, default=20)
+    ap.add_argument("--method", default="gl_ProxGD_primal")
+    ap.add_argument("--dtype", default="f64", choices=["f64", "f32"])
+    ap.add_argument("--m", type=int, default=8192)
+    ap.add_argument("--n", type=int, default=16384)
+    ap.add_argument("--l", type=int, default=32)
+    ap.add_argument("--variant", type=int, default=0)
+    ap.add_argument("--exact", type=int, default=0)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        log("note: WORLD_SIZE=%d, --gpus=%d; using WORLD_SIZE" % (world, args.gpus))
+    torch.cuda.set_device(local)
+    device = torch.device("cuda", local)
+
+    import glx
+    from glx.dist import Comm, shard_rows
+    dist = None
+    comm = None
+    if world > 1:
+        import torch.distributed as dist
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+        comm = Comm.from_torch_distributed()
+
+    m, n, l = args.m, args.n, args.l
+    dtype = torch.float64 if args.dtype == "f64" else torch.float32
+    r0, r1 = shard_rows(m, world, rank)
+    t_gen = time.perf_counter()
+    A, b, x0 = make_instance(m, n, l, r0, r1, dtype, device)
+    torch.cuda.synchronize()
+    log("rank %d: instance rows [%d,%d) x %d x %d %s generated in %.1fs" %
+        (rank, r0, r1, n, l, args.dtype, time.perf_counter() - t_gen))
+    mu = 1e-2
+    alpha0 = float(1.0 / (math.sqrt(m) + math.sqrt(n)) ** 2)
+    total = args.warmup + args.steps
+    opts = {"alpha0": alpha0, "maxit": max(total + 1, 2500), "max_total_iters": total,
+            "profile": 1, "ax_variant": args.variant, "exact_objective": args.exact}
+    x = x0.clone()
+    s = glx.Session(args.method, x, A, b, mu, opts, comm=comm)
+    s.run(args.warmup)
+    s.kernel_time(0)
+    s.kernel_time(1)
+
+    if dist is not None:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    done = s.run(args.steps)
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    if dist is not None:
+        t = torch.tensor([elapsed], dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+        dist.barrier()
+    ax_n, ax_ms = s.kernel_time(0)
+    atr_n, atr_ms = s.kernel_time(1)
+    res = s.finish()
+    s.close()
+    if done != args.steps:
+        log("warning: solver finished after %d of %d timed steps" % (done, args.steps))
+
+    if rank == 0:
+        es = 8 if args.dtype == "f64" else 4
+        ml = r1 - r0
+        ax_avg_s = (ax_ms / max(1, ax_n)) / 1e3
+        atr_avg_s = (atr_ms / max(1, atr_n)) / 1e3
+        ax_bytes = es * (ml * n + (ml + n) * l)
+        ax_flops = 2.0 * ml * n * l
+        ach = ax_bytes / ax_avg_s / 1e9 if ax_n else None
+        cfg_key = "%s_%s_%dx%dx%d_g%d" % (args.method, args.dtype, m, n, l, world)
+        roof = {"bound": "hbm", "achieved": ach, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                "frac": (ach / HBM_PEAK_GBS) if ach else None, "traffic": pmc_traffic(cfg_key),
+                "kernel": "A@x (k_ax_mfma)", "bytes_per_launch": ax_bytes,
+                "avg_launch_us": ax_avg_s * 1e6, "launches": ax_n,
+                "mfma_tflops": ax_flops / ax_avg_s / 1e12 if ax_n else None,
+                "mfma_frac": (ax_flops / ax_avg_s / 1e12) / MFMA_PEAK_TFS[args.dtype] if ax_n else None,
+                "atr_avg_launch_us": atr_avg_s * 1e6,
+                "atr_GBs": ax_bytes / atr_avg_s / 1e9 if atr_n else None,
+                "pair_mfma_frac": (2 * ax_flops / (ax_avg_s + atr_avg_s) / 1e12) / MFMA_PEAK_TFS[args.dtype]
+                if (ax_n and atr_n) else None}
+        steps = max(1, done)
+        line = {
+            "metric": METRIC, "value": steps / elapsed, "unit": "iters/s", "n_gpus": world,
+            "steps": steps, "warmup": args.warmup, "ms_per_step": 1e3 * elapsed / steps,
+            "higher_is_better": True, "scaling": "strong", "vs_baseline": None,
+            "dtype": args.dtype,
+            "data": "synthetic: Gaussian A, 10% row-sparse ground truth u, b = A u (main.py:37-51 "
+                    "recipe, generated on device per 256-row block)",
+            "config": {"workload": "%s %s (m,n,l)=(%d,%d,%d), mu0=1e-2, alpha0=1/(sqrt(m)+sqrt(n))^2"
+                                   % (args.method, args.dtype, m, n, l, ),
+                       "method": args.method, "m": m, "n": n, "l": l,
+                       "parallelism": "row-shard x%d (RCCL all-reduce of A^T r)" % world if world > 1 else "single GPU",
+                       "exact_objective": args.exact, "ax_variant": args.variant},
+            "roofline": roof,
+            "work": {"ax_per_iter": ax_n / steps, "atr_per_iter": atr_n / steps,
+                     "syncs_total": res["syncs"], "iters_total": res["k"]},
+        }
+        if world == 1 and not args.no_cpu_baseline:
+            try:
+                line["cpu_baseline"] = cpu_baseline(args.method, A, b, x0, mu,
+                                                    {"alpha0": alpha0})
+            except Exception as e:  # report, never fake
+                line["cpu_baseline"] = {"value": None, "error": repr(e)}
+        print(json.dumps(line), flush=True)
+    if comm is not None:
+        comm.close()
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,629 @@
+// kernels_elem.hip — per-group (row of x) and elementwise kernels of the solvers, each fused
+// with the scalar reductions the host control flow needs.
+//
+// Everything here is HBM/L2 streaming over n*l or m*l elements (4 MiB at the north-star
+// size); the work per element is a handful of flops. Rows of x (groups, l contiguous values)
+// are owned by LPR lanes (LPR = min(16, next_pow2(l))), each lane holding EPL elements strided
+// by LPR, so a group's l2 norm is an in-register sum plus log2(LPR) xor-shuffles.
+//
+// Floating-point expressions keep the reference's NumPy evaluation order (the library is
+// built with -ffp-contract=off, so a*b+c is never fused behind our back):
+//   prox   (gl_ProxGD_primal.py:65-71)  p = (w * max(||w_i|| - t*mu, 0)) / ((||w_i|| < thres) + ||w_i||)
+//   G_t    (gl_ProxGD_primal.py:73-74)  G = (x - p) / t,  trial point z = x - t*G  (:91)
+//   FISTA  (gl_FProxGD_primal.py:139,145)  y = (1-θ) x + θ v,  v = x + (x_new - x)/θ
+//   SGD    (gl_SGD_primal.py:56-61,96)  x - α (g + μ x/((||x_i||<thres)+||x_i||))
+//   GD     (gl_GD_primal.py:59-63,98)   x - α (g + μ x/sqrt(Σx_i² + δ²))
+// Scalars (t, μ, α, thres …) arrive as double and are rounded to T first, as NumPy does with
+// Python-float operands of a T array (NEP 50 weak scalars).
+//
+// Reductions are deterministic: block partials in a fixed tree order, then the last block to
+// arrive (agent-scope release/acquire ticket, cdna_hip_programming.md Guideline 16) sums the
+// block partials in block order. max() propagates NaN like np.max.
+#include "glx_internal.h"
+
+namespace glx {
+
+enum { OP_SUM = 0, OP_MAX = 1 };
+
+__device__ inline double nan_max(double a, double b) {
+  if (a != a) return a;
+  if (b != b) return b;
+  return a > b ? a : b;
+}
+__device__ inline double combine(int op, double a, double b) { return op == OP_MAX ? nan_max(a, b) : a + b; }
+__device__ inline double identity(int op) { return op == OP_MAX ? -__builtin_inf() : 0.0; }
+
+// Reduce NV per-thread values over the grid; block size must be 256. MAXMASK bit v = max op.
+template <int NV, unsigned MAXMASK>
+__device__ void grid_reduce(double (&v)[NV], const Red& red) {
+  __shared__ double sh[NV][4];
+  __shared__ int is_last;
+  const int lane = threadIdx.x & 63;
+  const int wave = threadIdx.x >> 6;
+#pragma unroll
+  for (int j = 0; j < NV; ++j) {
+    const int op = (MAXMASK >> j) & 1;
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) v[j] = combine(op, v[j], __shfl_xor(v[j], off));
+  }
+  if (lane == 0) {
+#pragma unroll
+    for (int j = 0; j < NV; ++j) sh[j][wave] = v[j];
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+#pragma unroll
+    for (int j = 0; j < NV; ++j) {
+      const int op = (MAXMASK >> j) & 1;
+      const double bv = combine(op, combine(op, sh[j][0], sh[j][1]), combine(op, sh[j][2], sh[j][3]));
+      red.part[j * kMaxBlocks + blockIdx.x] = bv;
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    const unsigned prev = __hip_atomic_fetch_add(red.ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    is_last = (prev == gridDim.x - 1) ? 1 : 0;
+  }
+  __syncthreads();
+  if (!is_last) return;
+  if (threadIdx.x == 0) {
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
+  __syncthreads();
+  double acc[NV];
+#pragma unroll
+  for (int j = 0; j < NV; ++j) {
+    const int op = (MAXMASK >> j) & 1;
+    acc[j] = identity(op);
+    for (unsigned b = threadIdx.x; b < gridDim.x; b += 256) acc[j] = combine(op, acc[j], red.part[j * kMaxBlocks + b]);
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) acc[j] = combine(op, acc[j], __shfl_xor(acc[j], off));
+  }
+  __syncthreads();
+  if (lane == 0) {
+#pragma unroll
+    for (int j = 0; j < NV; ++j) sh[j][wave] = acc[j];
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+#pragma unroll
+    for (int j = 0; j < NV; ++j) {
+      const int op = (MAXMASK >> j) & 1;
+      red.out[j] = combine(op, combine(op, sh[j][0], sh[j][1]), combine(op, sh[j][2], sh[j][3]));
+    }
+    __hip_atomic_store(red.ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+}
+
+static inline unsigned grid_for(int64_t work, int per_block) {
+  int64_t g = (work + per_block - 1) / per_block;
+  if (g < 1) g = 1;
+  if (g > kMaxBlocks) g = kMaxBlocks;
+  return (unsigned)g;
+}
+
+template <typename T> __device__ inline T tabs(T v) { return v < T(0) ? -v : v; }
+
+// ------------------------------------------------------------------------------------------
+// residual finalize: R = sum_s P[s] - B; sum R^2
+// ------------------------------------------------------------------------------------------
+template <typename T>
+__global__ __launch_bounds__(256) void k_finalize_residual(const T* __restrict__ P, int S,
+                                                           const T* __restrict__ B, T* __restrict__ R,
+                                                           int64_t ml, const int* __restrict__ gate,
+                                                           int gate_mode, Red red) {
+  const bool live = (gate == nullptr) || (*gate != 0);
+  if (!live && gate_mode == 0) return;  // uniform over the grid: nobody touches the ticket
+  double v[1] = {0.0};
+  const int64_t stride = (int64_t)gridDim.x * 256;
+  for (int64_t idx = (int64_t)blockIdx.x * 256 + threadIdx.x; idx < ml; idx += stride) {
+    T r;
+    if (live) {
+      T s = P[idx];
+      for (int k = 1; k < S; ++k) s = s + P[(int64_t)k * ml + idx];
+      r = s - B[idx];
+      R[idx] = r;
+    } else {
+      r = R[idx];
+    }
+    v[0] += (double)(r * r);
+  }
+  grid_reduce<1, 0u>(v, red);
+}
+
+template <typename T>
+__global__ __launch_bounds__(256) void k_sum_partials(const T* __restrict__ Gp, int S, T* __restrict__ G,
+                                                      int64_t nl) {
+  const int64_t stride = (int64_t)gridDim.x * 256;
+  for (int64_t idx = (int64_t)blockIdx.x * 256 + threadIdx.x; idx < nl; idx += stride) {
+    T s = Gp[idx];
+    for (int k = 1; k < S; ++k) s = s + Gp[(int64_t)k * nl + idx];
+    G[idx] = s;
+  }
+}
+
+// ------------------------------------------------------------------------------------------
+// row helpers
+// ------------------------------------------------------------------------------------------
+template <int LPR>
+__device__ inline double row_allsum(double v) {
+#pragma unroll
+  for (int off = LPR / 2; off > 0; off >>= 1) v += __shfl_xor(v, off);
+  return v;
+}
+template <int LPR>
+__device__ inline float row_allsum(float v) {
+#pragma unroll
+  for (int off = LPR / 2; off > 0; off >>= 1) v += __shfl_xor(v, off);
+  return v;
+}
+
+// Iterate over rows: each group of LPR lanes owns one row per trip.
+#define GLX_ROW_LOOP_BEGIN(LPR)                                                        \
+  const int sub = threadIdx.x & ((LPR)-1);                                             \
+  const int64_t rows_per_block = 256 / (LPR);                                          \
+  const int64_t row_stride = (int64_t)gridDim.x * rows_per_block;                      \
+  const int64_t n_trips = (n + row_stride - 1) / row_stride;                           \
+  for (int64_t trip = 0; trip < n_trips; ++trip) {                                     \
+    const int64_t row = trip * row_stride + (int64_t)blockIdx.x * rows_per_block +     \
+                        (threadIdx.x / (LPR));                                         \
+    const bool rv = row < n;                                                           \
+    const int64_t base = (rv ? row : 0) * l;
+#define GLX_ROW_LOOP_END }
+
+// ------------------------------------------------------------------------------------------
+// ProxGD line-search trial (gl_ProxGD_primal.py:73-74, 89-92)
+// ------------------------------------------------------------------------------------------
+template <typename T, int LPR, int EPL>
+__global__ __launch_bounds__(256) void k_prox_pgd(const T* __restrict__ x, const T* __restrict__ g,
+                                                  T* __restrict__ p, T* __restrict__ z, int64_t n,
+                                                  int64_t l, double t_, double tmu_, double thres_,
+                                                  Red red) {
+  const T t = (T)t_, tmu = (T)tmu_, thres = (T)thres_;
+  double acc[4] = {0.0, 0.0, 0.0, -__builtin_inf()};
+  GLX_ROW_LOOP_BEGIN(LPR)
+  T xv[EPL], gv[EPL], w[EPL];
+  T sq = T(0);
+#pragma unroll
+  for (int e = 0; e < EPL; ++e) {
+    const int64_t j = sub + (int64_t)e * LPR;
+    const bool ok = rv && j < l;
+    xv[e] = ok ? x[base + j] : T(0);
+    gv[e] = ok ? g[base + j] : T(0);
+    w[e] = xv[e] - t * gv[e];
+    sq = sq + w[e] * w[e];
+  }
+  const T nrm = __builtin_sqrt(row_allsum<LPR>(sq));
+  T c = nrm - tmu;
+  c = (c < T(0)) ? T(0) : c;                        // np.clip(., 0, None): NaN stays NaN
+  const T d = ((nrm < thres) ? T(1) : T(0)) + nrm;
+  T psq = T(0);
+#pragma unroll
+  for (int e = 0; e < EPL; ++e) {
+    const int64_t j = sub + (int64_t)e * LPR;
+    const bool ok = rv && j < l;
+    const T pv = (w[e] * c) / d;
+    const T G = (xv[e] - pv) / t;
+    const T zv = xv[e] - t * G;
+    if (ok) {
+      p[base + j] = pv;
+      z[base + j] = zv;
+      acc[0] += (double)(gv[e] * G);
+      acc[1] += (double)(G * G);
+      acc[3] = nan_max(acc[3], (double)tabs(pv));
+      psq = psq + pv * pv;
+    }
+  }
+  const T pn = __builtin_sqrt(row_allsum<LPR>(psq));
+  if (rv && sub == 0) acc[2] += (double)pn;
+  GLX_ROW_LOOP_END
+  grid_reduce<4, 0x8u>(acc, red);
+}
+
+// FISTA trial (gl_FProxGD_primal.py:92-102)
+template <typename T, int LPR, int EPL>
+__global__ __launch_bounds__(256) void k_prox_fista(const T* __restrict__ y, const T* __restrict__ g,
+                                                    T* __restrict__ xc, int64_t n, int64_t l,
+                                                    double t_, double tmu_, double thres_, Red red) {
+  const T t = (T)t_, tmu = (T)tmu_, thres = (T)thres_;
+  double acc[4] = {0.0, 0.0, 0.0, -__builtin_inf()};
+  GLX_ROW_LOOP_BEGIN(LPR)
+  T yv[EPL], gv[EPL], w[EPL];
+  T sq = T(0);
+#pragma unroll
+  for (int e = 0; e < EPL; ++e) {
+    const int64_t j = sub + (int64_t)e * LPR;
+    const bool ok = rv && j < l;
+    yv[e] = ok ? y[base + j] : T(0);
+    gv[e] = ok ? g[base + j] : T(0);
+    w[e] = yv[e] - t * gv[e];
+    sq = sq + w[e] * w[e];
+  }
+  const T nrm = __builtin_sqrt(row_allsum<LPR>(sq));
+  T c = nrm - tmu;
+  c = (c < T(0)) ? T(0) : c;
+  const T d = ((nrm < thres) ? T(1) : T(0)) + nrm;
+  T psq = T(0);
+#pragma unroll
+  for (int e = 0; e < EPL; ++e) {
+    const int64_t j = sub + (int64_t)e * LPR;
+    const bool ok = rv && j < l;
+    const T pv = (w[e] * c) / d;
+    const T dl = pv - yv[e];
+    if (ok) {
+      xc[base + j] = pv;
+      acc[0] += (double)(gv[e] * dl);
+      acc[1] += (double)(dl * dl);
+      acc[3] = nan_max(acc[3], (double)tabs(pv));
+      psq = psq + pv * pv;
+    }
+  }
+  const T pn = __builtin_sqrt(row_allsum<LPR>(psq));
+  if (rv && sub == 0) acc[2] += (double)pn;
+  GLX_ROW_LOOP_END
+  grid_reduce<4, 0x8u>(acc, red);
+}
+
+// plain prox (C-ABI glx_prox): out [sum ||x_i||, max |x|]
+template <typename T, int LPR, int EPL>
+__global__ __launch_bounds__(256) void k_prox_plain(const T* __restrict__ wsrc, T* __restrict__ xo,
+                                                    int64_t n, int64_t l, double tmu_, double thres_,
+                                                    Red red) {
+  const T tmu = (T)tmu_, thres = (T)thres_;
+  double acc[2] = {0.0, -__builtin_inf()};
+  GLX_ROW_LOOP_BEGIN(LPR)
+  T w[EPL];
+  T sq = T(0);
+#pragma unroll
+  for (int e = 0; e < EPL; ++e) {
+    const int64_t j = sub + (int64_t)e * LPR;
+    w[e] = (rv && j < l) ? wsrc[base + j] : T(0);
+    sq = sq + w[e] * w[e];
+  }
+  const T nrm = __builtin_sqrt(row_allsum<LPR>(sq));
+  T c = nrm - tmu;
+  c = (c < T(0)) ? T(0) : c;
+  const T d = ((nrm < thres) ? T(1) : T(0)) + nrm;
+  T psq = T(0);
+#pragma unroll
+  for (int e = 0; e < EPL; ++e) {
+    const int64_t j = sub + (int64_t)e * LPR;
+    const T pv = (w[e] * c) / d;
+    if (rv && j < l) {
+      xo[base + j] = pv;
+      acc[1] = nan_max(acc[1], (double)tabs(pv));
+      psq = psq + pv * pv;
+    }
+  }
+  const T pn = __builtin_sqrt(row_allsum<LPR>(psq));
+  if (rv && sub == 0) acc[0] += (double)pn;
+  GLX_ROW_LOOP_END
+  grid_reduce<2, 0x2u>(acc, red);
+}
+
+// row-norm sum and max|x| (objective + sparsity of the current iterate)
+template <typename T, int LPR, int EPL>
+__global__ __launch_bounds__(256) void k_rownorm_max(const T* __restrict__ x, int64_t n, int64_t l, Red red) {
+  double acc[2] = {0.0, -__builtin_inf()};
+  GLX_ROW_LOOP_BEGIN(LPR)
+  T sq = T(0);
+#pragma unroll
+  for (int e = 0; e < EPL; ++e) {
+    const int64_t j = sub + (int64_t)e * LPR;
+    if (rv && j < l) {
+      const T v = x[base + j];
+      sq = sq + v * v;
+      acc[1] = nan_max(acc[1], (double)tabs(v));
+    }
+  }
+  const T nr = __builtin_sqrt(row_allsum<LPR>(sq));
+  if (rv && sub == 0) acc[0] += (double)nr;
+  GLX_ROW_LOOP_END
+  grid_reduce<2, 0x2u>(acc, red);
+}
+
+// SGD (MODE 0, gl_SGD_primal.py:56-61) / GD (MODE 1, gl_GD_primal.py:59-63) step, in place.
+template <typename T, int LPR, int EPL, int MODE>
+__global__ __launch_bounds__(256) void k_descent(T* __restrict__ x, const T* __restrict__ g, int64_t n,
+                                                 int64_t l, double alpha_, double mu_, double thres_,
+                                                 double dd_, Red red) {
+  const T alpha = (T)alpha_, mu = (T)mu_, thres = (T)thres_, dd = (T)dd_;
+  double acc[1] = {0.0};
+  GLX_ROW_LOOP_BEGIN(LPR)
+  T xv[EPL], gv[EPL];
+  T sq = T(0);
+#pragma unroll
+  for (int e = 0; e < EPL; ++e) {
+    const int64_t j = sub + (int64_t)e * LPR;
+    const bool ok = rv && j < l;
+    xv[e] = ok ? x[base + j] : T(0);
+    gv[e] = ok ? g[base + j] : T(0);
+    sq = sq + xv[e] * xv[e];
+  }
+  const T s = row_allsum<LPR>(sq);
+  T d;
+  if (MODE == 0) {
+    const T nrm = __builtin_sqrt(s);
+    d = ((nrm < thres) ? T(1) : T(0)) + nrm;
+  } else {
+    d = __builtin_sqrt(s + dd);
+  }
+  T nsq = T(0);
+#pragma unroll
+  for (int e = 0; e < EPL; ++e) {
+    const int64_t j = sub + (int64_t)e * LPR;
+    const T sub_g = gv[e] + mu * (xv[e] / d);
+    const T xn = xv[e] - alpha * sub_g;
+    if (rv && j < l) {
+      x[base + j] = xn;
+      nsq = nsq + xn * xn;
+    }
+  }
+  const T nn = __builtin_sqrt(row_allsum<LPR>(nsq));
+  if (rv && sub == 0) acc[0] += (double)nn;
+  GLX_ROW_LOOP_END
+  grid_reduce<1, 0u>(acc, red);
+}
+
+// FGD: g += mu * y / sqrt(sum y^2 + delta^2) (gl_FGD_primal.py:69-72);
+//      out: sum_i (sqrt(sum y_i^2 + delta^2) - delta) (:64-67)
+template <typename T, int LPR, int EPL>
+__global__ __launch_bounds__(256) void k_fgd_grad(const T* __restrict__ y, T* __restrict__ g, int64_t n,
+                                                  int64_t l, double mu_, double dd_, double delta_,
+                                                  Red red) {
+  const T mu = (T)mu_, dd = (T)dd_, delta = (T)delta_;
+  double acc[1] = {0.0};
+  GLX_ROW_LOOP_BEGIN(LPR)
+  T yv[EPL];
+  T sq = T(0);
+#pragma unroll
+  for (int e = 0; e < EPL; ++e) {
+    const int64_t j = sub + (int64_t)e * LPR;
+    yv[e] = (rv && j < l) ? y[base + j] : T(0);
+    sq = sq + yv[e] * yv[e];
+  }
+  const T s = row_allsum<LPR>(sq);
+  const T d = __builtin_sqrt(s + dd);
+#pragma unroll
+  for (int e = 0; e < EPL; ++e) {
+    const int64_t j = sub + (int64_t)e * LPR;
+    if (rv && j < l) g[base + j] = g[base + j] + mu * (yv[e] / d);
+  }
+  if (rv && sub == 0) acc[0] += (double)(d - delta);
+  GLX_ROW_LOOP_END
+  grid_reduce<1, 0u>(acc, red);
+}
+
+// FGD trial: xc = y - t g (identity prox, gl_FGD_primal.py:77-80, 209-212)
+// out: [sum g*(xc-y), sum (xc-y)^2, sum (sqrt(||xc_i||^2+delta^2)-delta), sum ||xc_i||, max|xc|]
+template <typename T, int LPR, int EPL>
+__global__ __launch_bounds__(256) void k_fgd_trial(const T* __restrict__ y, const T* __restrict__ g,
+                                                   T* __restrict__ xc, int64_t n, int64_t l, double t_,
+                                                   double dd_, double delta_, Red red) {
+  const T t = (T)t_, dd = (T)dd_, delta = (T)delta_;
+  double acc[5] = {0.0, 0.0, 0.0, 0.0, -__builtin_inf()};
+  GLX_ROW_LOOP_BEGIN(LPR)
+  T sq = T(0);
+#pragma unroll
+  for (int e = 0; e < EPL; ++e) {
+    const int64_t j = sub + (int64_t)e * LPR;
+    if (rv && j < l) {
+      const T yv = y[base + j], gv = g[base + j];
+      const T xv = yv - t * gv;
+      const T dl = xv - yv;
+      xc[base + j] = xv;
+      acc[0] += (double)(gv * dl);
+      acc[1] += (double)(dl * dl);
+      acc[4] = nan_max(acc[4], (double)tabs(xv));
+      sq = sq + xv * xv;
+    }
+  }
+  const T s = row_allsum<LPR>(sq);
+  if (rv && sub == 0) {
+    acc[2] += (double)(__builtin_sqrt(s + dd) - delta);
+    acc[3] += (double)__builtin_sqrt(s);
+  }
+  GLX_ROW_LOOP_END
+  grid_reduce<5, 0x10u>(acc, red);
+}
+
+// ------------------------------------------------------------------------------------------
+// flat elementwise kernels
+// ------------------------------------------------------------------------------------------
+template <typename T>
+__global__ __launch_bounds__(256) void k_count_above(const T* __restrict__ x, int64_t nl,
+                                                     const double* __restrict__ maxv, Red red) {
+  const T thr = (T)1e-6 * (T)(*maxv);
+  double v[1] = {0.0};
+  const int64_t stride = (int64_t)gridDim.x * 256;
+  for (int64_t idx = (int64_t)blockIdx.x * 256 + threadIdx.x; idx < nl; idx += stride)
+    v[0] += (tabs(x[idx]) > thr) ? 1.0 : 0.0;
+  grid_reduce<1, 0u>(v, red);
+}
+
+template <typename T>
+__global__ __launch_bounds__(256) void k_threshold(T* __restrict__ x, int64_t nl, double thres_, int* flag) {
+  const T thres = (T)thres_;
+  int changed = 0;
+  const int64_t stride = (int64_t)gridDim.x * 256;
+  for (int64_t idx = (int64_t)blockIdx.x * 256 + threadIdx.x; idx < nl; idx += stride) {
+    const T v = x[idx];
+    if (tabs(v) < thres) {
+      if (v != T(0)) changed = 1;
+      x[idx] = T(0);
+    }
+  }
+  if (__any(changed) && (threadIdx.x & 63) == 0) atomicOr(flag, 1);
+}
+
+template <typename T>
+__global__ __launch_bounds__(256) void k_axpby(const T* __restrict__ xk, const T* __restrict__ vk,
+                                               T* __restrict__ y, int64_t nl, double a_, double b_) {
+  const T a = (T)a_, b = (T)b_;
+  const int64_t stride = (int64_t)gridDim.x * 256;
+  for (int64_t idx = (int64_t)blockIdx.x * 256 + threadIdx.x; idx < nl; idx += stride)
+    y[idx] = a * xk[idx] + b * vk[idx];
+}
+
+template <typename T>
+__global__ __launch_bounds__(256) void k_fista_v(const T* __restrict__ xk, const T* __restrict__ x,
+                                                 T* __restrict__ v, int64_t nl, double theta_) {
+  const T theta = (T)theta_;
+  const int64_t stride = (int64_t)gridDim.x * 256;
+  for (int64_t idx = (int64_t)blockIdx.x * 256 + threadIdx.x; idx < nl; idx += stride) {
+    const T xo = xk[idx];
+    v[idx] = xo + (x[idx] - xo) / theta;
+  }
+}
+
+__global__ void k_record_f(const double* __restrict__ s, int i_sumsq, int i_reg, double mu,
+                           double* __restrict__ fh, int64_t idx) {
+  if (threadIdx.x == 0) fh[idx] = 0.5 * s[i_sumsq] + mu * s[i_reg];
+}
+
+// ------------------------------------------------------------------------------------------
+// launchers
+// ------------------------------------------------------------------------------------------
+template <int LPR, typename F>
+static void dispatch_epl(int64_t l, F&& f) {
+  const int64_t epl = (l + LPR - 1) / LPR;
+  switch (epl) {
+    case 1: f(std::integral_constant<int, 1>{}); break;
+    case 2: f(std::integral_constant<int, 2>{}); break;
+    case 3: f(std::integral_constant<int, 3>{}); break;
+    case 4: f(std::integral_constant<int, 4>{}); break;
+    case 5: f(std::integral_constant<int, 5>{}); break;
+    case 6: f(std::integral_constant<int, 6>{}); break;
+    case 7: f(std::integral_constant<int, 7>{}); break;
+    default: f(std::integral_constant<int, 8>{}); break;
+  }
+}
+// F receives (lpr_constant, epl_constant)
+template <typename F>
+static void dispatch_row(int64_t l, F&& f) {
+  if (l <= 1) f(std::integral_constant<int, 1>{}, std::integral_constant<int, 1>{});
+  else if (l <= 2) f(std::integral_constant<int, 2>{}, std::integral_constant<int, 1>{});
+  else if (l <= 4) f(std::integral_constant<int, 4>{}, std::integral_constant<int, 1>{});
+  else if (l <= 8) f(std::integral_constant<int, 8>{}, std::integral_constant<int, 1>{});
+  else dispatch_epl<16>(l, [&](auto epl) { f(std::integral_constant<int, 16>{}, epl); });
+}
+static inline unsigned row_grid(int64_t n, int lpr) { return grid_for(n, 256 / lpr); }
+
+template <typename T>
+void launch_finalize_residual(const T* P, int S, const T* B, T* R, int64_t ml, const int* gate,
+                              int gate_mode, Red red, hipStream_t st) {
+  hipLaunchKernelGGL(k_finalize_residual<T>, dim3(grid_for(ml, 256 * 4)), dim3(256), 0, st, P, S, B, R,
+                     ml, gate, gate_mode, red);
+}
+template <typename T>
+void launch_sum_partials(const T* Gp, int S, T* G, int64_t nl, hipStream_t st) {
+  hipLaunchKernelGGL(k_sum_partials<T>, dim3(grid_for(nl, 256 * 4)), dim3(256), 0, st, Gp, S, G, nl);
+}
+template <typename T>
+void launch_prox_pgd(const T* x, const T* g, T* p, T* z, int64_t n, int64_t l, double t, double mu,
+                     double thres, Red red, hipStream_t st) {
+  dispatch_row(l, [&](auto lpr, auto epl) {
+    hipLaunchKernelGGL((k_prox_pgd<T, decltype(lpr)::value, decltype(epl)::value>),
+                       dim3(row_grid(n, lpr)), dim3(256), 0, st, x, g, p, z, n, l, t, t * mu, thres, red);
+  });
+}
+template <typename T>
+void launch_prox_fista(const T* y, const T* g, T* xc, int64_t n, int64_t l, double t, double mu,
+                       double thres, Red red, hipStream_t st) {
+  dispatch_row(l, [&](auto lpr, auto epl) {
+    hipLaunchKernelGGL((k_prox_fista<T, decltype(lpr)::value, decltype(epl)::value>),
+                       dim3(row_grid(n, lpr)), dim3(256), 0, st, y, g, xc, n, l, t, t * mu, thres, red);
+  });
+}
+template <typename T>
+void launch_prox_plain(const T* w, T* x, int64_t n, int64_t l, double t, double mu, double thres,
+                       Red red, hipStream_t st) {
+  dispatch_row(l, [&](auto lpr, auto epl) {
+    hipLaunchKernelGGL((k_prox_plain<T, decltype(lpr)::value, decltype(epl)::value>),
+                       dim3(row_grid(n, lpr)), dim3(256), 0, st, w, x, n, l, t * mu, thres, red);
+  });
+}
+template <typename T>
+void launch_rownorm_max(const T* x, int64_t n, int64_t l, Red red, hipStream_t st) {
+  dispatch_row(l, [&](auto lpr, auto epl) {
+    hipLaunchKernelGGL((k_rownorm_max<T, decltype(lpr)::value, decltype(epl)::value>),
+                       dim3(row_grid(n, lpr)), dim3(256), 0, st, x, n, l, red);
+  });
+}
+template <typename T>
+void launch_descent(T* x, const T* g, int64_t n, int64_t l, double alpha, double mu, double thres,
+                    double delta, int mode, Red red, hipStream_t st) {
+  dispatch_row(l, [&](auto lpr, auto epl) {
+    if (mode == 0)
+      hipLaunchKernelGGL((k_descent<T, decltype(lpr)::value, decltype(epl)::value, 0>),
+                         dim3(row_grid(n, lpr)), dim3(256), 0, st, x, g, n, l, alpha, mu, thres,
+                         delta * delta, red);
+    else
+      hipLaunchKernelGGL((k_descent<T, decltype(lpr)::value, decltype(epl)::value, 1>),
+                         dim3(row_grid(n, lpr)), dim3(256), 0, st, x, g, n, l, alpha, mu, thres,
+                         delta * delta, red);
+  });
+}
+template <typename T>
+void launch_fgd_grad(const T* y, T* g, int64_t n, int64_t l, double mu, double delta, Red red,
+                     hipStream_t st) {
+  dispatch_row(l, [&](auto lpr, auto epl) {
+    hipLaunchKernelGGL((k_fgd_grad<T, decltype(lpr)::value, decltype(epl)::value>),
+                       dim3(row_grid(n, lpr)), dim3(256), 0, st, y, g, n, l, mu, delta * delta, delta, red);
+  });
+}
+template <typename T>
+void launch_fgd_trial(const T* y, const T* g, T* xc, int64_t n, int64_t l, double t, double delta,
+                      Red red, hipStream_t st) {
+  dispatch_row(l, [&](auto lpr, auto epl) {
+    hipLaunchKernelGGL((k_fgd_trial<T, decltype(lpr)::value, decltype(epl)::value>),
+                       dim3(row_grid(n, lpr)), dim3(256), 0, st, y, g, xc, n, l, t, delta * delta, delta, red);
+  });
+}
+template <typename T>
+void launch_count_above(const T* x, int64_t nl, const double* maxv, Red red, hipStream_t st) {
+  hipLaunchKernelGGL(k_count_above<T>, dim3(grid_for(nl, 256 * 4)), dim3(256), 0, st, x, nl, maxv, red);
+}
+template <typename T>
+void launch_threshold(T* x, int64_t nl, double thres, int* flag, hipStream_t st) {
+  hipLaunchKernelGGL(k_threshold<T>, dim3(grid_for(nl, 256 * 4)), dim3(256), 0, st, x, nl, thres, flag);
+}
+template <typename T>
+void launch_axpby(const T* xk, const T* vk, T* y, int64_t nl, double a, double b, hipStream_t st) {
+  hipLaunchKernelGGL(k_axpby<T>, dim3(grid_for(nl, 256 * 4)), dim3(256), 0, st, xk, vk, y, nl, a, b);
+}
+template <typename T>
+void launch_fista_v(const T* xk, const T* x, T* v, int64_t nl, double theta, hipStream_t st) {
+  hipLaunchKernelGGL(k_fista_v<T>, dim3(grid_for(nl, 256 * 4)), dim3(256), 0, st, xk, x, v, nl, theta);
+}
+void launch_record_f(const double* s, int i_sumsq, int i_reg, double mu, double* fh, int64_t idx,
+                     hipStream_t st) {
+  hipLaunchKernelGGL(k_record_f, dim3(1), dim3(64), 0, st, s, i_sumsq, i_reg, mu, fh, idx);
+}
+
+#define GLX_INST(T)                                                                                  \
+  template void launch_finalize_residual<T>(const T*, int, const T*, T*, int64_t, const int*, int,  \
+                                            Red, hipStream_t);                                      \
+  template void launch_sum_partials<T>(const T*, int, T*, int64_t, hipStream_t);                    \
+  template void launch_prox_pgd<T>(const T*, const T*, T*, T*, int64_t, int64_t, double, double,    \
+                                   double, Red, hipStream_t);                                       \
+  template void launch_prox_fista<T>(const T*, const T*, T*, int64_t, int64_t, double, double,      \
+                                     double, Red, hipStream_t);                                     \
+  template void launch_prox_plain<T>(const T*, T*, int64_t, int64_t, double, double, double, Red,   \
+                                     hipStream_t);                                                  \
+  template void launch_rownorm_max<T>(const T*, int64_t, int64_t, Red, hipStream_t);                \
+  template void launch_descent<T>(T*, const T*, int64_t, int64_t, double, double, double, double,   \
+                                  int, Red, hipStream_t);                                           \
+  template void launch_fgd_grad<T>(const T*, T*, int64_t, int64_t, double, double, Red,             \
+                                   hipStream_t);                                                    \
+  template void launch_fgd_trial<T>(const T*, const T*, T*, int64_t, int64_t, double, double, Red,  \
+                                    hipStream_t);                                                   \
+  template void launch_count_above<T>(const T*, int64_t, const double*, Red, hipStream_t);          \
+  template void launch_threshold<T>(T*, int64_t, double, int*, hipStream_t);                        \
+  template void launch_axpby<T>(const T*, const T*, T*, int64_t, double, double, hipStream_t);      \
+  template void launch_fista_v<T>(const T*, const T*, T*, int64_t, double, hipStream_t);
+
+GLX_INST(double)
+GLX_INST(float)
+
+}  // namespace glx

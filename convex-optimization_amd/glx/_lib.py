@@ -1,0 +1,116 @@
+"""ctypes binding of libglx.so (the C ABI in include/glx.h).
+
+The library is built in-tree (``make -C convex-optimization_amd``) and is linked against
+PyTorch's bundled HIP runtime; ``torch`` is imported before the library is loaded so that the
+process holds exactly one HIP runtime and torch's device pointers / streams are native to it.
+There is no fallback: if the library is missing, :func:`lib` raises.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+from ctypes import POINTER, c_char_p, c_double, c_int, c_int32, c_int64, c_size_t, c_uint8, c_void_p
+
+import torch  # noqa: F401  (must be loaded first: it owns the HIP runtime libglx binds to)
+
+LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "libglx.so")
+
+GLX_F32, GLX_F64 = 0, 1
+GLX_PROXGD, GLX_FPROXGD, GLX_SGD, GLX_GD, GLX_FGD = range(5)
+STEP_TYPES = {"line_search": 0, "fixed": 1, "diminishing": 2, "diminishing2": 3}
+METHODS = {"gl_ProxGD_primal": GLX_PROXGD, "gl_FProxGD_primal": GLX_FPROXGD,
+           "gl_SGD_primal": GLX_SGD, "gl_GD_primal": GLX_GD, "gl_FGD_primal": GLX_FGD}
+COMM_ID_BYTES = 128
+
+
+class GlxOpts(ctypes.Structure):
+    _fields_ = [("maxit", c_int32), ("thres", c_double), ("step_type", c_int32),
+                ("alpha0", c_double), ("ftol", c_double), ("stable_len_threshold", c_int32),
+                ("ls_coeff", c_double), ("ls_maxit", c_int32), ("delta", c_double),
+                ("continuous_subgradient", c_int32), ("exact_objective", c_int32),
+                ("profile", c_int32), ("max_total_iters", c_int64), ("ax_variant", c_int32),
+                ("reserved", c_int32 * 7)]
+
+
+class GlxProblem(ctypes.Structure):
+    _fields_ = [("dtype", c_int32), ("method", c_int32), ("m", c_int64), ("n", c_int64),
+                ("l", c_int64), ("A", c_void_p), ("b", c_void_p), ("x", c_void_p),
+                ("mu0", c_double), ("comm", c_void_p)]
+
+
+class GlxResult(ctypes.Structure):
+    _fields_ = [("iters", c_int64), ("fval", c_double), ("tt", c_double),
+                ("f_hist", POINTER(c_double)), ("f_hist_best", POINTER(c_double)),
+                ("f_cap", c_int64), ("n_fhist", c_int64), ("ax_calls", c_int64),
+                ("atr_calls", c_int64), ("syncs", c_int64)]
+
+
+class GlxError(RuntimeError):
+    """Error returned by libglx (message from glx_last_error())."""
+
+    def __init__(self, code: int, msg: str):
+        super().__init__("libglx error %d: %s" % (code, msg))
+        self.code = code
+
+
+_LIB = None
+
+_SIGS = {
+    "glx_abi_version": (c_int, []),
+    "glx_last_error": (c_char_p, []),
+    "glx_default_opts": (c_int, [c_int, POINTER(GlxOpts)]),
+    "glx_workspace_bytes": (c_int, [POINTER(GlxProblem), POINTER(GlxOpts), POINTER(c_size_t)]),
+    "glx_session_create": (c_int, [POINTER(c_void_p), POINTER(GlxProblem), POINTER(GlxOpts),
+                                   c_void_p, c_size_t, c_void_p]),
+    "glx_session_run": (c_int, [c_void_p, c_int64, POINTER(c_int64), POINTER(c_int32)]),
+    "glx_session_finish": (c_int, [c_void_p, POINTER(GlxResult)]),
+    "glx_session_kernel_time": (c_int, [c_void_p, c_int, POINTER(c_int64), POINTER(c_double)]),
+    "glx_session_destroy": (None, [c_void_p]),
+    "glx_solve": (c_int, [POINTER(GlxProblem), POINTER(GlxOpts), c_void_p, c_size_t,
+                          POINTER(GlxResult), c_void_p]),
+    "glx_residual": (c_int, [c_int, c_int64, c_int64, c_int64, c_void_p, c_void_p, c_void_p,
+                             c_void_p, c_void_p, c_void_p, c_size_t, c_int, c_void_p]),
+    "glx_gradient": (c_int, [c_int, c_int64, c_int64, c_int64, c_void_p, c_void_p, c_void_p,
+                             c_void_p, c_size_t, c_void_p]),
+    "glx_prox": (c_int, [c_int, c_int64, c_int64, c_void_p, c_double, c_double, c_double,
+                         c_void_p, c_void_p, c_void_p, c_size_t, c_void_p]),
+    "glx_kernel_workspace_bytes": (c_int, [c_int, c_int64, c_int64, c_int64, POINTER(c_size_t)]),
+    "glx_comm_unique_id": (c_int, [POINTER(c_uint8)]),
+    "glx_comm_create": (c_int, [POINTER(c_void_p), POINTER(c_uint8), c_int, c_int]),
+    "glx_comm_allreduce": (c_int, [c_void_p, c_void_p, c_int64, c_int, c_void_p]),
+    "glx_comm_destroy": (None, [c_void_p]),
+}
+
+EXPORTED = tuple(_SIGS)
+
+
+def lib():
+    """Load (once) and return the libglx handle; raise if it has not been built."""
+    global _LIB
+    if _LIB is None:
+        if not os.path.exists(LIB_PATH):
+            raise RuntimeError("libglx.so not found at %s — build it with "
+                               "`python -c 'import __graft_entry__ as g; g.build()'` "
+                               "(no CPU fallback exists)" % LIB_PATH)
+        h = ctypes.CDLL(LIB_PATH)
+        for name, (res, args) in _SIGS.items():
+            fn = getattr(h, name)
+            fn.restype = res
+            fn.argtypes = args
+        if h.glx_abi_version() != 1:
+            raise RuntimeError("libglx ABI mismatch")
+        _LIB = h
+    return _LIB
+
+
+def check(rc: int):
+    if rc != 0:
+        msg = lib().glx_last_error()
+        raise GlxError(rc, msg.decode() if msg else "?")
+    return rc
+
+
+def default_opts(method: int) -> GlxOpts:
+    o = GlxOpts()
+    check(lib().glx_default_opts(method, ctypes.byref(o)))
+    return o

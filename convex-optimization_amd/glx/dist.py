@@ -1,0 +1,64 @@
+"""Multi-GPU plumbing: one process per GPU, A and b row-sharded, RCCL inside libglx.
+
+The bootstrap (exchanging RCCL's unique id) rides on ``torch.distributed`` with whatever
+backend the launcher initialised (gloo is enough); every GPU collective of the solve itself
+is issued by libglx on the compute stream (src/comm.cpp): one sum all-reduce of the n x l
+gradient per A^T r, plus 8-byte all-reduces of squared residual norms.
+"""
+from __future__ import annotations
+
+import ctypes
+from typing import Tuple
+
+import torch
+
+from . import _lib
+from ._lib import check, lib
+
+
+def shard_rows(m: int, world: int, rank: int) -> Tuple[int, int]:
+    """Contiguous row range [r0, r1) of rank ``rank`` (sizes differ by at most one row)."""
+    if world < 1 or not 0 <= rank < world:
+        raise ValueError("bad world/rank")
+    return (m * rank) // world, (m * (rank + 1)) // world
+
+
+class Comm:
+    """An RCCL communicator created from a unique id broadcast over torch.distributed."""
+
+    def __init__(self, handle: ctypes.c_void_p, world: int, rank: int):
+        self.handle = handle
+        self.world = world
+        self.rank = rank
+
+    @classmethod
+    def from_torch_distributed(cls, group=None) -> "Comm":
+        import torch.distributed as dist
+        rank, world = dist.get_rank(group), dist.get_world_size(group)
+        uid = torch.zeros(_lib.COMM_ID_BYTES, dtype=torch.uint8)
+        if rank == 0:
+            arr = (ctypes.c_uint8 * _lib.COMM_ID_BYTES)()
+            check(lib().glx_comm_unique_id(arr))
+            uid.copy_(torch.tensor(list(bytes(arr)), dtype=torch.uint8))
+        if dist.get_backend(group) == "nccl":
+            dev_uid = uid.cuda()
+            dist.broadcast(dev_uid, src=0, group=group)
+            uid = dev_uid.cpu()
+        else:
+            dist.broadcast(uid, src=0, group=group)
+        arr = (ctypes.c_uint8 * _lib.COMM_ID_BYTES)(*uid.tolist())
+        h = ctypes.c_void_p()
+        check(lib().glx_comm_create(ctypes.byref(h), arr, world, rank))
+        return cls(h, world, rank)
+
+    def allreduce_(self, t: torch.Tensor) -> torch.Tensor:
+        """In-place sum all-reduce of a contiguous float32/float64 device tensor."""
+        dt = _lib.GLX_F64 if t.dtype == torch.float64 else _lib.GLX_F32
+        stream = ctypes.c_void_p(torch.cuda.current_stream(t.device).cuda_stream)
+        check(lib().glx_comm_allreduce(self.handle, ctypes.c_void_p(t.data_ptr()), t.numel(), dt, stream))
+        return t
+
+    def close(self):
+        if self.handle:
+            lib().glx_comm_destroy(self.handle)
+            self.handle = None

@@ -1,0 +1,73 @@
+"""Single-kernel entry points of libglx (``glx_residual`` / ``glx_gradient`` / ``glx_prox``).
+
+These are the dense products and the group prox of the reference iteration exposed one at a
+time — ``A @ x - b`` (gl_ProxGD_primal.py:25,61), ``A.T @ r`` (:129) and ``prox_th``
+(:65-71) — used by the kernel-level tests and available for composition. All tensors are
+contiguous device tensors of one dtype (float32 / float64).
+"""
+from __future__ import annotations
+
+import ctypes
+from typing import Tuple
+
+import torch
+
+from . import _lib
+from ._lib import check, lib
+
+
+def _dt(t: torch.Tensor) -> int:
+    if t.dtype == torch.float64:
+        return _lib.GLX_F64
+    if t.dtype == torch.float32:
+        return _lib.GLX_F32
+    raise ValueError("float32 or float64 required")
+
+
+def _ws(dtype: int, m: int, n: int, l: int, device) -> torch.Tensor:
+    nb = ctypes.c_size_t(0)
+    check(lib().glx_kernel_workspace_bytes(dtype, m, n, l, ctypes.byref(nb)))
+    return torch.empty(int(nb.value), dtype=torch.uint8, device=device)
+
+
+def _stream(device) -> ctypes.c_void_p:
+    return ctypes.c_void_p(torch.cuda.current_stream(device).cuda_stream)
+
+
+def residual(A: torch.Tensor, X: torch.Tensor, B: torch.Tensor, variant: int = 0
+             ) -> Tuple[torch.Tensor, torch.Tensor]:
+    """R = A X - B and 1/2 ||R||_F^2 (a 1-element float64 device tensor)."""
+    m, n = A.shape
+    l = X.shape[1]
+    dt = _dt(A)
+    R = torch.empty((m, l), dtype=A.dtype, device=A.device)
+    h = torch.empty(1, dtype=torch.float64, device=A.device)
+    ws = _ws(dt, m, n, l, A.device)
+    check(lib().glx_residual(dt, m, n, l, A.data_ptr(), X.data_ptr(), B.data_ptr(), R.data_ptr(),
+                             h.data_ptr(), ws.data_ptr(), ws.numel(), variant, _stream(A.device)))
+    return R, h
+
+
+def gradient(A: torch.Tensor, R: torch.Tensor) -> torch.Tensor:
+    """G = A^T R."""
+    m, n = A.shape
+    l = R.shape[1]
+    dt = _dt(A)
+    G = torch.empty((n, l), dtype=A.dtype, device=A.device)
+    ws = _ws(dt, m, n, l, A.device)
+    check(lib().glx_gradient(dt, m, n, l, A.data_ptr(), R.data_ptr(), G.data_ptr(), ws.data_ptr(),
+                             ws.numel(), _stream(A.device)))
+    return G
+
+
+def prox(W: torch.Tensor, t: float, mu: float, thres: float = 1e-3
+         ) -> Tuple[torch.Tensor, torch.Tensor]:
+    """Group prox with the reference's denominator quirk; returns (X, [sum ||x_i||, max|x|])."""
+    n, l = W.shape
+    dt = _dt(W)
+    X = torch.empty_like(W)
+    sums = torch.empty(2, dtype=torch.float64, device=W.device)
+    ws = _ws(dt, 1, n, l, W.device)
+    check(lib().glx_prox(dt, n, l, W.data_ptr(), float(t), float(mu), float(thres), X.data_ptr(),
+                         sums.data_ptr(), ws.data_ptr(), ws.numel(), _stream(W.device)))
+    return X, sums

@@ -1,0 +1,156 @@
+/*
+ * glx.h — C ABI of libglx.so, the MI355X-native group-lasso first-order solver.
+ *
+ * Problem:  min_x  1/2 ||A x - b||_F^2 + mu * sum_i ||x_i||_2,   A: m x n, b: m x l, x: n x l
+ * (row-major, contiguous; group i = row i of x, contiguous along l).
+ *
+ * This ABI replaces the bodies of the reference's solver functions, which all share the
+ * signature  gl_<method>(x0, A, b, mu_0, opts) -> (x, iters, out):
+ *   GLX_PROXGD  <- code/gl_ProxGD_primal.py:9-146   (proximal gradient + Armijo line search)
+ *   GLX_FPROXGD <- code/gl_FProxGD_primal.py:9-161  (FISTA + backtracking)
+ *   GLX_SGD     <- code/gl_SGD_primal.py:9-109      (subgradient)
+ *   GLX_GD      <- code/gl_GD_primal.py:9-112       (gradient on the smoothed problem)
+ *   GLX_FGD     <- code/gl_FGD_primal.py:9-163      (Nesterov on the smoothed problem)
+ * and the dense products inside them (A @ x at gl_ProxGD_primal.py:25,61,129 and
+ * A.T @ r at :129), which NumPy sends to host BLAS.
+ *
+ * Conventions
+ *   - Every pointer named "device" is HBM memory on the current HIP device; the library never
+ *     allocates it: callers (the Python layer, through PyTorch) own A, b, x and the workspace.
+ *   - `stream` is a hipStream_t passed as void* (NULL = the null stream). All calls are
+ *     stream-ordered; glx_session_run() additionally synchronises the stream to read the
+ *     scalars its control flow needs (line-search tests, the stop rule).
+ *   - Return value: 0 on success, a GLX_E* code otherwise; glx_last_error() describes the
+ *     failure (thread-local). No C++ exception crosses the ABI.
+ *   - dtype is the compute type: GLX_F64 (double) or GLX_F32 (float). Scalars cross the ABI as
+ *     double and are rounded to dtype where the reference's NumPy would (NEP 50 weak scalars).
+ */
+#ifndef GLX_H_
+#define GLX_H_
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define GLX_ABI_VERSION 1
+
+enum glx_dtype { GLX_F32 = 0, GLX_F64 = 1 };
+enum glx_method { GLX_PROXGD = 0, GLX_FPROXGD = 1, GLX_SGD = 2, GLX_GD = 3, GLX_FGD = 4 };
+/* step_type option (gl_ProxGD_primal.py:78-101) */
+enum glx_step { GLX_STEP_LINE_SEARCH = 0, GLX_STEP_FIXED = 1, GLX_STEP_DIMINISHING = 2,
+                GLX_STEP_DIMINISHING2 = 3 };
+enum glx_status { GLX_OK = 0, GLX_E_INVALID = 1, GLX_E_HIP = 2, GLX_E_RCCL = 3,
+                  GLX_E_WORKSPACE = 4, GLX_E_STATE = 5 };
+
+/* Solver options; field names and defaults follow the reference's default_opts dicts
+ * (gl_ProxGD_primal.py:10-19 etc.). glx_default_opts() fills the per-method defaults. */
+typedef struct glx_opts {
+  int32_t maxit;                  /* iterations per continuation phase                   */
+  double  thres;                  /* hard threshold / prox denominator switch (1e-3)      */
+  int32_t step_type;              /* enum glx_step                                        */
+  double  alpha0;                 /* initial / fixed step                                 */
+  double  ftol;                   /* stop rule relative tolerance                         */
+  int32_t stable_len_threshold;   /* stop after this many consecutive stable iterations   */
+  double  ls_coeff;               /* line_search_attenuation_coeffi                       */
+  int32_t ls_maxit;               /* maxit_line_search_iter                               */
+  double  delta;                  /* smoothing parameter (GD / FGD)                       */
+  int32_t continuous_subgradient; /* SGD/GD: alpha0 = 1/lambda_max(A^T A) (caller-computed:
+                                     pass alpha0 accordingly; kept for ABI completeness)   */
+  /* ---- build-only keys (the reference has no equivalent) ---- */
+  int32_t exact_objective;        /* ProxGD: 1 = recompute A@x for every objective (3 passes
+                                     over A per iteration, bit-faithful to the reference's
+                                     evaluation order); 0 = reuse the accepted line-search
+                                     residual A@z, z = x - t*G_t (ulp-level difference)      */
+  int32_t profile;                /* 1 = time every A@x / A^T r launch with HIP events      */
+  int64_t max_total_iters;        /* stop after this many iterations in total (0 = off)     */
+  int32_t ax_variant;             /* A@x kernel variant for A/B tests (0 = auto)            */
+  int32_t reserved[7];
+} glx_opts;
+
+/* One problem instance. For multi-GPU runs A and b are this rank's row shard
+ * (m = local rows) and `comm` is a communicator from glx_comm_create(); x, mu and the
+ * options are replicated on every rank. */
+typedef struct glx_problem {
+  int32_t dtype;        /* enum glx_dtype                                    */
+  int32_t method;       /* enum glx_method                                   */
+  int64_t m, n, l;      /* local rows of A, columns of A (= groups), columns of b/x */
+  const void* A;        /* device, m x n row-major                          */
+  const void* b;        /* device, m x l                                    */
+  void* x;              /* device, n x l: x0 on entry, the iterate on return */
+  double mu0;           /* mu_0                                             */
+  void* comm;           /* glx_comm* or NULL                                */
+} glx_problem;
+
+typedef struct glx_result {
+  int64_t iters;        /* k: total iterations (the reference's second return value) */
+  double fval;          /* objective of the returned x (out["fval"])                 */
+  double tt;            /* seconds spent in the iteration loop, stream-synchronised   */
+  double* f_hist;       /* host, capacity f_cap: objective per iteration (out["f_hist"]) */
+  double* f_hist_best;  /* host, capacity f_cap (out["f_hist_best"])                 */
+  int64_t f_cap;
+  int64_t n_fhist;      /* entries written                                           */
+  int64_t ax_calls;     /* passes of A@x issued (executed-work accounting)            */
+  int64_t atr_calls;    /* passes of A^T r issued                                     */
+  int64_t syncs;        /* host<->device synchronisations                             */
+} glx_result;
+
+typedef struct glx_session glx_session;
+typedef struct glx_comm glx_comm;
+
+int         glx_abi_version(void);
+const char* glx_last_error(void);
+int         glx_default_opts(int method, glx_opts* out);
+
+/* Workspace (device bytes) a session needs for this problem. */
+int glx_workspace_bytes(const glx_problem* prob, const glx_opts* opts, size_t* bytes);
+
+/* Session API: the reference loop split so that a caller can time exactly K iterations.
+ * create  — validates shapes, carves the workspace, copies nothing (x is used in place).
+ * run     — runs up to max_steps further iterations (<=0: to completion); *done = steps run.
+ *           *finished = 1 once all continuation phases are over.
+ * finish  — evaluates fval of the current x and copies the histories into res.
+ * destroy — frees host-side state (pinned buffers, events). */
+int  glx_session_create(glx_session** out, const glx_problem* prob, const glx_opts* opts,
+                        void* workspace, size_t workspace_bytes, void* stream);
+int  glx_session_run(glx_session* s, int64_t max_steps, int64_t* done, int32_t* finished);
+int  glx_session_finish(glx_session* s, glx_result* res);
+/* average device time (ms) of the A@x (kind 0) / A^T r (kind 1) launches recorded while
+ * opts.profile = 1; resets the accumulators. */
+int  glx_session_kernel_time(glx_session* s, int kind, int64_t* launches, double* total_ms);
+void glx_session_destroy(glx_session* s);
+
+/* One-shot solve: create + run to completion + finish + destroy. */
+int glx_solve(const glx_problem* prob, const glx_opts* opts, void* workspace,
+              size_t workspace_bytes, glx_result* res, void* stream);
+
+/* ---- single kernels (test / composition surface) ---- */
+/* R = A X - B (m x l); *half_sumsq_dev = 1/2 ||R||^2 (device double). */
+int glx_residual(int dtype, int64_t m, int64_t n, int64_t l, const void* A, const void* X,
+                 const void* B, void* R, void* half_sumsq_dev, void* workspace,
+                 size_t workspace_bytes, int variant, void* stream);
+/* G = A^T R (n x l). */
+int glx_gradient(int dtype, int64_t m, int64_t n, int64_t l, const void* A, const void* R,
+                 void* G, void* workspace, size_t workspace_bytes, void* stream);
+/* X_out = prox_{t*mu*||.||_{1,2}}(W) with the reference's (||w_i|| < thres) + ||w_i||
+ * denominator (gl_ProxGD_primal.py:65-71); sums_dev[0] = sum_i ||X_out_i||,
+ * sums_dev[1] = max |X_out| (device doubles). */
+int glx_prox(int dtype, int64_t n, int64_t l, const void* W, double t, double mu, double thres,
+             void* X_out, void* sums_dev, void* workspace, size_t workspace_bytes, void* stream);
+/* Workspace bytes for the single-kernel entry points above. */
+int glx_kernel_workspace_bytes(int dtype, int64_t m, int64_t n, int64_t l, size_t* bytes);
+
+/* ---- multi-GPU (row-sharded A, one RCCL all-reduce of A^T r per gradient) ---- */
+#define GLX_COMM_ID_BYTES 128
+int  glx_comm_unique_id(uint8_t id[GLX_COMM_ID_BYTES]);
+int  glx_comm_create(glx_comm** out, const uint8_t id[GLX_COMM_ID_BYTES], int nranks, int rank);
+/* in-place sum all-reduce of `count` elements of dtype on `stream` (exposed for tests) */
+int  glx_comm_allreduce(glx_comm* c, void* buf, int64_t count, int dtype, void* stream);
+void glx_comm_destroy(glx_comm* c);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* GLX_H_ */

@@ -83,6 +83,13 @@ CASES.append(("ragged_gl_FProxGD_primal", "gl_FProxGD_primal", (333, 250, 17), 7
               {"alpha0": step_size_for(333, 250), "maxit": 50}))
 CASES.append(("ragged_gl_SGD_primal", "gl_SGD_primal", (301, 517, 3), 79, "f64",
               {"alpha0": step_size_for(301, 517), "maxit": 30}))
+for s in ("gl_FGD_primal", "gl_GD_primal", "gl_SGD_primal"):
+    for it in (3, 40):
+        CASES.append(("short%d_%s" % (it, s), s, DEF, 97006855, "f64", {"maxit": it}))
+CASES.append(("mid_512x1024x16_f64_gl_FGD_primal", "gl_FGD_primal", (512, 1024, 16), 1250, "f64",
+              {"alpha0": step_size_for(512, 1024), "maxit": 40}))
+CASES.append(("mid_256x512x32_f32_gl_SGD_primal", "gl_SGD_primal", (256, 512, 32), 1266, "f32",
+              {"alpha0": step_size_for(256, 512), "maxit": 40, "step_type": "fixed"}))
 CASES.append(("steps_fixed_gl_ProxGD_primal", "gl_ProxGD_primal", DEF, 97006855, "f64",
               {"step_type": "fixed", "maxit": 100}))
 CASES.append(("steps_dim_gl_FProxGD_primal", "gl_FProxGD_primal", DEF, 97006855, "f64",
