@@ -86,7 +86,7 @@ def cpu_baseline(method, A, b, x0, mu, opts, budget_s=15.0):
     _, k1, _ = fn(xn, An, bn, mu, o)
     t1 = time.perf_counter() - t0
     per_iter = t1 / max(1, k1)
-    maxit = int(max(1, min(20, budget_s / (3 * per_iter))))
+    maxit = int(max(1, min(200, budget_s / (3 * per_iter))))
     o = dict(opts, maxit=maxit)
     t0 = time.perf_counter()
     _, k, _ = fn(xn, An, bn, mu, o)
@@ -119,6 +119,7 @@ def main():
     ap.add_argument("--l", type=int, default=32)
     ap.add_argument("--variant", type=int, default=0)
     ap.add_argument("--exact", type=int, default=0)
+    ap.add_argument("--profile", type=int, default=1, help="HIP events around A@x / A^T r launches")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     args = ap.parse_args()
 
@@ -151,7 +152,7 @@ def main():
     alpha0 = float(1.0 / (math.sqrt(m) + math.sqrt(n)) ** 2)
     total = args.warmup + args.steps
     opts = {"alpha0": alpha0, "maxit": max(total + 1, 2500), "max_total_iters": total,
-            "profile": 1, "ax_variant": args.variant, "exact_objective": args.exact}
+            "profile": args.profile, "ax_variant": args.variant, "exact_objective": args.exact}
     x = x0.clone()
     s = glx.Session(args.method, x, A, b, mu, opts, comm=comm)
     s.run(args.warmup)
@@ -182,8 +183,12 @@ def main():
         ml = r1 - r0
         ax_avg_s = (ax_ms / max(1, ax_n)) / 1e3
         atr_avg_s = (atr_ms / max(1, atr_n)) / 1e3
-        ax_bytes = es * (ml * n + (ml + n) * l)
-        ax_flops = 2.0 * ml * n * l
+        # right-hand sides batched per A@x launch (e.g. A @ [z | p_thr] for ProxGD)
+        nsrc = res["ax_sources"] / max(1, res["ax_calls"])
+        ax_bytes = es * (ml * n + (ml + n) * l * nsrc)
+        atr_bytes = es * (ml * n + (ml + n) * l)
+        ax_flops = 2.0 * ml * n * l * nsrc
+        atr_flops = 2.0 * ml * n * l
         ach = ax_bytes / ax_avg_s / 1e9 if ax_n else None
         cfg_key = "%s_%s_%dx%dx%d_g%d" % (args.method, args.dtype, m, n, l, world)
         roof = {"bound": "hbm", "achieved": ach, "peak": HBM_PEAK_GBS, "unit": "GB/s",
@@ -192,9 +197,11 @@ def main():
                 "avg_launch_us": ax_avg_s * 1e6, "launches": ax_n,
                 "mfma_tflops": ax_flops / ax_avg_s / 1e12 if ax_n else None,
                 "mfma_frac": (ax_flops / ax_avg_s / 1e12) / MFMA_PEAK_TFS[args.dtype] if ax_n else None,
+                "rhs_per_launch": nsrc,
                 "atr_avg_launch_us": atr_avg_s * 1e6,
-                "atr_GBs": ax_bytes / atr_avg_s / 1e9 if atr_n else None,
-                "pair_mfma_frac": (2 * ax_flops / (ax_avg_s + atr_avg_s) / 1e12) / MFMA_PEAK_TFS[args.dtype]
+                "atr_GBs": atr_bytes / atr_avg_s / 1e9 if atr_n else None,
+                "atr_mfma_frac": (atr_flops / atr_avg_s / 1e12) / MFMA_PEAK_TFS[args.dtype] if atr_n else None,
+                "pair_mfma_frac": ((ax_flops + atr_flops) / (ax_avg_s + atr_avg_s) / 1e12) / MFMA_PEAK_TFS[args.dtype]
                 if (ax_n and atr_n) else None}
         steps = max(1, done)
         line = {
@@ -211,6 +218,9 @@ def main():
                        "exact_objective": args.exact, "ax_variant": args.variant},
             "roofline": roof,
             "work": {"ax_per_iter": ax_n / steps, "atr_per_iter": atr_n / steps,
+                     "passes_over_A_per_iter": (ax_n + atr_n) / steps,
+                     "thr_changed_entries_per_step": res["stats"][0] / max(1.0, res["stats"][2]),
+                     "thr_changed_rows_per_step": res["stats"][1] / max(1.0, res["stats"][2]),
                      "syncs_total": res["syncs"], "iters_total": res["k"]},
         }
         if world == 1 and not args.no_cpu_baseline:

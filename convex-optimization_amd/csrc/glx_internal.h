@@ -35,11 +35,15 @@ struct GemmPlan {
   int64_t m, n, l;
   // A @ X  ->  P[ax_S][m][l] partial slabs (summed by finalize_residual)
   int ax_kind;      // 1 = MFMA direct row loads, 2 = MFMA quad loads + bpermute, 3 = VALU
+  int ax_mt, ax_pf; // MFMA: 16-row tiles per wave, chunks in flight per wave
+  int ax_code;      // MFMA variant code (kind*1000 + MT*100 + PF*10 + non-temporal)
   int ax_S;         // K (= n) splits across workgroups
   int ax_lb;        // VALU: column block width (1,2,4,8); ax_ncb = ceil(l / ax_lb)
   int ax_vec;       // VALU: 16-byte loads
   // A^T R  ->  Gp[atr_S][n][l]
   int atr_kind;     // 1 = MFMA, 3 = VALU
+  int atr_wl, atr_pf; // MFMA: wave layout (0 = waves split rows, 1 = waves split columns), ring depth
+  int atr_ntl;      // non-temporal A loads
   int atr_S;        // M (= m) splits across workgroups
   int atr_lb, atr_vec;
 };
@@ -47,28 +51,43 @@ struct GemmPlan {
 GemmPlan make_plan(int esize, int64_t m, int64_t n, int64_t l, int ax_variant);
 
 // ---- dense products (kernels_gemm.hip) ----
+// A @ [X[0] | .. | X[nsrc-1]] (nsrc <= 3, each n x l) in one pass over A: partial slabs
+// P[src][ax_S][m][l]; skipped entirely unless gate == NULL or *gate == epoch.
 template <typename T>
-void launch_ax(const GemmPlan& p, const T* A, const T* X, T* P, const int* gate, hipStream_t st);
+void launch_ax(const GemmPlan& p, int nsrc, const T* A, const T* const* X, T* P, const int* gate,
+               int epoch, hipStream_t st);
 template <typename T>
 void launch_atr(const GemmPlan& p, const T* A, const T* R, T* Gp, hipStream_t st);
 
 // ---- row / elementwise kernels (kernels_elem.hip) ----
-// R = sum_s P[s] - B (if gate == NULL or *gate); out[0] = sum R^2.
-// gate_mode: what to do when *gate == 0: 0 = nothing, 1 = recompute sum R^2 from R.
+// Gradient inputs `g` with an `S` argument are S split-K slabs of n*l values summed in slab
+// order on the fly (S = 1: an already-summed array).
+//
+// R[src] = sum_s P[src][s] - B for src < nsrc (if gate == NULL or *gate == epoch);
+// out[src] = sum R[src]^2 (out[0..2]), out[3] = count(|cx| > 1e-6 * (*cmax)) when cx != NULL;
+// fh != NULL: *fh = 0.5 out[0] + fh_mu * (*fh_rn) (device-side objective history).
+// gate_mode: when gated off, 0 = do nothing, 1 = recompute out[0] from R[0] (nsrc = 1).
 template <typename T>
-void launch_finalize_residual(const T* P, int S, const T* B, T* R, int64_t ml, const int* gate,
-                              int gate_mode, Red red, hipStream_t st);
+void launch_finalize_residual(const T* P, int S, const T* B, int nsrc, T* const* R, int64_t ml,
+                              const int* gate, int epoch, int gate_mode, const T* cx, int64_t cn,
+                              const double* cmax, double* fh, double fh_mu, const double* fh_rn,
+                              Red red, hipStream_t st);
 template <typename T>
 void launch_sum_partials(const T* Gp, int S, T* G, int64_t nl, hipStream_t st);
-// ProxGD trial: p = prox(x - t g, t), G_t = (x - p)/t, z = x - t G_t.
-// out: [sum g*G_t, sum G_t^2, sum_i ||p_i||, max |p|]
+// ProxGD trial: p = prox(x - t g, t), G_t = (x - p)/t, z = x - t G_t, pthr = p thresholded.
+// out: [sum g*G_t, sum G_t^2, sum_i ||p_i||, max |p|, #changed by the threshold]
 template <typename T>
-void launch_prox_pgd(const T* x, const T* g, T* p, T* z, int64_t n, int64_t l, double t,
-                     double mu, double thres, Red red, hipStream_t st);
-// FISTA trial: xc = prox(y - t g, t). out: [sum g*(xc-y), sum (xc-y)^2, sum ||xc_i||, max |xc|]
+void launch_prox_pgd(const T* x, const T* g, int S, T* gout, T* p, T* pthr, T* z, int64_t n,
+                     int64_t l, double t, double mu, double thres, Red red, hipStream_t st);
+// FISTA (prox = true) / FGD (prox = false: identity) trial fused with the next combine:
+// xc = prox(y - t g, t); vnext = thr(xk) + (xc - thr(xk))/theta;
+// ynext = (1 - theta_next) thr(xc) + theta_next vnext.
+// out: prox: [sum g*(xc-y), sum (xc-y)^2, sum ||xc_i||, max |xc|]
+//      FGD : [sum g*(xc-y), sum (xc-y)^2, sum (sqrt(||xc_i||^2+d^2)-d), sum ||xc_i||, max |xc|]
 template <typename T>
-void launch_prox_fista(const T* y, const T* g, T* xc, int64_t n, int64_t l, double t, double mu,
-                       double thres, Red red, hipStream_t st);
+void launch_fista_trial(bool prox, const T* y, const T* g, int S, T* gout, const T* xk, T* xc,
+                        T* vnext, T* ynext, int64_t n, int64_t l, double t, double mu, double thres,
+                        double theta, double theta_next, double delta, Red red, hipStream_t st);
 // plain prox of W (glx_prox): out: [sum ||x_i||, max |x|]
 template <typename T>
 void launch_prox_plain(const T* w, T* x, int64_t n, int64_t l, double t, double mu, double thres,
@@ -76,32 +95,34 @@ void launch_prox_plain(const T* w, T* x, int64_t n, int64_t l, double t, double 
 // out[0] = count(|x| > 1e-6 * (*maxv))
 template <typename T>
 void launch_count_above(const T* x, int64_t nl, const double* maxv, Red red, hipStream_t st);
-// x[|x| < thres] = 0 in place; *flag |= any value changed (caller zeroes *flag)
+// xo = x with |x| < thres zeroed (xo may alias x); *flag = epoch if any value changed
 template <typename T>
-void launch_threshold(T* x, int64_t nl, double thres, int* flag, hipStream_t st);
-// y = a*xk + b*vk
+void launch_threshold(const T* x, T* xo, int64_t nl, double thres, int* flag, int epoch, hipStream_t st);
+// xk[|xk| < thres] = 0 in place; y = a*xk + b*vk
 template <typename T>
-void launch_axpby(const T* xk, const T* vk, T* y, int64_t nl, double a, double b, hipStream_t st);
+void launch_thr_axpby(T* xk, const T* vk, T* y, int64_t nl, double thres, double a, double b,
+                      hipStream_t st);
 // v = xk + (x - xk)/theta
 template <typename T>
 void launch_fista_v(const T* xk, const T* x, T* v, int64_t nl, double theta, hipStream_t st);
-// SGD (mode 0) / GD (mode 1) step, in place. out: [sum ||x_new_i||]
+// SGD (mode 0) / GD (mode 1) step from the thresholded iterate xt: x = xt - alpha (g + mu xt/d),
+// xt = thr(x). out: [sum ||x_new_i||]
 template <typename T>
-void launch_descent(T* x, const T* g, int64_t n, int64_t l, double alpha, double mu, double thres,
-                    double delta, int mode, Red red, hipStream_t st);
+void launch_descent(T* x, T* xt, const T* g, int S, int64_t n, int64_t l, double alpha, double mu,
+                    double thres, double delta, int mode, Red red, hipStream_t st);
 // out: [sum ||x_i||, max |x|]
 template <typename T>
 void launch_rownorm_max(const T* x, int64_t n, int64_t l, Red red, hipStream_t st);
-// FGD: g += mu * y / sqrt(||y_i||^2 + delta^2); out: [sum (sqrt(||y_i||^2+delta^2) - delta)]
+// FGD: g = sum(gp slabs) + mu * y / sqrt(||y_i||^2 + delta^2);
+// out: [sum (sqrt(||y_i||^2+delta^2) - delta)]
 template <typename T>
-void launch_fgd_grad(const T* y, T* g, int64_t n, int64_t l, double mu, double delta, Red red,
-                     hipStream_t st);
-// FGD trial: xc = y - t g. out: [sum g*(xc-y), sum (xc-y)^2, smooth reg(xc), sum ||xc_i||, max |xc|]
-template <typename T>
-void launch_fgd_trial(const T* y, const T* g, T* xc, int64_t n, int64_t l, double t, double delta,
-                      Red red, hipStream_t st);
+void launch_fgd_grad(const T* y, const T* gp, int S, T* g, int64_t n, int64_t l, double mu,
+                     double delta, Red red, hipStream_t st);
 // fh[idx] = 0.5 * s[i_sumsq] + mu * s[i_reg]
 void launch_record_f(const double* s, int i_sumsq, int i_reg, double mu, double* fh, int64_t idx,
                      hipStream_t st);
+// host[0..ns) = s[0..ns), then *host_seq = seq (system-scope release); host memory is mapped
+void launch_publish(const double* s, int ns, double* host, unsigned* host_seq, unsigned seq,
+                    hipStream_t st);
 
 }  // namespace glx

@@ -35,7 +35,7 @@ __device__ inline double identity(int op) { return op == OP_MAX ? -__builtin_inf
 
 // Reduce NV per-thread values over the grid; block size must be 256. MAXMASK bit v = max op.
 template <int NV, unsigned MAXMASK>
-__device__ void grid_reduce(double (&v)[NV], const Red& red) {
+__device__ bool grid_reduce(double (&v)[NV], const Red& red) {
   __shared__ double sh[NV][4];
   __shared__ int is_last;
   const int lane = threadIdx.x & 63;
@@ -52,30 +52,29 @@ __device__ void grid_reduce(double (&v)[NV], const Red& red) {
   }
   __syncthreads();
   if (threadIdx.x == 0) {
+    // write-through (sc1) partial stores + drained vmcnt before the ticket: no release fence
+    // (MI355X_MICROARCH.md, visibility "Valid forms" table, row 1)
 #pragma unroll
     for (int j = 0; j < NV; ++j) {
       const int op = (MAXMASK >> j) & 1;
       const double bv = combine(op, combine(op, sh[j][0], sh[j][1]), combine(op, sh[j][2], sh[j][3]));
-      red.part[j * kMaxBlocks + blockIdx.x] = bv;
+      __hip_atomic_store(&red.part[j * kMaxBlocks + blockIdx.x], bv, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     const unsigned prev = __hip_atomic_fetch_add(red.ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     is_last = (prev == gridDim.x - 1) ? 1 : 0;
   }
   __syncthreads();
-  if (!is_last) return;
-  if (threadIdx.x == 0) {
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  }
-  __syncthreads();
+  if (!is_last) return false;
   double acc[NV];
 #pragma unroll
   for (int j = 0; j < NV; ++j) {
     const int op = (MAXMASK >> j) & 1;
     acc[j] = identity(op);
-    for (unsigned b = threadIdx.x; b < gridDim.x; b += 256) acc[j] = combine(op, acc[j], red.part[j * kMaxBlocks + b]);
+    // every load of the partials is an sc1 load (L1 bypass): no acquire fence needed
+    for (unsigned b = threadIdx.x; b < gridDim.x; b += 256)
+      acc[j] = combine(op, acc[j], __hip_atomic_load(&red.part[j * kMaxBlocks + b], __ATOMIC_RELAXED,
+                                                     __HIP_MEMORY_SCOPE_AGENT));
 #pragma unroll
     for (int off = 32; off > 0; off >>= 1) acc[j] = combine(op, acc[j], __shfl_xor(acc[j], off));
   }
@@ -93,6 +92,15 @@ __device__ void grid_reduce(double (&v)[NV], const Red& red) {
     }
     __hip_atomic_store(red.ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
+  return true;
+}
+
+// g = sum_s slabs[s][idx] in slab order (S = 1: a plain load)
+template <typename T>
+__device__ inline T slab_sum(const T* __restrict__ g, int S, int64_t stride, int64_t idx) {
+  T v = g[idx];
+  for (int k = 1; k < S; ++k) v = v + g[(int64_t)k * stride + idx];
+  return v;
 }
 
 static inline unsigned grid_for(int64_t work, int per_block) {
@@ -105,41 +113,50 @@ static inline unsigned grid_for(int64_t work, int per_block) {
 template <typename T> __device__ inline T tabs(T v) { return v < T(0) ? -v : v; }
 
 // ------------------------------------------------------------------------------------------
-// residual finalize: R = sum_s P[s] - B; sum R^2
+// residual finalize: R = sum_s P[s] - B; out[0] = sum R^2, out[1] = count(|c| > 1e-6 *cmax)
+// over a second array c (the candidate iterate, fused here to save a launch); the last block
+// optionally records f = 0.5 out[0] + mu * (*rn) into fh (SGD/GD device-side history).
 // ------------------------------------------------------------------------------------------
-template <typename T>
-__global__ __launch_bounds__(256) void k_finalize_residual(const T* __restrict__ P, int S,
-                                                           const T* __restrict__ B, T* __restrict__ R,
-                                                           int64_t ml, const int* __restrict__ gate,
-                                                           int gate_mode, Red red) {
-  const bool live = (gate == nullptr) || (*gate != 0);
+template <typename T, int NSRC>
+__global__ __launch_bounds__(256) void k_finalize_residual(
+    const T* __restrict__ P, int S, const T* __restrict__ B, T* __restrict__ R0, T* __restrict__ R1,
+    T* __restrict__ R2, int64_t ml, const int* __restrict__ gate, int epoch, int gate_mode,
+    const T* __restrict__ cx, int64_t cn, const double* __restrict__ cmax, double* __restrict__ fh,
+    double fh_mu, const double* __restrict__ fh_rn, Red red) {
+  const bool live = (gate == nullptr) || (*gate == epoch);
   if (!live && gate_mode == 0) return;  // uniform over the grid: nobody touches the ticket
-  double v[1] = {0.0};
+  double v[4] = {0.0, 0.0, 0.0, 0.0};
+  T* rs[3] = {R0, R1, R2};
   const int64_t stride = (int64_t)gridDim.x * 256;
   for (int64_t idx = (int64_t)blockIdx.x * 256 + threadIdx.x; idx < ml; idx += stride) {
-    T r;
-    if (live) {
-      T s = P[idx];
-      for (int k = 1; k < S; ++k) s = s + P[(int64_t)k * ml + idx];
-      r = s - B[idx];
-      R[idx] = r;
-    } else {
-      r = R[idx];
+    const T bv = B[idx];
+#pragma unroll
+    for (int sr = 0; sr < NSRC; ++sr) {
+      T r;
+      if (live) {
+        r = slab_sum(P + (int64_t)sr * S * ml, S, ml, idx) - bv;
+        rs[sr][idx] = r;
+      } else {
+        r = rs[sr][idx];
+      }
+      v[sr] += (double)(r * r);
     }
-    v[0] += (double)(r * r);
   }
-  grid_reduce<1, 0u>(v, red);
+  if (cx != nullptr) {
+    const T thr = (T)1e-6 * (T)(*cmax);
+    for (int64_t idx = (int64_t)blockIdx.x * 256 + threadIdx.x; idx < cn; idx += stride)
+      v[3] += (tabs(cx[idx]) > thr) ? 1.0 : 0.0;
+  }
+  const bool last = grid_reduce<4, 0u>(v, red);
+  if (last && fh != nullptr && threadIdx.x == 0) *fh = 0.5 * red.out[0] + fh_mu * (*fh_rn);
 }
 
 template <typename T>
 __global__ __launch_bounds__(256) void k_sum_partials(const T* __restrict__ Gp, int S, T* __restrict__ G,
                                                       int64_t nl) {
   const int64_t stride = (int64_t)gridDim.x * 256;
-  for (int64_t idx = (int64_t)blockIdx.x * 256 + threadIdx.x; idx < nl; idx += stride) {
-    T s = Gp[idx];
-    for (int k = 1; k < S; ++k) s = s + Gp[(int64_t)k * nl + idx];
-    G[idx] = s;
-  }
+  for (int64_t idx = (int64_t)blockIdx.x * 256 + threadIdx.x; idx < nl; idx += stride)
+    G[idx] = slab_sum(Gp, S, nl, idx);
 }
 
 // ------------------------------------------------------------------------------------------
@@ -173,14 +190,20 @@ __device__ inline float row_allsum(float v) {
 
 // ------------------------------------------------------------------------------------------
 // ProxGD line-search trial (gl_ProxGD_primal.py:73-74, 89-92)
+// g = sum of S gradient slabs (written to gout when non-null so later trials read one array);
+// outputs p, p_thr = p with |p| < thres zeroed (the next iteration's x after :127), z.
+// out: [sum g*G_t, sum G_t^2, sum_i ||p_i||, max |p|, #{p changed by the threshold},
+//       #{rows of p changed by the threshold}]
 // ------------------------------------------------------------------------------------------
 template <typename T, int LPR, int EPL>
 __global__ __launch_bounds__(256) void k_prox_pgd(const T* __restrict__ x, const T* __restrict__ g,
-                                                  T* __restrict__ p, T* __restrict__ z, int64_t n,
+                                                  int S, T* __restrict__ gout, T* __restrict__ p,
+                                                  T* __restrict__ pthr, T* __restrict__ z, int64_t n,
                                                   int64_t l, double t_, double tmu_, double thres_,
                                                   Red red) {
   const T t = (T)t_, tmu = (T)tmu_, thres = (T)thres_;
-  double acc[4] = {0.0, 0.0, 0.0, -__builtin_inf()};
+  const int64_t nl = n * l;
+  double acc[6] = {0.0, 0.0, 0.0, -__builtin_inf(), 0.0, 0.0};
   GLX_ROW_LOOP_BEGIN(LPR)
   T xv[EPL], gv[EPL], w[EPL];
   T sq = T(0);
@@ -189,7 +212,8 @@ __global__ __launch_bounds__(256) void k_prox_pgd(const T* __restrict__ x, const
     const int64_t j = sub + (int64_t)e * LPR;
     const bool ok = rv && j < l;
     xv[e] = ok ? x[base + j] : T(0);
-    gv[e] = ok ? g[base + j] : T(0);
+    gv[e] = ok ? slab_sum(g, S, nl, base + j) : T(0);
+    if (ok && gout != nullptr) gout[base + j] = gv[e];
     w[e] = xv[e] - t * gv[e];
     sq = sq + w[e] * w[e];
   }
@@ -198,6 +222,7 @@ __global__ __launch_bounds__(256) void k_prox_pgd(const T* __restrict__ x, const
   c = (c < T(0)) ? T(0) : c;                        // np.clip(., 0, None): NaN stays NaN
   const T d = ((nrm < thres) ? T(1) : T(0)) + nrm;
   T psq = T(0);
+  bool rch = false;
 #pragma unroll
   for (int e = 0; e < EPL; ++e) {
     const int64_t j = sub + (int64_t)e * LPR;
@@ -206,27 +231,51 @@ __global__ __launch_bounds__(256) void k_prox_pgd(const T* __restrict__ x, const
     const T G = (xv[e] - pv) / t;
     const T zv = xv[e] - t * G;
     if (ok) {
+      const bool small = tabs(pv) < thres;
       p[base + j] = pv;
+      pthr[base + j] = small ? T(0) : pv;
       z[base + j] = zv;
       acc[0] += (double)(gv[e] * G);
       acc[1] += (double)(G * G);
       acc[3] = nan_max(acc[3], (double)tabs(pv));
+      const bool ch = small && pv != T(0);
+      acc[4] += ch ? 1.0 : 0.0;
+      rch = rch || ch;
       psq = psq + pv * pv;
     }
   }
   const T pn = __builtin_sqrt(row_allsum<LPR>(psq));
-  if (rv && sub == 0) acc[2] += (double)pn;
+  const double rowch = row_allsum<LPR>(rch ? 1.0 : 0.0);
+  if (rv && sub == 0) {
+    acc[2] += (double)pn;
+    acc[5] += rowch > 0.0 ? 1.0 : 0.0;
+  }
   GLX_ROW_LOOP_END
-  grid_reduce<4, 0x8u>(acc, red);
+  grid_reduce<6, 0x8u>(acc, red);
 }
 
-// FISTA trial (gl_FProxGD_primal.py:92-102)
-template <typename T, int LPR, int EPL>
-__global__ __launch_bounds__(256) void k_prox_fista(const T* __restrict__ y, const T* __restrict__ g,
-                                                    T* __restrict__ xc, int64_t n, int64_t l,
-                                                    double t_, double tmu_, double thres_, Red red) {
-  const T t = (T)t_, tmu = (T)tmu_, thres = (T)thres_;
-  double acc[4] = {0.0, 0.0, 0.0, -__builtin_inf()};
+// FISTA / FGD trial (gl_FProxGD_primal.py:92-102, gl_FGD_primal.py:209-212), fused with the
+// next iteration's combine so that A @ [xc | y_next] is one pass over A:
+//   xc     = prox(y - t g, t)        (PROX) or y - t g (FGD's identity prox)
+//   v_next = xk_thr + (xc - xk_thr) / theta                           (:145)
+//   y_next = (1 - theta') thr(xc) + theta' v_next                     (:136, :139 of the next step)
+// with xk_thr = xk with |xk| < thres zeroed (xk itself is left untouched; :136).
+// out: PROX: [sum g*(xc-y), sum (xc-y)^2, sum ||xc_i||, max |xc|]
+//      FGD : [sum g*(xc-y), sum (xc-y)^2, sum (sqrt(||xc_i||^2+d^2)-d), sum ||xc_i||, max |xc|]
+template <typename T, int LPR, int EPL, bool PROX>
+__global__ __launch_bounds__(256) void k_fista_trial(
+    const T* __restrict__ y, const T* __restrict__ g, int S, T* __restrict__ gout,
+    const T* __restrict__ xk, T* __restrict__ xc, T* __restrict__ vnext, T* __restrict__ ynext,
+    int64_t n, int64_t l, double t_, double tmu_, double thres_, double theta_, double a1_,
+    double b1_, double dd_, double delta_, Red red) {
+  const T t = (T)t_, tmu = (T)tmu_, thres = (T)thres_, theta = (T)theta_, a1 = (T)a1_, b1 = (T)b1_;
+  const T dd = (T)dd_, delta = (T)delta_;
+  const int64_t nl = n * l;
+  constexpr int NV = PROX ? 4 : 5;
+  double acc[NV];
+#pragma unroll
+  for (int j = 0; j < NV; ++j) acc[j] = 0.0;
+  acc[NV - 1] = -__builtin_inf();
   GLX_ROW_LOOP_BEGIN(LPR)
   T yv[EPL], gv[EPL], w[EPL];
   T sq = T(0);
@@ -235,33 +284,50 @@ __global__ __launch_bounds__(256) void k_prox_fista(const T* __restrict__ y, con
     const int64_t j = sub + (int64_t)e * LPR;
     const bool ok = rv && j < l;
     yv[e] = ok ? y[base + j] : T(0);
-    gv[e] = ok ? g[base + j] : T(0);
+    gv[e] = ok ? slab_sum(g, S, nl, base + j) : T(0);
+    if (ok && gout != nullptr) gout[base + j] = gv[e];
     w[e] = yv[e] - t * gv[e];
     sq = sq + w[e] * w[e];
   }
-  const T nrm = __builtin_sqrt(row_allsum<LPR>(sq));
-  T c = nrm - tmu;
-  c = (c < T(0)) ? T(0) : c;
-  const T d = ((nrm < thres) ? T(1) : T(0)) + nrm;
+  T c = T(1), d = T(1);
+  if (PROX) {
+    const T nrm = __builtin_sqrt(row_allsum<LPR>(sq));
+    c = nrm - tmu;
+    c = (c < T(0)) ? T(0) : c;
+    d = ((nrm < thres) ? T(1) : T(0)) + nrm;
+  }
   T psq = T(0);
 #pragma unroll
   for (int e = 0; e < EPL; ++e) {
     const int64_t j = sub + (int64_t)e * LPR;
     const bool ok = rv && j < l;
-    const T pv = (w[e] * c) / d;
+    const T pv = PROX ? (w[e] * c) / d : w[e];
     const T dl = pv - yv[e];
     if (ok) {
+      T xo = xk[base + j];
+      if (tabs(xo) < thres) xo = T(0);
+      const T vn = xo + (pv - xo) / theta;
+      const T pt = (tabs(pv) < thres) ? T(0) : pv;
       xc[base + j] = pv;
+      vnext[base + j] = vn;
+      ynext[base + j] = a1 * pt + b1 * vn;
       acc[0] += (double)(gv[e] * dl);
       acc[1] += (double)(dl * dl);
-      acc[3] = nan_max(acc[3], (double)tabs(pv));
+      acc[NV - 1] = nan_max(acc[NV - 1], (double)tabs(pv));
       psq = psq + pv * pv;
     }
   }
-  const T pn = __builtin_sqrt(row_allsum<LPR>(psq));
-  if (rv && sub == 0) acc[2] += (double)pn;
+  const T ps = row_allsum<LPR>(psq);
+  if (rv && sub == 0) {
+    if (PROX) {
+      acc[2] += (double)__builtin_sqrt(ps);
+    } else {
+      acc[2] += (double)(__builtin_sqrt(ps + dd) - delta);
+      acc[3] += (double)__builtin_sqrt(ps);
+    }
+  }
   GLX_ROW_LOOP_END
-  grid_reduce<4, 0x8u>(acc, red);
+  grid_reduce<NV, (1u << (NV - 1))>(acc, red);
 }
 
 // plain prox (C-ABI glx_prox): out [sum ||x_i||, max |x|]
@@ -323,11 +389,15 @@ __global__ __launch_bounds__(256) void k_rownorm_max(const T* __restrict__ x, in
 }
 
 // SGD (MODE 0, gl_SGD_primal.py:56-61) / GD (MODE 1, gl_GD_primal.py:59-63) step, in place.
+// reads the thresholded iterate xt; writes x = x_new and xt = thr(x_new) (the next
+// iteration's threshold, :93, precomputed so A @ [x | xt] is one pass). out: [sum ||x_new_i||]
 template <typename T, int LPR, int EPL, int MODE>
-__global__ __launch_bounds__(256) void k_descent(T* __restrict__ x, const T* __restrict__ g, int64_t n,
-                                                 int64_t l, double alpha_, double mu_, double thres_,
-                                                 double dd_, Red red) {
+__global__ __launch_bounds__(256) void k_descent(T* __restrict__ x, T* __restrict__ xt,
+                                                 const T* __restrict__ g, int S,
+                                                 int64_t n, int64_t l, double alpha_, double mu_,
+                                                 double thres_, double dd_, Red red) {
   const T alpha = (T)alpha_, mu = (T)mu_, thres = (T)thres_, dd = (T)dd_;
+  const int64_t nl = n * l;
   double acc[1] = {0.0};
   GLX_ROW_LOOP_BEGIN(LPR)
   T xv[EPL], gv[EPL];
@@ -336,8 +406,8 @@ __global__ __launch_bounds__(256) void k_descent(T* __restrict__ x, const T* __r
   for (int e = 0; e < EPL; ++e) {
     const int64_t j = sub + (int64_t)e * LPR;
     const bool ok = rv && j < l;
-    xv[e] = ok ? x[base + j] : T(0);
-    gv[e] = ok ? g[base + j] : T(0);
+    xv[e] = ok ? xt[base + j] : T(0);
+    gv[e] = ok ? slab_sum(g, S, nl, base + j) : T(0);
     sq = sq + xv[e] * xv[e];
   }
   const T s = row_allsum<LPR>(sq);
@@ -356,6 +426,7 @@ __global__ __launch_bounds__(256) void k_descent(T* __restrict__ x, const T* __r
     const T xn = xv[e] - alpha * sub_g;
     if (rv && j < l) {
       x[base + j] = xn;
+      xt[base + j] = (tabs(xn) < thres) ? T(0) : xn;
       nsq = nsq + xn * xn;
     }
   }
@@ -368,10 +439,11 @@ __global__ __launch_bounds__(256) void k_descent(T* __restrict__ x, const T* __r
 // FGD: g += mu * y / sqrt(sum y^2 + delta^2) (gl_FGD_primal.py:69-72);
 //      out: sum_i (sqrt(sum y_i^2 + delta^2) - delta) (:64-67)
 template <typename T, int LPR, int EPL>
-__global__ __launch_bounds__(256) void k_fgd_grad(const T* __restrict__ y, T* __restrict__ g, int64_t n,
-                                                  int64_t l, double mu_, double dd_, double delta_,
-                                                  Red red) {
+__global__ __launch_bounds__(256) void k_fgd_grad(const T* __restrict__ y, const T* __restrict__ gp,
+                                                  int S, T* __restrict__ g, int64_t n, int64_t l,
+                                                  double mu_, double dd_, double delta_, Red red) {
   const T mu = (T)mu_, dd = (T)dd_, delta = (T)delta_;
+  const int64_t nl = n * l;
   double acc[1] = {0.0};
   GLX_ROW_LOOP_BEGIN(LPR)
   T yv[EPL];
@@ -387,44 +459,11 @@ __global__ __launch_bounds__(256) void k_fgd_grad(const T* __restrict__ y, T* __
 #pragma unroll
   for (int e = 0; e < EPL; ++e) {
     const int64_t j = sub + (int64_t)e * LPR;
-    if (rv && j < l) g[base + j] = g[base + j] + mu * (yv[e] / d);
+    if (rv && j < l) g[base + j] = slab_sum(gp, S, nl, base + j) + mu * (yv[e] / d);
   }
   if (rv && sub == 0) acc[0] += (double)(d - delta);
   GLX_ROW_LOOP_END
   grid_reduce<1, 0u>(acc, red);
-}
-
-// FGD trial: xc = y - t g (identity prox, gl_FGD_primal.py:77-80, 209-212)
-// out: [sum g*(xc-y), sum (xc-y)^2, sum (sqrt(||xc_i||^2+delta^2)-delta), sum ||xc_i||, max|xc|]
-template <typename T, int LPR, int EPL>
-__global__ __launch_bounds__(256) void k_fgd_trial(const T* __restrict__ y, const T* __restrict__ g,
-                                                   T* __restrict__ xc, int64_t n, int64_t l, double t_,
-                                                   double dd_, double delta_, Red red) {
-  const T t = (T)t_, dd = (T)dd_, delta = (T)delta_;
-  double acc[5] = {0.0, 0.0, 0.0, 0.0, -__builtin_inf()};
-  GLX_ROW_LOOP_BEGIN(LPR)
-  T sq = T(0);
-#pragma unroll
-  for (int e = 0; e < EPL; ++e) {
-    const int64_t j = sub + (int64_t)e * LPR;
-    if (rv && j < l) {
-      const T yv = y[base + j], gv = g[base + j];
-      const T xv = yv - t * gv;
-      const T dl = xv - yv;
-      xc[base + j] = xv;
-      acc[0] += (double)(gv * dl);
-      acc[1] += (double)(dl * dl);
-      acc[4] = nan_max(acc[4], (double)tabs(xv));
-      sq = sq + xv * xv;
-    }
-  }
-  const T s = row_allsum<LPR>(sq);
-  if (rv && sub == 0) {
-    acc[2] += (double)(__builtin_sqrt(s + dd) - delta);
-    acc[3] += (double)__builtin_sqrt(s);
-  }
-  GLX_ROW_LOOP_END
-  grid_reduce<5, 0x10u>(acc, red);
 }
 
 // ------------------------------------------------------------------------------------------
@@ -441,8 +480,10 @@ __global__ __launch_bounds__(256) void k_count_above(const T* __restrict__ x, in
   grid_reduce<1, 0u>(v, red);
 }
 
+// xo = x with |x| < thres zeroed (xo may alias x); *flag = epoch when any value changed
 template <typename T>
-__global__ __launch_bounds__(256) void k_threshold(T* __restrict__ x, int64_t nl, double thres_, int* flag) {
+__global__ __launch_bounds__(256) void k_threshold(const T* x, T* xo, int64_t nl, double thres_,
+                                                   int* flag, int epoch) {
   const T thres = (T)thres_;
   int changed = 0;
   const int64_t stride = (int64_t)gridDim.x * 256;
@@ -450,19 +491,41 @@ __global__ __launch_bounds__(256) void k_threshold(T* __restrict__ x, int64_t nl
     const T v = x[idx];
     if (tabs(v) < thres) {
       if (v != T(0)) changed = 1;
-      x[idx] = T(0);
+      xo[idx] = T(0);
+    } else if (xo != x) {
+      xo[idx] = v;
     }
   }
-  if (__any(changed) && (threadIdx.x & 63) == 0) atomicOr(flag, 1);
+  if (__any(changed) && (threadIdx.x & 63) == 0) *flag = epoch;   // same value from every writer
 }
 
+// FISTA: x_k[|x_k| < thres] = 0 in place (gl_FProxGD_primal.py:136), then
+// y = (1 - theta) x_k + theta v_k (:139)
 template <typename T>
-__global__ __launch_bounds__(256) void k_axpby(const T* __restrict__ xk, const T* __restrict__ vk,
-                                               T* __restrict__ y, int64_t nl, double a_, double b_) {
-  const T a = (T)a_, b = (T)b_;
+__global__ __launch_bounds__(256) void k_thr_axpby(T* __restrict__ xk, const T* __restrict__ vk,
+                                                   T* __restrict__ y, int64_t nl, double thres_,
+                                                   double a_, double b_) {
+  const T thres = (T)thres_, a = (T)a_, b = (T)b_;
   const int64_t stride = (int64_t)gridDim.x * 256;
-  for (int64_t idx = (int64_t)blockIdx.x * 256 + threadIdx.x; idx < nl; idx += stride)
-    y[idx] = a * xk[idx] + b * vk[idx];
+  for (int64_t idx = (int64_t)blockIdx.x * 256 + threadIdx.x; idx < nl; idx += stride) {
+    T v = xk[idx];
+    if (tabs(v) < thres) {
+      v = T(0);
+      xk[idx] = v;
+    }
+    y[idx] = a * v + b * vk[idx];
+  }
+}
+
+// publish the scalar packet to host-mapped memory: data, then (system-scope release) seq
+__global__ void k_publish(const double* __restrict__ s, int ns, volatile double* host,
+                          volatile unsigned* host_seq, unsigned seq) {
+  if (threadIdx.x < ns) host[threadIdx.x] = s[threadIdx.x];
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    __threadfence_system();
+    *host_seq = seq;
+  }
 }
 
 template <typename T>
@@ -510,29 +573,52 @@ static void dispatch_row(int64_t l, F&& f) {
 static inline unsigned row_grid(int64_t n, int lpr) { return grid_for(n, 256 / lpr); }
 
 template <typename T>
-void launch_finalize_residual(const T* P, int S, const T* B, T* R, int64_t ml, const int* gate,
-                              int gate_mode, Red red, hipStream_t st) {
-  hipLaunchKernelGGL(k_finalize_residual<T>, dim3(grid_for(ml, 256 * 4)), dim3(256), 0, st, P, S, B, R,
-                     ml, gate, gate_mode, red);
+void launch_finalize_residual(const T* P, int S, const T* B, int nsrc, T* const* R, int64_t ml,
+                              const int* gate, int epoch, int gate_mode, const T* cx, int64_t cn,
+                              const double* cmax, double* fh, double fh_mu, const double* fh_rn,
+                              Red red, hipStream_t st) {
+  const int64_t work = ml > cn ? ml : cn;
+  const dim3 grid(grid_for(work, 256 * 2));
+  T* r1 = nsrc > 1 ? R[1] : nullptr;
+  T* r2 = nsrc > 2 ? R[2] : nullptr;
+  if (nsrc == 1)
+    hipLaunchKernelGGL((k_finalize_residual<T, 1>), grid, dim3(256), 0, st, P, S, B, R[0], r1, r2, ml,
+                       gate, epoch, gate_mode, cx, cn, cmax, fh, fh_mu, fh_rn, red);
+  else if (nsrc == 2)
+    hipLaunchKernelGGL((k_finalize_residual<T, 2>), grid, dim3(256), 0, st, P, S, B, R[0], r1, r2, ml,
+                       gate, epoch, gate_mode, cx, cn, cmax, fh, fh_mu, fh_rn, red);
+  else
+    hipLaunchKernelGGL((k_finalize_residual<T, 3>), grid, dim3(256), 0, st, P, S, B, R[0], r1, r2, ml,
+                       gate, epoch, gate_mode, cx, cn, cmax, fh, fh_mu, fh_rn, red);
 }
 template <typename T>
 void launch_sum_partials(const T* Gp, int S, T* G, int64_t nl, hipStream_t st) {
   hipLaunchKernelGGL(k_sum_partials<T>, dim3(grid_for(nl, 256 * 4)), dim3(256), 0, st, Gp, S, G, nl);
 }
 template <typename T>
-void launch_prox_pgd(const T* x, const T* g, T* p, T* z, int64_t n, int64_t l, double t, double mu,
-                     double thres, Red red, hipStream_t st) {
+void launch_prox_pgd(const T* x, const T* g, int S, T* gout, T* p, T* pthr, T* z, int64_t n,
+                     int64_t l, double t, double mu, double thres, Red red, hipStream_t st) {
   dispatch_row(l, [&](auto lpr, auto epl) {
     hipLaunchKernelGGL((k_prox_pgd<T, decltype(lpr)::value, decltype(epl)::value>),
-                       dim3(row_grid(n, lpr)), dim3(256), 0, st, x, g, p, z, n, l, t, t * mu, thres, red);
+                       dim3(row_grid(n, lpr)), dim3(256), 0, st, x, g, S, gout, p, pthr, z, n, l, t,
+                       t * mu, thres, red);
   });
 }
 template <typename T>
-void launch_prox_fista(const T* y, const T* g, T* xc, int64_t n, int64_t l, double t, double mu,
-                       double thres, Red red, hipStream_t st) {
+void launch_fista_trial(bool prox, const T* y, const T* g, int S, T* gout, const T* xk, T* xc,
+                        T* vnext, T* ynext, int64_t n, int64_t l, double t, double mu, double thres,
+                        double theta, double theta_next, double delta, Red red, hipStream_t st) {
   dispatch_row(l, [&](auto lpr, auto epl) {
-    hipLaunchKernelGGL((k_prox_fista<T, decltype(lpr)::value, decltype(epl)::value>),
-                       dim3(row_grid(n, lpr)), dim3(256), 0, st, y, g, xc, n, l, t, t * mu, thres, red);
+    if (prox)
+      hipLaunchKernelGGL((k_fista_trial<T, decltype(lpr)::value, decltype(epl)::value, true>),
+                         dim3(row_grid(n, lpr)), dim3(256), 0, st, y, g, S, gout, xk, xc, vnext, ynext,
+                         n, l, t, t * mu, thres, theta, 1.0 - theta_next, theta_next, delta * delta,
+                         delta, red);
+    else
+      hipLaunchKernelGGL((k_fista_trial<T, decltype(lpr)::value, decltype(epl)::value, false>),
+                         dim3(row_grid(n, lpr)), dim3(256), 0, st, y, g, S, gout, xk, xc, vnext, ynext,
+                         n, l, t, t * mu, thres, theta, 1.0 - theta_next, theta_next, delta * delta,
+                         delta, red);
   });
 }
 template <typename T>
@@ -551,33 +637,26 @@ void launch_rownorm_max(const T* x, int64_t n, int64_t l, Red red, hipStream_t s
   });
 }
 template <typename T>
-void launch_descent(T* x, const T* g, int64_t n, int64_t l, double alpha, double mu, double thres,
-                    double delta, int mode, Red red, hipStream_t st) {
+void launch_descent(T* x, T* xt, const T* g, int S, int64_t n, int64_t l, double alpha, double mu,
+                    double thres, double delta, int mode, Red red, hipStream_t st) {
   dispatch_row(l, [&](auto lpr, auto epl) {
     if (mode == 0)
       hipLaunchKernelGGL((k_descent<T, decltype(lpr)::value, decltype(epl)::value, 0>),
-                         dim3(row_grid(n, lpr)), dim3(256), 0, st, x, g, n, l, alpha, mu, thres,
+                         dim3(row_grid(n, lpr)), dim3(256), 0, st, x, xt, g, S, n, l, alpha, mu, thres,
                          delta * delta, red);
     else
       hipLaunchKernelGGL((k_descent<T, decltype(lpr)::value, decltype(epl)::value, 1>),
-                         dim3(row_grid(n, lpr)), dim3(256), 0, st, x, g, n, l, alpha, mu, thres,
+                         dim3(row_grid(n, lpr)), dim3(256), 0, st, x, xt, g, S, n, l, alpha, mu, thres,
                          delta * delta, red);
   });
 }
 template <typename T>
-void launch_fgd_grad(const T* y, T* g, int64_t n, int64_t l, double mu, double delta, Red red,
-                     hipStream_t st) {
+void launch_fgd_grad(const T* y, const T* gp, int S, T* g, int64_t n, int64_t l, double mu,
+                     double delta, Red red, hipStream_t st) {
   dispatch_row(l, [&](auto lpr, auto epl) {
     hipLaunchKernelGGL((k_fgd_grad<T, decltype(lpr)::value, decltype(epl)::value>),
-                       dim3(row_grid(n, lpr)), dim3(256), 0, st, y, g, n, l, mu, delta * delta, delta, red);
-  });
-}
-template <typename T>
-void launch_fgd_trial(const T* y, const T* g, T* xc, int64_t n, int64_t l, double t, double delta,
-                      Red red, hipStream_t st) {
-  dispatch_row(l, [&](auto lpr, auto epl) {
-    hipLaunchKernelGGL((k_fgd_trial<T, decltype(lpr)::value, decltype(epl)::value>),
-                       dim3(row_grid(n, lpr)), dim3(256), 0, st, y, g, xc, n, l, t, delta * delta, delta, red);
+                       dim3(row_grid(n, lpr)), dim3(256), 0, st, y, gp, S, g, n, l, mu, delta * delta,
+                       delta, red);
   });
 }
 template <typename T>
@@ -585,12 +664,15 @@ void launch_count_above(const T* x, int64_t nl, const double* maxv, Red red, hip
   hipLaunchKernelGGL(k_count_above<T>, dim3(grid_for(nl, 256 * 4)), dim3(256), 0, st, x, nl, maxv, red);
 }
 template <typename T>
-void launch_threshold(T* x, int64_t nl, double thres, int* flag, hipStream_t st) {
-  hipLaunchKernelGGL(k_threshold<T>, dim3(grid_for(nl, 256 * 4)), dim3(256), 0, st, x, nl, thres, flag);
+void launch_threshold(const T* x, T* xo, int64_t nl, double thres, int* flag, int epoch, hipStream_t st) {
+  hipLaunchKernelGGL(k_threshold<T>, dim3(grid_for(nl, 256 * 4)), dim3(256), 0, st, x, xo, nl, thres,
+                     flag, epoch);
 }
 template <typename T>
-void launch_axpby(const T* xk, const T* vk, T* y, int64_t nl, double a, double b, hipStream_t st) {
-  hipLaunchKernelGGL(k_axpby<T>, dim3(grid_for(nl, 256 * 4)), dim3(256), 0, st, xk, vk, y, nl, a, b);
+void launch_thr_axpby(T* xk, const T* vk, T* y, int64_t nl, double thres, double a, double b,
+                      hipStream_t st) {
+  hipLaunchKernelGGL(k_thr_axpby<T>, dim3(grid_for(nl, 256 * 4)), dim3(256), 0, st, xk, vk, y, nl, thres,
+                     a, b);
 }
 template <typename T>
 void launch_fista_v(const T* xk, const T* x, T* v, int64_t nl, double theta, hipStream_t st) {
@@ -600,27 +682,31 @@ void launch_record_f(const double* s, int i_sumsq, int i_reg, double mu, double*
                      hipStream_t st) {
   hipLaunchKernelGGL(k_record_f, dim3(1), dim3(64), 0, st, s, i_sumsq, i_reg, mu, fh, idx);
 }
+void launch_publish(const double* s, int ns, double* host, unsigned* host_seq, unsigned seq,
+                    hipStream_t st) {
+  hipLaunchKernelGGL(k_publish, dim3(1), dim3(64), 0, st, s, ns, host, host_seq, seq);
+}
 
 #define GLX_INST(T)                                                                                  \
-  template void launch_finalize_residual<T>(const T*, int, const T*, T*, int64_t, const int*, int,  \
-                                            Red, hipStream_t);                                      \
+  template void launch_finalize_residual<T>(const T*, int, const T*, int, T* const*, int64_t,       \
+                                            const int*, int, int, const T*, int64_t, const double*, \
+                                            double*, double, const double*, Red, hipStream_t);      \
   template void launch_sum_partials<T>(const T*, int, T*, int64_t, hipStream_t);                    \
-  template void launch_prox_pgd<T>(const T*, const T*, T*, T*, int64_t, int64_t, double, double,    \
-                                   double, Red, hipStream_t);                                       \
-  template void launch_prox_fista<T>(const T*, const T*, T*, int64_t, int64_t, double, double,      \
-                                     double, Red, hipStream_t);                                     \
+  template void launch_prox_pgd<T>(const T*, const T*, int, T*, T*, T*, T*, int64_t, int64_t,       \
+                                   double, double, double, Red, hipStream_t);                       \
+  template void launch_fista_trial<T>(bool, const T*, const T*, int, T*, const T*, T*, T*, T*,      \
+                                      int64_t, int64_t, double, double, double, double, double,     \
+                                      double, Red, hipStream_t);                                    \
   template void launch_prox_plain<T>(const T*, T*, int64_t, int64_t, double, double, double, Red,   \
                                      hipStream_t);                                                  \
   template void launch_rownorm_max<T>(const T*, int64_t, int64_t, Red, hipStream_t);                \
-  template void launch_descent<T>(T*, const T*, int64_t, int64_t, double, double, double, double,   \
-                                  int, Red, hipStream_t);                                           \
-  template void launch_fgd_grad<T>(const T*, T*, int64_t, int64_t, double, double, Red,             \
-                                   hipStream_t);                                                    \
-  template void launch_fgd_trial<T>(const T*, const T*, T*, int64_t, int64_t, double, double, Red,  \
-                                    hipStream_t);                                                   \
+  template void launch_descent<T>(T*, T*, const T*, int, int64_t, int64_t, double, double, double,  \
+                                  double, int, Red, hipStream_t);                                   \
+  template void launch_fgd_grad<T>(const T*, const T*, int, T*, int64_t, int64_t, double, double,   \
+                                   Red, hipStream_t);                                               \
   template void launch_count_above<T>(const T*, int64_t, const double*, Red, hipStream_t);          \
-  template void launch_threshold<T>(T*, int64_t, double, int*, hipStream_t);                        \
-  template void launch_axpby<T>(const T*, const T*, T*, int64_t, double, double, hipStream_t);      \
+  template void launch_threshold<T>(const T*, T*, int64_t, double, int*, int, hipStream_t);        \
+  template void launch_thr_axpby<T>(T*, const T*, T*, int64_t, double, double, double, hipStream_t);\
   template void launch_fista_v<T>(const T*, const T*, T*, int64_t, double, hipStream_t);
 
 GLX_INST(double)

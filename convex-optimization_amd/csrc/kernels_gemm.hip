@@ -25,6 +25,9 @@
 // Split-K: each workgroup is 4 waves; the waves of a workgroup split the K range and are
 // summed through LDS in a fixed order, and workgroups along gridDim.y write partial slabs that
 // the consumer sums in slab order — the result is deterministic run to run.
+#include <algorithm>
+#include <cstdlib>
+
 #include "glx_internal.h"
 
 namespace glx {
@@ -66,22 +69,37 @@ __device__ inline V bpermute_vec(V v, int src_lane) {
 
 // ------------------------------------------------------------------------------------------
 // A @ X on MFMA: block = 4 waves; a wave owns MT 16-row tiles x NT 16-col tiles over its share
-// of the K chunks; the block's 4 waves split the block's chunks; blockIdx.y = K split.
-// P[blockIdx.y][m][16*NT] receives the block's partial.
+// of the K chunks (CK = 4E values of k per chunk); the block's 4 waves split the block's chunks;
+// blockIdx.y = K split. PF chunks are kept in flight per wave (a register ring, statically
+// indexed). P[blockIdx.y][m][16*NT] receives the block's partial.
 // ------------------------------------------------------------------------------------------
-template <typename T, int MT, int NT, bool QUAD>
-__global__ __launch_bounds__(256) void k_ax_mfma(const T* __restrict__ A, const T* __restrict__ X,
+__device__ inline bool gate_live(const int* gate, int epoch) { return gate == nullptr || *gate == epoch; }
+
+template <typename T, bool NTL>
+__device__ inline typename MF<T>::vec_t load_vec(const T* p) {
+  typedef typename MF<T>::vec_t V;
+  if constexpr (NTL) return __builtin_nontemporal_load(reinterpret_cast<const V*>(p));
+  else return *reinterpret_cast<const V*>(p);
+}
+
+// NSRC right-hand sides X0..X2 (each n x 16NT) share every loaded A fragment: the batched
+// products of the next iteration (e.g. A @ [z | p_thr]) cost one pass over A.
+// P[src][S][m][16NT]. NTL: A streamed with non-temporal loads (keeps X resident in L2).
+template <typename T, int MT, int NT, int NSRC, int PF, bool QUAD, bool NTL>
+__global__ __launch_bounds__(256) void k_ax_mfma(const T* __restrict__ A, const T* __restrict__ X0,
+                                                 const T* __restrict__ X1, const T* __restrict__ X2,
                                                  T* __restrict__ P, int64_t m, int64_t n,
                                                  int64_t chunks, int S,
-                                                 const int* __restrict__ gate) {
+                                                 const int* __restrict__ gate, int epoch) {
   typedef MF<T> M;
   typedef typename M::vec_t V;
   typedef typename M::acc_t C;
   constexpr int E = M::E;
   constexpr int CK = 4 * E;   // k per chunk
   constexpr int L = 16 * NT;  // == l
-  if (gate != nullptr && *gate == 0) return;
-  __shared__ C red[MT * NT][64];
+  constexpr int NC = NT * NSRC;
+  if (!gate_live(gate, epoch)) return;
+  __shared__ C red[MT * NC][64];
 
   const int lane = threadIdx.x & 63;
   const int wave = threadIdx.x >> 6;
@@ -101,56 +119,62 @@ __global__ __launch_bounds__(256) void k_ax_mfma(const T* __restrict__ A, const 
     r = r < m ? r : m - 1;
     ap[mt] = A + r * n + cb * CK + (int64_t)lchk * E;
   }
-  const T* xp = X + (cb * CK + (int64_t)q * E) * L + i;
+  const int64_t xoff = (cb * CK + (int64_t)q * E) * L + i;
+  const T* xp[NSRC];
+  xp[0] = X0 + xoff;
+  if (NSRC > 1) xp[1] = X1 + xoff;
+  if (NSRC > 2) xp[2] = X2 + xoff;
 
-  C acc[MT][NT];
+  C acc[MT][NC];
 #pragma unroll
   for (int mt = 0; mt < MT; ++mt)
 #pragma unroll
-    for (int nt = 0; nt < NT; ++nt) acc[mt][nt] = C{};
+    for (int c = 0; c < NC; ++c) acc[mt][c] = C{};
 
-  V a[MT];
-  T xb[E][NT];
-  if (cb < ce) {
+  V a[PF][MT];
+  T xb[PF][E][NC];
 #pragma unroll
-    for (int mt = 0; mt < MT; ++mt) a[mt] = *reinterpret_cast<const V*>(ap[mt]);
+  for (int p = 0; p < PF; ++p) {
+    if (cb + p < ce) {
+      const int64_t off = (int64_t)p * CK;
 #pragma unroll
-    for (int e = 0; e < E; ++e)
+      for (int mt = 0; mt < MT; ++mt) a[p][mt] = load_vec<T, NTL>(ap[mt] + off);
 #pragma unroll
-      for (int nt = 0; nt < NT; ++nt) xb[e][nt] = xp[e * L + nt * 16];
-  }
-  for (int64_t c = cb; c < ce; ++c) {
-    // prefetch chunk c+1 (re-read chunk c on the last trip: harmless, keeps the loop branch-free)
-    const int64_t adv = (c + 1 < ce) ? CK : 0;
-    V an[MT];
-    T xn[E][NT];
+      for (int e = 0; e < E; ++e)
 #pragma unroll
-    for (int mt = 0; mt < MT; ++mt) {
-      ap[mt] += adv;
-      an[mt] = *reinterpret_cast<const V*>(ap[mt]);
+        for (int c = 0; c < NC; ++c) xb[p][e][c] = xp[c / NT][off * L + e * L + (c % NT) * 16];
     }
-    xp += adv * L;
+  }
+  for (int64_t c0 = cb; c0 < ce; c0 += PF) {
 #pragma unroll
-    for (int e = 0; e < E; ++e)
+    for (int p = 0; p < PF; ++p) {
+      const int64_t c = c0 + p;
+      if (c < ce) {
+        V av[MT];
 #pragma unroll
-      for (int nt = 0; nt < NT; ++nt) xn[e][nt] = xp[e * L + nt * 16];
-
-    V av[MT];
+        for (int mt = 0; mt < MT; ++mt) av[mt] = QUAD ? bpermute_vec(a[p][mt], src) : a[p][mt];
+        T xv[E][NC];
 #pragma unroll
-    for (int mt = 0; mt < MT; ++mt) av[mt] = QUAD ? bpermute_vec(a[mt], src) : a[mt];
+        for (int e = 0; e < E; ++e)
 #pragma unroll
-    for (int e = 0; e < E; ++e)
+          for (int cc = 0; cc < NC; ++cc) xv[e][cc] = xb[p][e][cc];
+        if (c + PF < ce) {   // refill this ring slot with chunk c + PF
+          const int64_t off = (c + PF - cb) * CK;
 #pragma unroll
-      for (int mt = 0; mt < MT; ++mt)
+          for (int mt = 0; mt < MT; ++mt) a[p][mt] = load_vec<T, NTL>(ap[mt] + off);
 #pragma unroll
-        for (int nt = 0; nt < NT; ++nt) acc[mt][nt] = M::mma(av[mt][e], xb[e][nt], acc[mt][nt]);
-
+          for (int e = 0; e < E; ++e)
 #pragma unroll
-    for (int mt = 0; mt < MT; ++mt) a[mt] = an[mt];
+            for (int cc = 0; cc < NC; ++cc) xb[p][e][cc] = xp[cc / NT][off * L + e * L + (cc % NT) * 16];
+        }
 #pragma unroll
-    for (int e = 0; e < E; ++e)
+        for (int e = 0; e < E; ++e)
 #pragma unroll
-      for (int nt = 0; nt < NT; ++nt) xb[e][nt] = xn[e][nt];
+          for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+            for (int cc = 0; cc < NC; ++cc) acc[mt][cc] = M::mma(av[mt][e], xv[e][cc], acc[mt][cc]);
+      }
+    }
   }
 
   // fixed-order reduction of the 4 waves: ((w0 + w1) + w2) + w3
@@ -161,65 +185,71 @@ __global__ __launch_bounds__(256) void k_ax_mfma(const T* __restrict__ A, const 
 #pragma unroll
       for (int mt = 0; mt < MT; ++mt)
 #pragma unroll
-        for (int nt = 0; nt < NT; ++nt) red[mt * NT + nt][lane] = acc[mt][nt];
+        for (int cc = 0; cc < NC; ++cc) red[mt * NC + cc][lane] = acc[mt][cc];
     }
     __syncthreads();
     if (wave == 0) {
 #pragma unroll
       for (int mt = 0; mt < MT; ++mt)
 #pragma unroll
-        for (int nt = 0; nt < NT; ++nt) acc[mt][nt] += red[mt * NT + nt][lane];
+        for (int cc = 0; cc < NC; ++cc) acc[mt][cc] += red[mt * NC + cc][lane];
     }
   }
   if (wave != 0) return;
-  T* pout = P + (int64_t)blockIdx.y * m * L;
 #pragma unroll
-  for (int mt = 0; mt < MT; ++mt)
+  for (int sr = 0; sr < NSRC; ++sr) {
+    T* pout = P + ((int64_t)sr * S + blockIdx.y) * m * L;
 #pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const int64_t row = row0 + mt * 16 + M::row(lane, r);
-      if (row < m) {
+    for (int mt = 0; mt < MT; ++mt)
 #pragma unroll
-        for (int nt = 0; nt < NT; ++nt) pout[row * L + nt * 16 + i] = acc[mt][nt][r];
+      for (int r = 0; r < 4; ++r) {
+        const int64_t row = row0 + mt * 16 + M::row(lane, r);
+        if (row < m) {
+#pragma unroll
+          for (int nt = 0; nt < NT; ++nt) pout[row * L + nt * 16 + i] = acc[mt][sr * NT + nt][r];
+        }
       }
-    }
+  }
 }
 
 // ------------------------------------------------------------------------------------------
-// A^T R on MFMA: a wave owns 64 columns of A (= 64 rows of G) x NT 16-col tiles of G; the
-// 4 waves of a block split the block's row range; blockIdx.y = row split. Needs n % 64 == 0,
-// m % 4 == 0. Gp[blockIdx.y][n][16*NT].
+// A^T R on MFMA: a wave owns 64 columns of A (= 64 rows of G) x NT 16-col tiles of G.
+//   WL = 0: a block = one 64-column panel, its 4 waves split the block's rows (LDS-reduced);
+//   WL = 1: a block = four adjacent panels (256 columns) sharing one row range, so the four
+//           waves read the same R fragments (L1 hits) and write their slabs directly.
+// blockIdx.y = row split. Needs n % 64 == 0 (n % 256 for WL = 1), m % 4 == 0.
+// Gp[split][n][16*NT].
 // ------------------------------------------------------------------------------------------
-template <typename T> struct Load4;
-template <> struct Load4<double> {
+template <typename T, bool NTL> struct Load4;
+template <bool NTL> struct Load4<double, NTL> {
   __device__ static inline void go(const double* p, double (&a)[4]) {
-    const d2_t v0 = *reinterpret_cast<const d2_t*>(p);
-    const d2_t v1 = *reinterpret_cast<const d2_t*>(p + 2);
+    const d2_t v0 = load_vec<double, NTL>(p);
+    const d2_t v1 = load_vec<double, NTL>(p + 2);
     a[0] = v0[0]; a[1] = v0[1]; a[2] = v1[0]; a[3] = v1[1];
   }
 };
-template <> struct Load4<float> {
+template <bool NTL> struct Load4<float, NTL> {
   __device__ static inline void go(const float* p, float (&a)[4]) {
-    const f4_t v = *reinterpret_cast<const f4_t*>(p);
+    const f4_t v = load_vec<float, NTL>(p);
     a[0] = v[0]; a[1] = v[1]; a[2] = v[2]; a[3] = v[3];
   }
 };
 
-template <typename T, int NT>
+template <typename T, int NT, int PF, int WL, bool NTL>
 __global__ __launch_bounds__(256) void k_atr_mfma(const T* __restrict__ A, const T* __restrict__ R,
                                                   T* __restrict__ Gp, int64_t m, int64_t n, int S) {
   typedef MF<T> M;
   typedef typename M::acc_t C;
   constexpr int L = 16 * NT;
-  __shared__ C red[4 * NT][64];
+  __shared__ C red[WL == 0 ? 4 * NT : 1][64];
 
   const int lane = threadIdx.x & 63;
   const int wave = threadIdx.x >> 6;
   const int i = lane & 15, q = lane >> 4;
-  const int64_t col0 = (int64_t)blockIdx.x * 64;
+  const int64_t col0 = WL == 0 ? (int64_t)blockIdx.x * 64 : (int64_t)blockIdx.x * 256 + wave * 64;
   const int64_t steps = m / 4;
-  const int64_t W = (int64_t)S * 4;
-  const int64_t w = (int64_t)blockIdx.y * 4 + wave;
+  const int64_t W = WL == 0 ? (int64_t)S * 4 : (int64_t)S;
+  const int64_t w = WL == 0 ? (int64_t)blockIdx.y * 4 + wave : (int64_t)blockIdx.y;
   const int64_t sb = steps * w / W, se = steps * (w + 1) / W;
 
   const T* ap = A + (sb * 4 + q) * n + col0 + 4 * i;
@@ -231,48 +261,59 @@ __global__ __launch_bounds__(256) void k_atr_mfma(const T* __restrict__ A, const
 #pragma unroll
     for (int nt = 0; nt < NT; ++nt) acc[e][nt] = C{};
 
-  T a[4], rb[NT];
-  if (sb < se) {
-    Load4<T>::go(ap, a);
+  T a[PF][4], rb[PF][NT];
 #pragma unroll
-    for (int nt = 0; nt < NT; ++nt) rb[nt] = rp[nt * 16];
+  for (int p = 0; p < PF; ++p) {
+    if (sb + p < se) {
+      Load4<T, NTL>::go(ap + (int64_t)p * 4 * n, a[p]);
+#pragma unroll
+      for (int nt = 0; nt < NT; ++nt) rb[p][nt] = rp[(int64_t)p * 4 * L + nt * 16];
+    }
   }
-  for (int64_t s = sb; s < se; ++s) {
-    const int64_t adv = (s + 1 < se) ? 4 : 0;
-    ap += adv * n;
-    rp += adv * L;
-    T an[4], rn[NT];
-    Load4<T>::go(ap, an);
+  for (int64_t s0 = sb; s0 < se; s0 += PF) {
 #pragma unroll
-    for (int nt = 0; nt < NT; ++nt) rn[nt] = rp[nt * 16];
+    for (int p = 0; p < PF; ++p) {
+      const int64_t s = s0 + p;
+      if (s < se) {
+        T av[4], rv[NT];
 #pragma unroll
-    for (int e = 0; e < 4; ++e)
+        for (int e = 0; e < 4; ++e) av[e] = a[p][e];
 #pragma unroll
-      for (int nt = 0; nt < NT; ++nt) acc[e][nt] = M::mma(a[e], rb[nt], acc[e][nt]);
+        for (int nt = 0; nt < NT; ++nt) rv[nt] = rb[p][nt];
+        if (s + PF < se) {
+          const int64_t off = (s + PF - sb) * 4;
+          Load4<T, NTL>::go(ap + off * n, a[p]);
 #pragma unroll
-    for (int e = 0; e < 4; ++e) a[e] = an[e];
+          for (int nt = 0; nt < NT; ++nt) rb[p][nt] = rp[off * L + nt * 16];
+        }
 #pragma unroll
-    for (int nt = 0; nt < NT; ++nt) rb[nt] = rn[nt];
+        for (int e = 0; e < 4; ++e)
+#pragma unroll
+          for (int nt = 0; nt < NT; ++nt) acc[e][nt] = M::mma(av[e], rv[nt], acc[e][nt]);
+      }
+    }
   }
 
+  if (WL == 0) {
 #pragma unroll
-  for (int s = 1; s < 4; ++s) {
-    __syncthreads();
-    if (wave == s) {
+    for (int s = 1; s < 4; ++s) {
+      __syncthreads();
+      if (wave == s) {
 #pragma unroll
-      for (int e = 0; e < 4; ++e)
+        for (int e = 0; e < 4; ++e)
 #pragma unroll
-        for (int nt = 0; nt < NT; ++nt) red[e * NT + nt][lane] = acc[e][nt];
+          for (int nt = 0; nt < NT; ++nt) red[e * NT + nt][lane] = acc[e][nt];
+      }
+      __syncthreads();
+      if (wave == 0) {
+#pragma unroll
+        for (int e = 0; e < 4; ++e)
+#pragma unroll
+          for (int nt = 0; nt < NT; ++nt) acc[e][nt] += red[e * NT + nt][lane];
+      }
     }
-    __syncthreads();
-    if (wave == 0) {
-#pragma unroll
-      for (int e = 0; e < 4; ++e)
-#pragma unroll
-        for (int nt = 0; nt < NT; ++nt) acc[e][nt] += red[e * NT + nt][lane];
-    }
+    if (wave != 0) return;
   }
-  if (wave != 0) return;
   T* gout = Gp + (int64_t)blockIdx.y * n * L;
 #pragma unroll
   for (int e = 0; e < 4; ++e)
@@ -300,13 +341,14 @@ __device__ inline float wave_sum(float v) {
   return v;
 }
 
-template <typename T, int LB, int RW, bool VEC>
-__global__ __launch_bounds__(256) void k_ax_valu(const T* __restrict__ A, const T* __restrict__ X,
+template <typename T, int LB, int RW, bool VEC, int NSRC>
+__global__ __launch_bounds__(256) void k_ax_valu(const T* __restrict__ A, const T* __restrict__ X0,
+                                                 const T* __restrict__ X1, const T* __restrict__ X2,
                                                  T* __restrict__ P, int64_t m, int64_t n,
                                                  int64_t l, int c0, int S,
-                                                 const int* __restrict__ gate) {
+                                                 const int* __restrict__ gate, int epoch) {
   constexpr int E = VEC ? (16 / (int)sizeof(T)) : 1;
-  if (gate != nullptr && *gate == 0) return;
+  if (!gate_live(gate, epoch)) return;
   const int lane = threadIdx.x & 63;
   const int wave = threadIdx.x >> 6;
   const int64_t row0 = ((int64_t)blockIdx.x * 4 + wave) * RW;
@@ -316,6 +358,7 @@ __global__ __launch_bounds__(256) void k_ax_valu(const T* __restrict__ A, const 
   const int64_t kb = E * (nv * s / S);
   const int64_t ke = (s == S - 1) ? n : E * (nv * (s + 1) / S);
   const int nc = (int)((l - c0) < LB ? (l - c0) : LB);
+  const T* xs[3] = {X0, X1, X2};
 
   const T* arow[RW];
 #pragma unroll
@@ -324,11 +367,13 @@ __global__ __launch_bounds__(256) void k_ax_valu(const T* __restrict__ A, const 
     rr = rr < m ? rr : m - 1;
     arow[r] = A + rr * n;
   }
-  T acc[RW][LB];
+  T acc[NSRC][RW][LB];
 #pragma unroll
-  for (int r = 0; r < RW; ++r)
+  for (int sr = 0; sr < NSRC; ++sr)
 #pragma unroll
-    for (int c = 0; c < LB; ++c) acc[r][c] = T(0);
+    for (int r = 0; r < RW; ++r)
+#pragma unroll
+      for (int c = 0; c < LB; ++c) acc[sr][r][c] = T(0);
 
   for (int64_t k = kb + (int64_t)lane * E; k < ke; k += 64 * E) {
     T a[RW][E];
@@ -345,28 +390,36 @@ __global__ __launch_bounds__(256) void k_ax_valu(const T* __restrict__ A, const 
     }
 #pragma unroll
     for (int e = 0; e < E; ++e) {
-      T xv[LB];
 #pragma unroll
-      for (int c = 0; c < LB; ++c) xv[c] = (c < nc) ? X[(k + e) * l + c0 + c] : T(0);
+      for (int sr = 0; sr < NSRC; ++sr) {
+        T xv[LB];
 #pragma unroll
-      for (int r = 0; r < RW; ++r)
+        for (int c = 0; c < LB; ++c) xv[c] = (c < nc) ? xs[sr][(k + e) * l + c0 + c] : T(0);
 #pragma unroll
-        for (int c = 0; c < LB; ++c) acc[r][c] = __builtin_fma(a[r][e], xv[c], acc[r][c]);
+        for (int r = 0; r < RW; ++r)
+#pragma unroll
+          for (int c = 0; c < LB; ++c) acc[sr][r][c] = __builtin_fma(a[r][e], xv[c], acc[sr][r][c]);
+      }
     }
   }
 #pragma unroll
-  for (int r = 0; r < RW; ++r)
+  for (int sr = 0; sr < NSRC; ++sr)
 #pragma unroll
-    for (int c = 0; c < LB; ++c) acc[r][c] = wave_sum(acc[r][c]);
+    for (int r = 0; r < RW; ++r)
+#pragma unroll
+      for (int c = 0; c < LB; ++c) acc[sr][r][c] = wave_sum(acc[sr][r][c]);
   if (lane == 0) {
-    T* pout = P + (int64_t)s * m * l;
 #pragma unroll
-    for (int r = 0; r < RW; ++r) {
-      const int64_t row = row0 + r;
-      if (row < m) {
+    for (int sr = 0; sr < NSRC; ++sr) {
+      T* pout = P + ((int64_t)sr * S + s) * m * l;
 #pragma unroll
-        for (int c = 0; c < LB; ++c)
-          if (c < nc) pout[row * l + c0 + c] = acc[r][c];
+      for (int r = 0; r < RW; ++r) {
+        const int64_t row = row0 + r;
+        if (row < m) {
+#pragma unroll
+          for (int c = 0; c < LB; ++c)
+            if (c < nc) pout[row * l + c0 + c] = acc[sr][r][c];
+        }
       }
     }
   }
@@ -434,6 +487,30 @@ static inline int64_t clampi(int64_t v, int64_t lo, int64_t hi) {
 static constexpr int64_t kTargetWaves = 2048;   // 8 waves per CU on 256 CUs
 static constexpr int kMaxSplit = 64;
 
+static int env_int(const char* name, int dflt) {
+  const char* v = std::getenv(name);
+  return (v && *v) ? std::atoi(v) : dflt;
+}
+
+// Defaults chosen by the sweep in scripts/kbench.py on MI355X.
+// ax code: kind*1000 + MT*100 + PF*10 + NTL (kind 1 = direct row loads, 2 = quad + bpermute).
+static constexpr int kAxDefault = 2820;
+static constexpr int kAtrDefault = 102;
+// batched right-hand sides (MFMA-bound at l = 32): f64 1420 / f32 1430 (2 RHS), 1220 (3 RHS)
+static int axb_default(int nsrc, int esize) {
+  if (nsrc == 3) return 1220;
+  return esize == 8 ? 1420 : 1430;
+}   // WL = 0, PF = 2 (+1000: non-temporal A loads)
+
+static bool valid_ax_code(int c) {
+  switch (c) {
+    case 1410: case 1420: case 1421: case 1430: case 1431: case 1820: case 1821: case 1810:
+    case 1811: case 2410: case 2420: case 2421: case 2820: case 2821: case 1220: case 1221:
+      return true;
+    default: return false;
+  }
+}
+
 GemmPlan make_plan(int esize, int64_t m, int64_t n, int64_t l, int ax_variant) {
   GemmPlan p{};
   p.esize = esize;
@@ -441,6 +518,10 @@ GemmPlan make_plan(int esize, int64_t m, int64_t n, int64_t l, int ax_variant) {
   const int E = 16 / esize;
   const bool mfma_l = (l == 16 || l == 32);
   // ---- A @ X ----
+  if (ax_variant == 0) ax_variant = env_int("GLX_AX_VARIANT", 0);
+  if (ax_variant == 1) ax_variant = 1410;
+  if (ax_variant == 2) ax_variant = 2410;
+  if (ax_variant >= 100 && ax_variant < 1000) ax_variant = ax_variant * 10;  // legacy 3-digit codes
   const bool ax_mfma_ok = mfma_l && (n % (4 * E) == 0);
   if (ax_variant == 3 || !ax_mfma_ok) {
     p.ax_kind = 3;
@@ -452,15 +533,26 @@ GemmPlan make_plan(int esize, int64_t m, int64_t n, int64_t l, int ax_variant) {
     const int64_t kunits = n / (64 * (p.ax_vec ? E : 1)); // 64-lane strides per row
     p.ax_S = (int)clampi(cdiv(kTargetWaves, waves), 1, std::max<int64_t>(1, std::min<int64_t>(kMaxSplit, kunits / 4)));
   } else {
-    p.ax_kind = (ax_variant == 2) ? 2 : 1;
-    const int64_t blocks = cdiv(m, 64);                   // MT = 4 -> 64 rows per block
+    const int code = valid_ax_code(ax_variant) ? ax_variant : kAxDefault;
+    p.ax_code = code;
+    p.ax_kind = code / 1000;
+    p.ax_mt = (code / 100) % 10;
+    p.ax_pf = (code / 10) % 10;
+    const int64_t blocks = cdiv(m, 16 * p.ax_mt);
     const int64_t chunks = n / (4 * E);
-    p.ax_S = (int)clampi(cdiv(kTargetWaves, blocks * 4), 1,
+    const int64_t target = (esize == 8 && p.ax_mt == 8) ? kTargetWaves / 2 : kTargetWaves;
+    p.ax_S = (int)clampi(cdiv(target, blocks * 4), 1,
                          std::max<int64_t>(1, std::min<int64_t>(kMaxSplit, chunks / 16)));
   }
+  const int s_ax = env_int("GLX_AX_S", 0);
+  if (s_ax > 0) p.ax_S = (int)std::min<int64_t>(s_ax, kMaxSplit);
   // ---- A^T R ----
-  const bool atr_mfma_ok = mfma_l && (n % 64 == 0) && (m % 4 == 0);
-  if (ax_variant == 3 || !atr_mfma_ok) {
+  int atr_code = env_int("GLX_ATR_VARIANT", 0);
+  if (atr_code == 0) atr_code = esize == 8 ? kAtrDefault : 1102;   // f32: non-temporal A wins
+  const int ntl = atr_code >= 1000 ? 1 : 0;
+  const int wl = (atr_code / 10) % 10, pf = atr_code % 10;
+  const bool atr_mfma_ok = mfma_l && (n % (wl ? 256 : 64) == 0) && (m % 4 == 0);
+  if (ax_variant == 3 || atr_code == 3 || !atr_mfma_ok) {
     p.atr_kind = 3;
     p.atr_lb = l >= 8 ? 8 : (l >= 4 ? 4 : (l >= 2 ? 2 : 1));
     if (l == 3) p.atr_lb = 4;
@@ -471,53 +563,117 @@ GemmPlan make_plan(int esize, int64_t m, int64_t n, int64_t l, int ax_variant) {
     p.atr_S = (int)clampi(cdiv(kTargetWaves / 4, blocks), 1, std::max<int64_t>(1, std::min<int64_t>(kMaxSplit, m / 16)));
   } else {
     p.atr_kind = 1;
-    const int64_t blocks = n / 64;
+    p.atr_wl = wl ? 1 : 0;
+    p.atr_pf = (pf >= 1 && pf <= 4) ? pf : 2;
+    p.atr_ntl = ntl;
     const int64_t steps = m / 4;
-    p.atr_S = (int)clampi(cdiv(kTargetWaves, blocks * 4), 1,
-                          std::max<int64_t>(1, std::min<int64_t>(kMaxSplit, steps / 16)));
+    if (p.atr_wl == 0) {
+      const int64_t blocks = n / 64;
+      const int64_t target = esize == 8 ? kTargetWaves : 2 * kTargetWaves;
+      p.atr_S = (int)clampi(cdiv(target, blocks * 4), 1,
+                            std::max<int64_t>(1, std::min<int64_t>(kMaxSplit, steps / 16)));
+    } else {
+      const int64_t blocks = n / 256;
+      p.atr_S = (int)clampi(cdiv(kTargetWaves / 4, blocks), 1,
+                            std::max<int64_t>(1, std::min<int64_t>(kMaxSplit, steps / 16)));
+    }
   }
+  const int s_atr = env_int("GLX_ATR_S", 0);
+  if (s_atr > 0) p.atr_S = (int)std::min<int64_t>(s_atr, kMaxSplit);
   return p;
 }
 
-template <typename T, int LB>
-static void ax_valu_lb(const GemmPlan& p, const T* A, const T* X, T* P, const int* gate,
-                       hipStream_t st) {
+template <typename T, int LB, int NSRC>
+static void ax_valu_lb(const GemmPlan& p, const T* A, const T* const* X, T* P, const int* gate,
+                       int epoch, hipStream_t st) {
   const dim3 grid((unsigned)cdiv(cdiv(p.m, 4), 4), (unsigned)p.ax_S);
   for (int64_t c0 = 0; c0 < p.l; c0 += LB) {
     if (p.ax_vec)
-      hipLaunchKernelGGL((k_ax_valu<T, LB, 4, true>), grid, dim3(256), 0, st, A, X, P, p.m, p.n,
-                         p.l, (int)c0, p.ax_S, gate);
+      hipLaunchKernelGGL((k_ax_valu<T, LB, 4, true, NSRC>), grid, dim3(256), 0, st, A, X[0], X[1],
+                         X[2], P, p.m, p.n, p.l, (int)c0, p.ax_S, gate, epoch);
     else
-      hipLaunchKernelGGL((k_ax_valu<T, LB, 4, false>), grid, dim3(256), 0, st, A, X, P, p.m, p.n,
-                         p.l, (int)c0, p.ax_S, gate);
+      hipLaunchKernelGGL((k_ax_valu<T, LB, 4, false, NSRC>), grid, dim3(256), 0, st, A, X[0], X[1],
+                         X[2], P, p.m, p.n, p.l, (int)c0, p.ax_S, gate, epoch);
+  }
+}
+
+template <typename T, int NSRC>
+static void ax_valu_src(const GemmPlan& p, const T* A, const T* const* X, T* P, const int* gate,
+                        int epoch, hipStream_t st) {
+  switch (p.ax_lb) {
+    case 1: ax_valu_lb<T, 1, NSRC>(p, A, X, P, gate, epoch, st); break;
+    case 2: ax_valu_lb<T, 2, NSRC>(p, A, X, P, gate, epoch, st); break;
+    case 4: ax_valu_lb<T, 4, NSRC>(p, A, X, P, gate, epoch, st); break;
+    default: ax_valu_lb<T, 8, NSRC>(p, A, X, P, gate, epoch, st); break;
+  }
+}
+
+template <typename T, int NT, int NSRC, int MT, int PF, bool QUAD, bool NTL>
+static void ax_mfma_go(const GemmPlan& p, const T* A, const T* const* X, T* P, const int* gate,
+                       int epoch, hipStream_t st) {
+  constexpr int E = 16 / sizeof(T);
+  const dim3 grid((unsigned)cdiv(p.m, 16 * MT), (unsigned)p.ax_S);
+  hipLaunchKernelGGL((k_ax_mfma<T, MT, NT, NSRC, PF, QUAD, NTL>), grid, dim3(256), 0, st, A, X[0],
+                     X[1], X[2], P, p.m, p.n, p.n / (4 * E), p.ax_S, gate, epoch);
+}
+
+// One source: the swept variant. Batched sources (2, 3) use fixed register-feasible tiles.
+template <typename T, int NT>
+static void ax_mfma_nt(const GemmPlan& p, int nsrc, const T* A, const T* const* X, T* P,
+                       const int* gate, int epoch, hipStream_t st) {
+  if (nsrc == 2) {
+    switch (env_int("GLX_AXB_VARIANT", axb_default(2, (int)sizeof(T)))) {
+      case 1220: ax_mfma_go<T, NT, 2, 2, 2, false, false>(p, A, X, P, gate, epoch, st); break;
+      case 1420: ax_mfma_go<T, NT, 2, 4, 2, false, false>(p, A, X, P, gate, epoch, st); break;
+      case 1430: ax_mfma_go<T, NT, 2, 4, 3, false, false>(p, A, X, P, gate, epoch, st); break;
+      case 2220: ax_mfma_go<T, NT, 2, 2, 2, true, false>(p, A, X, P, gate, epoch, st); break;
+      case 2230: ax_mfma_go<T, NT, 2, 2, 3, true, false>(p, A, X, P, gate, epoch, st); break;
+      case 2421: ax_mfma_go<T, NT, 2, 4, 2, true, true>(p, A, X, P, gate, epoch, st); break;
+      case 2430: ax_mfma_go<T, NT, 2, 4, 3, true, false>(p, A, X, P, gate, epoch, st); break;
+      case 2420: ax_mfma_go<T, NT, 2, 4, 2, true, false>(p, A, X, P, gate, epoch, st); break;
+      default: ax_mfma_go<T, NT, 2, 4, 2, false, false>(p, A, X, P, gate, epoch, st); break;
+    }
+    return;
+  }
+  if (nsrc == 3) {
+    switch (env_int("GLX_AXB_VARIANT", axb_default(3, (int)sizeof(T)))) {
+      case 2220: ax_mfma_go<T, NT, 3, 2, 2, true, false>(p, A, X, P, gate, epoch, st); break;
+      case 2230: ax_mfma_go<T, NT, 3, 2, 3, true, false>(p, A, X, P, gate, epoch, st); break;
+      default: ax_mfma_go<T, NT, 3, 2, 2, false, false>(p, A, X, P, gate, epoch, st); break;
+    }
+    return;
+  }
+  switch (p.ax_code) {
+    case 1410: ax_mfma_go<T, NT, 1, 4, 1, false, false>(p, A, X, P, gate, epoch, st); break;
+    case 1420: ax_mfma_go<T, NT, 1, 4, 2, false, false>(p, A, X, P, gate, epoch, st); break;
+    case 1421: ax_mfma_go<T, NT, 1, 4, 2, false, true>(p, A, X, P, gate, epoch, st); break;
+    case 1430: ax_mfma_go<T, NT, 1, 4, 3, false, false>(p, A, X, P, gate, epoch, st); break;
+    case 1431: ax_mfma_go<T, NT, 1, 4, 3, false, true>(p, A, X, P, gate, epoch, st); break;
+    case 1810: ax_mfma_go<T, NT, 1, 8, 1, false, false>(p, A, X, P, gate, epoch, st); break;
+    case 1811: ax_mfma_go<T, NT, 1, 8, 1, false, true>(p, A, X, P, gate, epoch, st); break;
+    case 1820: ax_mfma_go<T, NT, 1, 8, 2, false, false>(p, A, X, P, gate, epoch, st); break;
+    case 1821: ax_mfma_go<T, NT, 1, 8, 2, false, true>(p, A, X, P, gate, epoch, st); break;
+    case 2410: ax_mfma_go<T, NT, 1, 4, 1, true, false>(p, A, X, P, gate, epoch, st); break;
+    case 2420: ax_mfma_go<T, NT, 1, 4, 2, true, false>(p, A, X, P, gate, epoch, st); break;
+    case 2820: ax_mfma_go<T, NT, 1, 8, 2, true, false>(p, A, X, P, gate, epoch, st); break;
+    case 2821: ax_mfma_go<T, NT, 1, 8, 2, true, true>(p, A, X, P, gate, epoch, st); break;
+    case 1220: ax_mfma_go<T, NT, 1, 2, 2, false, false>(p, A, X, P, gate, epoch, st); break;
+    case 1221: ax_mfma_go<T, NT, 1, 2, 2, false, true>(p, A, X, P, gate, epoch, st); break;
+    default: ax_mfma_go<T, NT, 1, 4, 2, true, true>(p, A, X, P, gate, epoch, st); break;
   }
 }
 
 template <typename T>
-void launch_ax(const GemmPlan& p, const T* A, const T* X, T* P, const int* gate, hipStream_t st) {
-  constexpr int E = 16 / sizeof(T);
+void launch_ax(const GemmPlan& p, int nsrc, const T* A, const T* const* X, T* P, const int* gate,
+               int epoch, hipStream_t st) {
   if (p.ax_kind == 3) {
-    switch (p.ax_lb) {
-      case 1: ax_valu_lb<T, 1>(p, A, X, P, gate, st); break;
-      case 2: ax_valu_lb<T, 2>(p, A, X, P, gate, st); break;
-      case 4: ax_valu_lb<T, 4>(p, A, X, P, gate, st); break;
-      default: ax_valu_lb<T, 8>(p, A, X, P, gate, st); break;
-    }
+    if (nsrc == 1) ax_valu_src<T, 1>(p, A, X, P, gate, epoch, st);
+    else if (nsrc == 2) ax_valu_src<T, 2>(p, A, X, P, gate, epoch, st);
+    else ax_valu_src<T, 3>(p, A, X, P, gate, epoch, st);
     return;
   }
-  const dim3 grid((unsigned)cdiv(p.m, 64), (unsigned)p.ax_S);
-  const int64_t chunks = p.n / (4 * E);
-  if (p.l == 16) {
-    if (p.ax_kind == 2)
-      hipLaunchKernelGGL((k_ax_mfma<T, 4, 1, true>), grid, dim3(256), 0, st, A, X, P, p.m, p.n, chunks, p.ax_S, gate);
-    else
-      hipLaunchKernelGGL((k_ax_mfma<T, 4, 1, false>), grid, dim3(256), 0, st, A, X, P, p.m, p.n, chunks, p.ax_S, gate);
-  } else {
-    if (p.ax_kind == 2)
-      hipLaunchKernelGGL((k_ax_mfma<T, 4, 2, true>), grid, dim3(256), 0, st, A, X, P, p.m, p.n, chunks, p.ax_S, gate);
-    else
-      hipLaunchKernelGGL((k_ax_mfma<T, 4, 2, false>), grid, dim3(256), 0, st, A, X, P, p.m, p.n, chunks, p.ax_S, gate);
-  }
+  if (p.l == 16) ax_mfma_nt<T, 1>(p, nsrc, A, X, P, gate, epoch, st);
+  else ax_mfma_nt<T, 2>(p, nsrc, A, X, P, gate, epoch, st);
 }
 
 template <typename T, int LB>
@@ -535,6 +691,27 @@ static void atr_valu_lb(const GemmPlan& p, const T* A, const T* R, T* Gp, hipStr
   }
 }
 
+template <typename T, int NT, int PF, int WL, bool NTL>
+static void atr_mfma_go(const GemmPlan& p, const T* A, const T* R, T* Gp, hipStream_t st) {
+  const dim3 grid((unsigned)(p.n / (WL ? 256 : 64)), (unsigned)p.atr_S);
+  hipLaunchKernelGGL((k_atr_mfma<T, NT, PF, WL, NTL>), grid, dim3(256), 0, st, A, R, Gp, p.m, p.n, p.atr_S);
+}
+
+template <typename T, int NT>
+static void atr_mfma_nt(const GemmPlan& p, const T* A, const T* R, T* Gp, hipStream_t st) {
+  switch (p.atr_ntl * 100 + p.atr_wl * 10 + p.atr_pf) {
+    case 1: atr_mfma_go<T, NT, 1, 0, false>(p, A, R, Gp, st); break;
+    case 3: atr_mfma_go<T, NT, 3, 0, false>(p, A, R, Gp, st); break;
+    case 4: atr_mfma_go<T, NT, 4, 0, false>(p, A, R, Gp, st); break;
+    case 12: atr_mfma_go<T, NT, 2, 1, false>(p, A, R, Gp, st); break;
+    case 101: atr_mfma_go<T, NT, 1, 0, true>(p, A, R, Gp, st); break;
+    case 102: atr_mfma_go<T, NT, 2, 0, true>(p, A, R, Gp, st); break;
+    case 103: atr_mfma_go<T, NT, 3, 0, true>(p, A, R, Gp, st); break;
+    case 112: atr_mfma_go<T, NT, 2, 1, true>(p, A, R, Gp, st); break;
+    default: atr_mfma_go<T, NT, 2, 0, false>(p, A, R, Gp, st); break;
+  }
+}
+
 template <typename T>
 void launch_atr(const GemmPlan& p, const T* A, const T* R, T* Gp, hipStream_t st) {
   if (p.atr_kind == 3) {
@@ -546,15 +723,12 @@ void launch_atr(const GemmPlan& p, const T* A, const T* R, T* Gp, hipStream_t st
     }
     return;
   }
-  const dim3 grid((unsigned)(p.n / 64), (unsigned)p.atr_S);
-  if (p.l == 16)
-    hipLaunchKernelGGL((k_atr_mfma<T, 1>), grid, dim3(256), 0, st, A, R, Gp, p.m, p.n, p.atr_S);
-  else
-    hipLaunchKernelGGL((k_atr_mfma<T, 2>), grid, dim3(256), 0, st, A, R, Gp, p.m, p.n, p.atr_S);
+  if (p.l == 16) atr_mfma_nt<T, 1>(p, A, R, Gp, st);
+  else atr_mfma_nt<T, 2>(p, A, R, Gp, st);
 }
 
-template void launch_ax<double>(const GemmPlan&, const double*, const double*, double*, const int*, hipStream_t);
-template void launch_ax<float>(const GemmPlan&, const float*, const float*, float*, const int*, hipStream_t);
+template void launch_ax<double>(const GemmPlan&, int, const double*, const double* const*, double*, const int*, int, hipStream_t);
+template void launch_ax<float>(const GemmPlan&, int, const float*, const float* const*, float*, const int*, int, hipStream_t);
 template void launch_atr<double>(const GemmPlan&, const double*, const double*, double*, hipStream_t);
 template void launch_atr<float>(const GemmPlan&, const float*, const float*, float*, hipStream_t);
 

@@ -15,6 +15,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cstdlib>
 #include <chrono>
 #include <cmath>
 #include <cstring>
@@ -43,16 +44,15 @@ static inline void check_launch() {
 
 // scalar slots in the device scalar array
 enum {
-  S_SQR = 0,    // sum r^2 of the working residual
-  S_SQZ = 1,    // sum r^2 of the trial residual
-  S_TR = 2,     // trial kernel outputs, up to 5 values (2..6)
-  S_CNT = 8,    // count(|cand| > 1e-6 max|cand|)
-  S_XRN = 9,    // sum ||x_i|| of the current iterate
-  S_XMAX = 10,  // max |x|
-  S_XCNT = 11,  // count for the current iterate
-  S_REGY = 12,  // FGD smooth regulariser at y
-  S_DRN = 13,   // row-norm sum written by the SGD/GD step
-  NSCAL = 16
+  S_TR = 0,     // trial kernel outputs, up to 6 values (0..5)
+  S_RT = 6,     // trial-pass finalize: [sum r_src0^2, r_src1^2, r_src2^2, count(candidate)]
+  S_RO = 10,    // prologue finalize:   [sum r_x^2, sum r_xt^2, -, count(x)]
+  S_XRN = 14,   // sum ||x_i|| of the current iterate   } rownorm_max: [sum, max]
+  S_XMAX = 15,  // max |x|
+  S_RG = 16,    // standalone residual finalize (FISTA y): [sum r^2, ...]
+  S_REGY = 20,  // FGD smooth regulariser at y
+  S_DRN = 21,   // row-norm sum written by the SGD/GD step (+1: max)
+  NSCAL = 24
 };
 
 struct Carver {
@@ -69,12 +69,14 @@ struct Carver {
 
 static int method_bufs(int method) {
   switch (method) {
-    case GLX_PROXGD: return 3;   // x, p, z
-    case GLX_FPROXGD: return 4;  // x_k, v_k, y, candidate
-    case GLX_FGD: return 4;
-    default: return 1;           // SGD / GD: x only
+    case GLX_PROXGD: return 5;   // (x, x_thr), (p, p_thr), z
+    case GLX_FPROXGD: return 6;  // (x_k, v_k, y) current + (x, v, y) of the trial
+    case GLX_FGD: return 6;
+    default: return 2;           // SGD / GD: x, thr(x)
   }
 }
+constexpr int kBufs = 6;
+constexpr int kRes = 4;
 
 static void validate(const glx_problem* P, const glx_opts* O) {
   if (!P || !O) throw Error{GLX_E_INVALID, "null problem/opts"};
@@ -92,10 +94,6 @@ static void validate(const glx_problem* P, const glx_opts* O) {
        reinterpret_cast<uintptr_t>(P->x)) & 15)
     throw Error{GLX_E_INVALID, "A, b, x must be 16-byte aligned"};
 }
-
-struct Layout {
-  size_t bytes;
-};
 
 // ------------------------------------------------------------------------------------------
 class SessionBase {
@@ -115,21 +113,22 @@ class Session : public SessionBase {
     Carver c(ws);
     const int64_t nl = P.n * P.l, ml = P.m * P.l;
     const int nb = method_bufs(P.method);
-    T* bufs[5] = {static_cast<T*>(P.x), nullptr, nullptr, nullptr, nullptr};
+    T* bufs[kBufs] = {static_cast<T*>(P.x), nullptr, nullptr, nullptr, nullptr, nullptr};
     for (int i = 1; i < nb; ++i) bufs[i] = static_cast<T*>(c.take(sizeof(T) * nl));
-    T* r0 = static_cast<T*>(c.take(sizeof(T) * ml));
-    T* r1 = static_cast<T*>(c.take(sizeof(T) * ml));
+    T* res[kRes];
+    for (int i = 0; i < kRes; ++i) res[i] = static_cast<T*>(c.take(sizeof(T) * ml));
     T* g = static_cast<T*>(c.take(sizeof(T) * nl));
     T* gp = plan.atr_S > 1 ? static_cast<T*>(c.take(sizeof(T) * nl * plan.atr_S)) : g;
-    T* pp = static_cast<T*>(c.take(sizeof(T) * ml * plan.ax_S));
+    T* pp = static_cast<T*>(c.take(sizeof(T) * ml * plan.ax_S * 3));   // up to 3 batched sources
     double* scal = static_cast<double*>(c.take(sizeof(double) * NSCAL));
     double* part = static_cast<double*>(c.take(sizeof(double) * kMaxRedVals * kMaxBlocks));
     unsigned* ticket = static_cast<unsigned*>(c.take(256));
     int* flag = static_cast<int*>(c.take(256));
-    double* fh = static_cast<double*>(c.take(sizeof(double) * (fh_cap > 0 ? fh_cap : 1)));
+    double* fh = static_cast<double*>(c.take(sizeof(double) * (fh_cap + 1)));
     if (s) {
-      for (int i = 0; i < 5; ++i) s->X_[i] = bufs[i];
-      s->R_[0] = r0; s->R_[1] = r1; s->G_ = g; s->Gp_ = gp; s->Pp_ = pp;
+      for (int i = 0; i < kBufs; ++i) s->X_[i] = bufs[i];
+      for (int i = 0; i < kRes; ++i) s->R_[i] = res[i];
+      s->G_ = g; s->Gp_ = gp; s->Pp_ = pp;
       s->scal_ = scal; s->part_ = part; s->ticket_ = ticket; s->flag_ = flag; s->fh_dev_ = fh;
     }
     return c.off + 256;
@@ -154,8 +153,17 @@ class Session : public SessionBase {
     carve(P, plan_, fh_cap_, ws, this);
     A_ = static_cast<const T*>(P.A);
     B_ = static_cast<const T*>(P.b);
-    GLX_HIP(hipHostMalloc(reinterpret_cast<void**>(&hs_), sizeof(double) * NSCAL, hipHostMallocDefault));
+    // scalar packet: host-mapped, coherent memory the GPU writes directly (k_publish)
+    GLX_HIP(hipHostMalloc(reinterpret_cast<void**>(&hs_), sizeof(double) * 32,
+                          hipHostMallocMapped | hipHostMallocCoherent));
+    hseq_ = reinterpret_cast<unsigned*>(hs_ + NSCAL + 2);
+    *hseq_ = 0;
+    GLX_HIP(hipHostGetDevicePointer(reinterpret_cast<void**>(&hs_dev_), hs_, 0));
+    hseq_dev_ = reinterpret_cast<unsigned*>(hs_dev_ + NSCAL + 2);
+    const char* rb = std::getenv("GLX_READBACK");
+    spin_readback_ = !(rb && std::strcmp(rb, "sync") == 0);
     GLX_HIP(hipMemsetAsync(ticket_, 0, 256, st_));
+    GLX_HIP(hipMemsetAsync(flag_, 0, 256, st_));
     GLX_HIP(hipMemsetAsync(scal_, 0, sizeof(double) * NSCAL, st_));
     mus_[0] = 100 * P.mu0;
     mus_[1] = 10 * P.mu0;
@@ -201,8 +209,8 @@ class Session : public SessionBase {
     if (!res) throw Error{GLX_E_INVALID, "null result"};
     // fval = objective of the returned x (gl_ProxGD_primal.py:141). SGD uses its phase mu.
     const double mu_obj = (method_ == GLX_SGD) ? mu_ : P_.mu0;
-    objective_of(X_[ix_], mu_obj, /*need_sparsity=*/false);
-    res->fval = 0.5 * hs_[S_SQR] + mu_obj * hs_[S_XRN];
+    objective_of(X_[ix_]);
+    res->fval = 0.5 * hs_[S_RO] + mu_obj * hs_[S_XRN];
     if (ix_ != 0) copy_buf(X_[0], X_[ix_]);
     if (device_hist_ && k_ > 0) {
       fh_.resize(k_);
@@ -224,8 +232,13 @@ class Session : public SessionBase {
     if (res->f_hist_best && cnt > 0) std::memcpy(res->f_hist_best, fhb_.data(), sizeof(double) * cnt);
     res->n_fhist = cnt;
     res->ax_calls = ax_calls_;
+    res->ax_sources = ax_cols_;
+    for (int i = 0; i < 8; ++i) res->stats[i] = stats_[i];
     res->atr_calls = atr_calls_;
     res->syncs = syncs_;
+    // finish() overwrote residual buffers: rebuild the iteration state if run() is called again
+    state_valid_ = false;
+    y_ready_ = false;
   }
 
   void kernel_time(int kind, int64_t* launches, double* ms) override {
@@ -250,13 +263,15 @@ class Session : public SessionBase {
   Red red(int slot) { return Red{part_, ticket_, scal_ + slot}; }
 
   hipEvent_t get_event() {
-    if (!ev_pool_.empty()) {
-      hipEvent_t e = ev_pool_.back();
-      ev_pool_.pop_back();
-      return e;
+    if (ev_pool_.empty()) {   // grow in batches: never create events inside a timed loop's steady state
+      for (int i = 0; i < 256; ++i) {
+        hipEvent_t e;
+        GLX_HIP(hipEventCreate(&e));
+        ev_pool_.push_back(e);
+      }
     }
-    hipEvent_t e;
-    GLX_HIP(hipEventCreate(&e));
+    hipEvent_t e = ev_pool_.back();
+    ev_pool_.pop_back();
     return e;
   }
 
@@ -269,51 +284,86 @@ class Session : public SessionBase {
     if (comm_) comm_allreduce(comm_, scal_ + slot, 1, GLX_F64, st_);
   }
 
-  // R_out = A x - b (+ sum r^2 into slot); gate: skip unless *gate (gate_mode as finalize)
-  void residual(const T* x, const int* gate, T* r_out, int slot, int gate_mode) {
-    const bool prof = O_.profile && gate == nullptr;
+  // R[src] = A X[src] - b for src < nsrc in one pass over A; scal[slot + src] = sum R[src]^2
+  // (summed over ranks), scal[slot + 3] = count(|cx| > 1e-6 * *cmax); fh: device f record.
+  void residuals(int nsrc, const T* const* xs, T* const* rs, int slot, const T* cx = nullptr,
+                 const double* cmax = nullptr, double* fh = nullptr, double fh_mu = 0.0) {
     hipEvent_t e0 = nullptr, e1 = nullptr;
-    if (prof) { e0 = get_event(); e1 = get_event(); GLX_HIP(hipEventRecord(e0, st_)); }
-    launch_ax<T>(plan_, A_, x, Pp_, gate, st_);
+    if (O_.profile) { e0 = get_event(); e1 = get_event(); GLX_HIP(hipEventRecord(e0, st_)); }
+    launch_ax<T>(plan_, nsrc, A_, xs, Pp_, nullptr, 0, st_);
     check_launch();
-    if (prof) { GLX_HIP(hipEventRecord(e1, st_)); ev_[0].push_back({e0, e1}); }
-    launch_finalize_residual<T>(Pp_, plan_.ax_S, B_, r_out, ml_, gate, gate_mode, red(slot), st_);
+    if (O_.profile) { GLX_HIP(hipEventRecord(e1, st_)); ev_[0].push_back({e0, e1}); }
+    ++ax_calls_;
+    ax_cols_ += nsrc;
+    launch_finalize_residual<T>(Pp_, plan_.ax_S, B_, nsrc, rs, ml_, nullptr, 0, 1, cx,
+                                cx ? nl_ : 0, cmax, comm_ ? nullptr : fh, fh_mu, scal_ + S_DRN,
+                                red(slot), st_);
     check_launch();
-    if (gate == nullptr) ++ax_calls_; else ++ax_gated_;
-    if (gate == nullptr || gate_mode == 1) allreduce_scalar(slot);
+    if (comm_) {
+      comm_allreduce(comm_, scal_ + slot, nsrc, GLX_F64, st_);
+      if (fh) {
+        launch_record_f(scal_, slot, S_DRN, fh_mu, fh, 0, st_);
+        check_launch();
+      }
+    }
+  }
+  void residual1(const T* x, T* r, int slot, const T* cx = nullptr, const double* cmax = nullptr) {
+    const T* xs[3] = {x, nullptr, nullptr};
+    T* rs[3] = {r, nullptr, nullptr};
+    residuals(1, xs, rs, slot, cx, cmax);
   }
 
-  // G = A^T r  (summed over row shards)
-  void gradient(const T* r) {
+  // G = A^T r as slabs; returns (source, S) for the consumer. With a communicator the slabs are
+  // summed and all-reduced first (S = 1).
+  std::pair<const T*, int> gradient(const T* r) {
     hipEvent_t e0 = nullptr, e1 = nullptr;
     if (O_.profile) { e0 = get_event(); e1 = get_event(); GLX_HIP(hipEventRecord(e0, st_)); }
     launch_atr<T>(plan_, A_, r, Gp_, st_);
     check_launch();
     if (O_.profile) { GLX_HIP(hipEventRecord(e1, st_)); ev_[1].push_back({e0, e1}); }
+    ++atr_calls_;
+    if (!comm_) return {Gp_, plan_.atr_S};
     if (plan_.atr_S > 1) {
       launch_sum_partials<T>(Gp_, plan_.atr_S, G_, nl_, st_);
       check_launch();
     }
-    ++atr_calls_;
-    if (comm_) comm_allreduce(comm_, G_, nl_, P_.dtype, st_);
+    comm_allreduce(comm_, G_, nl_, P_.dtype, st_);
+    return {G_, 1};
   }
 
   void readback() {
-    GLX_HIP(hipMemcpyAsync(hs_, scal_, sizeof(double) * NSCAL, hipMemcpyDeviceToHost, st_));
-    GLX_HIP(hipStreamSynchronize(st_));
     ++syncs_;
+    if (!spin_readback_) {
+      GLX_HIP(hipMemcpyAsync(hs_, scal_, sizeof(double) * NSCAL, hipMemcpyDeviceToHost, st_));
+      GLX_HIP(hipStreamSynchronize(st_));
+      return;
+    }
+    const unsigned seq = ++seq_;
+    launch_publish(scal_, NSCAL, hs_dev_, hseq_dev_, seq, st_);
+    check_launch();
+    // spin on the sequence word the GPU writes after the packet (system-scope release)
+    volatile unsigned* hs = hseq_;
+    uint64_t spins = 0;
+    auto t0 = std::chrono::steady_clock::time_point{};
+    while (*hs != seq) {
+      __builtin_ia32_pause();
+      if ((++spins & 0xFFFFF) == 0) {
+        if (spins == 0x100000) t0 = std::chrono::steady_clock::now();
+        else if (std::chrono::steady_clock::now() - t0 > std::chrono::seconds(5)) {
+          GLX_HIP(hipStreamSynchronize(st_));   // surfaces a device error, if any
+          if (*hs != seq) throw Error{GLX_E_HIP, "scalar readback timed out"};
+        }
+      }
+    }
+    __atomic_thread_fence(__ATOMIC_ACQUIRE);
   }
 
-  // objective (and sparsity) of x into hs_: r = A x - b -> R_[ir_], S_SQR, S_XRN, S_XMAX, S_XCNT
-  void objective_of(T* x, double mu_obj, bool need_sparsity) {
-    (void)mu_obj;
-    residual(x, nullptr, R_[ir_], S_SQR, 1);
+  // objective of x (used by finish and as the FISTA prologue): S_XRN, S_XMAX, S_RO (sum r^2),
+  // S_RO + 3 (count); r = A x - b -> R_[0]
+  void objective_of(T* x) {
     launch_rownorm_max<T>(x, n_, l_, red(S_XRN), st_);
     check_launch();
-    if (need_sparsity) {
-      launch_count_above<T>(x, nl_, scal_ + S_XMAX, red(S_XCNT), st_);
-      check_launch();
-    }
+    residual1(x, R_[0], S_RO, use_sparsity_ ? x : nullptr, scal_ + S_XMAX);
     readback();
   }
 
@@ -347,6 +397,7 @@ class Session : public SessionBase {
     if (method_ == GLX_FPROXGD || method_ == GLX_FGD) {  // gl_FProxGD_primal.py:68-69
       copy_x(iv_, ix_);
       tk_ = O_.alpha0;
+      y_ready_ = false;
     }
   }
 
@@ -360,154 +411,193 @@ class Session : public SessionBase {
     }
   }
 
-  void ensure_objective() {
-    if (f_known_) return;
-    objective_of(X_[ix_], P_.mu0, use_sparsity_);
-    f_cur_ = 0.5 * hs_[S_SQR] + P_.mu0 * hs_[S_XRN];
-    s_cur_ = hs_[S_XCNT] / (double)nl_;
-    f_known_ = true;
-  }
-
   // ------------------------------------------------------------------ ProxGD
-  void iter_proxgd() {
-    if (O_.exact_objective) f_known_ = false;
-    ensure_objective();                           // R_[ir_] = A x - b for this x
-    record(f_cur_, s_cur_);
-    if (stop_rule()) { end_phase(); return; }     // f stays valid for the next phase's record
-    T* x = X_[ix_];
-    GLX_HIP(hipMemsetAsync(flag_, 0, sizeof(int), st_));
-    launch_threshold<T>(x, nl_, O_.thres, flag_, st_);
-    check_launch();
-    residual(x, flag_, R_[ir_], S_SQR, 1);        // recompute only if the threshold changed x
-    gradient(R_[ir_]);
-    const int ip = (ix_ + 1) % 3, iz = (ix_ + 2) % 3;
-    double t;
-    bool accepted = false;
-    if (O_.step_type == GLX_STEP_LINE_SEARCH) {
-      t = O_.alpha0;
-      for (int it = 0; it < O_.ls_maxit; ++it) {
-        launch_prox_pgd<T>(x, G_, X_[ip], X_[iz], n_, l_, t, mu_, O_.thres, red(S_TR), st_);
-        check_launch();
-        launch_count_above<T>(X_[ip], nl_, scal_ + S_TR + 3, red(S_CNT), st_);
-        check_launch();
-        residual(X_[iz], nullptr, R_[1 - ir_], S_SQZ, 1);
-        readback();
-        const double gx = 0.5 * hs_[S_SQR], gz = 0.5 * hs_[S_SQZ];
-        if (gz <= gx - t * hs_[S_TR + 0] + 0.5 * t * hs_[S_TR + 1]) { accepted = true; break; }
-        t *= O_.ls_coeff;
-      }
-      if (!accepted) {   // reference returns alpha0*coeff^maxit untested (gl_ProxGD_primal.py:99)
-        launch_prox_pgd<T>(x, G_, X_[ip], X_[iz], n_, l_, t, mu_, O_.thres, red(S_TR), st_);
-        check_launch();
-      }
-    } else {
-      t = schedule(inner_);
-      launch_prox_pgd<T>(x, G_, X_[ip], X_[iz], n_, l_, t, mu_, O_.thres, red(S_TR), st_);
+  // Invariants between iterations (state_valid_): X_[ix_] = x (unthresholded, what is recorded
+  // and returned), X_[ixt_] = thr(x) (:127), R_[irg_] = A thr(x) - b (the gradient residual,
+  // :129, exact), gx_ = 1/2 ||R_[irg_]||^2, f_cur_/s_cur_ = objective and sparsity of x.
+  void proxgd_prologue(bool have_thr) {
+    if (!have_thr) {
+      launch_threshold<T>(X_[ix_], X_[ixt_], nl_, O_.thres, flag_, ++epoch_, st_);
       check_launch();
     }
-    ix_ = ip;                                     // x = prox(x - t grad, t)  (:132)
-    if (accepted && !O_.exact_objective) {
-      // reuse the accepted trial's residual A z - b (z = x - t G_t, ulp-close to the new x)
-      ir_ = 1 - ir_;
-      f_cur_ = 0.5 * hs_[S_SQZ] + P_.mu0 * hs_[S_TR + 2];
-      s_cur_ = hs_[S_CNT] / (double)nl_;
-      f_known_ = true;
+    launch_rownorm_max<T>(X_[ix_], n_, l_, red(S_XRN), st_);
+    check_launch();
+    const int ro = (irg_ + 1) % kRes;
+    const T* xs[3] = {X_[ix_], X_[ixt_], nullptr};
+    T* rs[3] = {R_[ro], R_[irg_], nullptr};
+    residuals(2, xs, rs, S_RO, X_[ix_], scal_ + S_XMAX);     // A @ [x | thr(x)]
+    readback();
+    f_cur_ = 0.5 * hs_[S_RO] + P_.mu0 * hs_[S_XRN];
+    s_cur_ = hs_[S_RO + 3] / (double)nl_;
+    gx_ = 0.5 * hs_[S_RO + 1];
+    state_valid_ = true;
+  }
+
+  void iter_proxgd() {
+    if (!state_valid_) proxgd_prologue(thr_from_trial_);
+    record(f_cur_, s_cur_);
+    if (stop_rule()) { end_phase(); return; }     // x and its state carry over to the next phase
+    const std::pair<const T*, int> g = gradient(R_[irg_]);
+    const T* xt = X_[ixt_];
+    const bool exact = O_.exact_objective != 0;
+    // trial residual buffers: never the gradient residual
+    const int rz = (irg_ + 1) % kRes, rpt = (irg_ + 2) % kRes, rp = (irg_ + 3) % kRes;
+    double t;
+    bool accepted = false;
+    auto trial = [&](double tt, bool first) {
+      launch_prox_pgd<T>(xt, first ? g.first : G_, first ? g.second : 1,
+                         (first && g.first != G_) ? G_ : nullptr, X_[ip_], X_[ipt_], X_[iz_], n_,
+                         l_, tt, mu_, O_.thres, red(S_TR), st_);
+      check_launch();
+    };
+    if (O_.step_type == GLX_STEP_LINE_SEARCH && O_.ls_maxit > 0) {
+      t = O_.alpha0;
+      for (int it = 0; it < O_.ls_maxit; ++it) {
+        trial(t, it == 0);
+        // one pass: g(z) for the test (:91) + the next iteration's residuals A p_thr (and A p)
+        const T* xs[3] = {X_[iz_], X_[ipt_], X_[ip_]};
+        T* rs[3] = {R_[rz], R_[rpt], R_[rp]};
+        residuals(exact ? 3 : 2, xs, rs, S_RT, X_[ip_], scal_ + S_TR + 3);
+        readback();
+        const double gz = 0.5 * hs_[S_RT];
+        if (gz <= gx_ - t * hs_[S_TR + 0] + 0.5 * t * hs_[S_TR + 1]) { accepted = true; break; }
+        t *= O_.ls_coeff;
+      }
+      // after ls_maxit failures the reference returns alpha0*coeff^maxit untested (:99)
+      if (!accepted) trial(t, false);
     } else {
-      f_known_ = false;
+      t = O_.step_type == GLX_STEP_LINE_SEARCH ? O_.alpha0 : schedule(inner_);
+      trial(t, true);
+    }
+    std::swap(ix_, ip_);                          // x = prox(x - t grad, t)  (:132)
+    std::swap(ixt_, ipt_);
+    if (accepted) {
+      stats_[0] += hs_[S_TR + 4];
+      stats_[1] += hs_[S_TR + 5];
+      stats_[2] += 1;
+      irg_ = rpt;
+      gx_ = 0.5 * hs_[S_RT + 1];
+      // exact: A p from the batch; fast: A z - b (z = x - t G_t is ulp-close to p) unless the
+      // threshold changed nothing, in which case A p_thr - b == A p - b exactly
+      const double sq_x = exact ? hs_[S_RT + 2] : (hs_[S_TR + 4] == 0 ? hs_[S_RT + 1] : hs_[S_RT]);
+      f_cur_ = 0.5 * sq_x + P_.mu0 * hs_[S_TR + 2];
+      s_cur_ = hs_[S_RT + 3] / (double)nl_;
+      state_valid_ = true;
+    } else {
+      state_valid_ = false;
+      thr_from_trial_ = true;                     // x_thr came out of the trial kernel
     }
   }
 
   // ------------------------------------------------------------------ FProxGD / FGD
+  // Between iterations: X_[ix_] = x_k, X_[iv_] = v_k; when y_ready_, X_[iy_] = y of the next
+  // iteration (formed by the accepted trial, bit-identical to :136/:139) and R_[iry_] = A y - b.
   void iter_fista(bool smooth) {
-    ensure_objective();
+    if (!f_known_) {
+      objective_of(X_[ix_]);
+      f_cur_ = 0.5 * hs_[S_RO] + P_.mu0 * hs_[S_XRN];
+      s_cur_ = hs_[S_RO + 3] / (double)nl_;
+      f_known_ = true;
+    }
     record(f_cur_, s_cur_);
     if (stop_rule()) { end_phase(); return; }
-    T* xk = X_[ix_];
-    launch_threshold<T>(xk, nl_, O_.thres, flag_, st_);   // flag unused here
-    check_launch();
     const double theta = 2.0 / (double)(inner_ + 1);       // gl_FProxGD_primal.py:138
-    T* y = X_[iy_];
-    launch_axpby<T>(xk, X_[iv_], y, nl_, 1.0 - theta, theta, st_);
-    check_launch();
-    residual(y, nullptr, R_[ir_], S_SQR, 1);              // g(y) and the gradient residual
-    gradient(R_[ir_]);
-    double gy = 0.5 * 0.0;
-    if (smooth) {
-      launch_fgd_grad<T>(y, G_, n_, l_, mu_, O_.delta, red(S_REGY), st_);
+    const double theta_next = 2.0 / (double)(inner_ + 2);
+    if (!y_ready_) {
+      launch_thr_axpby<T>(X_[ix_], X_[iv_], X_[iy_], nl_, O_.thres, 1.0 - theta, theta, st_);
       check_launch();
+      residual1(X_[iy_], R_[iry_], S_RG);                 // g(y) and the gradient residual
+      gy_pending_ = true;
     }
-    T* xc = X_[ic_];
+    const T* y = X_[iy_];
+    std::pair<const T*, int> g = gradient(R_[iry_]);
+    if (smooth) {                                         // G = A^T r + mu y / sqrt(|y_i|^2 + d^2)
+      launch_fgd_grad<T>(y, g.first, g.second, G_, n_, l_, mu_, O_.delta, red(S_REGY), st_);
+      check_launch();
+      g = {G_, 1};
+    }
+    const int rc = (iry_ + 1) % kRes, ryn = (iry_ + 2) % kRes;
     double t;
     bool accepted = false;
-    auto trial = [&](double tt) {
-      if (smooth) launch_fgd_trial<T>(y, G_, xc, n_, l_, tt, O_.delta, red(S_TR), st_);
-      else launch_prox_fista<T>(y, G_, xc, n_, l_, tt, mu_, O_.thres, red(S_TR), st_);
+    auto trial = [&](double tt, bool first) {
+      launch_fista_trial<T>(!smooth, y, first ? g.first : G_, first ? g.second : 1,
+                            (first && g.first != G_) ? G_ : nullptr, X_[ix_], X_[ic_], X_[ivn_],
+                            X_[iyn_], n_, l_, tt, mu_, O_.thres, theta, theta_next, O_.delta,
+                            red(S_TR), st_);
       check_launch();
     };
     const int i_rn = smooth ? 3 : 2, i_max = smooth ? 4 : 3;
-    if (O_.step_type == GLX_STEP_LINE_SEARCH) {
+    if (O_.step_type == GLX_STEP_LINE_SEARCH && O_.ls_maxit > 0) {
       t = tk_;
       for (int it = 0; it < O_.ls_maxit; ++it) {
-        trial(t);
-        launch_count_above<T>(xc, nl_, scal_ + S_TR + i_max, red(S_CNT), st_);
-        check_launch();
-        residual(xc, nullptr, R_[1 - ir_], S_SQZ, 1);
+        trial(t, it == 0);
+        const T* xs[3] = {X_[ic_], X_[iyn_], nullptr};
+        T* rs[3] = {R_[rc], R_[ryn], nullptr};
+        residuals(2, xs, rs, S_RT, X_[ic_], scal_ + S_TR + i_max);   // A @ [x | y_next]
         readback();
-        double gxc;
+        if (gy_pending_) { gy_sq_ = hs_[S_RG]; gy_pending_ = false; }
+        double gy = 0.5 * gy_sq_, gxc = 0.5 * hs_[S_RT];
         if (smooth) {
-          gy = 0.5 * hs_[S_SQR] + mu_ * hs_[S_REGY];
-          gxc = 0.5 * hs_[S_SQZ] + mu_ * hs_[S_TR + 2];
-        } else {
-          gy = 0.5 * hs_[S_SQR];
-          gxc = 0.5 * hs_[S_SQZ];
+          gy = gy + mu_ * hs_[S_REGY];
+          gxc = gxc + mu_ * hs_[S_TR + 2];
         }
         if (gxc <= gy + hs_[S_TR + 0] + hs_[S_TR + 1] / (2 * t)) { accepted = true; break; }
         t *= O_.ls_coeff;
       }
-      if (!accepted) trial(t);
+      if (!accepted) trial(t, false);
     } else {
-      t = schedule(inner_);
-      trial(t);
+      t = O_.step_type == GLX_STEP_LINE_SEARCH ? tk_ : schedule(inner_);
+      trial(t, true);
     }
-    // v = x_k + (x - x_k)/theta, written over v_k (no longer needed)
-    launch_fista_v<T>(xk, xc, X_[iv_], nl_, theta, st_);
-    check_launch();
-    std::swap(ix_, ic_);                                  // x_k <- x (the candidate buffer)
+    // x_k <- x, v_k <- v (:145, :147), y <- y_next
+    std::swap(ix_, ic_);
+    std::swap(iv_, ivn_);
+    std::swap(iy_, iyn_);
     tk_ = t;
     if (accepted) {
-      ir_ = 1 - ir_;
-      f_cur_ = 0.5 * hs_[S_SQZ] + P_.mu0 * hs_[S_TR + i_rn];
-      s_cur_ = hs_[S_CNT] / (double)nl_;
+      iry_ = ryn;
+      gy_sq_ = hs_[S_RT + 1];
+      y_ready_ = true;
+      f_cur_ = 0.5 * hs_[S_RT] + P_.mu0 * hs_[S_TR + i_rn];   // A x exact: same x as recorded
+      s_cur_ = hs_[S_RT + 3] / (double)nl_;
       f_known_ = true;
     } else {
+      y_ready_ = false;
       f_known_ = false;
     }
   }
 
   // ------------------------------------------------------------------ SGD / GD (no syncs)
+  // Between iterations: X_[0] = x, X_[1] = thr(x) (:93), R_[0] = A x - b, R_[1] = A thr(x) - b,
+  // fh_dev_[k_] = the objective of x (recorded on the device by the finalize kernel).
+  double descent_mu_obj(int64_t phase) const {
+    return method_ == GLX_GD ? P_.mu0 : mus_[std::min<int64_t>(phase, 2)];
+  }
+  void descent_residuals(int64_t phase) {
+    const T* xs[3] = {X_[0], X_[1], nullptr};
+    T* rs[3] = {R_[0], R_[1], nullptr};
+    residuals(2, xs, rs, S_RO, nullptr, nullptr, fh_dev_ + k_, descent_mu_obj(phase));
+  }
   void iter_descent() {
     const bool gd = (method_ == GLX_GD);
-    const double mu_obj = gd ? P_.mu0 : mu_;   // GD records real_obj_func (mu0), SGD obj_func (mu)
-    T* x = X_[0];
-    if (!rn_known_) {
-      launch_rownorm_max<T>(x, n_, l_, red(S_XRN), st_);
+    if (!state_valid_) {
+      launch_rownorm_max<T>(X_[0], n_, l_, red(S_DRN), st_);
       check_launch();
-      GLX_HIP(hipMemcpyAsync(scal_ + S_DRN, scal_ + S_XRN, sizeof(double), hipMemcpyDeviceToDevice, st_));
-      rn_known_ = true;
+      launch_threshold<T>(X_[0], X_[1], nl_, O_.thres, flag_, ++epoch_, st_);
+      check_launch();
+      descent_residuals(phase_);
+      state_valid_ = true;
     }
-    residual(x, nullptr, R_[0], S_SQR, 1);
-    launch_record_f(scal_, S_SQR, S_DRN, mu_obj, fh_dev_, k_, st_);
-    check_launch();
     ++k_;
     ++inner_;
-    GLX_HIP(hipMemsetAsync(flag_, 0, sizeof(int), st_));
-    launch_threshold<T>(x, nl_, O_.thres, flag_, st_);
-    check_launch();
-    residual(x, flag_, R_[0], S_SQR, 0);
-    gradient(R_[0]);
+    const std::pair<const T*, int> g = gradient(R_[1]);
     const double alpha = (O_.step_type == GLX_STEP_FIXED || mu_ > P_.mu0) ? O_.alpha0 : schedule(inner_);
-    launch_descent<T>(x, G_, n_, l_, alpha, mu_, O_.thres, O_.delta, gd ? 1 : 0, red(S_DRN), st_);
+    launch_descent<T>(X_[0], X_[1], g.first, g.second, n_, l_, alpha, mu_, O_.thres, O_.delta,
+                      gd ? 1 : 0, red(S_DRN), st_);
     check_launch();
+    // next iteration's objective residual and gradient residual, one pass
+    const int64_t next_phase = (inner_ >= O_.maxit) ? phase_ + 1 : phase_;
+    descent_residuals(next_phase);
   }
 
  public:
@@ -520,19 +610,27 @@ class Session : public SessionBase {
   int64_t m_ = 0, n_ = 0, l_ = 0, nl_ = 0, ml_ = 0;
   const T* A_ = nullptr;
   const T* B_ = nullptr;
-  T* X_[5] = {nullptr, nullptr, nullptr, nullptr, nullptr};
-  T* R_[2] = {nullptr, nullptr};
+  T* X_[kBufs] = {nullptr, nullptr, nullptr, nullptr, nullptr, nullptr};
+  T* R_[kRes] = {nullptr, nullptr, nullptr, nullptr};
   T *G_ = nullptr, *Gp_ = nullptr, *Pp_ = nullptr;
-  double *scal_ = nullptr, *part_ = nullptr, *fh_dev_ = nullptr, *hs_ = nullptr;
+  double *scal_ = nullptr, *part_ = nullptr, *fh_dev_ = nullptr;
+  double *hs_ = nullptr, *hs_dev_ = nullptr;
+  unsigned *hseq_ = nullptr, *hseq_dev_ = nullptr;
   unsigned* ticket_ = nullptr;
   int* flag_ = nullptr;
   int64_t fh_cap_ = 0;
 
  private:
   int method_ = 0;
-  bool use_sparsity_ = true, device_hist_ = false;
+  bool use_sparsity_ = true, device_hist_ = false, spin_readback_ = true;
+  unsigned seq_ = 0;
+  int epoch_ = 0;
   // buffer roles
-  int ix_ = 0, iv_ = 1, iy_ = 2, ic_ = 3, ir_ = 0;
+  int ix_ = 0, iv_ = 1, iy_ = 2, ic_ = 3, ivn_ = 4, iyn_ = 5;   // FISTA
+  int ixt_ = 1, ip_ = 2, ipt_ = 3, iz_ = 4;                      // ProxGD
+  int irg_ = 0, iry_ = 0;
+  bool state_valid_ = false, thr_from_trial_ = false, y_ready_ = false, gy_pending_ = false;
+  double gx_ = 0, gy_sq_ = 0;
   // algorithm state
   int phase_ = 0;
   int64_t inner_ = 0, k_ = 0;
@@ -542,7 +640,8 @@ class Session : public SessionBase {
   double f_cur_ = 0, s_cur_ = 0, fbest_ = 0, sp_cur_ = 0, sp_prev_ = 0;
   std::vector<double> fh_, fhb_;
   double tt_ = 0;
-  int64_t ax_calls_ = 0, ax_gated_ = 0, atr_calls_ = 0, syncs_ = 0;
+  int64_t ax_calls_ = 0, ax_cols_ = 0, atr_calls_ = 0, syncs_ = 0;
+  double stats_[8] = {0, 0, 0, 0, 0, 0, 0, 0};
   std::vector<std::pair<hipEvent_t, hipEvent_t>> ev_[2];
   std::vector<hipEvent_t> ev_pool_;
 };
@@ -578,8 +677,17 @@ struct KernelWs {
 };
 static size_t kernel_ws(int es, const GemmPlan& p, void* base, KernelWs* out) {
   Carver c(base);
-  void* pp = c.take((size_t)es * p.m * p.l * p.ax_S);
-  void* gp = c.take((size_t)es * p.n * p.l * p.atr_S);
+  // room for the largest split any variant of this shape plans (MFMA tiles, VALU)
+  int64_t s_ax = 1, s_atr = 1;
+  for (int v : {0, 3, 1220, 1410, 1820}) {
+    const GemmPlan q = make_plan(es, p.m, p.n, p.l, v);
+    s_ax = std::max<int64_t>(s_ax, q.ax_S);
+    s_atr = std::max<int64_t>(s_atr, q.atr_S);
+  }
+  s_ax = std::max<int64_t>(s_ax, p.ax_S);
+  s_atr = std::max<int64_t>(s_atr, p.atr_S);
+  void* pp = c.take((size_t)es * p.m * p.l * s_ax * 3);
+  void* gp = c.take((size_t)es * p.n * p.l * s_atr);
   double* part = static_cast<double*>(c.take(sizeof(double) * kMaxRedVals * kMaxBlocks));
   unsigned* ticket = static_cast<unsigned*>(c.take(256));
   double* scal = static_cast<double*>(c.take(sizeof(double) * NSCAL));
@@ -722,11 +830,17 @@ int glx_residual(int dtype, int64_t m, int64_t n, int64_t l, const void* A, cons
     KernelWs k = kernel_setup(dtype, m, n, l, ws, wsb, variant, st, &p);
     Red r{k.part, k.ticket, k.scal};
     if (dtype == GLX_F64) {
-      launch_ax<double>(p, (const double*)A, (const double*)X, (double*)k.pp, nullptr, st);
-      launch_finalize_residual<double>((const double*)k.pp, p.ax_S, (const double*)B, (double*)R, m * l, nullptr, 1, r, st);
+      const double* xs[3] = {(const double*)X, nullptr, nullptr};
+      double* rs[3] = {(double*)R, nullptr, nullptr};
+      launch_ax<double>(p, 1, (const double*)A, xs, (double*)k.pp, nullptr, 0, st);
+      launch_finalize_residual<double>((const double*)k.pp, p.ax_S, (const double*)B, 1, rs, m * l,
+                                       nullptr, 0, 1, nullptr, 0, nullptr, nullptr, 0.0, nullptr, r, st);
     } else {
-      launch_ax<float>(p, (const float*)A, (const float*)X, (float*)k.pp, nullptr, st);
-      launch_finalize_residual<float>((const float*)k.pp, p.ax_S, (const float*)B, (float*)R, m * l, nullptr, 1, r, st);
+      const float* xs[3] = {(const float*)X, nullptr, nullptr};
+      float* rs[3] = {(float*)R, nullptr, nullptr};
+      launch_ax<float>(p, 1, (const float*)A, xs, (float*)k.pp, nullptr, 0, st);
+      launch_finalize_residual<float>((const float*)k.pp, p.ax_S, (const float*)B, 1, rs, m * l,
+                                      nullptr, 0, 1, nullptr, 0, nullptr, nullptr, 0.0, nullptr, r, st);
     }
     check_launch();
     if (half_sumsq_dev) {
@@ -734,6 +848,34 @@ int glx_residual(int dtype, int64_t m, int64_t n, int64_t l, const void* A, cons
       launch_record_f(k.scal, 0, 0, 0.0, static_cast<double*>(half_sumsq_dev), 0, st);
       check_launch();
     }
+  });
+}
+
+int glx_residual_batch(int dtype, int64_t m, int64_t n, int64_t l, const void* A, int nsrc,
+                       const void* const* X, const void* B, void* const* R, void* sumsq_dev,
+                       void* ws, size_t wsb, int variant, void* stream) {
+  return guarded([&] {
+    if (nsrc < 1 || nsrc > 3 || !X || !R) throw Error{GLX_E_INVALID, "nsrc must be 1..3"};
+    hipStream_t st = static_cast<hipStream_t>(stream);
+    GemmPlan p;
+    KernelWs k = kernel_setup(dtype, m, n, l, ws, wsb, variant, st, &p);
+    Red r{k.part, k.ticket, sumsq_dev ? static_cast<double*>(sumsq_dev) : k.scal};
+    if (dtype == GLX_F64) {
+      const double* xs[3] = {nullptr, nullptr, nullptr};
+      double* rs[3] = {nullptr, nullptr, nullptr};
+      for (int i = 0; i < nsrc; ++i) { xs[i] = (const double*)X[i]; rs[i] = (double*)R[i]; }
+      launch_ax<double>(p, nsrc, (const double*)A, xs, (double*)k.pp, nullptr, 0, st);
+      launch_finalize_residual<double>((const double*)k.pp, p.ax_S, (const double*)B, nsrc, rs, m * l,
+                                       nullptr, 0, 1, nullptr, 0, nullptr, nullptr, 0.0, nullptr, r, st);
+    } else {
+      const float* xs[3] = {nullptr, nullptr, nullptr};
+      float* rs[3] = {nullptr, nullptr, nullptr};
+      for (int i = 0; i < nsrc; ++i) { xs[i] = (const float*)X[i]; rs[i] = (float*)R[i]; }
+      launch_ax<float>(p, nsrc, (const float*)A, xs, (float*)k.pp, nullptr, 0, st);
+      launch_finalize_residual<float>((const float*)k.pp, p.ax_S, (const float*)B, nsrc, rs, m * l,
+                                      nullptr, 0, 1, nullptr, 0, nullptr, nullptr, 0.0, nullptr, r, st);
+    }
+    check_launch();
   });
 }
 

@@ -42,7 +42,8 @@ class GlxResult(ctypes.Structure):
     _fields_ = [("iters", c_int64), ("fval", c_double), ("tt", c_double),
                 ("f_hist", POINTER(c_double)), ("f_hist_best", POINTER(c_double)),
                 ("f_cap", c_int64), ("n_fhist", c_int64), ("ax_calls", c_int64),
-                ("atr_calls", c_int64), ("syncs", c_int64)]
+                ("atr_calls", c_int64), ("syncs", c_int64), ("ax_sources", c_int64),
+                ("stats", c_double * 8)]
 
 
 class GlxError(RuntimeError):
@@ -70,6 +71,9 @@ _SIGS = {
                           POINTER(GlxResult), c_void_p]),
     "glx_residual": (c_int, [c_int, c_int64, c_int64, c_int64, c_void_p, c_void_p, c_void_p,
                              c_void_p, c_void_p, c_void_p, c_size_t, c_int, c_void_p]),
+    "glx_residual_batch": (c_int, [c_int, c_int64, c_int64, c_int64, c_void_p, c_int,
+                                   POINTER(c_void_p), c_void_p, POINTER(c_void_p), c_void_p,
+                                   c_void_p, c_size_t, c_int, c_void_p]),
     "glx_gradient": (c_int, [c_int, c_int64, c_int64, c_int64, c_void_p, c_void_p, c_void_p,
                              c_void_p, c_size_t, c_void_p]),
     "glx_prox": (c_int, [c_int, c_int64, c_int64, c_void_p, c_double, c_double, c_double,

@@ -48,6 +48,23 @@ def residual(A: torch.Tensor, X: torch.Tensor, B: torch.Tensor, variant: int = 0
     return R, h
 
 
+def residual_batch(A: torch.Tensor, Xs, B: torch.Tensor, variant: int = 0):
+    """R_i = A X_i - B for up to three right-hand sides in one pass over A; also returns the
+    squared norms ||R_i||^2 (float64 device tensor)."""
+    m, n = A.shape
+    l = Xs[0].shape[1]
+    dt = _dt(A)
+    Rs = [torch.empty((m, l), dtype=A.dtype, device=A.device) for _ in Xs]
+    sq = torch.empty(4, dtype=torch.float64, device=A.device)
+    ws = _ws(dt, m, n, l, A.device)
+    xp = (ctypes.c_void_p * 3)(*[x.data_ptr() for x in Xs], *([None] * (3 - len(Xs))))
+    rp = (ctypes.c_void_p * 3)(*[r.data_ptr() for r in Rs], *([None] * (3 - len(Rs))))
+    check(lib().glx_residual_batch(dt, m, n, l, A.data_ptr(), len(Xs), xp, B.data_ptr(), rp,
+                                   sq.data_ptr(), ws.data_ptr(), ws.numel(), variant,
+                                   _stream(A.device)))
+    return Rs, sq
+
+
 def gradient(A: torch.Tensor, R: torch.Tensor) -> torch.Tensor:
     """G = A^T R."""
     m, n = A.shape

@@ -165,7 +165,8 @@ class Session:
                 "f_hist": [np.float64(v) for v in fh[:n]],
                 "f_hist_best": [np.float64(v) for v in fb[:n]],
                 "ax_calls": int(res.ax_calls), "atr_calls": int(res.atr_calls),
-                "syncs": int(res.syncs)}
+                "syncs": int(res.syncs), "ax_sources": int(res.ax_sources),
+                "stats": [float(v) for v in res.stats]}
 
     def close(self):
         if getattr(self, "h", None):

@@ -95,6 +95,9 @@ typedef struct glx_result {
   int64_t ax_calls;     /* passes of A@x issued (executed-work accounting)            */
   int64_t atr_calls;    /* passes of A^T r issued                                     */
   int64_t syncs;        /* host<->device synchronisations                             */
+  int64_t ax_sources;   /* right-hand sides batched into those A@x passes (>= ax_calls) */
+  double stats[8];      /* diagnostics: [0] threshold-changed entries and [1] rows summed over
+                           accepted ProxGD steps, [2] accepted steps                    */
 } glx_result;
 
 typedef struct glx_session glx_session;
@@ -131,6 +134,11 @@ int glx_solve(const glx_problem* prob, const glx_opts* opts, void* workspace,
 int glx_residual(int dtype, int64_t m, int64_t n, int64_t l, const void* A, const void* X,
                  const void* B, void* R, void* half_sumsq_dev, void* workspace,
                  size_t workspace_bytes, int variant, void* stream);
+/* Batched right-hand sides in one pass over A: R[i] = A X[i] - B for i < nsrc (nsrc <= 3);
+ * sumsq_dev[i] = ||R[i]||^2 (device doubles, 4 slots). */
+int glx_residual_batch(int dtype, int64_t m, int64_t n, int64_t l, const void* A, int nsrc,
+                       const void* const* X, const void* B, void* const* R, void* sumsq_dev,
+                       void* workspace, size_t workspace_bytes, int variant, void* stream);
 /* G = A^T R (n x l). */
 int glx_gradient(int dtype, int64_t m, int64_t n, int64_t l, const void* A, const void* R,
                  void* G, void* workspace, size_t workspace_bytes, void* stream);
