@@ -19,10 +19,16 @@ extern thread_local std::string g_last_error;
 constexpr int kMaxBlocks = 1024;   // grid cap of every reducing kernel (size of a partials row)
 constexpr int kMaxRedVals = 6;     // max scalars one reducing kernel produces
 constexpr int kMaxL = 128;         // largest l (columns of x) supported by the row kernels
+// Arrival tickets: kTicketShards per-XCD counters plus one final counter, each on its own
+// 128-B line (32 unsigned words apart). Word 0 = final counter, shard s at (1 + s) * 32.
+constexpr int kTicketShards = 8;
+constexpr int kTicketStride = 32;
+constexpr int kTicketBytes = 2048;  // >= (kTicketShards + 1) * 128, keeps 256-B alignment
 
 // Deterministic grid-wide reduction target: each block writes its partial to
 // part[v * kMaxBlocks + block]; the last block (arrival ticket) sums them in block order
-// and writes out[v]. `ticket` must be zero before the first launch; the last block resets it.
+// and writes out[v]. `ticket` (kTicketBytes) must be zero before the first launch; the last
+// block resets it.
 struct Red {
   double* part;
   unsigned* ticket;
@@ -38,6 +44,7 @@ struct GemmPlan {
   int ax_mt, ax_pf; // MFMA: 16-row tiles per wave, chunks in flight per wave
   int ax_code;      // MFMA variant code (kind*1000 + MT*100 + PF*10 + non-temporal)
   int ax_S;         // K (= n) splits across workgroups
+  int ax_xmap;      // MFMA: group K splits by XCD (L2 locality of X)
   int ax_lb;        // VALU: column block width (1,2,4,8); ax_ncb = ceil(l / ax_lb)
   int ax_vec;       // VALU: 16-byte loads
   // A^T R  ->  Gp[atr_S][n][l]

@@ -17,7 +17,7 @@
 // Python-float operands of a T array (NEP 50 weak scalars).
 //
 // Reductions are deterministic: block partials in a fixed tree order, then the last block to
-// arrive (agent-scope release/acquire ticket, cdna_hip_programming.md Guideline 16) sums the
+// arrive (sc1 partials + a two-level agent-scope arrival ticket, see grid_reduce) sums the
 // block partials in block order. max() propagates NaN like np.max.
 #include "glx_internal.h"
 
@@ -61,20 +61,46 @@ __device__ bool grid_reduce(double (&v)[NV], const Red& red) {
       __hip_atomic_store(&red.part[j * kMaxBlocks + blockIdx.x], bv, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    const unsigned prev = __hip_atomic_fetch_add(red.ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    is_last = (prev == gridDim.x - 1) ? 1 : 0;
+    // Two-level arrival: one device-scope counter costs ~12 ns per arriving block
+    // (MI355X_MICROARCH.md, "fanin"), so 1024 blocks on one word serialise for ~12 us. Blocks
+    // arrive on the counter of their shard (blockIdx % 8, i.e. their XCD under round-robin
+    // dispatch); the last arriver of each shard, whose add returned after every add of its
+    // shard, arrives on the final counter, and the last arriver there owns the sum.
+    const unsigned G = gridDim.x;
+    const unsigned sh = blockIdx.x & (kTicketShards - 1);
+    const unsigned nsh = G < (unsigned)kTicketShards ? G : (unsigned)kTicketShards;
+    const unsigned cnt = (G - sh + kTicketShards - 1) / kTicketShards;
+    const unsigned prev = __hip_atomic_fetch_add(red.ticket + (1 + sh) * kTicketStride, 1u,
+                                                 __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    int last = 0;
+    if (prev == cnt - 1)
+      last = __hip_atomic_fetch_add(red.ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == nsh - 1;
+    is_last = last;
   }
   __syncthreads();
   if (!is_last) return false;
+  // every load of the partials is an sc1 load (L1 bypass): no acquire fence needed. All of them
+  // are issued before the first is consumed (clamped index, select afterwards), so the last
+  // block pays one round trip instead of one per partial.
+  constexpr int PER = kMaxBlocks / 256;
+  double pv[NV][PER];
+#pragma unroll
+  for (int j = 0; j < NV; ++j)
+#pragma unroll
+    for (int t = 0; t < PER; ++t) {
+      const unsigned b = threadIdx.x + 256u * t;
+      const unsigned bc = b < gridDim.x ? b : gridDim.x - 1;
+      pv[j][t] = __hip_atomic_load(&red.part[j * kMaxBlocks + bc], __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_AGENT);
+    }
   double acc[NV];
 #pragma unroll
   for (int j = 0; j < NV; ++j) {
     const int op = (MAXMASK >> j) & 1;
     acc[j] = identity(op);
-    // every load of the partials is an sc1 load (L1 bypass): no acquire fence needed
-    for (unsigned b = threadIdx.x; b < gridDim.x; b += 256)
-      acc[j] = combine(op, acc[j], __hip_atomic_load(&red.part[j * kMaxBlocks + b], __ATOMIC_RELAXED,
-                                                     __HIP_MEMORY_SCOPE_AGENT));
+#pragma unroll
+    for (int t = 0; t < PER; ++t)
+      if (threadIdx.x + 256u * t < gridDim.x) acc[j] = combine(op, acc[j], pv[j][t]);
 #pragma unroll
     for (int off = 32; off > 0; off >>= 1) acc[j] = combine(op, acc[j], __shfl_xor(acc[j], off));
   }
@@ -90,7 +116,8 @@ __device__ bool grid_reduce(double (&v)[NV], const Red& red) {
       const int op = (MAXMASK >> j) & 1;
       red.out[j] = combine(op, combine(op, sh[j][0], sh[j][1]), combine(op, sh[j][2], sh[j][3]));
     }
-    __hip_atomic_store(red.ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    for (int k = 0; k <= kTicketShards; ++k)
+      __hip_atomic_store(red.ticket + k * kTicketStride, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
   return true;
 }

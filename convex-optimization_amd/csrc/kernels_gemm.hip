@@ -85,28 +85,63 @@ __device__ inline typename MF<T>::vec_t load_vec(const T* p) {
 // NSRC right-hand sides X0..X2 (each n x 16NT) share every loaded A fragment: the batched
 // products of the next iteration (e.g. A @ [z | p_thr]) cost one pass over A.
 // P[src][S][m][16NT]. NTL: A streamed with non-temporal loads (keeps X resident in L2).
-template <typename T, int MT, int NT, int NSRC, int PF, bool QUAD, bool NTL>
+// Logical (row block, K split) of a 1-D launch. xmap = 1 groups K splits by XCD: blocks are
+// observed to be dealt round-robin over the 8 XCDs (lin % 8 shares an L2), so split s is
+// given to XCD group s (S | 8: 8/S XCDs per split; 8 | S: S/8 splits per XCD). Each XCD's L2
+// then holds only its own slice of X instead of all of it. Placement is a speed matter only:
+// any other placement computes the same result.
+__device__ inline bool ax_block(int xmap, int gx, int S, int& bx, int& by) {
+  const int lin = blockIdx.x;
+  if (xmap) {
+    const int xcd = lin & 7, slot = lin >> 3;
+    if (S <= 8) {
+      const int G = 8 / S;
+      by = xcd / G;
+      bx = slot * G + (xcd % G);
+    } else {
+      by = xcd + 8 * (slot / gx);
+      bx = slot % gx;
+    }
+    return bx < gx && by < S;
+  }
+  bx = lin % gx;
+  by = lin / gx;
+  return true;
+}
+static inline int ax_grid(int xmap, int gx, int S) {
+  if (xmap && S <= 8) {
+    const int G = 8 / S;
+    return ((gx + G - 1) / G) * G * S;
+  }
+  return gx * S;
+}
+static inline int ax_xmap_ok(int S) { return (S <= 8) ? (8 % S == 0) : (S % 8 == 0); }
+
+template <typename T, int MT, int NT, int NSRC, int PF, bool QUAD, bool NTL, int VPL>
 __global__ __launch_bounds__(256) void k_ax_mfma(const T* __restrict__ A, const T* __restrict__ X0,
                                                  const T* __restrict__ X1, const T* __restrict__ X2,
                                                  T* __restrict__ P, int64_t m, int64_t n,
-                                                 int64_t chunks, int S,
+                                                 int64_t chunks, int S, int gx, int xmap,
                                                  const int* __restrict__ gate, int epoch) {
   typedef MF<T> M;
   typedef typename M::vec_t V;
   typedef typename M::acc_t C;
   constexpr int E = M::E;
-  constexpr int CK = 4 * E;   // k per chunk
-  constexpr int L = 16 * NT;  // == l
+  constexpr int EL = VPL * E;   // contiguous k values a lane streams from its row per chunk
+  constexpr int CK = 4 * EL;    // k per chunk
+  constexpr int L = 16 * NT;    // == l
   constexpr int NC = NT * NSRC;
   if (!gate_live(gate, epoch)) return;
+  int bx, by;
+  if (!ax_block(xmap, gx, S, bx, by)) return;   // padding block of the XCD map (block-uniform)
   __shared__ C red[MT * NC][64];
 
   const int lane = threadIdx.x & 63;
   const int wave = threadIdx.x >> 6;
   const int i = lane & 15, q = lane >> 4;
-  const int64_t row0 = (int64_t)blockIdx.x * (16 * MT);
+  const int64_t row0 = (int64_t)bx * (16 * MT);
   const int64_t W = (int64_t)S * 4;
-  const int64_t w = (int64_t)blockIdx.y * 4 + wave;
+  const int64_t w = (int64_t)by * 4 + wave;
   const int64_t cb = chunks * w / W, ce = chunks * (w + 1) / W;
 
   const int lrow = QUAD ? (lane >> 2) : i;
@@ -117,9 +152,9 @@ __global__ __launch_bounds__(256) void k_ax_mfma(const T* __restrict__ A, const 
   for (int mt = 0; mt < MT; ++mt) {
     int64_t r = row0 + mt * 16 + lrow;
     r = r < m ? r : m - 1;
-    ap[mt] = A + r * n + cb * CK + (int64_t)lchk * E;
+    ap[mt] = A + r * n + cb * CK + (int64_t)lchk * EL;
   }
-  const int64_t xoff = (cb * CK + (int64_t)q * E) * L + i;
+  const int64_t xoff = (cb * CK + (int64_t)q * EL) * L + i;
   const T* xp[NSRC];
   xp[0] = X0 + xoff;
   if (NSRC > 1) xp[1] = X1 + xoff;
@@ -131,16 +166,18 @@ __global__ __launch_bounds__(256) void k_ax_mfma(const T* __restrict__ A, const 
 #pragma unroll
     for (int c = 0; c < NC; ++c) acc[mt][c] = C{};
 
-  V a[PF][MT];
-  T xb[PF][E][NC];
+  V a[PF][MT][VPL];
+  T xb[PF][EL][NC];
 #pragma unroll
   for (int p = 0; p < PF; ++p) {
     if (cb + p < ce) {
       const int64_t off = (int64_t)p * CK;
 #pragma unroll
-      for (int mt = 0; mt < MT; ++mt) a[p][mt] = load_vec<T, NTL>(ap[mt] + off);
+      for (int mt = 0; mt < MT; ++mt)
 #pragma unroll
-      for (int e = 0; e < E; ++e)
+        for (int v = 0; v < VPL; ++v) a[p][mt][v] = load_vec<T, NTL>(ap[mt] + off + v * E);
+#pragma unroll
+      for (int e = 0; e < EL; ++e)
 #pragma unroll
         for (int c = 0; c < NC; ++c) xb[p][e][c] = xp[c / NT][off * L + e * L + (c % NT) * 16];
     }
@@ -150,29 +187,36 @@ __global__ __launch_bounds__(256) void k_ax_mfma(const T* __restrict__ A, const 
     for (int p = 0; p < PF; ++p) {
       const int64_t c = c0 + p;
       if (c < ce) {
-        V av[MT];
+        V av[MT][VPL];
 #pragma unroll
-        for (int mt = 0; mt < MT; ++mt) av[mt] = QUAD ? bpermute_vec(a[p][mt], src) : a[p][mt];
-        T xv[E][NC];
+        for (int mt = 0; mt < MT; ++mt)
 #pragma unroll
-        for (int e = 0; e < E; ++e)
+          for (int v = 0; v < VPL; ++v) av[mt][v] = QUAD ? bpermute_vec(a[p][mt][v], src) : a[p][mt][v];
+        T xv[EL][NC];
+#pragma unroll
+        for (int e = 0; e < EL; ++e)
 #pragma unroll
           for (int cc = 0; cc < NC; ++cc) xv[e][cc] = xb[p][e][cc];
         if (c + PF < ce) {   // refill this ring slot with chunk c + PF
           const int64_t off = (c + PF - cb) * CK;
 #pragma unroll
-          for (int mt = 0; mt < MT; ++mt) a[p][mt] = load_vec<T, NTL>(ap[mt] + off);
+          for (int mt = 0; mt < MT; ++mt)
 #pragma unroll
-          for (int e = 0; e < E; ++e)
+            for (int v = 0; v < VPL; ++v) a[p][mt][v] = load_vec<T, NTL>(ap[mt] + off + v * E);
+#pragma unroll
+          for (int e = 0; e < EL; ++e)
 #pragma unroll
             for (int cc = 0; cc < NC; ++cc) xb[p][e][cc] = xp[cc / NT][off * L + e * L + (cc % NT) * 16];
         }
 #pragma unroll
-        for (int e = 0; e < E; ++e)
+        for (int v = 0; v < VPL; ++v)
 #pragma unroll
-          for (int mt = 0; mt < MT; ++mt)
+          for (int e = 0; e < E; ++e)
 #pragma unroll
-            for (int cc = 0; cc < NC; ++cc) acc[mt][cc] = M::mma(av[mt][e], xv[e][cc], acc[mt][cc]);
+            for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+              for (int cc = 0; cc < NC; ++cc)
+                acc[mt][cc] = M::mma(av[mt][v][e], xv[v * E + e][cc], acc[mt][cc]);
       }
     }
   }
@@ -198,7 +242,7 @@ __global__ __launch_bounds__(256) void k_ax_mfma(const T* __restrict__ A, const 
   if (wave != 0) return;
 #pragma unroll
   for (int sr = 0; sr < NSRC; ++sr) {
-    T* pout = P + ((int64_t)sr * S + blockIdx.y) * m * L;
+    T* pout = P + ((int64_t)sr * S + by) * m * L;
 #pragma unroll
     for (int mt = 0; mt < MT; ++mt)
 #pragma unroll
@@ -494,18 +538,20 @@ static int env_int(const char* name, int dflt) {
 
 // Defaults chosen by the sweep in scripts/kbench.py on MI355X.
 // ax code: kind*1000 + MT*100 + PF*10 + NTL (kind 1 = direct row loads, 2 = quad + bpermute).
-static constexpr int kAxDefault = 2820;
+static constexpr int kAxDefault = 21820;   // f64: VPL 2, direct loads, MT 8, PF 2
+static constexpr int kAxDefault32 = 21410; // f32: VPL 2, direct loads, MT 4, PF 1
 static constexpr int kAtrDefault = 102;
 // batched right-hand sides (MFMA-bound at l = 32): f64 1420 / f32 1430 (2 RHS), 1220 (3 RHS)
 static int axb_default(int nsrc, int esize) {
   if (nsrc == 3) return 1220;
-  return esize == 8 ? 1420 : 1430;
+  return esize == 8 ? 21420 : 21410;
 }   // WL = 0, PF = 2 (+1000: non-temporal A loads)
 
 static bool valid_ax_code(int c) {
   switch (c) {
     case 1410: case 1420: case 1421: case 1430: case 1431: case 1820: case 1821: case 1810:
     case 1811: case 2410: case 2420: case 2421: case 2820: case 2821: case 1220: case 1221:
+    case 21420: case 22420: case 21410: case 41220: case 41210: case 41410: case 21820:
       return true;
     default: return false;
   }
@@ -533,19 +579,23 @@ GemmPlan make_plan(int esize, int64_t m, int64_t n, int64_t l, int ax_variant) {
     const int64_t kunits = n / (64 * (p.ax_vec ? E : 1)); // 64-lane strides per row
     p.ax_S = (int)clampi(cdiv(kTargetWaves, waves), 1, std::max<int64_t>(1, std::min<int64_t>(kMaxSplit, kunits / 4)));
   } else {
-    const int code = valid_ax_code(ax_variant) ? ax_variant : kAxDefault;
+    int code = valid_ax_code(ax_variant) ? ax_variant : (esize == 8 ? kAxDefault : kAxDefault32);
+    int vpl = code / 10000 ? code / 10000 : 1;
+    if (n % (4 * E * vpl) != 0) { code = kAxDefault; vpl = 1; }   // wider chunks need n % 4*E*VPL
     p.ax_code = code;
-    p.ax_kind = code / 1000;
+    p.ax_kind = (code / 1000) % 10;
     p.ax_mt = (code / 100) % 10;
     p.ax_pf = (code / 10) % 10;
     const int64_t blocks = cdiv(m, 16 * p.ax_mt);
-    const int64_t chunks = n / (4 * E);
-    const int64_t target = (esize == 8 && p.ax_mt == 8) ? kTargetWaves / 2 : kTargetWaves;
+    const int64_t chunks = n / (4 * E * vpl);
+    // sweep (scripts/kbench.py): f64 at MT 8 wants 1024 waves, f32 4096
+    const int64_t target = esize == 8 ? (p.ax_mt == 8 ? kTargetWaves / 2 : kTargetWaves) : 2 * kTargetWaves;
     p.ax_S = (int)clampi(cdiv(target, blocks * 4), 1,
                          std::max<int64_t>(1, std::min<int64_t>(kMaxSplit, chunks / 16)));
   }
   const int s_ax = env_int("GLX_AX_S", 0);
   if (s_ax > 0) p.ax_S = (int)std::min<int64_t>(s_ax, kMaxSplit);
+  p.ax_xmap = env_int("GLX_AX_XCD", 1);
   // ---- A^T R ----
   int atr_code = env_int("GLX_ATR_VARIANT", 0);
   if (atr_code == 0) atr_code = esize == 8 ? kAtrDefault : 1102;   // f32: non-temporal A wins
@@ -608,13 +658,16 @@ static void ax_valu_src(const GemmPlan& p, const T* A, const T* const* X, T* P, 
   }
 }
 
-template <typename T, int NT, int NSRC, int MT, int PF, bool QUAD, bool NTL>
+template <typename T, int NT, int NSRC, int MT, int PF, bool QUAD, bool NTL, int VPL = 1>
 static void ax_mfma_go(const GemmPlan& p, const T* A, const T* const* X, T* P, const int* gate,
                        int epoch, hipStream_t st) {
   constexpr int E = 16 / sizeof(T);
-  const dim3 grid((unsigned)cdiv(p.m, 16 * MT), (unsigned)p.ax_S);
-  hipLaunchKernelGGL((k_ax_mfma<T, MT, NT, NSRC, PF, QUAD, NTL>), grid, dim3(256), 0, st, A, X[0],
-                     X[1], X[2], P, p.m, p.n, p.n / (4 * E), p.ax_S, gate, epoch);
+  const int gx = (int)cdiv(p.m, 16 * MT);
+  const int xmap = (p.ax_xmap && ax_xmap_ok(p.ax_S)) ? 1 : 0;
+  const dim3 grid((unsigned)ax_grid(xmap, gx, p.ax_S));
+  hipLaunchKernelGGL((k_ax_mfma<T, MT, NT, NSRC, PF, QUAD, NTL, VPL>), grid, dim3(256), 0, st, A,
+                     X[0], X[1], X[2], P, p.m, p.n, p.n / (4 * VPL * E), p.ax_S, gx, xmap, gate,
+                     epoch);
 }
 
 // One source: the swept variant. Batched sources (2, 3) use fixed register-feasible tiles.
@@ -622,7 +675,9 @@ template <typename T, int NT>
 static void ax_mfma_nt(const GemmPlan& p, int nsrc, const T* A, const T* const* X, T* P,
                        const int* gate, int epoch, hipStream_t st) {
   if (nsrc == 2) {
-    switch (env_int("GLX_AXB_VARIANT", axb_default(2, (int)sizeof(T)))) {
+    int code = env_int("GLX_AXB_VARIANT", axb_default(2, (int)sizeof(T)));
+    if (code >= 10000 && p.n % (4 * (16 / (int)sizeof(T)) * (code / 10000)) != 0) code = 1420;
+    switch (code) {
       case 1220: ax_mfma_go<T, NT, 2, 2, 2, false, false>(p, A, X, P, gate, epoch, st); break;
       case 1420: ax_mfma_go<T, NT, 2, 4, 2, false, false>(p, A, X, P, gate, epoch, st); break;
       case 1430: ax_mfma_go<T, NT, 2, 4, 3, false, false>(p, A, X, P, gate, epoch, st); break;
@@ -631,6 +686,9 @@ static void ax_mfma_nt(const GemmPlan& p, int nsrc, const T* A, const T* const* 
       case 2421: ax_mfma_go<T, NT, 2, 4, 2, true, true>(p, A, X, P, gate, epoch, st); break;
       case 2430: ax_mfma_go<T, NT, 2, 4, 3, true, false>(p, A, X, P, gate, epoch, st); break;
       case 2420: ax_mfma_go<T, NT, 2, 4, 2, true, false>(p, A, X, P, gate, epoch, st); break;
+      case 21420: ax_mfma_go<T, NT, 2, 4, 2, false, false, 2>(p, A, X, P, gate, epoch, st); break;
+      case 21410: ax_mfma_go<T, NT, 2, 4, 1, false, false, 2>(p, A, X, P, gate, epoch, st); break;
+      case 41210: ax_mfma_go<T, NT, 2, 2, 1, false, false, 4>(p, A, X, P, gate, epoch, st); break;
       default: ax_mfma_go<T, NT, 2, 4, 2, false, false>(p, A, X, P, gate, epoch, st); break;
     }
     return;
@@ -659,6 +717,13 @@ static void ax_mfma_nt(const GemmPlan& p, int nsrc, const T* A, const T* const* 
     case 2821: ax_mfma_go<T, NT, 1, 8, 2, true, true>(p, A, X, P, gate, epoch, st); break;
     case 1220: ax_mfma_go<T, NT, 1, 2, 2, false, false>(p, A, X, P, gate, epoch, st); break;
     case 1221: ax_mfma_go<T, NT, 1, 2, 2, false, true>(p, A, X, P, gate, epoch, st); break;
+    case 21420: ax_mfma_go<T, NT, 1, 4, 2, false, false, 2>(p, A, X, P, gate, epoch, st); break;
+    case 22420: ax_mfma_go<T, NT, 1, 4, 2, true, false, 2>(p, A, X, P, gate, epoch, st); break;
+    case 21410: ax_mfma_go<T, NT, 1, 4, 1, false, false, 2>(p, A, X, P, gate, epoch, st); break;
+    case 41220: ax_mfma_go<T, NT, 1, 2, 2, false, false, 4>(p, A, X, P, gate, epoch, st); break;
+    case 41210: ax_mfma_go<T, NT, 1, 2, 1, false, false, 4>(p, A, X, P, gate, epoch, st); break;
+    case 41410: ax_mfma_go<T, NT, 1, 4, 1, false, false, 4>(p, A, X, P, gate, epoch, st); break;
+    case 21820: ax_mfma_go<T, NT, 1, 8, 2, false, false, 2>(p, A, X, P, gate, epoch, st); break;
     default: ax_mfma_go<T, NT, 1, 4, 2, true, true>(p, A, X, P, gate, epoch, st); break;
   }
 }

@@ -122,7 +122,7 @@ class Session : public SessionBase {
     T* pp = static_cast<T*>(c.take(sizeof(T) * ml * plan.ax_S * 3));   // up to 3 batched sources
     double* scal = static_cast<double*>(c.take(sizeof(double) * NSCAL));
     double* part = static_cast<double*>(c.take(sizeof(double) * kMaxRedVals * kMaxBlocks));
-    unsigned* ticket = static_cast<unsigned*>(c.take(256));
+    unsigned* ticket = static_cast<unsigned*>(c.take(kTicketBytes));
     int* flag = static_cast<int*>(c.take(256));
     double* fh = static_cast<double*>(c.take(sizeof(double) * (fh_cap + 1)));
     if (s) {
@@ -162,7 +162,7 @@ class Session : public SessionBase {
     hseq_dev_ = reinterpret_cast<unsigned*>(hs_dev_ + NSCAL + 2);
     const char* rb = std::getenv("GLX_READBACK");
     spin_readback_ = !(rb && std::strcmp(rb, "sync") == 0);
-    GLX_HIP(hipMemsetAsync(ticket_, 0, 256, st_));
+    GLX_HIP(hipMemsetAsync(ticket_, 0, kTicketBytes, st_));
     GLX_HIP(hipMemsetAsync(flag_, 0, 256, st_));
     GLX_HIP(hipMemsetAsync(scal_, 0, sizeof(double) * NSCAL, st_));
     mus_[0] = 100 * P.mu0;
@@ -689,7 +689,7 @@ static size_t kernel_ws(int es, const GemmPlan& p, void* base, KernelWs* out) {
   void* pp = c.take((size_t)es * p.m * p.l * s_ax * 3);
   void* gp = c.take((size_t)es * p.n * p.l * s_atr);
   double* part = static_cast<double*>(c.take(sizeof(double) * kMaxRedVals * kMaxBlocks));
-  unsigned* ticket = static_cast<unsigned*>(c.take(256));
+  unsigned* ticket = static_cast<unsigned*>(c.take(kTicketBytes));
   double* scal = static_cast<double*>(c.take(sizeof(double) * NSCAL));
   if (out) *out = KernelWs{pp, gp, part, ticket, scal};
   return c.off + 256;
@@ -817,7 +817,7 @@ static KernelWs kernel_setup(int dtype, int64_t m, int64_t n, int64_t l, void* w
   if (reinterpret_cast<uintptr_t>(ws) & 255) throw Error{GLX_E_WORKSPACE, "workspace must be 256-byte aligned"};
   KernelWs k;
   kernel_ws(es, *plan, ws, &k);
-  GLX_HIP(hipMemsetAsync(k.ticket, 0, 256, st));
+  GLX_HIP(hipMemsetAsync(k.ticket, 0, kTicketBytes, st));
   return k;
 }
 

@@ -31,7 +31,7 @@ SHAPES = [
 
 @pytest.mark.parametrize("dtype", ["f64", "f32"])
 @pytest.mark.parametrize("shape", SHAPES)
-@pytest.mark.parametrize("variant", [0, 2, 3])
+@pytest.mark.parametrize("variant", [0, 2, 3, 21420, 41210])
 def test_residual_and_gradient(shape, dtype, variant):
     k = _glx()
     m, n, l = shape
