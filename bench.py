@@ -9,12 +9,17 @@ N > 1 (launched by torch.distributed.run, one process per GPU): A and b are row-
 gradient is summed with RCCL, and the same global problem is solved (strong scaling); the
 reported value is iterations/s of the whole job (max of the per-rank times).
 
-Also reported, for the dominant kernel (A@x, launched every line-search trial):
-  roofline — algorithmic bytes (A streamed once + x, b, r: s*(m n + (m+n) l)) / average launch
-             time from HIP events recorded on the solver's stream over the timed region; peak
-             8 TB/s (MI355X HBM3E); `traffic` = HBM bytes per launch from rocprofv3 PMC
-             (profiles/pmc_traffic.json, 2*FETCH_SIZE + WRITE_SIZE per the gfx950 correction) when
-             that file holds the same config, else null;
+Also reported, for the dominant kernel (A@x with its batched right-hand sides, ~55-60% of the
+iteration):
+  roofline — the kernel's bound is whichever of MFMA time (flops / dense MFMA peak) and HBM time
+             (bytes / 8 TB/s) is larger for this (m, n, l, dtype): with l = 32 and two right-hand
+             sides it is MFMA-bound in fp64 and fp32 (BASELINE.json's metric is the MFMA roofline
+             %), with l = 1 (SGD) HBM-bound. achieved = algorithmic flops 2*m*n*l*rhs (or bytes
+             s*(m n + (m+n) l rhs)) per launch / average launch time from HIP events recorded on
+             the solver's stream over the timed region. `pair_frac` is the same fraction for the
+             A@x + A^T r pair (the north-star target). `traffic` = HBM bytes per launch from
+             rocprofv3 PMC (profiles/pmc_traffic.json, 2*FETCH_SIZE + WRITE_SIZE per the gfx950
+             correction) when that file holds the same config, else null;
   cpu_baseline — the repo's NumPy oracle (oracle/numpy_ref.py) on the host cores, on a bounded
              sample of the same instance (rank 0, N = 1 only).
 """
@@ -191,18 +196,28 @@ def main():
         atr_flops = 2.0 * ml * n * l
         ach = ax_bytes / ax_avg_s / 1e9 if ax_n else None
         cfg_key = "%s_%s_%dx%dx%d_g%d" % (args.method, args.dtype, m, n, l, world)
-        roof = {"bound": "hbm", "achieved": ach, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                "frac": (ach / HBM_PEAK_GBS) if ach else None, "traffic": pmc_traffic(cfg_key),
-                "kernel": "A@x (k_ax_mfma)", "bytes_per_launch": ax_bytes,
-                "avg_launch_us": ax_avg_s * 1e6, "launches": ax_n,
-                "mfma_tflops": ax_flops / ax_avg_s / 1e12 if ax_n else None,
-                "mfma_frac": (ax_flops / ax_avg_s / 1e12) / MFMA_PEAK_TFS[args.dtype] if ax_n else None,
-                "rhs_per_launch": nsrc,
+        peak_tf = MFMA_PEAK_TFS[args.dtype]
+        mfma_bound = ax_flops / (peak_tf * 1e12) >= ax_bytes / (HBM_PEAK_GBS * 1e9)
+        ax_tf = ax_flops / ax_avg_s / 1e12 if ax_n else None
+        ax_gbs = ax_bytes / ax_avg_s / 1e9 if ax_n else None
+        pair_tf = ((ax_flops + atr_flops) / (ax_avg_s + atr_avg_s) / 1e12) if (ax_n and atr_n) else None
+        if mfma_bound:
+            ach, peak, unit = ax_tf, peak_tf, "TFLOP/s"
+        else:
+            ach, peak, unit = ax_gbs, HBM_PEAK_GBS, "GB/s"
+        roof = {"bound": "mfma" if mfma_bound else "hbm", "achieved": ach, "peak": peak,
+                "unit": unit, "frac": (ach / peak) if ach else None,
+                "traffic": pmc_traffic(cfg_key),
+                "kernel": "A@x (k_ax_mfma)", "flops_per_launch": ax_flops,
+                "bytes_per_launch": ax_bytes, "avg_launch_us": ax_avg_s * 1e6, "launches": ax_n,
+                "rhs_per_launch": nsrc, "hbm_GBs": ax_gbs, "hbm_frac": ax_gbs / HBM_PEAK_GBS if ax_n else None,
+                "mfma_tflops": ax_tf, "mfma_frac": ax_tf / peak_tf if ax_n else None,
                 "atr_avg_launch_us": atr_avg_s * 1e6,
                 "atr_GBs": atr_bytes / atr_avg_s / 1e9 if atr_n else None,
-                "atr_mfma_frac": (atr_flops / atr_avg_s / 1e12) / MFMA_PEAK_TFS[args.dtype] if atr_n else None,
-                "pair_mfma_frac": ((ax_flops + atr_flops) / (ax_avg_s + atr_avg_s) / 1e12) / MFMA_PEAK_TFS[args.dtype]
-                if (ax_n and atr_n) else None}
+                "atr_mfma_frac": (atr_flops / atr_avg_s / 1e12) / peak_tf if atr_n else None,
+                "pair_tflops": pair_tf, "pair_frac": pair_tf / peak_tf if pair_tf else None,
+                # all MFMA flops issued in the timed region / its wall time (gaps, prox included)
+                "iter_frac": (ax_n * ax_flops + atr_n * atr_flops) / elapsed / 1e12 / peak_tf}
         steps = max(1, done)
         line = {
             "metric": METRIC, "value": steps / elapsed, "unit": "iters/s", "n_gpus": world,

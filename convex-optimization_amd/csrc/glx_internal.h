@@ -47,6 +47,10 @@ struct GemmPlan {
   int ax_xmap;      // MFMA: group K splits by XCD (L2 locality of X)
   int ax_lb;        // VALU: column block width (1,2,4,8); ax_ncb = ceil(l / ax_lb)
   int ax_vec;       // VALU: 16-byte loads
+  // per number of batched right-hand sides (index 1..3; [1] mirrors ax_code / ax_S):
+  // MFMA variant code (kind 5 = X staged in LDS: 5 MT PF VPL WAVES) and its K split
+  int axb_code[4];
+  int axb_S[4];
   // A^T R  ->  Gp[atr_S][n][l]
   int atr_kind;     // 1 = MFMA, 3 = VALU
   int atr_wl, atr_pf; // MFMA: wave layout (0 = waves split rows, 1 = waves split columns), ring depth
@@ -56,10 +60,19 @@ struct GemmPlan {
 };
 
 GemmPlan make_plan(int esize, int64_t m, int64_t n, int64_t l, int ax_variant);
+// K split (number of partial slabs per source) of an A@X launch with nsrc right-hand sides
+inline int ax_split(const GemmPlan& p, int nsrc) { return nsrc > 1 ? p.axb_S[nsrc] : p.ax_S; }
+inline int ax_split_max(const GemmPlan& p) {
+  int s = p.ax_S;
+  for (int k = 2; k <= 3; ++k) s = s > p.axb_S[k] ? s : p.axb_S[k];
+  return s;
+}
+// largest K split any A@X variant (single or batched) plans for this shape
+int max_ax_split(int esize, int64_t m, int64_t n, int64_t l);
 
 // ---- dense products (kernels_gemm.hip) ----
 // A @ [X[0] | .. | X[nsrc-1]] (nsrc <= 3, each n x l) in one pass over A: partial slabs
-// P[src][ax_S][m][l]; skipped entirely unless gate == NULL or *gate == epoch.
+// P[src][ax_split(p, nsrc)][m][l]; skipped entirely unless gate == NULL or *gate == epoch.
 template <typename T>
 void launch_ax(const GemmPlan& p, int nsrc, const T* A, const T* const* X, T* P, const int* gate,
                int epoch, hipStream_t st);

@@ -257,6 +257,187 @@ __global__ __launch_bounds__(256) void k_ax_mfma(const T* __restrict__ A, const 
 }
 
 // ------------------------------------------------------------------------------------------
+// A @ X with X staged through LDS (kind 5). A block of WAVES waves walks ONE K range; wave w
+// owns rows row0 + 16*MT*w .. +16*MT, so there is no cross-wave reduction. Each K chunk of X
+// (CK rows x 16NT columns per source, 8 KiB at l = 32 with two sources) is loaded from L2 once
+// per block, one 16-B vector per thread, and kept in LDS in its natural [k][column] order with
+// a padded row of LP = L + 4 (f64) / L + 2 (f32) elements: the MFMA B-operand reads (lane
+// (i, q) <- X[q*EL + e][16nt + i], ds_read_b64 / _b32) and the staging stores (ds_write_b128,
+// or 2 x _b64 when the f32 row is not 16-B aligned) are then free of bank conflicts under the
+// CDNA4 LDS lane-group model (MI355X_MICROARCH.md §LDS; checked with a small simulator).
+// Compared with kind 1/2 (every wave gathers its own X chunk into registers) this cuts the
+// L2->CU traffic of X by WAVES and frees the X register ring: the f64 2-RHS tile fits 2 waves
+// per SIMD. Pipeline per chunk c: issue X(c+PF) and A(c+PF) (register rings), write X(c+1) to
+// the other LDS slot, read X(c) from this slot, MFMAs, one barrier. A is read exactly once.
+// ------------------------------------------------------------------------------------------
+// one 16-B X vector into LDS: a b128 store, or two 8-B stores when the row is only 8-B aligned
+template <typename T, bool W16>
+__device__ inline void lds_put(T* dst, typename MF<T>::vec_t v) {
+  typedef typename MF<T>::vec_t V;
+  if constexpr (W16) {
+    *reinterpret_cast<V*>(dst) = v;
+  } else {
+    typedef T h2 __attribute__((ext_vector_type(2)));
+    constexpr int E = MF<T>::E;
+#pragma unroll
+    for (int h = 0; h < E / 2; ++h) *reinterpret_cast<h2*>(dst + 2 * h) = h2{v[2 * h], v[2 * h + 1]};
+  }
+}
+
+template <typename T, int MT, int NT, int NSRC, int PF, int VPL, int WAVES>
+__global__ __launch_bounds__(64 * WAVES) void k_ax_lds(const T* __restrict__ A,
+                                                      const T* __restrict__ X0,
+                                                      const T* __restrict__ X1,
+                                                      const T* __restrict__ X2,
+                                                      T* __restrict__ P, int64_t m, int64_t n,
+                                                      int64_t chunks, int S, int gx, int xmap,
+                                                      const int* __restrict__ gate, int epoch) {
+  typedef MF<T> M;
+  typedef typename M::vec_t V;
+  typedef typename M::acc_t C;
+  constexpr int E = M::E;
+  constexpr int EL = VPL * E;             // k per lane per chunk
+  constexpr int CK = 4 * EL;              // k per chunk
+  constexpr int L = 16 * NT;              // == l
+  constexpr int NC = NT * NSRC;
+  constexpr int LP = L + (sizeof(T) == 8 ? 4 : 2);   // padded LDS row (see header)
+  constexpr bool W16 = (LP * sizeof(T)) % 16 == 0;    // rows 16-B aligned: one b128 store
+  constexpr int XCH = NSRC * CK * LP;     // elements of one staged chunk
+  constexpr int NTHR = 64 * WAVES;
+  constexpr int XV = NSRC * CK * L / E;   // 16-B vectors of X per chunk
+  constexpr int XPT = (XV + NTHR - 1) / NTHR;
+  constexpr int VPR = L / E;              // vectors per X row
+  static_assert(PF >= 2, "X(c+1) must sit in another ring slot than X(c + PF)");
+  __shared__ __attribute__((aligned(16))) T xs[2][XCH];
+  if (!gate_live(gate, epoch)) return;
+  int bx, by;
+  if (!ax_block(xmap, gx, S, bx, by)) return;
+
+  const int lane = threadIdx.x & 63;
+  const int wave = threadIdx.x >> 6;
+  const int i = lane & 15, q = lane >> 4;
+  const int64_t row0 = (int64_t)bx * (16 * MT * WAVES) + (int64_t)wave * (16 * MT);
+  const int64_t cb = chunks * by / S, ce = chunks * (by + 1) / S;
+  if (cb >= ce) return;   // block-uniform
+
+  const T* ap[MT];
+#pragma unroll
+  for (int mt = 0; mt < MT; ++mt) {
+    int64_t r = row0 + mt * 16 + i;
+    r = r < m ? r : m - 1;
+    ap[mt] = A + r * n + cb * CK + (int64_t)q * EL;
+  }
+  // X staging: thread t moves vectors t, t + NTHR, ... of the chunk (src, k, column vector)
+  const T* xg[XPT];
+  int xo[XPT];
+  bool xon[XPT];
+#pragma unroll
+  for (int j = 0; j < XPT; ++j) {
+    const int v = threadIdx.x + NTHR * j;
+    xon[j] = v < XV;
+    const int vv = xon[j] ? v : 0;
+    const int src = vv / (CK * VPR), rem = vv % (CK * VPR);
+    const int k = rem / VPR, c = (rem % VPR) * E;
+    const T* xb = src == 0 ? X0 : (src == 1 ? X1 : X2);
+    xg[j] = xb + (cb * CK + k) * L + c;
+    xo[j] = src * CK * LP + k * LP + c;
+  }
+
+  C acc[MT][NC];
+#pragma unroll
+  for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+    for (int c = 0; c < NC; ++c) acc[mt][c] = C{};
+
+  V a[PF][MT][VPL];
+  V xr[PF][XPT];
+#pragma unroll
+  for (int p = 0; p < PF; ++p) {
+    if (cb + p < ce) {
+#pragma unroll
+      for (int j = 0; j < XPT; ++j)
+        if (xon[j]) xr[p][j] = *reinterpret_cast<const V*>(xg[j] + (int64_t)p * CK * L);
+#pragma unroll
+      for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+        for (int v = 0; v < VPL; ++v) a[p][mt][v] = load_vec<T, false>(ap[mt] + p * CK + v * E);
+    }
+  }
+  // chunk cb -> slot 0
+#pragma unroll
+  for (int j = 0; j < XPT; ++j)
+    if (xon[j]) lds_put<T, W16>(&xs[0][xo[j]], xr[0][j]);
+  __syncthreads();
+
+  for (int64_t c0 = cb; c0 < ce; c0 += PF) {
+#pragma unroll
+    for (int p = 0; p < PF; ++p) {
+      const int64_t c = c0 + p;
+      if (c < ce) {
+        const int slot = (int)((c - cb) & 1);
+        V av[MT][VPL];
+#pragma unroll
+        for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+          for (int v = 0; v < VPL; ++v) av[mt][v] = a[p][mt][v];
+        V xn[XPT];   // X(c+1), loaded PF-1 chunks ago
+        const int pn = (p + 1) % PF;
+#pragma unroll
+        for (int j = 0; j < XPT; ++j) xn[j] = xr[pn][j];
+        if (c + PF < ce) {   // refill this ring slot with chunk c + PF (X first: see header)
+          const int64_t off = c + PF - cb;
+#pragma unroll
+          for (int j = 0; j < XPT; ++j)
+            if (xon[j]) xr[p][j] = *reinterpret_cast<const V*>(xg[j] + off * CK * L);
+#pragma unroll
+          for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+            for (int v = 0; v < VPL; ++v) a[p][mt][v] = load_vec<T, false>(ap[mt] + off * CK + v * E);
+        }
+        if (c + 1 < ce) {
+#pragma unroll
+          for (int j = 0; j < XPT; ++j)
+            if (xon[j]) lds_put<T, W16>(&xs[slot ^ 1][xo[j]], xn[j]);
+        }
+        T xv[NC][EL];
+#pragma unroll
+        for (int cc = 0; cc < NC; ++cc) {
+          const int src = cc / NT, nt = cc % NT;
+          const T* xp = &xs[slot][src * CK * LP + q * EL * LP + nt * 16 + i];
+#pragma unroll
+          for (int e = 0; e < EL; ++e) xv[cc][e] = xp[e * LP];
+        }
+#pragma unroll
+        for (int v = 0; v < VPL; ++v)
+#pragma unroll
+          for (int e = 0; e < E; ++e)
+#pragma unroll
+            for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+              for (int cc = 0; cc < NC; ++cc)
+                acc[mt][cc] = M::mma(av[mt][v][e], xv[cc][v * E + e], acc[mt][cc]);
+        __syncthreads();
+      }
+    }
+  }
+
+#pragma unroll
+  for (int sr = 0; sr < NSRC; ++sr) {
+    T* pout = P + ((int64_t)sr * S + by) * m * L;
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int64_t row = row0 + mt * 16 + M::row(lane, r);
+        if (row < m) {
+#pragma unroll
+          for (int nt = 0; nt < NT; ++nt) pout[row * L + nt * 16 + i] = acc[mt][sr * NT + nt][r];
+        }
+      }
+  }
+}
+
+// ------------------------------------------------------------------------------------------
 // A^T R on MFMA: a wave owns 64 columns of A (= 64 rows of G) x NT 16-col tiles of G.
 //   WL = 0: a block = one 64-column panel, its 4 waves split the block's rows (LDS-reduced);
 //   WL = 1: a block = four adjacent panels (256 columns) sharing one row range, so the four
@@ -538,14 +719,33 @@ static int env_int(const char* name, int dflt) {
 
 // Defaults chosen by the sweep in scripts/kbench.py on MI355X.
 // ax code: kind*1000 + MT*100 + PF*10 + NTL (kind 1 = direct row loads, 2 = quad + bpermute).
-static constexpr int kAxDefault = 21820;   // f64: VPL 2, direct loads, MT 8, PF 2
-static constexpr int kAxDefault32 = 21410; // f32: VPL 2, direct loads, MT 4, PF 1
-static constexpr int kAtrDefault = 102;
-// batched right-hand sides (MFMA-bound at l = 32): f64 1420 / f32 1430 (2 RHS), 1220 (3 RHS)
+// kind 5 (X staged in LDS) code: 5 MT PF VPL WAVES. Kind-5 defaults fall back to the register
+// tiles below when the shape does not fit them (l not 16/32, n not a multiple of 4*E*VPL).
+static constexpr int kAxDefault = 52228;       // f64 single RHS: LDS, MT 2, PF 2, VPL 2, 8 waves
+static constexpr int kAxFallback = 21820;      // f64: VPL 2, direct loads, MT 8, PF 2
+static constexpr int kAxDefault32 = 21410;     // f32: VPL 2, direct loads, MT 4, PF 1
+static constexpr int kAtrDefault = 102;        // WL = 0, PF = 2 (+1000: non-temporal A loads)
+// batched right-hand sides (MFMA-bound at l = 32, both dtypes): the LDS tile, 2 waves per SIMD
 static int axb_default(int nsrc, int esize) {
-  if (nsrc == 3) return 1220;
-  return esize == 8 ? 21420 : 21410;
-}   // WL = 0, PF = 2 (+1000: non-temporal A loads)
+  (void)nsrc; (void)esize;
+  return 52224;
+}
+
+static constexpr int kLdsCodes[] = {52224, 52324, 52228, 54224, 52214, 54214};
+static bool lds_code_ok(int c, int64_t n, int64_t l, int esize) {
+  bool known = false;
+  for (int k : kLdsCodes) known |= (k == c);
+  if (!known) return false;
+  const int E = 16 / esize, vpl = (c / 10) % 10;
+  return (l == 16 || l == 32) && n % (4 * E * vpl) == 0;
+}
+// K split of a kind-5 launch: enough blocks for 2 (4-wave) blocks per CU
+static int lds_split(int esize, int64_t m, int64_t n, int code) {
+  const int E = 16 / esize, mt = (code / 1000) % 10, vpl = (code / 10) % 10, waves = code % 10;
+  const int64_t rb = cdiv(m, 16 * mt * waves), chunks = n / (4 * E * vpl);
+  const int64_t target = env_int("GLX_AXL_BLOCKS", waves == 8 ? 256 : 512);
+  return (int)clampi(cdiv(target, rb), 1, std::max<int64_t>(1, std::min<int64_t>(kMaxSplit, chunks / 8)));
+}
 
 static bool valid_ax_code(int c) {
   switch (c) {
@@ -578,10 +778,17 @@ GemmPlan make_plan(int esize, int64_t m, int64_t n, int64_t l, int ax_variant) {
     const int64_t waves = cdiv(m, 4);                    // RW = 4 rows per wave
     const int64_t kunits = n / (64 * (p.ax_vec ? E : 1)); // 64-lane strides per row
     p.ax_S = (int)clampi(cdiv(kTargetWaves, waves), 1, std::max<int64_t>(1, std::min<int64_t>(kMaxSplit, kunits / 4)));
+  } else if (lds_code_ok(ax_variant ? ax_variant : (esize == 8 ? kAxDefault : kAxDefault32), n, l, esize)) {
+    const int code = ax_variant ? ax_variant : (esize == 8 ? kAxDefault : kAxDefault32);
+    p.ax_code = code;
+    p.ax_kind = 5;
+    p.ax_mt = (code / 1000) % 10;
+    p.ax_pf = (code / 100) % 10;
+    p.ax_S = lds_split(esize, m, n, code);
   } else {
-    int code = valid_ax_code(ax_variant) ? ax_variant : (esize == 8 ? kAxDefault : kAxDefault32);
+    int code = valid_ax_code(ax_variant) ? ax_variant : (esize == 8 ? kAxFallback : kAxDefault32);
     int vpl = code / 10000 ? code / 10000 : 1;
-    if (n % (4 * E * vpl) != 0) { code = kAxDefault; vpl = 1; }   // wider chunks need n % 4*E*VPL
+    if (n % (4 * E * vpl) != 0) { code = 1820; vpl = 1; }   // wider chunks need n % 4*E*VPL
     p.ax_code = code;
     p.ax_kind = (code / 1000) % 10;
     p.ax_mt = (code / 100) % 10;
@@ -596,6 +803,25 @@ GemmPlan make_plan(int esize, int64_t m, int64_t n, int64_t l, int ax_variant) {
   const int s_ax = env_int("GLX_AX_S", 0);
   if (s_ax > 0) p.ax_S = (int)std::min<int64_t>(s_ax, kMaxSplit);
   p.ax_xmap = env_int("GLX_AX_XCD", 1);
+  // batched right-hand sides
+  p.axb_code[0] = p.axb_code[1] = p.ax_code;
+  p.axb_S[0] = p.axb_S[1] = p.ax_S;
+  for (int ns = 2; ns <= 3; ++ns) {
+    int code = env_int("GLX_AXB_VARIANT", axb_default(ns, esize));
+    int S = p.ax_S;
+    if (p.ax_kind == 3) {
+      code = 0;
+    } else if (code / 10000 == 5) {
+      if (lds_code_ok(code, n, l, esize)) S = lds_split(esize, m, n, code);
+      else code = ns == 2 ? 1420 : 1220;
+    } else if (code >= 10000 && n % (4 * E * (code / 10000)) != 0) {
+      code = ns == 2 ? 1420 : 1220;
+    }
+    const int s_axb = env_int("GLX_AXB_S", 0);
+    if (s_axb > 0 && code / 10000 == 5) S = (int)std::min<int64_t>(s_axb, kMaxSplit);
+    p.axb_code[ns] = code;
+    p.axb_S[ns] = S;
+  }
   // ---- A^T R ----
   int atr_code = env_int("GLX_ATR_VARIANT", 0);
   if (atr_code == 0) atr_code = esize == 8 ? kAtrDefault : 1102;   // f32: non-temporal A wins
@@ -631,6 +857,13 @@ GemmPlan make_plan(int esize, int64_t m, int64_t n, int64_t l, int ax_variant) {
   const int s_atr = env_int("GLX_ATR_S", 0);
   if (s_atr > 0) p.atr_S = (int)std::min<int64_t>(s_atr, kMaxSplit);
   return p;
+}
+
+int max_ax_split(int esize, int64_t m, int64_t n, int64_t l) {
+  int s = 1;
+  for (int v : {0, 3, 1220, 1410, 1820}) s = std::max(s, ax_split_max(make_plan(esize, m, n, l, v)));
+  for (int v : kLdsCodes) s = std::max(s, ax_split_max(make_plan(esize, m, n, l, v)));
+  return s;
 }
 
 template <typename T, int LB, int NSRC>
@@ -670,13 +903,43 @@ static void ax_mfma_go(const GemmPlan& p, const T* A, const T* const* X, T* P, c
                      epoch);
 }
 
+template <typename T, int NT, int NSRC, int MT, int PF, int VPL, int WAVES>
+static void ax_lds_go(const GemmPlan& p, int S, const T* A, const T* const* X, T* P,
+                      const int* gate, int epoch, hipStream_t st) {
+  constexpr int E = 16 / sizeof(T);
+  const int gx = (int)cdiv(p.m, 16 * MT * WAVES);
+  const int xmap = (p.ax_xmap && ax_xmap_ok(S)) ? 1 : 0;
+  hipLaunchKernelGGL((k_ax_lds<T, MT, NT, NSRC, PF, VPL, WAVES>), dim3((unsigned)ax_grid(xmap, gx, S)),
+                     dim3(64 * WAVES), 0, st, A, X[0], X[1], X[2], P, p.m, p.n,
+                     p.n / (4 * VPL * E), S, gx, xmap, gate, epoch);
+}
+
+// kind 5 codes: 5 MT PF VPL WAVES
+template <typename T, int NT, int NSRC>
+static void ax_lds_code(const GemmPlan& p, int code, int S, const T* A, const T* const* X, T* P,
+                        const int* gate, int epoch, hipStream_t st) {
+  switch (code) {
+    case 52324: ax_lds_go<T, NT, NSRC, 2, 3, 2, 4>(p, S, A, X, P, gate, epoch, st); break;
+    case 52228: ax_lds_go<T, NT, NSRC, 2, 2, 2, 8>(p, S, A, X, P, gate, epoch, st); break;
+    case 54224: ax_lds_go<T, NT, NSRC, 4, 2, 2, 4>(p, S, A, X, P, gate, epoch, st); break;
+    case 52214: ax_lds_go<T, NT, NSRC, 2, 2, 1, 4>(p, S, A, X, P, gate, epoch, st); break;
+    case 54214: ax_lds_go<T, NT, NSRC, 4, 2, 1, 4>(p, S, A, X, P, gate, epoch, st); break;
+    default: ax_lds_go<T, NT, NSRC, 2, 2, 2, 4>(p, S, A, X, P, gate, epoch, st); break;   // 52224
+  }
+}
+
 // One source: the swept variant. Batched sources (2, 3) use fixed register-feasible tiles.
 template <typename T, int NT>
 static void ax_mfma_nt(const GemmPlan& p, int nsrc, const T* A, const T* const* X, T* P,
                        const int* gate, int epoch, hipStream_t st) {
+  const int code = p.axb_code[nsrc];
+  if (code / 10000 == 5) {
+    if (nsrc == 1) ax_lds_code<T, NT, 1>(p, code, p.axb_S[1], A, X, P, gate, epoch, st);
+    else if (nsrc == 2) ax_lds_code<T, NT, 2>(p, code, p.axb_S[2], A, X, P, gate, epoch, st);
+    else ax_lds_code<T, NT, 3>(p, code, p.axb_S[3], A, X, P, gate, epoch, st);
+    return;
+  }
   if (nsrc == 2) {
-    int code = env_int("GLX_AXB_VARIANT", axb_default(2, (int)sizeof(T)));
-    if (code >= 10000 && p.n % (4 * (16 / (int)sizeof(T)) * (code / 10000)) != 0) code = 1420;
     switch (code) {
       case 1220: ax_mfma_go<T, NT, 2, 2, 2, false, false>(p, A, X, P, gate, epoch, st); break;
       case 1420: ax_mfma_go<T, NT, 2, 4, 2, false, false>(p, A, X, P, gate, epoch, st); break;
@@ -694,7 +957,7 @@ static void ax_mfma_nt(const GemmPlan& p, int nsrc, const T* A, const T* const* 
     return;
   }
   if (nsrc == 3) {
-    switch (env_int("GLX_AXB_VARIANT", axb_default(3, (int)sizeof(T)))) {
+    switch (code) {
       case 2220: ax_mfma_go<T, NT, 3, 2, 2, true, false>(p, A, X, P, gate, epoch, st); break;
       case 2230: ax_mfma_go<T, NT, 3, 2, 3, true, false>(p, A, X, P, gate, epoch, st); break;
       default: ax_mfma_go<T, NT, 3, 2, 2, false, false>(p, A, X, P, gate, epoch, st); break;

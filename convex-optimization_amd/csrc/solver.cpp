@@ -119,7 +119,7 @@ class Session : public SessionBase {
     for (int i = 0; i < kRes; ++i) res[i] = static_cast<T*>(c.take(sizeof(T) * ml));
     T* g = static_cast<T*>(c.take(sizeof(T) * nl));
     T* gp = plan.atr_S > 1 ? static_cast<T*>(c.take(sizeof(T) * nl * plan.atr_S)) : g;
-    T* pp = static_cast<T*>(c.take(sizeof(T) * ml * plan.ax_S * 3));   // up to 3 batched sources
+    T* pp = static_cast<T*>(c.take(sizeof(T) * ml * ax_split_max(plan) * 3));   // up to 3 batched sources
     double* scal = static_cast<double*>(c.take(sizeof(double) * NSCAL));
     double* part = static_cast<double*>(c.take(sizeof(double) * kMaxRedVals * kMaxBlocks));
     unsigned* ticket = static_cast<unsigned*>(c.take(kTicketBytes));
@@ -295,7 +295,7 @@ class Session : public SessionBase {
     if (O_.profile) { GLX_HIP(hipEventRecord(e1, st_)); ev_[0].push_back({e0, e1}); }
     ++ax_calls_;
     ax_cols_ += nsrc;
-    launch_finalize_residual<T>(Pp_, plan_.ax_S, B_, nsrc, rs, ml_, nullptr, 0, 1, cx,
+    launch_finalize_residual<T>(Pp_, ax_split(plan_, nsrc), B_, nsrc, rs, ml_, nullptr, 0, 1, cx,
                                 cx ? nl_ : 0, cmax, comm_ ? nullptr : fh, fh_mu, scal_ + S_DRN,
                                 red(slot), st_);
     check_launch();
@@ -679,12 +679,8 @@ static size_t kernel_ws(int es, const GemmPlan& p, void* base, KernelWs* out) {
   Carver c(base);
   // room for the largest split any variant of this shape plans (MFMA tiles, VALU)
   int64_t s_ax = 1, s_atr = 1;
-  for (int v : {0, 3, 1220, 1410, 1820}) {
-    const GemmPlan q = make_plan(es, p.m, p.n, p.l, v);
-    s_ax = std::max<int64_t>(s_ax, q.ax_S);
-    s_atr = std::max<int64_t>(s_atr, q.atr_S);
-  }
-  s_ax = std::max<int64_t>(s_ax, p.ax_S);
+  for (int v : {0, 3}) s_atr = std::max<int64_t>(s_atr, make_plan(es, p.m, p.n, p.l, v).atr_S);
+  s_ax = std::max<int64_t>(max_ax_split(es, p.m, p.n, p.l), ax_split_max(p));
   s_atr = std::max<int64_t>(s_atr, p.atr_S);
   void* pp = c.take((size_t)es * p.m * p.l * s_ax * 3);
   void* gp = c.take((size_t)es * p.n * p.l * s_atr);
@@ -865,14 +861,14 @@ int glx_residual_batch(int dtype, int64_t m, int64_t n, int64_t l, const void* A
       double* rs[3] = {nullptr, nullptr, nullptr};
       for (int i = 0; i < nsrc; ++i) { xs[i] = (const double*)X[i]; rs[i] = (double*)R[i]; }
       launch_ax<double>(p, nsrc, (const double*)A, xs, (double*)k.pp, nullptr, 0, st);
-      launch_finalize_residual<double>((const double*)k.pp, p.ax_S, (const double*)B, nsrc, rs, m * l,
+      launch_finalize_residual<double>((const double*)k.pp, ax_split(p, nsrc), (const double*)B, nsrc, rs, m * l,
                                        nullptr, 0, 1, nullptr, 0, nullptr, nullptr, 0.0, nullptr, r, st);
     } else {
       const float* xs[3] = {nullptr, nullptr, nullptr};
       float* rs[3] = {nullptr, nullptr, nullptr};
       for (int i = 0; i < nsrc; ++i) { xs[i] = (const float*)X[i]; rs[i] = (float*)R[i]; }
       launch_ax<float>(p, nsrc, (const float*)A, xs, (float*)k.pp, nullptr, 0, st);
-      launch_finalize_residual<float>((const float*)k.pp, p.ax_S, (const float*)B, nsrc, rs, m * l,
+      launch_finalize_residual<float>((const float*)k.pp, ax_split(p, nsrc), (const float*)B, nsrc, rs, m * l,
                                       nullptr, 0, 1, nullptr, 0, nullptr, nullptr, 0.0, nullptr, r, st);
     }
     check_launch();

@@ -1,6 +1,6 @@
 set -o pipefail
 cd $GRAFT_REPO_ROOT && export TMPDIR=/tmp
-O=gpurun_out/r10; mkdir -p $O
+O=gpurun_out/r17; mkdir -p $O
 timeout -k 10 300 python -m pytest tests/test_gpu_kernels.py tests/test_gpu_comm.py -m gpu -q --maxfail=5 > $O/pytest_kernels.log 2>&1 ; echo "kernels rc=$?" >> $O/status.txt
 timeout -k 10 600 python -m pytest tests/test_gpu_parity.py -m gpu -q --maxfail=20 > $O/pytest_parity.log 2>&1 ; echo "parity rc=$?" >> $O/status.txt
 tail -3 $O/pytest_kernels.log; tail -3 $O/pytest_parity.log

@@ -72,6 +72,7 @@ def main():
             for S in [int(s) for s in args.splits.split(",")]:
                 os.environ["GLX_AXB_VARIANT"] = str(v)
                 os.environ["GLX_AX_S"] = str(S)
+                os.environ["GLX_AXB_S"] = str(S)   # kind-5 (LDS) tiles take their own split
                 Rs, _ = kernels.residual_batch(A, Xs, B)
                 err = max(float((r.double() - rf).abs().max() / rf.abs().max()) for r, rf in zip(Rs, refs))
                 t = timeit(lambda: kernels.residual_batch(A, Xs, B), args.reps)
@@ -80,6 +81,7 @@ def main():
                                   "TFs": 2.0 * m * n * l * nsrc / t / 1e12, "relerr": err,
                                   "dtype": args.dtype, "shape": [m, n, l]}), flush=True)
     os.environ["GLX_AX_S"] = "0"
+    os.environ["GLX_AXB_S"] = "0"
     for v in [int(s) for s in args.atr.split(",")]:
         for S in [int(s) for s in args.splits.split(",")]:
             os.environ["GLX_ATR_VARIANT"] = str(v)
