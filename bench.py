@@ -101,6 +101,17 @@ def cpu_baseline(method, A, b, x0, mu, opts, budget_s=15.0):
                       "%.1f s; BLAS %s" % (method, k, maxit, dt, blas)}
 
 
+def ax_kernel_name(dtype, m, n, l, nsrc):
+    """The A@X tile libglx launched for this shape and right-hand-side count (its own planner)."""
+    from glx import _lib
+    desc = _lib.plan_describe(_lib.GLX_F64 if dtype == "f64" else _lib.GLX_F32, m, n, l)
+    key = "ax%d=" % max(1, min(3, int(round(nsrc))))
+    for part in desc.split("; "):
+        if part.startswith(key):
+            return "A@X: " + part[len(key):]
+    return desc
+
+
 def pmc_traffic(cfg_key):
     path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
     try:
@@ -208,7 +219,7 @@ def main():
         roof = {"bound": "mfma" if mfma_bound else "hbm", "achieved": ach, "peak": peak,
                 "unit": unit, "frac": (ach / peak) if ach else None,
                 "traffic": pmc_traffic(cfg_key),
-                "kernel": "A@x (k_ax_mfma)", "flops_per_launch": ax_flops,
+                "kernel": ax_kernel_name(args.dtype, ml, n, l, nsrc), "flops_per_launch": ax_flops,
                 "bytes_per_launch": ax_bytes, "avg_launch_us": ax_avg_s * 1e6, "launches": ax_n,
                 "rhs_per_launch": nsrc, "hbm_GBs": ax_gbs, "hbm_frac": ax_gbs / HBM_PEAK_GBS if ax_n else None,
                 "mfma_tflops": ax_tf, "mfma_frac": ax_tf / peak_tf if ax_n else None,

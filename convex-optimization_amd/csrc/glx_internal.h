@@ -69,6 +69,8 @@ inline int ax_split_max(const GemmPlan& p) {
 }
 // largest K split any A@X variant (single or batched) plans for this shape
 int max_ax_split(int esize, int64_t m, int64_t n, int64_t l);
+// one-line description of the kernels and splits a plan launches (glx_plan_describe)
+std::string describe_plan(const GemmPlan& p);
 
 // ---- dense products (kernels_gemm.hip) ----
 // A @ [X[0] | .. | X[nsrc-1]] (nsrc <= 3, each n x l) in one pass over A: partial slabs

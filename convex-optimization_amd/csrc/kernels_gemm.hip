@@ -26,7 +26,9 @@
 // summed through LDS in a fixed order, and workgroups along gridDim.y write partial slabs that
 // the consumer sums in slab order — the result is deterministic run to run.
 #include <algorithm>
+#include <cstdio>
 #include <cstdlib>
+#include <string>
 
 #include "glx_internal.h"
 
@@ -857,6 +859,33 @@ GemmPlan make_plan(int esize, int64_t m, int64_t n, int64_t l, int ax_variant) {
   const int s_atr = env_int("GLX_ATR_S", 0);
   if (s_atr > 0) p.atr_S = (int)std::min<int64_t>(s_atr, kMaxSplit);
   return p;
+}
+
+static std::string ax_name(const GemmPlan& p, int nsrc) {
+  const int code = p.axb_code[nsrc];
+  char buf[128];
+  if (p.ax_kind == 3 || code == 0) {
+    std::snprintf(buf, sizeof buf, "k_ax_valu<LB%d,VEC%d> S=%d", p.ax_lb, p.ax_vec, ax_split(p, nsrc));
+  } else if (code / 10000 == 5) {
+    std::snprintf(buf, sizeof buf, "k_ax_lds<MT%d,PF%d,VPL%d,W%d> S=%d", (code / 1000) % 10,
+                  (code / 100) % 10, (code / 10) % 10, code % 10, ax_split(p, nsrc));
+  } else {
+    const int vpl = code / 10000 ? code / 10000 : 1;
+    std::snprintf(buf, sizeof buf, "k_ax_mfma<kind%d,MT%d,PF%d,NTL%d,VPL%d> S=%d", (code / 1000) % 10,
+                  (code / 100) % 10, (code / 10) % 10, code % 10, vpl, ax_split(p, nsrc));
+  }
+  return buf;
+}
+
+std::string describe_plan(const GemmPlan& p) {
+  std::string s;
+  for (int ns = 1; ns <= 3; ++ns) s += "ax" + std::to_string(ns) + "=" + ax_name(p, ns) + "; ";
+  char buf[128];
+  if (p.atr_kind == 3)
+    std::snprintf(buf, sizeof buf, "atr=k_atr_valu<LB%d,VEC%d> S=%d", p.atr_lb, p.atr_vec, p.atr_S);
+  else
+    std::snprintf(buf, sizeof buf, "atr=k_atr_mfma<WL%d,PF%d,NTL%d> S=%d", p.atr_wl, p.atr_pf, p.atr_ntl, p.atr_S);
+  return s + buf;
 }
 
 int max_ax_split(int esize, int64_t m, int64_t n, int64_t l) {

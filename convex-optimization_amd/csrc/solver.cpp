@@ -803,6 +803,15 @@ int glx_kernel_workspace_bytes(int dtype, int64_t m, int64_t n, int64_t l, size_
   });
 }
 
+int glx_plan_describe(int dtype, int64_t m, int64_t n, int64_t l, char* out, size_t cap) {
+  return guarded([&] {
+    if (dtype != GLX_F32 && dtype != GLX_F64) throw Error{GLX_E_INVALID, "bad dtype"};
+    if (m <= 0 || n <= 0 || l <= 0 || l > kMaxL || !out || cap == 0) throw Error{GLX_E_INVALID, "bad arguments"};
+    const std::string d = describe_plan(make_plan(dtype == GLX_F64 ? 8 : 4, m, n, l, 0));
+    std::snprintf(out, cap, "%s", d.c_str());
+  });
+}
+
 static KernelWs kernel_setup(int dtype, int64_t m, int64_t n, int64_t l, void* ws, size_t wsb,
                              int variant, hipStream_t st, GemmPlan* plan) {
   if (dtype != GLX_F32 && dtype != GLX_F64) throw Error{GLX_E_INVALID, "bad dtype"};

@@ -79,6 +79,7 @@ _SIGS = {
     "glx_prox": (c_int, [c_int, c_int64, c_int64, c_void_p, c_double, c_double, c_double,
                          c_void_p, c_void_p, c_void_p, c_size_t, c_void_p]),
     "glx_kernel_workspace_bytes": (c_int, [c_int, c_int64, c_int64, c_int64, POINTER(c_size_t)]),
+    "glx_plan_describe": (c_int, [c_int, c_int64, c_int64, c_int64, c_char_p, c_size_t]),
     "glx_comm_unique_id": (c_int, [POINTER(c_uint8)]),
     "glx_comm_create": (c_int, [POINTER(c_void_p), POINTER(c_uint8), c_int, c_int]),
     "glx_comm_allreduce": (c_int, [c_void_p, c_void_p, c_int64, c_int, c_void_p]),
@@ -112,6 +113,13 @@ def check(rc: int):
         msg = lib().glx_last_error()
         raise GlxError(rc, msg.decode() if msg else "?")
     return rc
+
+
+def plan_describe(dtype: int, m: int, n: int, l: int) -> str:
+    """The kernels and K splits libglx plans for this shape (see glx_plan_describe)."""
+    buf = ctypes.create_string_buffer(512)
+    check(lib().glx_plan_describe(dtype, m, n, l, buf, len(buf)))
+    return buf.value.decode()
 
 
 def default_opts(method: int) -> GlxOpts:

@@ -60,10 +60,12 @@ typedef struct glx_opts {
   int32_t continuous_subgradient; /* SGD/GD: alpha0 = 1/lambda_max(A^T A) (caller-computed:
                                      pass alpha0 accordingly; kept for ABI completeness)   */
   /* ---- build-only keys (the reference has no equivalent) ---- */
-  int32_t exact_objective;        /* ProxGD: 1 = recompute A@x for every objective (3 passes
-                                     over A per iteration, bit-faithful to the reference's
-                                     evaluation order); 0 = reuse the accepted line-search
-                                     residual A@z, z = x - t*G_t (ulp-level difference)      */
+  int32_t exact_objective;        /* ProxGD: 1 = evaluate the next objective at the accepted
+                                     x = prox(x - t*grad) itself (a third right-hand side in
+                                     the same pass over A: A@[z | p_thr | p]), bit-faithful to
+                                     the reference's evaluation order; 0 = reuse the accepted
+                                     line-search residual A@z, z = x - t*G_t (ulp-level
+                                     difference, SURVEY.md §8a reuse table)                   */
   int32_t profile;                /* 1 = time every A@x / A^T r launch with HIP events      */
   int64_t max_total_iters;        /* stop after this many iterations in total (0 = off)     */
   int32_t ax_variant;             /* A@x kernel variant for A/B tests (0 = auto)            */
@@ -149,6 +151,9 @@ int glx_prox(int dtype, int64_t n, int64_t l, const void* W, double t, double mu
              void* X_out, void* sums_dev, void* workspace, size_t workspace_bytes, void* stream);
 /* Workspace bytes for the single-kernel entry points above. */
 int glx_kernel_workspace_bytes(int dtype, int64_t m, int64_t n, int64_t l, size_t* bytes);
+/* One-line description of the kernels (tile, split) the planner picks for this shape, for
+ * A @ X with 1, 2, 3 right-hand sides and for A^T R (NUL-terminated, truncated to cap). */
+int glx_plan_describe(int dtype, int64_t m, int64_t n, int64_t l, char* out, size_t cap);
 
 /* ---- multi-GPU (row-sharded A, one RCCL all-reduce of A^T r per gradient) ---- */
 #define GLX_COMM_ID_BYTES 128

@@ -139,3 +139,29 @@ def test_shard_rows_partition():
             assert all(a[1] == b[0] for a, b in zip(ranges, ranges[1:]))
             sizes = [b - a for a, b in ranges]
             assert max(sizes) - min(sizes) <= 1
+
+
+def test_plan_describe_picks_tiles_by_shape():
+    """The planner (host code) picks MFMA tiles for l = 16/32 and VALU for other l."""
+    from glx import _lib
+    ns = _lib.plan_describe(_lib.GLX_F64, 8192, 16384, 32)
+    assert "ax2=k_ax_lds<" in ns and "atr=k_atr_mfma<" in ns, ns
+    gemv = _lib.plan_describe(_lib.GLX_F64, 65536, 8192, 1)
+    assert "k_ax_valu" in gemv and "k_atr_valu" in gemv, gemv
+    # n not a multiple of the LDS chunk: falls back to a register tile, never an invalid one
+    odd = _lib.plan_describe(_lib.GLX_F64, 1000, 1000, 32)
+    assert "ax2=" in odd and "ax3=" in odd, odd
+    with pytest.raises(_lib.GlxError):
+        _lib.plan_describe(_lib.GLX_F64, 0, 16, 16)
+
+
+def test_kernel_workspace_covers_every_planned_split():
+    """glx_kernel_workspace_bytes must hold the partial slabs of the largest K split any tile
+    (single or batched, register or LDS) plans, else the single-kernel calls refuse to run."""
+    from glx import _lib
+    for shp in [(512, 1024, 16), (512, 1024, 32), (4096, 8192, 16), (129, 640, 32)]:
+        nb = ctypes.c_size_t(0)
+        _lib.check(_lib.lib().glx_kernel_workspace_bytes(_lib.GLX_F64, *shp, ctypes.byref(nb)))
+        splits = [int(s) for s in re.findall(r"S=(\d+)", _lib.plan_describe(_lib.GLX_F64, *shp))]
+        m, n, l = shp
+        assert nb.value >= 8 * m * l * max(splits) * 3, (shp, nb.value, splits)
