@@ -2,7 +2,7 @@
 
 The bootstrap (exchanging RCCL's unique id) rides on ``torch.distributed`` with whatever
 backend the launcher initialised (gloo is enough); every GPU collective of the solve itself
-is issued by libglx on the compute stream (src/comm.cpp): one sum all-reduce of the n x l
+is issued by libglx on the compute stream (csrc/comm.cpp): one sum all-reduce of the n x l
 gradient per A^T r, plus 8-byte all-reduces of squared residual norms.
 """
 from __future__ import annotations
