@@ -269,8 +269,9 @@ __global__ __launch_bounds__(256) void k_ax_mfma(const T* __restrict__ A, const 
 // CDNA4 LDS lane-group model (MI355X_MICROARCH.md §LDS; checked with a small simulator).
 // Compared with kind 1/2 (every wave gathers its own X chunk into registers) this cuts the
 // L2->CU traffic of X by WAVES and frees the X register ring: the f64 2-RHS tile fits 2 waves
-// per SIMD. Pipeline per chunk c: issue X(c+PF) and A(c+PF) (register rings), write X(c+1) to
-// the other LDS slot, read X(c) from this slot, MFMAs, one barrier. A is read exactly once.
+// per SIMD. Pipeline per chunk c: write X(c+1) (loaded PF-1 chunks ago) to the other LDS slot,
+// issue X(c+PF), read X(c) from this slot, then per row tile its MFMAs followed by the refill
+// of that tile's A registers with chunk c+PF; one barrier. A is read exactly once.
 // ------------------------------------------------------------------------------------------
 // one 16-B X vector into LDS: a b128 store, or two 8-B stores when the row is only 8-B aligned
 template <typename T, bool W16>
@@ -286,7 +287,9 @@ __device__ inline void lds_put(T* dst, typename MF<T>::vec_t v) {
   }
 }
 
-template <typename T, int MT, int NT, int NSRC, int PF, int VPL, int WAVES>
+// ABL (timing ablation, never used for results; GLX_AXL_ABL): 1 = no barriers, 2 = no X
+// staging or LDS reads (constant B operand), 3 = no A loads (constant A operand), 4 = 3 + 1.
+template <typename T, int MT, int NT, int NSRC, int PF, int VPL, int WAVES, int ABL = 0>
 __global__ __launch_bounds__(64 * WAVES) void k_ax_lds(const T* __restrict__ A,
                                                       const T* __restrict__ X0,
                                                       const T* __restrict__ X1,
@@ -308,6 +311,7 @@ __global__ __launch_bounds__(64 * WAVES) void k_ax_lds(const T* __restrict__ A,
   constexpr int NTHR = 64 * WAVES;
   constexpr int XV = NSRC * CK * L / E;   // 16-B vectors of X per chunk
   constexpr int XPT = (XV + NTHR - 1) / NTHR;
+  constexpr bool XFULL = (XV % NTHR) == 0; // every thread moves XPT vectors: no predicate
   constexpr int VPR = L / E;              // vectors per X row
   static_assert(PF >= 2, "X(c+1) must sit in another ring slot than X(c + PF)");
   __shared__ __attribute__((aligned(16))) T xs[2][XCH];
@@ -320,7 +324,8 @@ __global__ __launch_bounds__(64 * WAVES) void k_ax_lds(const T* __restrict__ A,
   const int i = lane & 15, q = lane >> 4;
   const int64_t row0 = (int64_t)bx * (16 * MT * WAVES) + (int64_t)wave * (16 * MT);
   const int64_t cb = chunks * by / S, ce = chunks * (by + 1) / S;
-  if (cb >= ce) return;   // block-uniform
+  const int64_t nch = ce - cb;
+  if (nch <= 0) return;   // block-uniform
 
   const T* ap[MT];
 #pragma unroll
@@ -336,7 +341,7 @@ __global__ __launch_bounds__(64 * WAVES) void k_ax_lds(const T* __restrict__ A,
 #pragma unroll
   for (int j = 0; j < XPT; ++j) {
     const int v = threadIdx.x + NTHR * j;
-    xon[j] = v < XV;
+    xon[j] = XFULL || v < XV;
     const int vv = xon[j] ? v : 0;
     const int src = vv / (CK * VPR), rem = vv % (CK * VPR);
     const int k = rem / VPR, c = (rem % VPR) * E;
@@ -351,75 +356,98 @@ __global__ __launch_bounds__(64 * WAVES) void k_ax_lds(const T* __restrict__ A,
 #pragma unroll
     for (int c = 0; c < NC; ++c) acc[mt][c] = C{};
 
+  // Ring loads at a clamped chunk offset: past the end they re-read the last chunk (unused),
+  // so the main loop has no load predicates. A predicate at a loop join point makes the
+  // compiler drain vmcnt to 0 there, which empties the prefetch ring every chunk.
   V a[PF][MT][VPL];
   V xr[PF][XPT];
+  auto load_x = [&](V (&dst)[XPT], int64_t off) {
+    off = off < nch ? off : nch - 1;
 #pragma unroll
-  for (int p = 0; p < PF; ++p) {
-    if (cb + p < ce) {
+    for (int j = 0; j < XPT; ++j)
+      if (XFULL || xon[j]) dst[j] = *reinterpret_cast<const V*>(xg[j] + off * CK * L);
+  };
+  auto load_a = [&](V (&dst)[MT][VPL], int64_t off) {
+    off = off < nch ? off : nch - 1;
 #pragma unroll
-      for (int j = 0; j < XPT; ++j)
-        if (xon[j]) xr[p][j] = *reinterpret_cast<const V*>(xg[j] + (int64_t)p * CK * L);
+    for (int mt = 0; mt < MT; ++mt)
 #pragma unroll
-      for (int mt = 0; mt < MT; ++mt)
+      for (int v = 0; v < VPL; ++v)
+        dst[mt][v] = (ABL == 3 || ABL == 4) ? V{} + (T)(lane + mt)
+                                           : load_vec<T, false>(ap[mt] + off * CK + v * E);
+  };
+  auto put_x = [&](int slot, const V (&src)[XPT]) {
 #pragma unroll
-        for (int v = 0; v < VPL; ++v) a[p][mt][v] = load_vec<T, false>(ap[mt] + p * CK + v * E);
+    for (int j = 0; j < XPT; ++j)
+      if (XFULL || xon[j]) lds_put<T, W16>(&xs[slot][xo[j]], src[j]);
+  };
+  // X(c) from LDS slot into registers
+  auto read_x = [&](int slot, T (&xv)[NC][EL]) {
+#pragma unroll
+    for (int cc = 0; cc < NC; ++cc) {
+      const int src = cc / NT, nt = cc % NT;
+      const T* xp = &xs[slot][src * CK * LP + q * EL * LP + nt * 16 + i];
+#pragma unroll
+      for (int e = 0; e < EL; ++e) xv[cc][e] = (ABL == 2) ? (T)(cc + e + i) : xp[e * LP];
     }
-  }
-  // chunk cb -> slot 0
+  };
+  // MFMAs of row tile mt for one chunk
+  auto mma_tile = [&](int mt, const V (&av)[VPL], const T (&xv)[NC][EL]) {
 #pragma unroll
-  for (int j = 0; j < XPT; ++j)
-    if (xon[j]) lds_put<T, W16>(&xs[0][xo[j]], xr[0][j]);
+    for (int v = 0; v < VPL; ++v)
+#pragma unroll
+      for (int e = 0; e < E; ++e)
+#pragma unroll
+        for (int cc = 0; cc < NC; ++cc)
+          acc[mt][cc] = M::mma(av[v][e], xv[cc][v * E + e], acc[mt][cc]);
+  };
+
+#pragma unroll
+  for (int p = 0; p < PF; ++p) {   // X first, then A, in every ring step (see header)
+    load_x(xr[p], p);
+    load_a(a[p], p);
+  }
+  put_x(0, xr[0]);                 // chunk 0 -> slot 0
   __syncthreads();
 
-  for (int64_t c0 = cb; c0 < ce; c0 += PF) {
+  // Main loop: PF chunks per trip, no predicates. Registers are consumed in place: a tile's
+  // A fragments feed its MFMAs and are then refilled with chunk c + PF in the same registers
+  // (copying them out first would force the refill loads to complete at the loop's back edge).
+  int64_t c0 = 0;
+  for (; c0 + PF <= nch; c0 += PF) {
 #pragma unroll
     for (int p = 0; p < PF; ++p) {
       const int64_t c = c0 + p;
-      if (c < ce) {
-        const int slot = (int)((c - cb) & 1);
-        V av[MT][VPL];
+      const int slot = (int)(c & 1);
+      if (ABL != 2) put_x(slot ^ 1, xr[(p + 1) % PF]);   // X(c+1), loaded PF-1 chunks ago
+      load_x(xr[p], c + PF);       // xr[p] (X(c)) has been in LDS since chunk c-1
+      T xv[NC][EL];
+      read_x(slot, xv);
 #pragma unroll
-        for (int mt = 0; mt < MT; ++mt)
+      for (int mt = 0; mt < MT; ++mt) {
+        mma_tile(mt, a[p][mt], xv);
+        if (ABL != 3 && ABL != 4) {
+          int64_t off = c + PF;
+          off = off < nch ? off : nch - 1;
 #pragma unroll
-          for (int v = 0; v < VPL; ++v) av[mt][v] = a[p][mt][v];
-        V xn[XPT];   // X(c+1), loaded PF-1 chunks ago
-        const int pn = (p + 1) % PF;
-#pragma unroll
-        for (int j = 0; j < XPT; ++j) xn[j] = xr[pn][j];
-        if (c + PF < ce) {   // refill this ring slot with chunk c + PF (X first: see header)
-          const int64_t off = c + PF - cb;
-#pragma unroll
-          for (int j = 0; j < XPT; ++j)
-            if (xon[j]) xr[p][j] = *reinterpret_cast<const V*>(xg[j] + off * CK * L);
-#pragma unroll
-          for (int mt = 0; mt < MT; ++mt)
-#pragma unroll
-            for (int v = 0; v < VPL; ++v) a[p][mt][v] = load_vec<T, false>(ap[mt] + off * CK + v * E);
+          for (int v = 0; v < VPL; ++v) a[p][mt][v] = load_vec<T, false>(ap[mt] + off * CK + v * E);
         }
-        if (c + 1 < ce) {
-#pragma unroll
-          for (int j = 0; j < XPT; ++j)
-            if (xon[j]) lds_put<T, W16>(&xs[slot ^ 1][xo[j]], xn[j]);
-        }
-        T xv[NC][EL];
-#pragma unroll
-        for (int cc = 0; cc < NC; ++cc) {
-          const int src = cc / NT, nt = cc % NT;
-          const T* xp = &xs[slot][src * CK * LP + q * EL * LP + nt * 16 + i];
-#pragma unroll
-          for (int e = 0; e < EL; ++e) xv[cc][e] = xp[e * LP];
-        }
-#pragma unroll
-        for (int v = 0; v < VPL; ++v)
-#pragma unroll
-          for (int e = 0; e < E; ++e)
-#pragma unroll
-            for (int mt = 0; mt < MT; ++mt)
-#pragma unroll
-              for (int cc = 0; cc < NC; ++cc)
-                acc[mt][cc] = M::mma(av[mt][v][e], xv[cc][v * E + e], acc[mt][cc]);
-        __syncthreads();
       }
+      if (ABL != 1 && ABL != 2 && ABL != 4) __syncthreads();
+    }
+  }
+  // tail: fewer than PF chunks left (their data is already in the ring)
+#pragma unroll
+  for (int p = 0; p < PF - 1; ++p) {
+    const int64_t c = c0 + p;
+    if (c < nch) {
+      const int slot = (int)(c & 1);
+      if (c + 1 < nch && ABL != 2) put_x(slot ^ 1, xr[(p + 1) % PF]);
+      T xv[NC][EL];
+      read_x(slot, xv);
+#pragma unroll
+      for (int mt = 0; mt < MT; ++mt) mma_tile(mt, a[p][mt], xv);
+      if (ABL != 1 && ABL != 2 && ABL != 4) __syncthreads();
     }
   }
 
@@ -728,12 +756,13 @@ static constexpr int kAxFallback = 21820;      // f64: VPL 2, direct loads, MT 8
 static constexpr int kAxDefault32 = 21410;     // f32: VPL 2, direct loads, MT 4, PF 1
 static constexpr int kAtrDefault = 102;        // WL = 0, PF = 2 (+1000: non-temporal A loads)
 // batched right-hand sides (MFMA-bound at l = 32, both dtypes): the LDS tile, 2 waves per SIMD
+// (end-to-end sweep, profiles/r1_tuning: f64 8-wave blocks, f32 4-wave blocks with PF 3)
 static int axb_default(int nsrc, int esize) {
-  (void)nsrc; (void)esize;
-  return 52224;
+  (void)nsrc;
+  return esize == 8 ? 52228 : 52324;
 }
 
-static constexpr int kLdsCodes[] = {52224, 52324, 52228, 54224, 52214, 54214};
+static constexpr int kLdsCodes[] = {52224, 52324, 52228, 52328, 52218, 54224, 52214, 54214};
 static bool lds_code_ok(int c, int64_t n, int64_t l, int esize) {
   bool known = false;
   for (int k : kLdsCodes) known |= (k == c);
@@ -932,13 +961,13 @@ static void ax_mfma_go(const GemmPlan& p, const T* A, const T* const* X, T* P, c
                      epoch);
 }
 
-template <typename T, int NT, int NSRC, int MT, int PF, int VPL, int WAVES>
+template <typename T, int NT, int NSRC, int MT, int PF, int VPL, int WAVES, int ABL = 0>
 static void ax_lds_go(const GemmPlan& p, int S, const T* A, const T* const* X, T* P,
                       const int* gate, int epoch, hipStream_t st) {
   constexpr int E = 16 / sizeof(T);
   const int gx = (int)cdiv(p.m, 16 * MT * WAVES);
   const int xmap = (p.ax_xmap && ax_xmap_ok(S)) ? 1 : 0;
-  hipLaunchKernelGGL((k_ax_lds<T, MT, NT, NSRC, PF, VPL, WAVES>), dim3((unsigned)ax_grid(xmap, gx, S)),
+  hipLaunchKernelGGL((k_ax_lds<T, MT, NT, NSRC, PF, VPL, WAVES, ABL>), dim3((unsigned)ax_grid(xmap, gx, S)),
                      dim3(64 * WAVES), 0, st, A, X[0], X[1], X[2], P, p.m, p.n,
                      p.n / (4 * VPL * E), S, gx, xmap, gate, epoch);
 }
@@ -950,10 +979,23 @@ static void ax_lds_code(const GemmPlan& p, int code, int S, const T* A, const T*
   switch (code) {
     case 52324: ax_lds_go<T, NT, NSRC, 2, 3, 2, 4>(p, S, A, X, P, gate, epoch, st); break;
     case 52228: ax_lds_go<T, NT, NSRC, 2, 2, 2, 8>(p, S, A, X, P, gate, epoch, st); break;
+    case 52328: ax_lds_go<T, NT, NSRC, 2, 3, 2, 8>(p, S, A, X, P, gate, epoch, st); break;
+    case 52218: ax_lds_go<T, NT, NSRC, 2, 2, 1, 8>(p, S, A, X, P, gate, epoch, st); break;
     case 54224: ax_lds_go<T, NT, NSRC, 4, 2, 2, 4>(p, S, A, X, P, gate, epoch, st); break;
     case 52214: ax_lds_go<T, NT, NSRC, 2, 2, 1, 4>(p, S, A, X, P, gate, epoch, st); break;
     case 54214: ax_lds_go<T, NT, NSRC, 4, 2, 1, 4>(p, S, A, X, P, gate, epoch, st); break;
-    default: ax_lds_go<T, NT, NSRC, 2, 2, 2, 4>(p, S, A, X, P, gate, epoch, st); break;   // 52224
+    default:   // 52224
+      if constexpr (sizeof(T) == 8 && NT == 2 && NSRC == 2) {
+        switch (env_int("GLX_AXL_ABL", 0)) {   // timing ablations (results are wrong)
+          case 1: ax_lds_go<T, NT, NSRC, 2, 2, 2, 4, 1>(p, S, A, X, P, gate, epoch, st); return;
+          case 2: ax_lds_go<T, NT, NSRC, 2, 2, 2, 4, 2>(p, S, A, X, P, gate, epoch, st); return;
+          case 3: ax_lds_go<T, NT, NSRC, 2, 2, 2, 4, 3>(p, S, A, X, P, gate, epoch, st); return;
+          case 4: ax_lds_go<T, NT, NSRC, 2, 2, 2, 4, 4>(p, S, A, X, P, gate, epoch, st); return;
+          default: break;
+        }
+      }
+      ax_lds_go<T, NT, NSRC, 2, 2, 2, 4>(p, S, A, X, P, gate, epoch, st);
+      break;
   }
 }
 

@@ -117,8 +117,13 @@ class Session : public SessionBase {
     for (int i = 1; i < nb; ++i) bufs[i] = static_cast<T*>(c.take(sizeof(T) * nl));
     T* res[kRes];
     for (int i = 0; i < kRes; ++i) res[i] = static_cast<T*>(c.take(sizeof(T) * ml));
-    T* g = static_cast<T*>(c.take(sizeof(T) * nl));
-    T* gp = plan.atr_S > 1 ? static_cast<T*>(c.take(sizeof(T) * nl * plan.atr_S)) : g;
+    // two gradient sets (G, its split-K slabs): the current one and the speculative one
+    T* g[2];
+    T* gp[2];
+    for (int k = 0; k < 2; ++k) {
+      g[k] = static_cast<T*>(c.take(sizeof(T) * nl));
+      gp[k] = plan.atr_S > 1 ? static_cast<T*>(c.take(sizeof(T) * nl * plan.atr_S)) : g[k];
+    }
     T* pp = static_cast<T*>(c.take(sizeof(T) * ml * ax_split_max(plan) * 3));   // up to 3 batched sources
     double* scal = static_cast<double*>(c.take(sizeof(double) * NSCAL));
     double* part = static_cast<double*>(c.take(sizeof(double) * kMaxRedVals * kMaxBlocks));
@@ -128,7 +133,8 @@ class Session : public SessionBase {
     if (s) {
       for (int i = 0; i < kBufs; ++i) s->X_[i] = bufs[i];
       for (int i = 0; i < kRes; ++i) s->R_[i] = res[i];
-      s->G_ = g; s->Gp_ = gp; s->Pp_ = pp;
+      for (int k = 0; k < 2; ++k) { s->Gs_[k] = g[k]; s->Gps_[k] = gp[k]; }
+      s->G_ = g[0]; s->Gp_ = gp[0]; s->Pp_ = pp;
       s->scal_ = scal; s->part_ = part; s->ticket_ = ticket; s->flag_ = flag; s->fh_dev_ = fh;
     }
     return c.off + 256;
@@ -162,6 +168,8 @@ class Session : public SessionBase {
     hseq_dev_ = reinterpret_cast<unsigned*>(hs_dev_ + NSCAL + 2);
     const char* rb = std::getenv("GLX_READBACK");
     spin_readback_ = !(rb && std::strcmp(rb, "sync") == 0);
+    const char* sp = std::getenv("GLX_SPEC_GRAD");
+    spec_off_env_ = (sp && std::strcmp(sp, "0") == 0);
     GLX_HIP(hipMemsetAsync(ticket_, 0, kTicketBytes, st_));
     GLX_HIP(hipMemsetAsync(flag_, 0, 256, st_));
     GLX_HIP(hipMemsetAsync(scal_, 0, sizeof(double) * NSCAL, st_));
@@ -239,6 +247,7 @@ class Session : public SessionBase {
     // finish() overwrote residual buffers: rebuild the iteration state if run() is called again
     state_valid_ = false;
     y_ready_ = false;
+    spec_ready_ = false;
   }
 
   void kernel_time(int kind, int64_t* launches, double* ms) override {
@@ -313,22 +322,44 @@ class Session : public SessionBase {
     residuals(1, xs, rs, slot, cx, cmax);
   }
 
-  // G = A^T r as slabs; returns (source, S) for the consumer. With a communicator the slabs are
-  // summed and all-reduced first (S = 1).
-  std::pair<const T*, int> gradient(const T* r) {
+  // G = A^T r as slabs of gradient set `set` (default: the current one); returns (source, S)
+  // for the consumer. With a communicator the slabs are summed and all-reduced first (S = 1).
+  std::pair<const T*, int> gradient(const T* r, int set = -1) {
+    if (set < 0) set = gset_;
+    T* G = Gs_[set];
+    T* Gp = Gps_[set];
     hipEvent_t e0 = nullptr, e1 = nullptr;
     if (O_.profile) { e0 = get_event(); e1 = get_event(); GLX_HIP(hipEventRecord(e0, st_)); }
-    launch_atr<T>(plan_, A_, r, Gp_, st_);
+    launch_atr<T>(plan_, A_, r, Gp, st_);
     check_launch();
     if (O_.profile) { GLX_HIP(hipEventRecord(e1, st_)); ev_[1].push_back({e0, e1}); }
     ++atr_calls_;
-    if (!comm_) return {Gp_, plan_.atr_S};
+    if (!comm_) return {Gp, plan_.atr_S};
     if (plan_.atr_S > 1) {
-      launch_sum_partials<T>(Gp_, plan_.atr_S, G_, nl_, st_);
+      launch_sum_partials<T>(Gp, plan_.atr_S, G, nl_, st_);
       check_launch();
     }
-    comm_allreduce(comm_, G_, nl_, P_.dtype, st_);
-    return {G_, 1};
+    comm_allreduce(comm_, G, nl_, P_.dtype, st_);
+    return {G, 1};
+  }
+  void use_gset(int set) { gset_ = set; G_ = Gs_[set]; Gp_ = Gps_[set]; }
+
+  // Speculative gradient (ProxGD / FISTA with line search). The next iteration's gradient
+  // residual is produced by the trial's batched A@X, and the next gradient depends only on
+  // whether that trial is accepted. So A^T r of the candidate is queued behind the trial
+  // and runs while the host reads the trial's scalars and decides, into the other gradient
+  // set. If the trial is rejected it is dropped. Used only while the previous iteration
+  // accepted its first trial, so a rejecting regime pays no extra passes.
+  std::pair<const T*, int> take_gradient(const T* r) {
+    if (spec_ready_) {
+      spec_ready_ = false;
+      use_gset(spec_set_);
+      return spec_g_;
+    }
+    return gradient(r);
+  }
+  bool want_spec(int trial_it) const {
+    return spec_on_ && trial_it == 0 && O_.step_type == GLX_STEP_LINE_SEARCH && !spec_off_env_;
   }
 
   void readback() {
@@ -398,6 +429,7 @@ class Session : public SessionBase {
       copy_x(iv_, ix_);
       tk_ = O_.alpha0;
       y_ready_ = false;
+      spec_ready_ = false;   // y is re-formed from the reset v: its gradient was not speculated
     }
   }
 
@@ -416,6 +448,7 @@ class Session : public SessionBase {
   // and returned), X_[ixt_] = thr(x) (:127), R_[irg_] = A thr(x) - b (the gradient residual,
   // :129, exact), gx_ = 1/2 ||R_[irg_]||^2, f_cur_/s_cur_ = objective and sparsity of x.
   void proxgd_prologue(bool have_thr) {
+    spec_ready_ = false;   // the gradient is recomputed from the rebuilt residual
     if (!have_thr) {
       launch_threshold<T>(X_[ix_], X_[ixt_], nl_, O_.thres, flag_, ++epoch_, st_);
       check_launch();
@@ -437,7 +470,7 @@ class Session : public SessionBase {
     if (!state_valid_) proxgd_prologue(thr_from_trial_);
     record(f_cur_, s_cur_);
     if (stop_rule()) { end_phase(); return; }     // x and its state carry over to the next phase
-    const std::pair<const T*, int> g = gradient(R_[irg_]);
+    const std::pair<const T*, int> g = take_gradient(R_[irg_]);
     const T* xt = X_[ixt_];
     const bool exact = O_.exact_objective != 0;
     // trial residual buffers: never the gradient residual
@@ -458,9 +491,18 @@ class Session : public SessionBase {
         const T* xs[3] = {X_[iz_], X_[ipt_], X_[ip_]};
         T* rs[3] = {R_[rz], R_[rpt], R_[rp]};
         residuals(exact ? 3 : 2, xs, rs, S_RT, X_[ip_], scal_ + S_TR + 3);
+        const bool spec = want_spec(it);
+        std::pair<const T*, int> sg;
+        if (spec) sg = gradient(R_[rpt], 1 - gset_);   // gradient at the candidate p_thr
         readback();
         const double gz = 0.5 * hs_[S_RT];
-        if (gz <= gx_ - t * hs_[S_TR + 0] + 0.5 * t * hs_[S_TR + 1]) { accepted = true; break; }
+        if (gz <= gx_ - t * hs_[S_TR + 0] + 0.5 * t * hs_[S_TR + 1]) {
+          accepted = true;
+          if (spec) { spec_ready_ = true; spec_g_ = sg; spec_set_ = 1 - gset_; }
+          spec_on_ = (it == 0);
+          break;
+        }
+        spec_on_ = false;
         t *= O_.ls_coeff;
       }
       // after ls_maxit failures the reference returns alpha0*coeff^maxit untested (:99)
@@ -510,7 +552,7 @@ class Session : public SessionBase {
       gy_pending_ = true;
     }
     const T* y = X_[iy_];
-    std::pair<const T*, int> g = gradient(R_[iry_]);
+    std::pair<const T*, int> g = take_gradient(R_[iry_]);
     if (smooth) {                                         // G = A^T r + mu y / sqrt(|y_i|^2 + d^2)
       launch_fgd_grad<T>(y, g.first, g.second, G_, n_, l_, mu_, O_.delta, red(S_REGY), st_);
       check_launch();
@@ -534,6 +576,9 @@ class Session : public SessionBase {
         const T* xs[3] = {X_[ic_], X_[iyn_], nullptr};
         T* rs[3] = {R_[rc], R_[ryn], nullptr};
         residuals(2, xs, rs, S_RT, X_[ic_], scal_ + S_TR + i_max);   // A @ [x | y_next]
+        const bool spec = want_spec(it);
+        std::pair<const T*, int> sg;
+        if (spec) sg = gradient(R_[ryn], 1 - gset_);   // gradient at the next y
         readback();
         if (gy_pending_) { gy_sq_ = hs_[S_RG]; gy_pending_ = false; }
         double gy = 0.5 * gy_sq_, gxc = 0.5 * hs_[S_RT];
@@ -541,7 +586,13 @@ class Session : public SessionBase {
           gy = gy + mu_ * hs_[S_REGY];
           gxc = gxc + mu_ * hs_[S_TR + 2];
         }
-        if (gxc <= gy + hs_[S_TR + 0] + hs_[S_TR + 1] / (2 * t)) { accepted = true; break; }
+        if (gxc <= gy + hs_[S_TR + 0] + hs_[S_TR + 1] / (2 * t)) {
+          accepted = true;
+          if (spec) { spec_ready_ = true; spec_g_ = sg; spec_set_ = 1 - gset_; }
+          spec_on_ = (it == 0);
+          break;
+        }
+        spec_on_ = false;
         t *= O_.ls_coeff;
       }
       if (!accepted) trial(t, false);
@@ -613,6 +664,8 @@ class Session : public SessionBase {
   T* X_[kBufs] = {nullptr, nullptr, nullptr, nullptr, nullptr, nullptr};
   T* R_[kRes] = {nullptr, nullptr, nullptr, nullptr};
   T *G_ = nullptr, *Gp_ = nullptr, *Pp_ = nullptr;
+  T* Gs_[2] = {nullptr, nullptr};
+  T* Gps_[2] = {nullptr, nullptr};
   double *scal_ = nullptr, *part_ = nullptr, *fh_dev_ = nullptr;
   double *hs_ = nullptr, *hs_dev_ = nullptr;
   unsigned *hseq_ = nullptr, *hseq_dev_ = nullptr;
@@ -630,6 +683,10 @@ class Session : public SessionBase {
   int ixt_ = 1, ip_ = 2, ipt_ = 3, iz_ = 4;                      // ProxGD
   int irg_ = 0, iry_ = 0;
   bool state_valid_ = false, thr_from_trial_ = false, y_ready_ = false, gy_pending_ = false;
+  // speculative gradient (take_gradient)
+  int gset_ = 0, spec_set_ = 1;
+  bool spec_on_ = true, spec_ready_ = false, spec_off_env_ = false;
+  std::pair<const T*, int> spec_g_{nullptr, 0};
   double gx_ = 0, gy_sq_ = 0;
   // algorithm state
   int phase_ = 0;
