@@ -139,6 +139,25 @@ static inline unsigned grid_for(int64_t work, int per_block) {
 
 template <typename T> __device__ inline T tabs(T v) { return v < T(0) ? -v : v; }
 
+// Hand ns scalars to the host through the mapped, fine-grained (uncached) packet: system-scope
+// stores (sc0 sc1, straight to host memory), drained with vmcnt(0) so every packet store is
+// acknowledged, then the sequence word the host spins on; no L2 writeback is needed for it.
+// All loads are issued before the first store (one latency, not ns). Runs as its own tiny
+// kernel: done by the last block of the preceding reduction it measured ~15 us slower
+// (profiles/r1_tuning, fused-publish attribution) than a separate launch (~5.5 us).
+constexpr int kPublishMax = 32;
+__device__ inline void publish_packet(const double* s, int ns, double* host, unsigned* host_seq,
+                                      unsigned seq) {
+  double v[kPublishMax];
+#pragma unroll
+  for (int k = 0; k < kPublishMax; ++k) v[k] = k < ns ? s[k] : 0.0;
+#pragma unroll
+  for (int k = 0; k < kPublishMax; ++k)
+    if (k < ns) __hip_atomic_store(host + k, v[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __hip_atomic_store(host_seq, seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
 // ------------------------------------------------------------------------------------------
 // residual finalize: R = sum_s P[s] - B; out[0] = sum R^2, out[1] = count(|c| > 1e-6 *cmax)
 // over a second array c (the candidate iterate, fused here to save a launch); the last block
@@ -154,25 +173,27 @@ __global__ __launch_bounds__(256) void k_finalize_residual(
   if (!live && gate_mode == 0) return;  // uniform over the grid: nobody touches the ticket
   double v[4] = {0.0, 0.0, 0.0, 0.0};
   T* rs[3] = {R0, R1, R2};
+  const T thr = cx != nullptr ? (T)1e-6 * (T)(*cmax) : T(0);
+  // one pass over max(ml, cn): the residual slabs and the count's iterate are loaded in the
+  // same trip, so both latency chains overlap
   const int64_t stride = (int64_t)gridDim.x * 256;
-  for (int64_t idx = (int64_t)blockIdx.x * 256 + threadIdx.x; idx < ml; idx += stride) {
-    const T bv = B[idx];
+  const int64_t work = ml > cn ? ml : cn;
+  for (int64_t idx = (int64_t)blockIdx.x * 256 + threadIdx.x; idx < work; idx += stride) {
+    if (idx < ml) {
+      const T bv = B[idx];
 #pragma unroll
-    for (int sr = 0; sr < NSRC; ++sr) {
-      T r;
-      if (live) {
-        r = slab_sum(P + (int64_t)sr * S * ml, S, ml, idx) - bv;
-        rs[sr][idx] = r;
-      } else {
-        r = rs[sr][idx];
+      for (int sr = 0; sr < NSRC; ++sr) {
+        T r;
+        if (live) {
+          r = slab_sum(P + (int64_t)sr * S * ml, S, ml, idx) - bv;
+          rs[sr][idx] = r;
+        } else {
+          r = rs[sr][idx];
+        }
+        v[sr] += (double)(r * r);
       }
-      v[sr] += (double)(r * r);
     }
-  }
-  if (cx != nullptr) {
-    const T thr = (T)1e-6 * (T)(*cmax);
-    for (int64_t idx = (int64_t)blockIdx.x * 256 + threadIdx.x; idx < cn; idx += stride)
-      v[3] += (tabs(cx[idx]) > thr) ? 1.0 : 0.0;
+    if (cx != nullptr && idx < cn) v[3] += (tabs(cx[idx]) > thr) ? 1.0 : 0.0;
   }
   const bool last = grid_reduce<4, 0u>(v, red);
   if (last && fh != nullptr && threadIdx.x == 0) *fh = 0.5 * red.out[0] + fh_mu * (*fh_rn);
@@ -545,14 +566,9 @@ __global__ __launch_bounds__(256) void k_thr_axpby(T* __restrict__ xk, const T* 
 }
 
 // publish the scalar packet to host-mapped memory: data, then (system-scope release) seq
-__global__ void k_publish(const double* __restrict__ s, int ns, volatile double* host,
-                          volatile unsigned* host_seq, unsigned seq) {
-  if (threadIdx.x < ns) host[threadIdx.x] = s[threadIdx.x];
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    __threadfence_system();
-    *host_seq = seq;
-  }
+__global__ void k_publish(const double* __restrict__ s, int ns, double* host, unsigned* host_seq,
+                          unsigned seq) {
+  if (threadIdx.x == 0) publish_packet(s, ns, host, host_seq, seq);
 }
 
 template <typename T>

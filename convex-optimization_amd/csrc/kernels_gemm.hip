@@ -516,37 +516,38 @@ __global__ __launch_bounds__(256) void k_atr_mfma(const T* __restrict__ A, const
 #pragma unroll
     for (int nt = 0; nt < NT; ++nt) acc[e][nt] = C{};
 
+  // Ring of PF row steps, consumed in place: a step's fragments feed its MFMAs and are then
+  // refilled with step s + PF in the same registers, at a clamped offset so that the main
+  // loop carries no load predicates (a predicate or a register copy at the loop's back edge
+  // makes the compiler drain vmcnt to 0 there). Lookahead = PF - 1 steps.
+  const int64_t nst = se - sb;
   T a[PF][4], rb[PF][NT];
+  auto ld = [&](int p, int64_t off) {
+    off = off < nst ? off : nst - 1;
+    Load4<T, NTL>::go(ap + off * 4 * n, a[p]);
 #pragma unroll
-  for (int p = 0; p < PF; ++p) {
-    if (sb + p < se) {
-      Load4<T, NTL>::go(ap + (int64_t)p * 4 * n, a[p]);
+    for (int nt = 0; nt < NT; ++nt) rb[p][nt] = rp[off * 4 * L + nt * 16];
+  };
+  auto mma_step = [&](int p) {
 #pragma unroll
-      for (int nt = 0; nt < NT; ++nt) rb[p][nt] = rp[(int64_t)p * 4 * L + nt * 16];
-    }
-  }
-  for (int64_t s0 = sb; s0 < se; s0 += PF) {
+    for (int e = 0; e < 4; ++e)
 #pragma unroll
-    for (int p = 0; p < PF; ++p) {
-      const int64_t s = s0 + p;
-      if (s < se) {
-        T av[4], rv[NT];
+      for (int nt = 0; nt < NT; ++nt) acc[e][nt] = M::mma(a[p][e], rb[p][nt], acc[e][nt]);
+  };
+  if (nst > 0) {
 #pragma unroll
-        for (int e = 0; e < 4; ++e) av[e] = a[p][e];
+    for (int p = 0; p < PF; ++p) ld(p, p);
+    int64_t s0 = 0;
+    for (; s0 + PF <= nst; s0 += PF) {
 #pragma unroll
-        for (int nt = 0; nt < NT; ++nt) rv[nt] = rb[p][nt];
-        if (s + PF < se) {
-          const int64_t off = (s + PF - sb) * 4;
-          Load4<T, NTL>::go(ap + off * n, a[p]);
-#pragma unroll
-          for (int nt = 0; nt < NT; ++nt) rb[p][nt] = rp[off * L + nt * 16];
-        }
-#pragma unroll
-        for (int e = 0; e < 4; ++e)
-#pragma unroll
-          for (int nt = 0; nt < NT; ++nt) acc[e][nt] = M::mma(av[e], rv[nt], acc[e][nt]);
+      for (int p = 0; p < PF; ++p) {
+        mma_step(p);
+        ld(p, s0 + p + PF);
       }
     }
+#pragma unroll
+    for (int p = 0; p < PF - 1; ++p)
+      if (s0 + p < nst) mma_step(p);
   }
 
   if (WL == 0) {
@@ -754,7 +755,9 @@ static int env_int(const char* name, int dflt) {
 static constexpr int kAxDefault = 52228;       // f64 single RHS: LDS, MT 2, PF 2, VPL 2, 8 waves
 static constexpr int kAxFallback = 21820;      // f64: VPL 2, direct loads, MT 8, PF 2
 static constexpr int kAxDefault32 = 21410;     // f32: VPL 2, direct loads, MT 4, PF 1
-static constexpr int kAtrDefault = 102;        // WL = 0, PF = 2 (+1000: non-temporal A loads)
+// A^T R code: NTL*1000 + WL*10 + PF (WL 1 = four panels of a block share rows, PF = ring depth)
+static constexpr int kAtrDefault = 108;        // f64: WL 0, PF 8
+static constexpr int kAtrDefault32 = 1114;     // f32: non-temporal A, WL 1, PF 4
 // batched right-hand sides (MFMA-bound at l = 32, both dtypes): the LDS tile, 2 waves per SIMD
 // (end-to-end sweep, profiles/r1_tuning: f64 8-wave blocks, f32 4-wave blocks with PF 3)
 static int axb_default(int nsrc, int esize) {
@@ -855,10 +858,12 @@ GemmPlan make_plan(int esize, int64_t m, int64_t n, int64_t l, int ax_variant) {
   }
   // ---- A^T R ----
   int atr_code = env_int("GLX_ATR_VARIANT", 0);
-  if (atr_code == 0) atr_code = esize == 8 ? kAtrDefault : 1102;   // f32: non-temporal A wins
+  if (atr_code == 0) atr_code = esize == 8 ? kAtrDefault : kAtrDefault32;
   const int ntl = atr_code >= 1000 ? 1 : 0;
-  const int wl = (atr_code / 10) % 10, pf = atr_code % 10;
-  const bool atr_mfma_ok = mfma_l && (n % (wl ? 256 : 64) == 0) && (m % 4 == 0);
+  int wl = (atr_code / 10) % 10;
+  const int pf = atr_code % 10;
+  if (wl && n % 256 != 0) wl = 0;   // four shared-row panels need n % 256: one panel per block
+  const bool atr_mfma_ok = mfma_l && (n % 64 == 0) && (m % 4 == 0);
   if (ax_variant == 3 || atr_code == 3 || !atr_mfma_ok) {
     p.atr_kind = 3;
     p.atr_lb = l >= 8 ? 8 : (l >= 4 ? 4 : (l >= 2 ? 2 : 1));
@@ -871,7 +876,7 @@ GemmPlan make_plan(int esize, int64_t m, int64_t n, int64_t l, int ax_variant) {
   } else {
     p.atr_kind = 1;
     p.atr_wl = wl ? 1 : 0;
-    p.atr_pf = (pf >= 1 && pf <= 4) ? pf : 2;
+    p.atr_pf = (pf >= 2 && pf <= 8) ? pf : 2;   // in-place ring: lookahead PF - 1 steps
     p.atr_ntl = ntl;
     const int64_t steps = m / 4;
     if (p.atr_wl == 0) {
@@ -1099,14 +1104,16 @@ static void atr_mfma_go(const GemmPlan& p, const T* A, const T* R, T* Gp, hipStr
 template <typename T, int NT>
 static void atr_mfma_nt(const GemmPlan& p, const T* A, const T* R, T* Gp, hipStream_t st) {
   switch (p.atr_ntl * 100 + p.atr_wl * 10 + p.atr_pf) {
-    case 1: atr_mfma_go<T, NT, 1, 0, false>(p, A, R, Gp, st); break;
     case 3: atr_mfma_go<T, NT, 3, 0, false>(p, A, R, Gp, st); break;
     case 4: atr_mfma_go<T, NT, 4, 0, false>(p, A, R, Gp, st); break;
-    case 12: atr_mfma_go<T, NT, 2, 1, false>(p, A, R, Gp, st); break;
-    case 101: atr_mfma_go<T, NT, 1, 0, true>(p, A, R, Gp, st); break;
+    case 6: atr_mfma_go<T, NT, 6, 0, false>(p, A, R, Gp, st); break;
+    case 8: atr_mfma_go<T, NT, 8, 0, false>(p, A, R, Gp, st); break;
+    case 14: atr_mfma_go<T, NT, 4, 1, false>(p, A, R, Gp, st); break;
     case 102: atr_mfma_go<T, NT, 2, 0, true>(p, A, R, Gp, st); break;
-    case 103: atr_mfma_go<T, NT, 3, 0, true>(p, A, R, Gp, st); break;
-    case 112: atr_mfma_go<T, NT, 2, 1, true>(p, A, R, Gp, st); break;
+    case 104: atr_mfma_go<T, NT, 4, 0, true>(p, A, R, Gp, st); break;
+    case 106: atr_mfma_go<T, NT, 6, 0, true>(p, A, R, Gp, st); break;
+    case 108: atr_mfma_go<T, NT, 8, 0, true>(p, A, R, Gp, st); break;
+    case 114: atr_mfma_go<T, NT, 4, 1, true>(p, A, R, Gp, st); break;
     default: atr_mfma_go<T, NT, 2, 0, false>(p, A, R, Gp, st); break;
   }
 }

@@ -295,8 +295,12 @@ class Session : public SessionBase {
 
   // R[src] = A X[src] - b for src < nsrc in one pass over A; scal[slot + src] = sum R[src]^2
   // (summed over ranks), scal[slot + 3] = count(|cx| > 1e-6 * *cmax); fh: device f record.
+  // pub_seq != NULL: also enqueue the scalar packet for the host once the sums are final
+  // (after the all-reduce with a communicator); *pub_seq receives the sequence number to wait
+  // for (wait_readback), so more work can be queued before the host blocks.
   void residuals(int nsrc, const T* const* xs, T* const* rs, int slot, const T* cx = nullptr,
-                 const double* cmax = nullptr, double* fh = nullptr, double fh_mu = 0.0) {
+                 const double* cmax = nullptr, double* fh = nullptr, double fh_mu = 0.0,
+                 unsigned* pub_seq = nullptr) {
     hipEvent_t e0 = nullptr, e1 = nullptr;
     if (O_.profile) { e0 = get_event(); e1 = get_event(); GLX_HIP(hipEventRecord(e0, st_)); }
     launch_ax<T>(plan_, nsrc, A_, xs, Pp_, nullptr, 0, st_);
@@ -315,11 +319,13 @@ class Session : public SessionBase {
         check_launch();
       }
     }
+    if (pub_seq != nullptr) *pub_seq = post_readback();
   }
-  void residual1(const T* x, T* r, int slot, const T* cx = nullptr, const double* cmax = nullptr) {
+  void residual1(const T* x, T* r, int slot, const T* cx = nullptr, const double* cmax = nullptr,
+                 unsigned* pub_seq = nullptr) {
     const T* xs[3] = {x, nullptr, nullptr};
     T* rs[3] = {r, nullptr, nullptr};
-    residuals(1, xs, rs, slot, cx, cmax);
+    residuals(1, xs, rs, slot, cx, cmax, nullptr, 0.0, pub_seq);
   }
 
   // G = A^T r as slabs of gradient set `set` (default: the current one); returns (source, S)
@@ -362,16 +368,23 @@ class Session : public SessionBase {
     return spec_on_ && trial_it == 0 && O_.step_type == GLX_STEP_LINE_SEARCH && !spec_off_env_;
   }
 
-  void readback() {
+  // Scalar readback in two halves so that work can be queued between them (the speculative
+  // gradient): post_readback enqueues the packet copy behind everything queued so far and
+  // returns its sequence number; wait_readback spins on the host-mapped sequence word.
+  unsigned post_readback() {
     ++syncs_;
+    if (!spin_readback_) return 0;
+    const unsigned seq = ++seq_;
+    launch_publish(scal_, NSCAL, hs_dev_, hseq_dev_, seq, st_);
+    check_launch();
+    return seq;
+  }
+  void wait_readback(unsigned seq) {
     if (!spin_readback_) {
       GLX_HIP(hipMemcpyAsync(hs_, scal_, sizeof(double) * NSCAL, hipMemcpyDeviceToHost, st_));
       GLX_HIP(hipStreamSynchronize(st_));
       return;
     }
-    const unsigned seq = ++seq_;
-    launch_publish(scal_, NSCAL, hs_dev_, hseq_dev_, seq, st_);
-    check_launch();
     // spin on the sequence word the GPU writes after the packet (system-scope release)
     volatile unsigned* hs = hseq_;
     uint64_t spins = 0;
@@ -388,14 +401,16 @@ class Session : public SessionBase {
     }
     __atomic_thread_fence(__ATOMIC_ACQUIRE);
   }
+  void readback() { wait_readback(post_readback()); }
 
   // objective of x (used by finish and as the FISTA prologue): S_XRN, S_XMAX, S_RO (sum r^2),
   // S_RO + 3 (count); r = A x - b -> R_[0]
   void objective_of(T* x) {
     launch_rownorm_max<T>(x, n_, l_, red(S_XRN), st_);
     check_launch();
-    residual1(x, R_[0], S_RO, use_sparsity_ ? x : nullptr, scal_ + S_XMAX);
-    readback();
+    unsigned seq = 0;
+    residual1(x, R_[0], S_RO, use_sparsity_ ? x : nullptr, scal_ + S_XMAX, &seq);
+    wait_readback(seq);
   }
 
   void record(double f, double s) {
@@ -458,8 +473,9 @@ class Session : public SessionBase {
     const int ro = (irg_ + 1) % kRes;
     const T* xs[3] = {X_[ix_], X_[ixt_], nullptr};
     T* rs[3] = {R_[ro], R_[irg_], nullptr};
-    residuals(2, xs, rs, S_RO, X_[ix_], scal_ + S_XMAX);     // A @ [x | thr(x)]
-    readback();
+    unsigned seq = 0;
+    residuals(2, xs, rs, S_RO, X_[ix_], scal_ + S_XMAX, nullptr, 0.0, &seq);   // A @ [x | thr(x)]
+    wait_readback(seq);
     f_cur_ = 0.5 * hs_[S_RO] + P_.mu0 * hs_[S_XRN];
     s_cur_ = hs_[S_RO + 3] / (double)nl_;
     gx_ = 0.5 * hs_[S_RO + 1];
@@ -490,11 +506,12 @@ class Session : public SessionBase {
         // one pass: g(z) for the test (:91) + the next iteration's residuals A p_thr (and A p)
         const T* xs[3] = {X_[iz_], X_[ipt_], X_[ip_]};
         T* rs[3] = {R_[rz], R_[rpt], R_[rp]};
-        residuals(exact ? 3 : 2, xs, rs, S_RT, X_[ip_], scal_ + S_TR + 3);
+        unsigned seq = 0;
+        residuals(exact ? 3 : 2, xs, rs, S_RT, X_[ip_], scal_ + S_TR + 3, nullptr, 0.0, &seq);
         const bool spec = want_spec(it);
         std::pair<const T*, int> sg;
         if (spec) sg = gradient(R_[rpt], 1 - gset_);   // gradient at the candidate p_thr
-        readback();
+        wait_readback(seq);
         const double gz = 0.5 * hs_[S_RT];
         if (gz <= gx_ - t * hs_[S_TR + 0] + 0.5 * t * hs_[S_TR + 1]) {
           accepted = true;
@@ -575,11 +592,12 @@ class Session : public SessionBase {
         trial(t, it == 0);
         const T* xs[3] = {X_[ic_], X_[iyn_], nullptr};
         T* rs[3] = {R_[rc], R_[ryn], nullptr};
-        residuals(2, xs, rs, S_RT, X_[ic_], scal_ + S_TR + i_max);   // A @ [x | y_next]
+        unsigned seq = 0;
+        residuals(2, xs, rs, S_RT, X_[ic_], scal_ + S_TR + i_max, nullptr, 0.0, &seq);   // A @ [x | y_next]
         const bool spec = want_spec(it);
         std::pair<const T*, int> sg;
         if (spec) sg = gradient(R_[ryn], 1 - gset_);   // gradient at the next y
-        readback();
+        wait_readback(seq);
         if (gy_pending_) { gy_sq_ = hs_[S_RG]; gy_pending_ = false; }
         double gy = 0.5 * gy_sq_, gxc = 0.5 * hs_[S_RT];
         if (smooth) {
