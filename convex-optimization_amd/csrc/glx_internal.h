@@ -80,6 +80,12 @@ void launch_ax(const GemmPlan& p, int nsrc, const T* A, const T* const* X, T* P,
                int epoch, hipStream_t st);
 template <typename T>
 void launch_atr(const GemmPlan& p, const T* A, const T* R, T* Gp, hipStream_t st);
+// ProxGD trial fused into A^T R (needs atr_prox_ok: MFMA panels, WL 0, one K split):
+// G = A^T R, then p = prox(x - t G), p_thr, z and the six trial sums of k_prox_pgd into red.
+bool atr_prox_ok(const GemmPlan& p);
+template <typename T>
+void launch_atr_prox(const GemmPlan& p, const T* A, const T* R, T* G, const T* x, T* pp, T* pthr,
+                     T* z, double t, double mu, double thres, Red red, hipStream_t st);
 
 // ---- row / elementwise kernels (kernels_elem.hip) ----
 // Gradient inputs `g` with an `S` argument are S split-K slabs of n*l values summed in slab

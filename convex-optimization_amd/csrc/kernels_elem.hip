@@ -19,116 +19,9 @@
 // Reductions are deterministic: block partials in a fixed tree order, then the last block to
 // arrive (sc1 partials + a two-level agent-scope arrival ticket, see grid_reduce) sums the
 // block partials in block order. max() propagates NaN like np.max.
-#include "glx_internal.h"
+#include "glx_device.h"
 
 namespace glx {
-
-enum { OP_SUM = 0, OP_MAX = 1 };
-
-__device__ inline double nan_max(double a, double b) {
-  if (a != a) return a;
-  if (b != b) return b;
-  return a > b ? a : b;
-}
-__device__ inline double combine(int op, double a, double b) { return op == OP_MAX ? nan_max(a, b) : a + b; }
-__device__ inline double identity(int op) { return op == OP_MAX ? -__builtin_inf() : 0.0; }
-
-// Reduce NV per-thread values over the grid; block size must be 256. MAXMASK bit v = max op.
-template <int NV, unsigned MAXMASK>
-__device__ bool grid_reduce(double (&v)[NV], const Red& red) {
-  __shared__ double sh[NV][4];
-  __shared__ int is_last;
-  const int lane = threadIdx.x & 63;
-  const int wave = threadIdx.x >> 6;
-#pragma unroll
-  for (int j = 0; j < NV; ++j) {
-    const int op = (MAXMASK >> j) & 1;
-#pragma unroll
-    for (int off = 32; off > 0; off >>= 1) v[j] = combine(op, v[j], __shfl_xor(v[j], off));
-  }
-  if (lane == 0) {
-#pragma unroll
-    for (int j = 0; j < NV; ++j) sh[j][wave] = v[j];
-  }
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    // write-through (sc1) partial stores + drained vmcnt before the ticket: no release fence
-    // (MI355X_MICROARCH.md, visibility "Valid forms" table, row 1)
-#pragma unroll
-    for (int j = 0; j < NV; ++j) {
-      const int op = (MAXMASK >> j) & 1;
-      const double bv = combine(op, combine(op, sh[j][0], sh[j][1]), combine(op, sh[j][2], sh[j][3]));
-      __hip_atomic_store(&red.part[j * kMaxBlocks + blockIdx.x], bv, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    // Two-level arrival: one device-scope counter costs ~12 ns per arriving block
-    // (MI355X_MICROARCH.md, "fanin"), so 1024 blocks on one word serialise for ~12 us. Blocks
-    // arrive on the counter of their shard (blockIdx % 8, i.e. their XCD under round-robin
-    // dispatch); the last arriver of each shard, whose add returned after every add of its
-    // shard, arrives on the final counter, and the last arriver there owns the sum.
-    const unsigned G = gridDim.x;
-    const unsigned sh = blockIdx.x & (kTicketShards - 1);
-    const unsigned nsh = G < (unsigned)kTicketShards ? G : (unsigned)kTicketShards;
-    const unsigned cnt = (G - sh + kTicketShards - 1) / kTicketShards;
-    const unsigned prev = __hip_atomic_fetch_add(red.ticket + (1 + sh) * kTicketStride, 1u,
-                                                 __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    int last = 0;
-    if (prev == cnt - 1)
-      last = __hip_atomic_fetch_add(red.ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == nsh - 1;
-    is_last = last;
-  }
-  __syncthreads();
-  if (!is_last) return false;
-  // every load of the partials is an sc1 load (L1 bypass): no acquire fence needed. All of them
-  // are issued before the first is consumed (clamped index, select afterwards), so the last
-  // block pays one round trip instead of one per partial.
-  constexpr int PER = kMaxBlocks / 256;
-  double pv[NV][PER];
-#pragma unroll
-  for (int j = 0; j < NV; ++j)
-#pragma unroll
-    for (int t = 0; t < PER; ++t) {
-      const unsigned b = threadIdx.x + 256u * t;
-      const unsigned bc = b < gridDim.x ? b : gridDim.x - 1;
-      pv[j][t] = __hip_atomic_load(&red.part[j * kMaxBlocks + bc], __ATOMIC_RELAXED,
-                                   __HIP_MEMORY_SCOPE_AGENT);
-    }
-  double acc[NV];
-#pragma unroll
-  for (int j = 0; j < NV; ++j) {
-    const int op = (MAXMASK >> j) & 1;
-    acc[j] = identity(op);
-#pragma unroll
-    for (int t = 0; t < PER; ++t)
-      if (threadIdx.x + 256u * t < gridDim.x) acc[j] = combine(op, acc[j], pv[j][t]);
-#pragma unroll
-    for (int off = 32; off > 0; off >>= 1) acc[j] = combine(op, acc[j], __shfl_xor(acc[j], off));
-  }
-  __syncthreads();
-  if (lane == 0) {
-#pragma unroll
-    for (int j = 0; j < NV; ++j) sh[j][wave] = acc[j];
-  }
-  __syncthreads();
-  if (threadIdx.x == 0) {
-#pragma unroll
-    for (int j = 0; j < NV; ++j) {
-      const int op = (MAXMASK >> j) & 1;
-      red.out[j] = combine(op, combine(op, sh[j][0], sh[j][1]), combine(op, sh[j][2], sh[j][3]));
-    }
-    for (int k = 0; k <= kTicketShards; ++k)
-      __hip_atomic_store(red.ticket + k * kTicketStride, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  }
-  return true;
-}
-
-// g = sum_s slabs[s][idx] in slab order (S = 1: a plain load)
-template <typename T>
-__device__ inline T slab_sum(const T* __restrict__ g, int S, int64_t stride, int64_t idx) {
-  T v = g[idx];
-  for (int k = 1; k < S; ++k) v = v + g[(int64_t)k * stride + idx];
-  return v;
-}
 
 static inline unsigned grid_for(int64_t work, int per_block) {
   int64_t g = (work + per_block - 1) / per_block;
@@ -137,7 +30,6 @@ static inline unsigned grid_for(int64_t work, int per_block) {
   return (unsigned)g;
 }
 
-template <typename T> __device__ inline T tabs(T v) { return v < T(0) ? -v : v; }
 
 // Hand ns scalars to the host through the mapped, fine-grained (uncached) packet: system-scope
 // stores (sc0 sc1, straight to host memory), drained with vmcnt(0) so every packet store is
@@ -207,22 +99,6 @@ __global__ __launch_bounds__(256) void k_sum_partials(const T* __restrict__ Gp, 
     G[idx] = slab_sum(Gp, S, nl, idx);
 }
 
-// ------------------------------------------------------------------------------------------
-// row helpers
-// ------------------------------------------------------------------------------------------
-template <int LPR>
-__device__ inline double row_allsum(double v) {
-#pragma unroll
-  for (int off = LPR / 2; off > 0; off >>= 1) v += __shfl_xor(v, off);
-  return v;
-}
-template <int LPR>
-__device__ inline float row_allsum(float v) {
-#pragma unroll
-  for (int off = LPR / 2; off > 0; off >>= 1) v += __shfl_xor(v, off);
-  return v;
-}
-
 // Iterate over rows: each group of LPR lanes owns one row per trip.
 #define GLX_ROW_LOOP_BEGIN(LPR)                                                        \
   const int sub = threadIdx.x & ((LPR)-1);                                             \
@@ -253,50 +129,25 @@ __global__ __launch_bounds__(256) void k_prox_pgd(const T* __restrict__ x, const
   const int64_t nl = n * l;
   double acc[6] = {0.0, 0.0, 0.0, -__builtin_inf(), 0.0, 0.0};
   GLX_ROW_LOOP_BEGIN(LPR)
-  T xv[EPL], gv[EPL], w[EPL];
-  T sq = T(0);
+  T xv[EPL], gv[EPL], pv[EPL], pth[EPL], zv[EPL];
+  bool ok[EPL];
 #pragma unroll
   for (int e = 0; e < EPL; ++e) {
     const int64_t j = sub + (int64_t)e * LPR;
-    const bool ok = rv && j < l;
-    xv[e] = ok ? x[base + j] : T(0);
-    gv[e] = ok ? slab_sum(g, S, nl, base + j) : T(0);
-    if (ok && gout != nullptr) gout[base + j] = gv[e];
-    w[e] = xv[e] - t * gv[e];
-    sq = sq + w[e] * w[e];
+    ok[e] = rv && j < l;
+    xv[e] = ok[e] ? x[base + j] : T(0);
+    gv[e] = ok[e] ? slab_sum(g, S, nl, base + j) : T(0);
+    if (ok[e] && gout != nullptr) gout[base + j] = gv[e];
   }
-  const T nrm = __builtin_sqrt(row_allsum<LPR>(sq));
-  T c = nrm - tmu;
-  c = (c < T(0)) ? T(0) : c;                        // np.clip(., 0, None): NaN stays NaN
-  const T d = ((nrm < thres) ? T(1) : T(0)) + nrm;
-  T psq = T(0);
-  bool rch = false;
+  prox_pgd_row<T, LPR, EPL>(xv, gv, ok, rv, sub, t, tmu, thres, pv, pth, zv, acc);
 #pragma unroll
   for (int e = 0; e < EPL; ++e) {
     const int64_t j = sub + (int64_t)e * LPR;
-    const bool ok = rv && j < l;
-    const T pv = (w[e] * c) / d;
-    const T G = (xv[e] - pv) / t;
-    const T zv = xv[e] - t * G;
-    if (ok) {
-      const bool small = tabs(pv) < thres;
-      p[base + j] = pv;
-      pthr[base + j] = small ? T(0) : pv;
-      z[base + j] = zv;
-      acc[0] += (double)(gv[e] * G);
-      acc[1] += (double)(G * G);
-      acc[3] = nan_max(acc[3], (double)tabs(pv));
-      const bool ch = small && pv != T(0);
-      acc[4] += ch ? 1.0 : 0.0;
-      rch = rch || ch;
-      psq = psq + pv * pv;
+    if (ok[e]) {
+      p[base + j] = pv[e];
+      pthr[base + j] = pth[e];
+      z[base + j] = zv[e];
     }
-  }
-  const T pn = __builtin_sqrt(row_allsum<LPR>(psq));
-  const double rowch = row_allsum<LPR>(rch ? 1.0 : 0.0);
-  if (rv && sub == 0) {
-    acc[2] += (double)pn;
-    acc[5] += rowch > 0.0 ? 1.0 : 0.0;
   }
   GLX_ROW_LOOP_END
   grid_reduce<6, 0x8u>(acc, red);

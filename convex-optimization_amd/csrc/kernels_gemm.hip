@@ -30,7 +30,7 @@
 #include <cstdlib>
 #include <string>
 
-#include "glx_internal.h"
+#include "glx_device.h"
 
 namespace glx {
 
@@ -490,13 +490,18 @@ template <bool NTL> struct Load4<float, NTL> {
   }
 };
 
+// One 64-column panel of A^T R over this wave's (WL 1: this block's) row range; returns the
+// panel's first column. acc[e][nt] holds rows col0 + 4 * M::row(lane, r) + e. For WL 0 the
+// block's four waves split the rows (K) and are summed through LDS in the fixed order
+// ((w0 + w1) + w2) + w3; afterwards wave w holds the complete sum for e == w in acc[w][*]
+// (the other e of a wave are partial and unused), so the four waves share the epilogue.
 template <typename T, int NT, int PF, int WL, bool NTL>
-__global__ __launch_bounds__(256) void k_atr_mfma(const T* __restrict__ A, const T* __restrict__ R,
-                                                  T* __restrict__ Gp, int64_t m, int64_t n, int S) {
+__device__ inline int64_t atr_panel(const T* __restrict__ A, const T* __restrict__ R, int64_t m,
+                                    int64_t n, int S, typename MF<T>::acc_t (&acc)[4][NT]) {
   typedef MF<T> M;
   typedef typename M::acc_t C;
   constexpr int L = 16 * NT;
-  __shared__ C red[WL == 0 ? 4 * NT : 1][64];
+  __shared__ C red[WL == 0 ? 4 : 1][WL == 0 ? 4 * NT : 1][64];   // [wave][e * NT + nt][lane]
 
   const int lane = threadIdx.x & 63;
   const int wave = threadIdx.x >> 6;
@@ -510,7 +515,6 @@ __global__ __launch_bounds__(256) void k_atr_mfma(const T* __restrict__ A, const
   const T* ap = A + (sb * 4 + q) * n + col0 + 4 * i;
   const T* rp = R + (sb * 4 + q) * L + i;
 
-  C acc[4][NT];
 #pragma unroll
   for (int e = 0; e < 4; ++e)
 #pragma unroll
@@ -552,33 +556,97 @@ __global__ __launch_bounds__(256) void k_atr_mfma(const T* __restrict__ A, const
 
   if (WL == 0) {
 #pragma unroll
-    for (int s = 1; s < 4; ++s) {
-      __syncthreads();
-      if (wave == s) {
+    for (int e = 0; e < 4; ++e)
 #pragma unroll
-        for (int e = 0; e < 4; ++e)
+      for (int nt = 0; nt < NT; ++nt) red[wave][e * NT + nt][lane] = acc[e][nt];
+    __syncthreads();
 #pragma unroll
-          for (int nt = 0; nt < NT; ++nt) red[e * NT + nt][lane] = acc[e][nt];
-      }
-      __syncthreads();
-      if (wave == 0) {
+    for (int nt = 0; nt < NT; ++nt) {
+      C v = red[0][wave * NT + nt][lane];
 #pragma unroll
-        for (int e = 0; e < 4; ++e)
+      for (int s = 1; s < 4; ++s) v += red[s][wave * NT + nt][lane];
 #pragma unroll
-          for (int nt = 0; nt < NT; ++nt) acc[e][nt] += red[e * NT + nt][lane];
-      }
+      for (int e = 0; e < 4; ++e)
+        if (e == wave) acc[e][nt] = v;   // static register index; e == wave selects one
     }
-    if (wave != 0) return;
   }
+  return col0;
+}
+
+template <typename T, int NT, int PF, int WL, bool NTL>
+__global__ __launch_bounds__(256) void k_atr_mfma(const T* __restrict__ A, const T* __restrict__ R,
+                                                  T* __restrict__ Gp, int64_t m, int64_t n, int S) {
+  typedef MF<T> M;
+  constexpr int L = 16 * NT;
+  const int lane = threadIdx.x & 63;
+  const int wave = threadIdx.x >> 6;
+  const int i = lane & 15;
+  typename M::acc_t acc[4][NT];
+  const int64_t col0 = atr_panel<T, NT, PF, WL, NTL>(A, R, m, n, S, acc);
   T* gout = Gp + (int64_t)blockIdx.y * n * L;
 #pragma unroll
-  for (int e = 0; e < 4; ++e)
+  for (int e = 0; e < 4; ++e) {
+    if (WL == 0 && e != wave) continue;   // WL 0: wave w owns the rows e == w
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       const int64_t grow = col0 + 4 * M::row(lane, r) + e;
 #pragma unroll
       for (int nt = 0; nt < NT; ++nt) gout[grow * L + nt * 16 + i] = acc[e][nt][r];
     }
+  }
+}
+
+// ProxGD's line-search trial fused into A^T R (WL 0, one K split): once the block's LDS
+// reduction leaves each wave w the 16 gradient rows e == w of its panel — lane (i, q) holding
+// columns i and 16 + i of 4 rows, exactly the 16-lanes-per-row layout of k_prox_pgd — every
+// wave writes its rows of G and runs the trial on them (prox_pgd_row, the same arithmetic as
+// k_prox_pgd) with x = the thresholded iterate; the six trial sums are reduced over the grid.
+template <typename T, int NT, int PF, bool NTL>
+__global__ __launch_bounds__(256) void k_atr_prox(const T* __restrict__ A, const T* __restrict__ R,
+                                                  T* __restrict__ G, int64_t m, int64_t n,
+                                                  const T* __restrict__ x, T* __restrict__ p,
+                                                  T* __restrict__ pthr, T* __restrict__ z,
+                                                  double t_, double tmu_, double thres_, Red red) {
+  typedef MF<T> M;
+  constexpr int L = 16 * NT;
+  const int lane = threadIdx.x & 63;
+  const int wave = threadIdx.x >> 6;
+  const int i = lane & 15;
+  typename M::acc_t acc[4][NT];
+  const int64_t col0 = atr_panel<T, NT, PF, 0, NTL>(A, R, m, n, 1, acc);
+  double accr[6] = {0.0, 0.0, 0.0, -__builtin_inf(), 0.0, 0.0};
+  const T t = (T)t_, tmu = (T)tmu_, thres = (T)thres_;
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    if (e != wave) continue;   // wave w owns the rows e == w (4 per lane group)
+    T xa[4][NT];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int64_t row = col0 + 4 * M::row(lane, r) + e;
+#pragma unroll
+      for (int nt = 0; nt < NT; ++nt) xa[r][nt] = x[row * L + nt * 16 + i];
+    }
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int64_t row = col0 + 4 * M::row(lane, r) + e;
+      T gv[NT], pv[NT], pth[NT], zv[NT];
+      bool ok[NT];
+#pragma unroll
+      for (int nt = 0; nt < NT; ++nt) {
+        gv[nt] = acc[e][nt][r];
+        ok[nt] = true;
+        G[row * L + nt * 16 + i] = gv[nt];
+      }
+      prox_pgd_row<T, 16, NT>(xa[r], gv, ok, true, i, t, tmu, thres, pv, pth, zv, accr);
+#pragma unroll
+      for (int nt = 0; nt < NT; ++nt) {
+        p[row * L + nt * 16 + i] = pv[nt];
+        pthr[row * L + nt * 16 + i] = pth[nt];
+        z[row * L + nt * 16 + i] = zv[nt];
+      }
+    }
+  }
+  grid_reduce<6, 0x8u>(accr, red);
 }
 
 // ------------------------------------------------------------------------------------------
@@ -881,7 +949,9 @@ GemmPlan make_plan(int esize, int64_t m, int64_t n, int64_t l, int ax_variant) {
     const int64_t steps = m / 4;
     if (p.atr_wl == 0) {
       const int64_t blocks = n / 64;
-      const int64_t target = esize == 8 ? kTargetWaves : 2 * kTargetWaves;
+      // f64: one wave per SIMD is enough with the PF-8 ring (and S = 1 at n = 16384 lets the
+      // ProxGD trial fuse into the kernel); f32 wants 4 per SIMD
+      const int64_t target = esize == 8 ? kTargetWaves / 2 : 2 * kTargetWaves;
       p.atr_S = (int)clampi(cdiv(target, blocks * 4), 1,
                             std::max<int64_t>(1, std::min<int64_t>(kMaxSplit, steps / 16)));
     } else {
@@ -1135,7 +1205,42 @@ void launch_atr(const GemmPlan& p, const T* A, const T* R, T* Gp, hipStream_t st
 
 template void launch_ax<double>(const GemmPlan&, int, const double*, const double* const*, double*, const int*, int, hipStream_t);
 template void launch_ax<float>(const GemmPlan&, int, const float*, const float* const*, float*, const int*, int, hipStream_t);
+bool atr_prox_ok(const GemmPlan& p) {
+  return p.atr_kind == 1 && p.atr_wl == 0 && p.atr_S == 1 && (p.l == 16 || p.l == 32) &&
+         p.n % 64 == 0 && p.n / 64 <= kMaxBlocks;
+}
+
+template <typename T, int NT, int PF, bool NTL>
+static void atr_prox_go(const GemmPlan& p, const T* A, const T* R, T* G, const T* x, T* pp,
+                        T* pthr, T* z, double t, double mu, double thres, Red red, hipStream_t st) {
+  hipLaunchKernelGGL((k_atr_prox<T, NT, PF, NTL>), dim3((unsigned)(p.n / 64)), dim3(256), 0, st, A, R,
+                     G, p.m, p.n, x, pp, pthr, z, t, t * mu, thres, red);
+}
+template <typename T, int NT>
+static void atr_prox_nt(const GemmPlan& p, const T* A, const T* R, T* G, const T* x, T* pp,
+                        T* pthr, T* z, double t, double mu, double thres, Red red, hipStream_t st) {
+  switch (p.atr_ntl * 100 + p.atr_pf) {
+    case 4: atr_prox_go<T, NT, 4, false>(p, A, R, G, x, pp, pthr, z, t, mu, thres, red, st); break;
+    case 6: atr_prox_go<T, NT, 6, false>(p, A, R, G, x, pp, pthr, z, t, mu, thres, red, st); break;
+    case 104: atr_prox_go<T, NT, 4, true>(p, A, R, G, x, pp, pthr, z, t, mu, thres, red, st); break;
+    case 108: atr_prox_go<T, NT, 8, true>(p, A, R, G, x, pp, pthr, z, t, mu, thres, red, st); break;
+    default: atr_prox_go<T, NT, 8, false>(p, A, R, G, x, pp, pthr, z, t, mu, thres, red, st); break;
+  }
+}
+template <typename T>
+void launch_atr_prox(const GemmPlan& p, const T* A, const T* R, T* G, const T* x, T* pp, T* pthr,
+                     T* z, double t, double mu, double thres, Red red, hipStream_t st) {
+  if (p.l == 16) atr_prox_nt<T, 1>(p, A, R, G, x, pp, pthr, z, t, mu, thres, red, st);
+  else atr_prox_nt<T, 2>(p, A, R, G, x, pp, pthr, z, t, mu, thres, red, st);
+}
+
 template void launch_atr<double>(const GemmPlan&, const double*, const double*, double*, hipStream_t);
+template void launch_atr_prox<double>(const GemmPlan&, const double*, const double*, double*,
+                                      const double*, double*, double*, double*, double, double,
+                                      double, Red, hipStream_t);
+template void launch_atr_prox<float>(const GemmPlan&, const float*, const float*, float*,
+                                     const float*, float*, float*, float*, double, double, double,
+                                     Red, hipStream_t);
 template void launch_atr<float>(const GemmPlan&, const float*, const float*, float*, hipStream_t);
 
 }  // namespace glx

@@ -69,13 +69,13 @@ struct Carver {
 
 static int method_bufs(int method) {
   switch (method) {
-    case GLX_PROXGD: return 5;   // (x, x_thr), (p, p_thr), z
+    case GLX_PROXGD: return 7;   // (x, x_thr), (p, p_thr), z + two spares (speculative trial)
     case GLX_FPROXGD: return 6;  // (x_k, v_k, y) current + (x, v, y) of the trial
     case GLX_FGD: return 6;
     default: return 2;           // SGD / GD: x, thr(x)
   }
 }
-constexpr int kBufs = 6;
+constexpr int kBufs = 7;
 constexpr int kRes = 4;
 
 static void validate(const glx_problem* P, const glx_opts* O) {
@@ -113,7 +113,7 @@ class Session : public SessionBase {
     Carver c(ws);
     const int64_t nl = P.n * P.l, ml = P.m * P.l;
     const int nb = method_bufs(P.method);
-    T* bufs[kBufs] = {static_cast<T*>(P.x), nullptr, nullptr, nullptr, nullptr, nullptr};
+    T* bufs[kBufs] = {static_cast<T*>(P.x), nullptr, nullptr, nullptr, nullptr, nullptr, nullptr};
     for (int i = 1; i < nb; ++i) bufs[i] = static_cast<T*>(c.take(sizeof(T) * nl));
     T* res[kRes];
     for (int i = 0; i < kRes; ++i) res[i] = static_cast<T*>(c.take(sizeof(T) * ml));
@@ -170,6 +170,10 @@ class Session : public SessionBase {
     spin_readback_ = !(rb && std::strcmp(rb, "sync") == 0);
     const char* sp = std::getenv("GLX_SPEC_GRAD");
     spec_off_env_ = (sp && std::strcmp(sp, "0") == 0);
+    const char* fz = std::getenv("GLX_FUSED_TRIAL");
+    fused_ok_ = P.method == GLX_PROXGD && comm_ == nullptr && atr_prox_ok(plan_) &&
+                (O.step_type == GLX_STEP_LINE_SEARCH || O.step_type == GLX_STEP_FIXED) &&
+                !(fz && std::strcmp(fz, "0") == 0);
     GLX_HIP(hipMemsetAsync(ticket_, 0, kTicketBytes, st_));
     GLX_HIP(hipMemsetAsync(flag_, 0, 256, st_));
     GLX_HIP(hipMemsetAsync(scal_, 0, sizeof(double) * NSCAL, st_));
@@ -248,6 +252,7 @@ class Session : public SessionBase {
     state_valid_ = false;
     y_ready_ = false;
     spec_ready_ = false;
+    spec_trial_ready_ = false;
   }
 
   void kernel_time(int kind, int64_t* launches, double* ms) override {
@@ -464,6 +469,7 @@ class Session : public SessionBase {
   // :129, exact), gx_ = 1/2 ||R_[irg_]||^2, f_cur_/s_cur_ = objective and sparsity of x.
   void proxgd_prologue(bool have_thr) {
     spec_ready_ = false;   // the gradient is recomputed from the rebuilt residual
+    spec_trial_ready_ = false;
     if (!have_thr) {
       launch_threshold<T>(X_[ix_], X_[ixt_], nl_, O_.thres, flag_, ++epoch_, st_);
       check_launch();
@@ -482,27 +488,45 @@ class Session : public SessionBase {
     state_valid_ = true;
   }
 
+  // First-trial sources: (1) a speculative fused kernel of the previous iteration left G and
+  // this trial ready (same mu and t); (2) otherwise A^T r with the trial fused into it
+  // (launch_atr_prox); (3) otherwise the gradient (speculative or not) and k_prox_pgd.
   void iter_proxgd() {
     if (!state_valid_) proxgd_prologue(thr_from_trial_);
     record(f_cur_, s_cur_);
-    if (stop_rule()) { end_phase(); return; }     // x and its state carry over to the next phase
-    const std::pair<const T*, int> g = take_gradient(R_[irg_]);
+    if (stop_rule()) { end_phase(); return; }
+    const bool ls = O_.step_type == GLX_STEP_LINE_SEARCH && O_.ls_maxit > 0;
+    const double t0 = ls ? O_.alpha0 : schedule(inner_);
+    std::pair<const T*, int> g{nullptr, 0};
+    bool first_done = false;
+    if (spec_trial_ready_) {
+      spec_trial_ready_ = false;
+      use_gset(spec_set_);
+      g = {G_, 1};
+      first_done = (spec_trial_mu_ == mu_ && spec_trial_t_ == t0);   // else: a phase change
+    } else if (fused_ok_) {
+      atr_prox(R_[irg_], gset_, X_[ixt_], ip_, ipt_, iz_, t0);
+      g = {G_, 1};
+      first_done = true;
+    } else {
+      g = take_gradient(R_[irg_]);
+    }
     const T* xt = X_[ixt_];
     const bool exact = O_.exact_objective != 0;
     // trial residual buffers: never the gradient residual
     const int rz = (irg_ + 1) % kRes, rpt = (irg_ + 2) % kRes, rp = (irg_ + 3) % kRes;
     double t;
-    bool accepted = false;
+    bool accepted = false, spec_trial = false;
     auto trial = [&](double tt, bool first) {
       launch_prox_pgd<T>(xt, first ? g.first : G_, first ? g.second : 1,
                          (first && g.first != G_) ? G_ : nullptr, X_[ip_], X_[ipt_], X_[iz_], n_,
                          l_, tt, mu_, O_.thres, red(S_TR), st_);
       check_launch();
     };
-    if (O_.step_type == GLX_STEP_LINE_SEARCH && O_.ls_maxit > 0) {
-      t = O_.alpha0;
+    if (ls) {
+      t = t0;
       for (int it = 0; it < O_.ls_maxit; ++it) {
-        trial(t, it == 0);
+        if (!(it == 0 && first_done)) trial(t, it == 0);
         // one pass: g(z) for the test (:91) + the next iteration's residuals A p_thr (and A p)
         const T* xs[3] = {X_[iz_], X_[ipt_], X_[ip_]};
         T* rs[3] = {R_[rz], R_[rpt], R_[rp]};
@@ -510,27 +534,33 @@ class Session : public SessionBase {
         residuals(exact ? 3 : 2, xs, rs, S_RT, X_[ip_], scal_ + S_TR + 3, nullptr, 0.0, &seq);
         const bool spec = want_spec(it);
         std::pair<const T*, int> sg;
-        if (spec) sg = gradient(R_[rpt], 1 - gset_);   // gradient at the candidate p_thr
+        if (spec && fused_ok_) {
+          // the next iteration's A^T r and first trial at the candidate p_thr, into the other
+          // gradient set and the spare buffers (z is free once this trial's A@X has read it)
+          atr_prox(R_[rpt], 1 - gset_, X_[ipt_], if1_, if2_, iz_, O_.alpha0);
+          spec_trial = true;
+        } else if (spec) {
+          sg = gradient(R_[rpt], 1 - gset_);   // gradient at the candidate p_thr
+        }
         wait_readback(seq);
         const double gz = 0.5 * hs_[S_RT];
         if (gz <= gx_ - t * hs_[S_TR + 0] + 0.5 * t * hs_[S_TR + 1]) {
           accepted = true;
-          if (spec) { spec_ready_ = true; spec_g_ = sg; spec_set_ = 1 - gset_; }
+          if (spec && !spec_trial) { spec_ready_ = true; spec_g_ = sg; spec_set_ = 1 - gset_; }
           spec_on_ = (it == 0);
           break;
         }
+        spec_trial = false;
         spec_on_ = false;
         t *= O_.ls_coeff;
       }
       // after ls_maxit failures the reference returns alpha0*coeff^maxit untested (:99)
       if (!accepted) trial(t, false);
     } else {
-      t = O_.step_type == GLX_STEP_LINE_SEARCH ? O_.alpha0 : schedule(inner_);
-      trial(t, true);
+      t = t0;
+      if (!first_done) trial(t, true);
     }
-    std::swap(ix_, ip_);                          // x = prox(x - t grad, t)  (:132)
-    std::swap(ixt_, ipt_);
-    if (accepted) {
+    if (accepted) {   // the packet holds the accepted trial's sums (read before any speculation)
       stats_[0] += hs_[S_TR + 4];
       stats_[1] += hs_[S_TR + 5];
       stats_[2] += 1;
@@ -546,6 +576,30 @@ class Session : public SessionBase {
       state_valid_ = false;
       thr_from_trial_ = true;                     // x_thr came out of the trial kernel
     }
+    // x = prox(x - t grad, t)  (:132)
+    if (spec_trial) {   // x <- p, x_thr <- p_thr, the speculative outputs become the trial's
+      const int ox = ix_, oxt = ixt_;
+      ix_ = ip_; ixt_ = ipt_; ip_ = if1_; ipt_ = if2_;   // z's buffer already holds the new z
+      if1_ = ox; if2_ = oxt;
+      spec_trial_ready_ = true;
+      spec_set_ = 1 - gset_;
+      spec_trial_mu_ = mu_;
+      spec_trial_t_ = O_.alpha0;
+    } else {
+      std::swap(ix_, ip_);
+      std::swap(ixt_, ipt_);
+    }
+  }
+
+  // A^T r fused with a ProxGD trial at x (gradient set `set`, outputs X_[op], X_[opt], X_[oz])
+  void atr_prox(const T* r, int set, const T* x, int op, int opt, int oz, double t) {
+    hipEvent_t e0 = nullptr, e1 = nullptr;
+    if (O_.profile) { e0 = get_event(); e1 = get_event(); GLX_HIP(hipEventRecord(e0, st_)); }
+    launch_atr_prox<T>(plan_, A_, r, Gs_[set], x, X_[op], X_[opt], X_[oz], t, mu_, O_.thres,
+                       red(S_TR), st_);
+    check_launch();
+    if (O_.profile) { GLX_HIP(hipEventRecord(e1, st_)); ev_[1].push_back({e0, e1}); }
+    ++atr_calls_;
   }
 
   // ------------------------------------------------------------------ FProxGD / FGD
@@ -679,7 +733,7 @@ class Session : public SessionBase {
   int64_t m_ = 0, n_ = 0, l_ = 0, nl_ = 0, ml_ = 0;
   const T* A_ = nullptr;
   const T* B_ = nullptr;
-  T* X_[kBufs] = {nullptr, nullptr, nullptr, nullptr, nullptr, nullptr};
+  T* X_[kBufs] = {nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr};
   T* R_[kRes] = {nullptr, nullptr, nullptr, nullptr};
   T *G_ = nullptr, *Gp_ = nullptr, *Pp_ = nullptr;
   T* Gs_[2] = {nullptr, nullptr};
@@ -698,12 +752,16 @@ class Session : public SessionBase {
   int epoch_ = 0;
   // buffer roles
   int ix_ = 0, iv_ = 1, iy_ = 2, ic_ = 3, ivn_ = 4, iyn_ = 5;   // FISTA
-  int ixt_ = 1, ip_ = 2, ipt_ = 3, iz_ = 4;                      // ProxGD
+  int ixt_ = 1, ip_ = 2, ipt_ = 3, iz_ = 4, if1_ = 5, if2_ = 6;   // ProxGD (+ two spares)
   int irg_ = 0, iry_ = 0;
   bool state_valid_ = false, thr_from_trial_ = false, y_ready_ = false, gy_pending_ = false;
   // speculative gradient (take_gradient)
   int gset_ = 0, spec_set_ = 1;
   bool spec_on_ = true, spec_ready_ = false, spec_off_env_ = false;
+  // ProxGD trial fused into A^T r (launch_atr_prox): fused_ok_ = the plan allows it; a
+  // speculative fused kernel leaves G and the next iteration's first trial (t, mu) ready
+  bool fused_ok_ = false, spec_trial_ready_ = false;
+  double spec_trial_mu_ = 0, spec_trial_t_ = 0;
   std::pair<const T*, int> spec_g_{nullptr, 0};
   double gx_ = 0, gy_sq_ = 0;
   // algorithm state

@@ -1,0 +1,80 @@
+"""The ProxGD trial fused into A^T r (k_atr_prox) and its speculative use.
+
+At (m, n, l) = (256, 16384, 32) fp64 the planner gives A^T r one K split, so the solver runs
+the first line-search trial of every iteration inside the gradient kernel's epilogue and, after
+an accepted first trial, queues the next iteration's fused kernel before the host has read
+the trial's scalars. Per element the fused epilogue does exactly k_prox_pgd's arithmetic on the
+same gradient, so the iterate must be bit-identical to the unfused path (GLX_FUSED_TRIAL=0);
+only the grid-sum order of the trial's scalars differs (ulp-level f_hist differences). Against
+the NumPy oracle the bar is the north-star 1e-8 on the objective.
+"""
+import numpy as np
+import pytest
+
+torch = pytest.importorskip("torch")
+
+pytestmark = pytest.mark.gpu
+
+SHAPE = (256, 16384, 32)
+
+
+def _instance():
+    from oracle import numpy_ref
+    m, n, l = SHAPE
+    A, b, u, x0, mu = numpy_ref.gen_data(m, n, l, 2024)
+    return A, b, x0, mu, numpy_ref.step_size_for(m, n)
+
+
+def _run(monkeypatch, fused, spec, opts):
+    import glx
+    monkeypatch.setenv("GLX_FUSED_TRIAL", "1" if fused else "0")
+    monkeypatch.setenv("GLX_SPEC_GRAD", "1" if spec else "0")
+    A, b, x0, mu, _ = _instance()
+    At, bt, xt = (torch.from_numpy(a).cuda() for a in (A, b, x0))
+    s = glx.Session("gl_ProxGD_primal", xt, At, bt, mu, opts)
+    s.run(0)
+    res = s.finish()
+    s.close()
+    torch.cuda.synchronize()
+    return xt.cpu().numpy(), res
+
+
+def test_plan_fuses_at_this_shape():
+    from glx import _lib
+    d = _lib.plan_describe(_lib.GLX_F64, *SHAPE)
+    assert "atr=k_atr_mfma<WL0" in d and d.rstrip().endswith("S=1"), d
+
+
+@pytest.mark.parametrize("spec", [False, True])
+def test_fused_trial_bit_identical_iterate(monkeypatch, spec):
+    _, _, _, _, alpha0 = _instance()
+    opts = {"alpha0": alpha0, "maxit": 40}
+    x_f, r_f = _run(monkeypatch, True, spec, opts)
+    x_u, r_u = _run(monkeypatch, False, False, opts)
+    assert r_f["k"] == r_u["k"]
+    assert np.array_equal(x_f, x_u)
+    np.testing.assert_allclose(np.asarray(r_f["f_hist"]), np.asarray(r_u["f_hist"]), rtol=1e-13)
+    if spec:   # every accepted first trial queued the next fused kernel
+        assert r_f["atr_calls"] >= r_u["atr_calls"]
+
+
+def test_fused_trial_matches_oracle(monkeypatch):
+    from oracle import numpy_ref
+    A, b, x0, mu, alpha0 = _instance()
+    opts = {"alpha0": alpha0, "maxit": 25}
+    x_g, r_g = _run(monkeypatch, True, True, opts)
+    x_r, k_r, out_r = numpy_ref.gl_ProxGD_primal(x0.copy(), A, b, mu, dict(opts))
+    assert r_g["k"] == k_r
+    f_g = np.asarray(r_g["f_hist"], dtype=float)
+    f_r = np.asarray(out_r["f_hist"], dtype=float)
+    assert np.max(np.abs(f_g - f_r) / np.abs(f_r)) < 1e-8
+    assert abs(float(r_g["fval"]) - float(out_r["fval"])) <= 1e-8 * abs(float(out_r["fval"]))
+
+
+def test_fused_trial_fixed_step(monkeypatch):
+    _, _, _, _, alpha0 = _instance()
+    opts = {"alpha0": alpha0, "maxit": 20, "step_type": "fixed"}
+    x_f, r_f = _run(monkeypatch, True, True, opts)
+    x_u, r_u = _run(monkeypatch, False, False, opts)
+    assert r_f["k"] == r_u["k"]
+    assert np.array_equal(x_f, x_u)
