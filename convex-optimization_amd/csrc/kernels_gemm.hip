@@ -468,6 +468,353 @@ __global__ __launch_bounds__(64 * WAVES) void k_ax_lds(const T* __restrict__ A,
 }
 
 // ------------------------------------------------------------------------------------------
+// A @ X, kind 7: kind 5 with a barrier every BAR chunks instead of every chunk. X(c+BAR) is
+// written at chunk c into slot (c+BAR) % (2 BAR) and read at chunk c+BAR: a barrier ends every
+// BAR chunks, so one lies between each write and its read (RAW), and between the last read of
+// a slot (chunk c+BAR-2BAR) and its next write (chunk c) (WAR). Waves then drift up to BAR
+// chunks apart, which absorbs their different A-load latencies. PF (A and X register rings) is a
+// multiple of BAR and > BAR.
+// ------------------------------------------------------------------------------------------
+template <typename T, int MT, int NT, int NSRC, int PF, int VPL, int WAVES, int BAR>
+__global__ __launch_bounds__(64 * WAVES) void k_ax_lds3(const T* __restrict__ A,
+                                                       const T* __restrict__ X0,
+                                                       const T* __restrict__ X1,
+                                                       const T* __restrict__ X2,
+                                                       T* __restrict__ P, int64_t m, int64_t n,
+                                                       int64_t chunks, int S, int gx, int xmap,
+                                                       const int* __restrict__ gate, int epoch) {
+  typedef MF<T> M;
+  typedef typename M::vec_t V;
+  typedef typename M::acc_t C;
+  constexpr int E = M::E;
+  constexpr int EL = VPL * E;
+  constexpr int CK = 4 * EL;
+  constexpr int L = 16 * NT;
+  constexpr int NC = NT * NSRC;
+  constexpr int LP = L + (sizeof(T) == 8 ? 4 : 2);
+  constexpr bool W16 = (LP * sizeof(T)) % 16 == 0;
+  constexpr int XCH = NSRC * CK * LP;
+  constexpr int NTHR = 64 * WAVES;
+  constexpr int XV = NSRC * CK * L / E;
+  constexpr int XPT = (XV + NTHR - 1) / NTHR;
+  constexpr bool XFULL = (XV % NTHR) == 0;
+  constexpr int VPR = L / E;
+  constexpr int NSLOT = 2 * BAR;
+  static_assert(PF % BAR == 0 && PF > BAR, "ring depth: a multiple of BAR, more than BAR");
+  __shared__ __attribute__((aligned(16))) T xs[NSLOT][XCH];
+  if (!gate_live(gate, epoch)) return;
+  int bx, by;
+  if (!ax_block(xmap, gx, S, bx, by)) return;
+
+  const int lane = threadIdx.x & 63;
+  const int wave = threadIdx.x >> 6;
+  const int i = lane & 15, q = lane >> 4;
+  const int64_t row0 = (int64_t)bx * (16 * MT * WAVES) + (int64_t)wave * (16 * MT);
+  const int64_t cb = chunks * by / S, ce = chunks * (by + 1) / S;
+  const int64_t nch = ce - cb;
+  if (nch <= 0) return;   // block-uniform
+
+  const T* ap[MT];
+#pragma unroll
+  for (int mt = 0; mt < MT; ++mt) {
+    int64_t r = row0 + mt * 16 + i;
+    r = r < m ? r : m - 1;
+    ap[mt] = A + r * n + cb * CK + (int64_t)q * EL;
+  }
+  const T* xg[XPT];
+  int xo[XPT];
+  bool xon[XPT];
+#pragma unroll
+  for (int j = 0; j < XPT; ++j) {
+    const int v = threadIdx.x + NTHR * j;
+    xon[j] = XFULL || v < XV;
+    const int vv = xon[j] ? v : 0;
+    const int src = vv / (CK * VPR), rem = vv % (CK * VPR);
+    const int k = rem / VPR, c = (rem % VPR) * E;
+    const T* xb = src == 0 ? X0 : (src == 1 ? X1 : X2);
+    xg[j] = xb + (cb * CK + k) * L + c;
+    xo[j] = src * CK * LP + k * LP + c;
+  }
+
+  C acc[MT][NC];
+#pragma unroll
+  for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+    for (int c = 0; c < NC; ++c) acc[mt][c] = C{};
+
+  V a[PF][MT][VPL];
+  V xr[PF][XPT];
+  auto load_x = [&](V (&dst)[XPT], int64_t off) {
+    off = off < nch ? off : nch - 1;
+#pragma unroll
+    for (int j = 0; j < XPT; ++j)
+      if (XFULL || xon[j]) dst[j] = *reinterpret_cast<const V*>(xg[j] + off * CK * L);
+  };
+  auto load_a_tile = [&](V (&dst)[VPL], int mt, int64_t off) {
+    off = off < nch ? off : nch - 1;
+#pragma unroll
+    for (int v = 0; v < VPL; ++v) dst[v] = load_vec<T, false>(ap[mt] + off * CK + v * E);
+  };
+  auto put_x = [&](int slot, const V (&src)[XPT]) {
+#pragma unroll
+    for (int j = 0; j < XPT; ++j)
+      if (XFULL || xon[j]) lds_put<T, W16>(&xs[slot][xo[j]], src[j]);
+  };
+  auto read_x = [&](int slot, T (&dst)[NC][EL]) {
+#pragma unroll
+    for (int cc = 0; cc < NC; ++cc) {
+      const int src = cc / NT, nt = cc % NT;
+      const T* xp = &xs[slot][src * CK * LP + q * EL * LP + nt * 16 + i];
+#pragma unroll
+      for (int e = 0; e < EL; ++e) dst[cc][e] = xp[e * LP];
+    }
+  };
+  auto mma_tile = [&](int mt, const V (&av)[VPL], const T (&x)[NC][EL]) {
+#pragma unroll
+    for (int v = 0; v < VPL; ++v)
+#pragma unroll
+      for (int e = 0; e < E; ++e)
+#pragma unroll
+        for (int cc = 0; cc < NC; ++cc)
+          acc[mt][cc] = M::mma(av[v][e], x[cc][v * E + e], acc[mt][cc]);
+  };
+
+  // prologue: rings hold chunks 0..PF-1; X(0..BAR-1) staged into slots 0..BAR-1, their X
+  // registers refilled with X(PF..PF+BAR-1)
+#pragma unroll
+  for (int p = 0; p < PF; ++p) {
+    load_x(xr[p], p);
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt) load_a_tile(a[p][mt], mt, p);
+  }
+#pragma unroll
+  for (int p = 0; p < BAR; ++p) {
+    put_x(p, xr[p]);
+    load_x(xr[p], PF + p);
+  }
+  __syncthreads();
+
+  int64_t c0 = 0;
+  for (; c0 + PF <= nch; c0 += PF) {
+#pragma unroll
+    for (int p = 0; p < PF; ++p) {
+      const int64_t c = c0 + p;
+      put_x((int)((c + BAR) % NSLOT), xr[(p + BAR) % PF]);   // X(c+BAR); past the end harmless
+      load_x(xr[(p + BAR) % PF], c + BAR + PF);
+      T xv[NC][EL];
+      read_x((int)(c % NSLOT), xv);
+#pragma unroll
+      for (int mt = 0; mt < MT; ++mt) {
+        mma_tile(mt, a[p][mt], xv);
+        load_a_tile(a[p][mt], mt, c + PF);
+      }
+      if (p % BAR == BAR - 1) __syncthreads();
+    }
+  }
+  // tail (fewer than PF chunks): end every chunk with a barrier, which keeps both rules
+#pragma unroll
+  for (int p = 0; p < PF - 1; ++p) {
+    const int64_t c = c0 + p;
+    if (c < nch) {
+      if (c + BAR < nch) put_x((int)((c + BAR) % NSLOT), xr[(p + BAR) % PF]);
+      T xv[NC][EL];
+      read_x((int)(c % NSLOT), xv);
+#pragma unroll
+      for (int mt = 0; mt < MT; ++mt) mma_tile(mt, a[p][mt], xv);
+      __syncthreads();
+    }
+  }
+
+#pragma unroll
+  for (int sr = 0; sr < NSRC; ++sr) {
+    T* pout = P + ((int64_t)sr * S + by) * m * L;
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int64_t row = row0 + mt * 16 + M::row(lane, r);
+        if (row < m) {
+#pragma unroll
+          for (int nt = 0; nt < NT; ++nt) pout[row * L + nt * 16 + i] = acc[mt][sr * NT + nt][r];
+        }
+      }
+  }
+}
+
+// ------------------------------------------------------------------------------------------
+// A @ X, kind 6: kind 5 with the X operand software-pipelined through a 3-slot LDS ring. At
+// chunk c a wave writes X(c+2) (loaded PF-2 chunks earlier) into slot (c+2) % 3, reads X(c+1)
+// (written at chunk c-1, visible since the last barrier) from slot (c+1) % 3 into the second
+// of two register sets, and runs chunk c's MFMAs on the first set, so the MFMAs after a barrier
+// never wait on LDS latency (kind 5: all waves read X(c) right after the barrier, an MFMA-pipe
+// bubble per chunk). One barrier per chunk; the slot written at chunk c was last read at chunk
+// c-2, before the barrier of chunk c-2. PF is the depth of both register rings (even, >= 4).
+// ------------------------------------------------------------------------------------------
+template <typename T, int MT, int NT, int NSRC, int PF, int VPL, int WAVES>
+__global__ __launch_bounds__(64 * WAVES) void k_ax_lds2(const T* __restrict__ A,
+                                                       const T* __restrict__ X0,
+                                                       const T* __restrict__ X1,
+                                                       const T* __restrict__ X2,
+                                                       T* __restrict__ P, int64_t m, int64_t n,
+                                                       int64_t chunks, int S, int gx, int xmap,
+                                                       const int* __restrict__ gate, int epoch) {
+  typedef MF<T> M;
+  typedef typename M::vec_t V;
+  typedef typename M::acc_t C;
+  constexpr int E = M::E;
+  constexpr int EL = VPL * E;
+  constexpr int CK = 4 * EL;
+  constexpr int L = 16 * NT;
+  constexpr int NC = NT * NSRC;
+  constexpr int LP = L + (sizeof(T) == 8 ? 4 : 2);
+  constexpr bool W16 = (LP * sizeof(T)) % 16 == 0;
+  constexpr int XCH = NSRC * CK * LP;
+  constexpr int NTHR = 64 * WAVES;
+  constexpr int XV = NSRC * CK * L / E;
+  constexpr int XPT = (XV + NTHR - 1) / NTHR;
+  constexpr bool XFULL = (XV % NTHR) == 0;
+  constexpr int VPR = L / E;
+  static_assert(PF >= 4 && PF % 2 == 0, "X(c+2) is written at chunk c; register sets alternate");
+  __shared__ __attribute__((aligned(16))) T xs[3][XCH];
+  if (!gate_live(gate, epoch)) return;
+  int bx, by;
+  if (!ax_block(xmap, gx, S, bx, by)) return;
+
+  const int lane = threadIdx.x & 63;
+  const int wave = threadIdx.x >> 6;
+  const int i = lane & 15, q = lane >> 4;
+  const int64_t row0 = (int64_t)bx * (16 * MT * WAVES) + (int64_t)wave * (16 * MT);
+  const int64_t cb = chunks * by / S, ce = chunks * (by + 1) / S;
+  const int64_t nch = ce - cb;
+  if (nch <= 0) return;   // block-uniform
+
+  const T* ap[MT];
+#pragma unroll
+  for (int mt = 0; mt < MT; ++mt) {
+    int64_t r = row0 + mt * 16 + i;
+    r = r < m ? r : m - 1;
+    ap[mt] = A + r * n + cb * CK + (int64_t)q * EL;
+  }
+  const T* xg[XPT];
+  int xo[XPT];
+  bool xon[XPT];
+#pragma unroll
+  for (int j = 0; j < XPT; ++j) {
+    const int v = threadIdx.x + NTHR * j;
+    xon[j] = XFULL || v < XV;
+    const int vv = xon[j] ? v : 0;
+    const int src = vv / (CK * VPR), rem = vv % (CK * VPR);
+    const int k = rem / VPR, c = (rem % VPR) * E;
+    const T* xb = src == 0 ? X0 : (src == 1 ? X1 : X2);
+    xg[j] = xb + (cb * CK + k) * L + c;
+    xo[j] = src * CK * LP + k * LP + c;
+  }
+
+  C acc[MT][NC];
+#pragma unroll
+  for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+    for (int c = 0; c < NC; ++c) acc[mt][c] = C{};
+
+  V a[PF][MT][VPL];
+  V xr[PF][XPT];
+  T xv[2][NC][EL];
+  auto load_x = [&](V (&dst)[XPT], int64_t off) {
+    off = off < nch ? off : nch - 1;
+#pragma unroll
+    for (int j = 0; j < XPT; ++j)
+      if (XFULL || xon[j]) dst[j] = *reinterpret_cast<const V*>(xg[j] + off * CK * L);
+  };
+  auto load_a_tile = [&](V (&dst)[VPL], int mt, int64_t off) {
+    off = off < nch ? off : nch - 1;
+#pragma unroll
+    for (int v = 0; v < VPL; ++v) dst[v] = load_vec<T, false>(ap[mt] + off * CK + v * E);
+  };
+  auto put_x = [&](int slot, const V (&src)[XPT]) {
+#pragma unroll
+    for (int j = 0; j < XPT; ++j)
+      if (XFULL || xon[j]) lds_put<T, W16>(&xs[slot][xo[j]], src[j]);
+  };
+  auto read_x = [&](int slot, T (&dst)[NC][EL]) {
+#pragma unroll
+    for (int cc = 0; cc < NC; ++cc) {
+      const int src = cc / NT, nt = cc % NT;
+      const T* xp = &xs[slot][src * CK * LP + q * EL * LP + nt * 16 + i];
+#pragma unroll
+      for (int e = 0; e < EL; ++e) dst[cc][e] = xp[e * LP];
+    }
+  };
+  auto mma_tile = [&](int mt, const V (&av)[VPL], const T (&x)[NC][EL]) {
+#pragma unroll
+    for (int v = 0; v < VPL; ++v)
+#pragma unroll
+      for (int e = 0; e < E; ++e)
+#pragma unroll
+        for (int cc = 0; cc < NC; ++cc)
+          acc[mt][cc] = M::mma(av[v][e], x[cc][v * E + e], acc[mt][cc]);
+  };
+
+  // prologue: rings hold chunks 0..PF-1; X(0), X(1) staged; X registers of those two slots
+  // refilled with X(PF), X(PF+1); X(0) read into register set 0
+#pragma unroll
+  for (int p = 0; p < PF; ++p) {
+    load_x(xr[p], p);
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt) load_a_tile(a[p][mt], mt, p);
+  }
+  put_x(0, xr[0]);
+  put_x(1, xr[1]);
+  load_x(xr[0], PF);
+  load_x(xr[1], PF + 1);
+  __syncthreads();
+  read_x(0, xv[0]);
+
+  int64_t c0 = 0;
+  for (; c0 + PF <= nch; c0 += PF) {
+#pragma unroll
+    for (int p = 0; p < PF; ++p) {
+      const int64_t c = c0 + p;
+      const int sw = (int)((c + 2) % 3), sr = (int)((c + 1) % 3);
+      put_x(sw, xr[(p + 2) % PF]);             // X(c+2); past the end: a harmless re-write
+      load_x(xr[(p + 2) % PF], c + 2 + PF);
+      read_x(sr, xv[(p + 1) & 1]);             // X(c+1) for the next chunk
+#pragma unroll
+      for (int mt = 0; mt < MT; ++mt) {
+        mma_tile(mt, a[p][mt], xv[p & 1]);
+        load_a_tile(a[p][mt], mt, c + PF);     // consumed in place, refilled in place
+      }
+      __syncthreads();
+    }
+  }
+#pragma unroll
+  for (int p = 0; p < PF - 1; ++p) {   // tail: fewer than PF chunks, data already in the rings
+    const int64_t c = c0 + p;
+    if (c < nch) {
+      if (c + 2 < nch) put_x((int)((c + 2) % 3), xr[(p + 2) % PF]);
+      if (c + 1 < nch) read_x((int)((c + 1) % 3), xv[(p + 1) & 1]);
+#pragma unroll
+      for (int mt = 0; mt < MT; ++mt) mma_tile(mt, a[p][mt], xv[p & 1]);
+      __syncthreads();
+    }
+  }
+
+#pragma unroll
+  for (int sr = 0; sr < NSRC; ++sr) {
+    T* pout = P + ((int64_t)sr * S + by) * m * L;
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int64_t row = row0 + mt * 16 + M::row(lane, r);
+        if (row < m) {
+#pragma unroll
+          for (int nt = 0; nt < NT; ++nt) pout[row * L + nt * 16 + i] = acc[mt][sr * NT + nt][r];
+        }
+      }
+  }
+}
+
+// ------------------------------------------------------------------------------------------
 // A^T R on MFMA: a wave owns 64 columns of A (= 64 rows of G) x NT 16-col tiles of G.
 //   WL = 0: a block = one 64-column panel, its 4 waves split the block's rows (LDS-reduced);
 //   WL = 1: a block = four adjacent panels (256 columns) sharing one row range, so the four
@@ -833,7 +1180,8 @@ static int axb_default(int nsrc, int esize) {
   return esize == 8 ? 52228 : 52324;
 }
 
-static constexpr int kLdsCodes[] = {52224, 52324, 52228, 52328, 52218, 54224, 52214, 54214};
+static constexpr int kLdsCodes[] = {52224, 52324, 52228, 52328, 52218, 54224, 52214, 54214,
+                                     52428, 62428, 62424, 62418, 72428, 72424, 72828};
 static bool lds_code_ok(int c, int64_t n, int64_t l, int esize) {
   bool known = false;
   for (int k : kLdsCodes) known |= (k == c);
@@ -913,14 +1261,14 @@ GemmPlan make_plan(int esize, int64_t m, int64_t n, int64_t l, int ax_variant) {
     int S = p.ax_S;
     if (p.ax_kind == 3) {
       code = 0;
-    } else if (code / 10000 == 5) {
+    } else if (code / 10000 >= 5 && code / 10000 <= 7) {
       if (lds_code_ok(code, n, l, esize)) S = lds_split(esize, m, n, code);
       else code = ns == 2 ? 1420 : 1220;
     } else if (code >= 10000 && n % (4 * E * (code / 10000)) != 0) {
       code = ns == 2 ? 1420 : 1220;
     }
     const int s_axb = env_int("GLX_AXB_S", 0);
-    if (s_axb > 0 && code / 10000 == 5) S = (int)std::min<int64_t>(s_axb, kMaxSplit);
+    if (s_axb > 0 && code / 10000 >= 5 && code / 10000 <= 7) S = (int)std::min<int64_t>(s_axb, kMaxSplit);
     p.axb_code[ns] = code;
     p.axb_S[ns] = S;
   }
@@ -970,8 +1318,10 @@ static std::string ax_name(const GemmPlan& p, int nsrc) {
   char buf[128];
   if (p.ax_kind == 3 || code == 0) {
     std::snprintf(buf, sizeof buf, "k_ax_valu<LB%d,VEC%d> S=%d", p.ax_lb, p.ax_vec, ax_split(p, nsrc));
-  } else if (code / 10000 == 5) {
-    std::snprintf(buf, sizeof buf, "k_ax_lds<MT%d,PF%d,VPL%d,W%d> S=%d", (code / 1000) % 10,
+  } else if (code / 10000 >= 5 && code / 10000 <= 7) {
+    std::snprintf(buf, sizeof buf, "%s<MT%d,PF%d,VPL%d,W%d> S=%d",
+                  code / 10000 == 7 ? "k_ax_lds3" : (code / 10000 == 6 ? "k_ax_lds2" : "k_ax_lds"),
+                  (code / 1000) % 10,
                   (code / 100) % 10, (code / 10) % 10, code % 10, ax_split(p, nsrc));
   } else {
     const int vpl = code / 10000 ? code / 10000 : 1;
@@ -1047,13 +1397,55 @@ static void ax_lds_go(const GemmPlan& p, int S, const T* A, const T* const* X, T
                      p.n / (4 * VPL * E), S, gx, xmap, gate, epoch);
 }
 
-// kind 5 codes: 5 MT PF VPL WAVES
+template <typename T, int NT, int NSRC, int MT, int PF, int VPL, int WAVES, int BAR>
+static void ax_lds3_go(const GemmPlan& p, int S, const T* A, const T* const* X, T* P,
+                       const int* gate, int epoch, hipStream_t st) {
+  constexpr int E = 16 / sizeof(T);
+  const int gx = (int)cdiv(p.m, 16 * MT * WAVES);
+  const int xmap = (p.ax_xmap && ax_xmap_ok(S)) ? 1 : 0;
+  hipLaunchKernelGGL((k_ax_lds3<T, MT, NT, NSRC, PF, VPL, WAVES, BAR>),
+                     dim3((unsigned)ax_grid(xmap, gx, S)), dim3(64 * WAVES), 0, st, A, X[0], X[1],
+                     X[2], P, p.m, p.n, p.n / (4 * VPL * E), S, gx, xmap, gate, epoch);
+}
+
+template <typename T, int NT, int NSRC, int MT, int PF, int VPL, int WAVES>
+static void ax_lds2_go(const GemmPlan& p, int S, const T* A, const T* const* X, T* P,
+                       const int* gate, int epoch, hipStream_t st) {
+  constexpr int E = 16 / sizeof(T);
+  const int gx = (int)cdiv(p.m, 16 * MT * WAVES);
+  const int xmap = (p.ax_xmap && ax_xmap_ok(S)) ? 1 : 0;
+  hipLaunchKernelGGL((k_ax_lds2<T, MT, NT, NSRC, PF, VPL, WAVES>), dim3((unsigned)ax_grid(xmap, gx, S)),
+                     dim3(64 * WAVES), 0, st, A, X[0], X[1], X[2], P, p.m, p.n,
+                     p.n / (4 * VPL * E), S, gx, xmap, gate, epoch);
+}
+
+// kind 5 codes: 5 MT PF VPL WAVES; kind 6 (pipelined X): 6 MT PF VPL WAVES
 template <typename T, int NT, int NSRC>
 static void ax_lds_code(const GemmPlan& p, int code, int S, const T* A, const T* const* X, T* P,
                         const int* gate, int epoch, hipStream_t st) {
   switch (code) {
+    case 62428: ax_lds2_go<T, NT, NSRC, 2, 4, 2, 8>(p, S, A, X, P, gate, epoch, st); return;
+    case 62424: ax_lds2_go<T, NT, NSRC, 2, 4, 2, 4>(p, S, A, X, P, gate, epoch, st); return;
+    case 62418: ax_lds2_go<T, NT, NSRC, 2, 4, 1, 8>(p, S, A, X, P, gate, epoch, st); return;
+    case 72428: ax_lds3_go<T, NT, NSRC, 2, 4, 2, 8, 2>(p, S, A, X, P, gate, epoch, st); return;   // barrier / 2
+    case 72424: ax_lds3_go<T, NT, NSRC, 2, 4, 2, 4, 2>(p, S, A, X, P, gate, epoch, st); return;
+    case 72828: ax_lds3_go<T, NT, NSRC, 2, 8, 2, 8, 4>(p, S, A, X, P, gate, epoch, st); return;   // barrier / 4
+    case 52428: ax_lds_go<T, NT, NSRC, 2, 4, 2, 8>(p, S, A, X, P, gate, epoch, st); return;
+    default: break;
+  }
+  switch (code) {
     case 52324: ax_lds_go<T, NT, NSRC, 2, 3, 2, 4>(p, S, A, X, P, gate, epoch, st); break;
-    case 52228: ax_lds_go<T, NT, NSRC, 2, 2, 2, 8>(p, S, A, X, P, gate, epoch, st); break;
+    case 52228:
+      if constexpr (sizeof(T) == 8 && NT == 2 && NSRC == 2) {
+        switch (env_int("GLX_AXL_ABL", 0)) {   // timing ablations (results are wrong)
+          case 1: ax_lds_go<T, NT, NSRC, 2, 2, 2, 8, 1>(p, S, A, X, P, gate, epoch, st); return;
+          case 2: ax_lds_go<T, NT, NSRC, 2, 2, 2, 8, 2>(p, S, A, X, P, gate, epoch, st); return;
+          case 3: ax_lds_go<T, NT, NSRC, 2, 2, 2, 8, 3>(p, S, A, X, P, gate, epoch, st); return;
+          default: break;
+        }
+      }
+      ax_lds_go<T, NT, NSRC, 2, 2, 2, 8>(p, S, A, X, P, gate, epoch, st);
+      break;
     case 52328: ax_lds_go<T, NT, NSRC, 2, 3, 2, 8>(p, S, A, X, P, gate, epoch, st); break;
     case 52218: ax_lds_go<T, NT, NSRC, 2, 2, 1, 8>(p, S, A, X, P, gate, epoch, st); break;
     case 54224: ax_lds_go<T, NT, NSRC, 4, 2, 2, 4>(p, S, A, X, P, gate, epoch, st); break;
@@ -1079,7 +1471,7 @@ template <typename T, int NT>
 static void ax_mfma_nt(const GemmPlan& p, int nsrc, const T* A, const T* const* X, T* P,
                        const int* gate, int epoch, hipStream_t st) {
   const int code = p.axb_code[nsrc];
-  if (code / 10000 == 5) {
+  if (code / 10000 >= 5 && code / 10000 <= 7) {
     if (nsrc == 1) ax_lds_code<T, NT, 1>(p, code, p.axb_S[1], A, X, P, gate, epoch, st);
     else if (nsrc == 2) ax_lds_code<T, NT, 2>(p, code, p.axb_S[2], A, X, P, gate, epoch, st);
     else ax_lds_code<T, NT, 3>(p, code, p.axb_S[3], A, X, P, gate, epoch, st);

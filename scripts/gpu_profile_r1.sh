@@ -21,5 +21,15 @@ run_pmc ns gl_ProxGD_primal_f64_8192x16384x32_g1 || exit 1
 run_pmc c3 gl_FProxGD_primal_f32_8192x16384x32_g1 --method gl_FProxGD_primal --dtype f32 || exit 1
 run_pmc c2 gl_ProxGD_primal_f64_4096x8192x16_g1 --m 4096 --n 8192 --l 16 || exit 1
 run_pmc c4 gl_SGD_primal_f64_65536x8192x1_g1 --method gl_SGD_primal --m 65536 --n 8192 --l 1 || exit 1
-cat $O/agree.log
+cat $O/agree.log; cat $O/status.txt | tr "\n" " "
 cat $O/status.txt
+timeout -k 10 400 python bench.py --steps 200 --warmup 20 > $O/bench_default.json 2> $O/bench_default.err; echo "bench_default rc=$?" >> $O/status.txt
+B="timeout -k 10 300 python bench.py --no-cpu-baseline --steps 200 --warmup 20"
+$B --exact 1 > $O/b_pgd_exact.json 2>> $O/bench.err; echo "b_pgd_exact rc=$?" >> $O/status.txt
+$B --method gl_FProxGD_primal > $O/b_fpgd.json 2>> $O/bench.err; echo "b_fpgd rc=$?" >> $O/status.txt
+$B --method gl_FProxGD_primal --dtype f32 > $O/b_fpgd32.json 2>> $O/bench.err; echo "b_fpgd32 rc=$?" >> $O/status.txt
+$B --m 4096 --n 8192 --l 16 > $O/b_c2.json 2>> $O/bench.err; echo "b_c2 rc=$?" >> $O/status.txt
+$B --method gl_SGD_primal --m 65536 --n 8192 --l 1 > $O/b_c4.json 2>> $O/bench.err; echo "b_c4 rc=$?" >> $O/status.txt
+$B --method gl_FProxGD_primal --m 16384 > $O/b_c5shard.json 2>> $O/bench.err; echo "b_c5shard rc=$?" >> $O/status.txt
+for f in $O/bench_default.json $O/b_*.json; do python -c "
+import json; d=json.load(open('$f')); r=d['roofline']; print('%-18s %8.1f it/s  %s %.1f %s frac %.3f pair %.3f  ax %.1fus atr %.1fus' % ('$f'.split('/')[-1], d['value'], r['bound'], r['achieved'], r['unit'], r['frac'], r['pair_frac'] or 0, r['avg_launch_us'], r['atr_avg_launch_us']), d.get('cpu_baseline', {}).get('value'))"; done
