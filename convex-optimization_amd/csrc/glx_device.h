@@ -186,5 +186,62 @@ __device__ inline void prox_pgd_row(const T (&xv)[EPL], const T (&gv)[EPL], cons
   }
 }
 
+// ------------------------------------------------------------------------------------------
+// FISTA / FGD trial arithmetic for one row (gl_FProxGD_primal.py:92-102, :136-145): with
+// w = y - t g, xc = prox(w, t) (PROX) or w (FGD), xk_thr = xk with |xk| < thres zeroed,
+// v_next = xk_thr + (xc - xk_thr)/theta, y_next = a1 thr(xc) + b1 v_next.
+// acc: PROX [sum g*(xc-y), sum (xc-y)^2, sum ||xc_i||, max |xc|];
+//      FGD  [sum g*(xc-y), sum (xc-y)^2, sum (sqrt(||xc_i||^2+d^2)-d), sum ||xc_i||, max |xc|].
+// ------------------------------------------------------------------------------------------
+template <typename T, int LPR, int EPL, bool PROX>
+__device__ inline void fista_row(const T (&yv)[EPL], const T (&gv)[EPL], const T (&xkv)[EPL],
+                                 const bool (&ok)[EPL], bool rv, int sub, T t, T tmu, T thres,
+                                 T theta, T a1, T b1, T dd, T delta, T (&xcv)[EPL],
+                                 T (&vnv)[EPL], T (&ynv)[EPL], double (&acc)[PROX ? 4 : 5]) {
+  constexpr int NV = PROX ? 4 : 5;
+  T w[EPL];
+  T sq = T(0);
+#pragma unroll
+  for (int e = 0; e < EPL; ++e) {
+    w[e] = yv[e] - t * gv[e];
+    sq = sq + w[e] * w[e];
+  }
+  T c = T(1), d = T(1);
+  if (PROX) {
+    const T nrm = __builtin_sqrt(row_allsum<LPR>(sq));
+    c = nrm - tmu;
+    c = (c < T(0)) ? T(0) : c;
+    d = ((nrm < thres) ? T(1) : T(0)) + nrm;
+  }
+  T psq = T(0);
+#pragma unroll
+  for (int e = 0; e < EPL; ++e) {
+    const T pv = PROX ? (w[e] * c) / d : w[e];
+    const T dl = pv - yv[e];
+    T xo = xkv[e];
+    if (tabs(xo) < thres) xo = T(0);
+    const T vn = xo + (pv - xo) / theta;
+    const T pt = (tabs(pv) < thres) ? T(0) : pv;
+    xcv[e] = pv;
+    vnv[e] = vn;
+    ynv[e] = a1 * pt + b1 * vn;
+    if (ok[e]) {
+      acc[0] += (double)(gv[e] * dl);
+      acc[1] += (double)(dl * dl);
+      acc[NV - 1] = nan_max(acc[NV - 1], (double)tabs(pv));
+      psq = psq + pv * pv;
+    }
+  }
+  const T ps = row_allsum<LPR>(psq);
+  if (rv && sub == 0) {
+    if (PROX) {
+      acc[2] += (double)__builtin_sqrt(ps);
+    } else {
+      acc[2] += (double)(__builtin_sqrt(ps + dd) - delta);
+      acc[3] += (double)__builtin_sqrt(ps);
+    }
+  }
+}
+
 }  // namespace glx
 #endif  // GLX_DEVICE_H_

@@ -86,6 +86,12 @@ bool atr_prox_ok(const GemmPlan& p);
 template <typename T>
 void launch_atr_prox(const GemmPlan& p, const T* A, const T* R, T* G, const T* x, T* pp, T* pthr,
                      T* z, double t, double mu, double thres, Red red, hipStream_t st);
+// FISTA trial fused into A^T R (same plan condition): G = A^T R, then xc, v_next, y_next and the
+// four trial sums of k_fista_trial (PROX) into red.
+template <typename T>
+void launch_atr_fista(const GemmPlan& p, const T* A, const T* R, T* G, const T* y, const T* xk,
+                      T* xc, T* vn, T* yn, double t, double mu, double thres, double theta,
+                      double theta_next, Red red, hipStream_t st);
 
 // ---- row / elementwise kernels (kernels_elem.hip) ----
 // Gradient inputs `g` with an `S` argument are S split-K slabs of n*l values summed in slab

@@ -176,53 +176,26 @@ __global__ __launch_bounds__(256) void k_fista_trial(
   for (int j = 0; j < NV; ++j) acc[j] = 0.0;
   acc[NV - 1] = -__builtin_inf();
   GLX_ROW_LOOP_BEGIN(LPR)
-  T yv[EPL], gv[EPL], w[EPL];
-  T sq = T(0);
+  T yv[EPL], gv[EPL], xkv[EPL], xcv[EPL], vnv[EPL], ynv[EPL];
+  bool ok[EPL];
 #pragma unroll
   for (int e = 0; e < EPL; ++e) {
     const int64_t j = sub + (int64_t)e * LPR;
-    const bool ok = rv && j < l;
-    yv[e] = ok ? y[base + j] : T(0);
-    gv[e] = ok ? slab_sum(g, S, nl, base + j) : T(0);
-    if (ok && gout != nullptr) gout[base + j] = gv[e];
-    w[e] = yv[e] - t * gv[e];
-    sq = sq + w[e] * w[e];
+    ok[e] = rv && j < l;
+    yv[e] = ok[e] ? y[base + j] : T(0);
+    gv[e] = ok[e] ? slab_sum(g, S, nl, base + j) : T(0);
+    xkv[e] = ok[e] ? xk[base + j] : T(0);
+    if (ok[e] && gout != nullptr) gout[base + j] = gv[e];
   }
-  T c = T(1), d = T(1);
-  if (PROX) {
-    const T nrm = __builtin_sqrt(row_allsum<LPR>(sq));
-    c = nrm - tmu;
-    c = (c < T(0)) ? T(0) : c;
-    d = ((nrm < thres) ? T(1) : T(0)) + nrm;
-  }
-  T psq = T(0);
+  fista_row<T, LPR, EPL, PROX>(yv, gv, xkv, ok, rv, sub, t, tmu, thres, theta, a1, b1, dd, delta,
+                               xcv, vnv, ynv, acc);
 #pragma unroll
   for (int e = 0; e < EPL; ++e) {
     const int64_t j = sub + (int64_t)e * LPR;
-    const bool ok = rv && j < l;
-    const T pv = PROX ? (w[e] * c) / d : w[e];
-    const T dl = pv - yv[e];
-    if (ok) {
-      T xo = xk[base + j];
-      if (tabs(xo) < thres) xo = T(0);
-      const T vn = xo + (pv - xo) / theta;
-      const T pt = (tabs(pv) < thres) ? T(0) : pv;
-      xc[base + j] = pv;
-      vnext[base + j] = vn;
-      ynext[base + j] = a1 * pt + b1 * vn;
-      acc[0] += (double)(gv[e] * dl);
-      acc[1] += (double)(dl * dl);
-      acc[NV - 1] = nan_max(acc[NV - 1], (double)tabs(pv));
-      psq = psq + pv * pv;
-    }
-  }
-  const T ps = row_allsum<LPR>(psq);
-  if (rv && sub == 0) {
-    if (PROX) {
-      acc[2] += (double)__builtin_sqrt(ps);
-    } else {
-      acc[2] += (double)(__builtin_sqrt(ps + dd) - delta);
-      acc[3] += (double)__builtin_sqrt(ps);
+    if (ok[e]) {
+      xc[base + j] = xcv[e];
+      vnext[base + j] = vnv[e];
+      ynext[base + j] = ynv[e];
     }
   }
   GLX_ROW_LOOP_END

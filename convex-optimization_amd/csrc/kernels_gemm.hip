@@ -3,28 +3,30 @@
 //   A @ X   (reference: gl_ProxGD_primal.py:25,61,129 — `A @ x`):   M = m, K = n, N = l
 //   A^T R   (reference: gl_ProxGD_primal.py:129 — `A.T @ (...)`):  M = n, K = m, N = l
 //
-// Both stream A (m x n, row-major, 1 GiB at the north-star size) once per launch. At
-// l = 16/32 their arithmetic intensity (l/4 flop/B fp64, l/2 fp32) is below the MI355X ridge,
-// so the kernels are built to keep HBM busy: 16-byte loads, many bytes in flight per CU, and
-// v_mfma_f64_16x16x4f64 / v_mfma_f32_16x16x4f32 so the multiply-adds never become the limit.
+// Both stream A (m x n, row-major, 1 GiB at the north-star size) once per launch. A^T R (one
+// right-hand side, l/4 flop/B in fp64) is HBM-bound; A @ X batches 2-3 right-hand sides per
+// pass (the solver's line-search trial and the next gradient residual), which makes it
+// MFMA-bound at l = 32 (v_mfma_f64_16x16x4f64 / v_mfma_f32_16x16x4f32).
 //
 // MFMA 16x16x4 operand maps (cdna_hip_programming.md §3): lane l supplies A_op[l&15][l>>4] and
 // B_op[l>>4][l&15]; the C/D map is row=(l>>4)+4r (f64) or 4(l>>4)+r (f32), col=l&15.
 //
 // A @ X: the K index sits on l>>4, i.e. the 16 lanes of a k-slice live in 16 different rows of
-// A. Each lane therefore loads 16 contiguous bytes (E = 2 f64 / 4 f32 consecutive k) of its
-// row and feeds them to E consecutive MFMAs: MFMA e covers k = k0 + 4*E*... (k permuted inside a
-// 4E-wide chunk; X is gathered with the same permutation, so the sum is unchanged).
-//   kind 1 — each lane loads its own row (lane -> row l&15, chunk l>>4);
-//   kind 2 — quad-coalesced loads (lane -> row L>>2, chunk L&3: 64 contiguous bytes per quad)
-//            and a ds_bpermute to the MFMA layout (no LDS storage, no barriers).
+// A. Each lane loads VPL x 16 contiguous bytes of its row and feeds them to consecutive MFMAs
+// (k permuted inside a chunk; X is read with the same permutation, so the sum is unchanged).
+//   kind 1/2 — X gathered by every wave into registers (2: quad loads + ds_bpermute);
+//   kind 5   — X staged once per block in LDS, natural [k][col] order, conflict-free padding;
+//              the default (f64: 8-wave blocks, f32: 4-wave blocks with a 3-deep ring);
+//   kind 6/7 — kind 5 with X software-pipelined / a barrier every 2-4 chunks (measured slower
+//              or equal, kept selectable for sweeps: DESIGN.md, tuning record).
 // A^T R: the K index (rows of A) is on l>>4 and the 16-wide M index (columns of A) on l&15,
 // so lanes 0..15 read consecutive columns: a lane loads 4 consecutive columns (32 B f64 /
-// 16 B f32) of one row and feeds 4 MFMAs whose output rows are columns c0+4i+e.
+// 16 B f32) of one row and feeds 4 MFMAs whose output rows are columns c0+4i+e. With one K
+// split the ProxGD / FISTA line-search trial runs in its epilogue (k_atr_prox, k_atr_fista).
 //
-// Split-K: each workgroup is 4 waves; the waves of a workgroup split the K range and are
-// summed through LDS in a fixed order, and workgroups along gridDim.y write partial slabs that
-// the consumer sums in slab order — the result is deterministic run to run.
+// All main loops keep their register rings predicate-free and consume each ring slot in place
+// (no vmcnt(0) drain at the back edge). Split-K partials (waves through LDS, workgroups as
+// slabs) are summed in a fixed order, so every result is deterministic run to run.
 #include <algorithm>
 #include <cstdio>
 #include <cstdlib>
@@ -996,6 +998,63 @@ __global__ __launch_bounds__(256) void k_atr_prox(const T* __restrict__ A, const
   grid_reduce<6, 0x8u>(accr, red);
 }
 
+// FISTA's backtracking trial fused into A^T R the same way (WL 0, one K split): each wave runs
+// fista_row (the arithmetic of k_fista_trial) on its 16 gradient rows, with y the extrapolated
+// point and xk the current iterate; writes G, xc, v_next, y_next and reduces the four sums.
+template <typename T, int NT, int PF, bool NTL>
+__global__ __launch_bounds__(256) void k_atr_fista(const T* __restrict__ A, const T* __restrict__ R,
+                                                   T* __restrict__ G, int64_t m, int64_t n,
+                                                   const T* __restrict__ y, const T* __restrict__ xk,
+                                                   T* __restrict__ xc, T* __restrict__ vnext,
+                                                   T* __restrict__ ynext, double t_, double tmu_,
+                                                   double thres_, double theta_, double a1_,
+                                                   double b1_, Red red) {
+  typedef MF<T> M;
+  constexpr int L = 16 * NT;
+  const int lane = threadIdx.x & 63;
+  const int wave = threadIdx.x >> 6;
+  const int i = lane & 15;
+  typename M::acc_t acc[4][NT];
+  const int64_t col0 = atr_panel<T, NT, PF, 0, NTL>(A, R, m, n, 1, acc);
+  double accr[4] = {0.0, 0.0, 0.0, -__builtin_inf()};
+  const T t = (T)t_, tmu = (T)tmu_, thres = (T)thres_, theta = (T)theta_, a1 = (T)a1_, b1 = (T)b1_;
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    if (e != wave) continue;   // wave w owns the rows e == w
+    T ya[4][NT], xa[4][NT];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int64_t row = col0 + 4 * M::row(lane, r) + e;
+#pragma unroll
+      for (int nt = 0; nt < NT; ++nt) {
+        ya[r][nt] = y[row * L + nt * 16 + i];
+        xa[r][nt] = xk[row * L + nt * 16 + i];
+      }
+    }
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int64_t row = col0 + 4 * M::row(lane, r) + e;
+      T gv[NT], xcv[NT], vnv[NT], ynv[NT];
+      bool ok[NT];
+#pragma unroll
+      for (int nt = 0; nt < NT; ++nt) {
+        gv[nt] = acc[e][nt][r];
+        ok[nt] = true;
+        G[row * L + nt * 16 + i] = gv[nt];
+      }
+      fista_row<T, 16, NT, true>(ya[r], gv, xa[r], ok, true, i, t, tmu, thres, theta, a1, b1, T(0),
+                                 T(0), xcv, vnv, ynv, accr);
+#pragma unroll
+      for (int nt = 0; nt < NT; ++nt) {
+        xc[row * L + nt * 16 + i] = xcv[nt];
+        vnext[row * L + nt * 16 + i] = vnv[nt];
+        ynext[row * L + nt * 16 + i] = ynv[nt];
+      }
+    }
+  }
+  grid_reduce<4, 0x8u>(accr, red);
+}
+
 // ------------------------------------------------------------------------------------------
 // VALU fallback for small l (GEMV-like, l <= 8 per pass) and ragged shapes.
 // A @ X: a wave owns RW rows and one K split; lanes stride the row with (16-byte) loads,
@@ -1626,7 +1685,40 @@ void launch_atr_prox(const GemmPlan& p, const T* A, const T* R, T* G, const T* x
   else atr_prox_nt<T, 2>(p, A, R, G, x, pp, pthr, z, t, mu, thres, red, st);
 }
 
+template <typename T, int NT, int PF, bool NTL>
+static void atr_fista_go(const GemmPlan& p, const T* A, const T* R, T* G, const T* y, const T* xk,
+                         T* xc, T* vn, T* yn, double t, double mu, double thres, double theta,
+                         double theta_next, Red red, hipStream_t st) {
+  hipLaunchKernelGGL((k_atr_fista<T, NT, PF, NTL>), dim3((unsigned)(p.n / 64)), dim3(256), 0, st, A,
+                     R, G, p.m, p.n, y, xk, xc, vn, yn, t, t * mu, thres, theta, 1.0 - theta_next,
+                     theta_next, red);
+}
+template <typename T, int NT>
+static void atr_fista_nt(const GemmPlan& p, const T* A, const T* R, T* G, const T* y, const T* xk,
+                         T* xc, T* vn, T* yn, double t, double mu, double thres, double theta,
+                         double theta_next, Red red, hipStream_t st) {
+  switch (p.atr_ntl * 100 + p.atr_pf) {
+    case 4: atr_fista_go<T, NT, 4, false>(p, A, R, G, y, xk, xc, vn, yn, t, mu, thres, theta, theta_next, red, st); break;
+    case 104: atr_fista_go<T, NT, 4, true>(p, A, R, G, y, xk, xc, vn, yn, t, mu, thres, theta, theta_next, red, st); break;
+    case 108: atr_fista_go<T, NT, 8, true>(p, A, R, G, y, xk, xc, vn, yn, t, mu, thres, theta, theta_next, red, st); break;
+    default: atr_fista_go<T, NT, 8, false>(p, A, R, G, y, xk, xc, vn, yn, t, mu, thres, theta, theta_next, red, st); break;
+  }
+}
+template <typename T>
+void launch_atr_fista(const GemmPlan& p, const T* A, const T* R, T* G, const T* y, const T* xk,
+                      T* xc, T* vn, T* yn, double t, double mu, double thres, double theta,
+                      double theta_next, Red red, hipStream_t st) {
+  if (p.l == 16) atr_fista_nt<T, 1>(p, A, R, G, y, xk, xc, vn, yn, t, mu, thres, theta, theta_next, red, st);
+  else atr_fista_nt<T, 2>(p, A, R, G, y, xk, xc, vn, yn, t, mu, thres, theta, theta_next, red, st);
+}
+
 template void launch_atr<double>(const GemmPlan&, const double*, const double*, double*, hipStream_t);
+template void launch_atr_fista<double>(const GemmPlan&, const double*, const double*, double*,
+                                       const double*, const double*, double*, double*, double*,
+                                       double, double, double, double, double, Red, hipStream_t);
+template void launch_atr_fista<float>(const GemmPlan&, const float*, const float*, float*,
+                                      const float*, const float*, float*, float*, float*, double,
+                                      double, double, double, double, Red, hipStream_t);
 template void launch_atr_prox<double>(const GemmPlan&, const double*, const double*, double*,
                                       const double*, double*, double*, double*, double, double,
                                       double, Red, hipStream_t);

@@ -70,12 +70,12 @@ struct Carver {
 static int method_bufs(int method) {
   switch (method) {
     case GLX_PROXGD: return 7;   // (x, x_thr), (p, p_thr), z + two spares (speculative trial)
-    case GLX_FPROXGD: return 6;  // (x_k, v_k, y) current + (x, v, y) of the trial
+    case GLX_FPROXGD: return 9;  // (x_k, v_k, y) current + (x, v, y) of the trial + 3 spares
     case GLX_FGD: return 6;
     default: return 2;           // SGD / GD: x, thr(x)
   }
 }
-constexpr int kBufs = 7;
+constexpr int kBufs = 9;
 constexpr int kRes = 4;
 
 static void validate(const glx_problem* P, const glx_opts* O) {
@@ -113,7 +113,7 @@ class Session : public SessionBase {
     Carver c(ws);
     const int64_t nl = P.n * P.l, ml = P.m * P.l;
     const int nb = method_bufs(P.method);
-    T* bufs[kBufs] = {static_cast<T*>(P.x), nullptr, nullptr, nullptr, nullptr, nullptr, nullptr};
+    T* bufs[kBufs] = {static_cast<T*>(P.x)};
     for (int i = 1; i < nb; ++i) bufs[i] = static_cast<T*>(c.take(sizeof(T) * nl));
     T* res[kRes];
     for (int i = 0; i < kRes; ++i) res[i] = static_cast<T*>(c.take(sizeof(T) * ml));
@@ -171,9 +171,11 @@ class Session : public SessionBase {
     const char* sp = std::getenv("GLX_SPEC_GRAD");
     spec_off_env_ = (sp && std::strcmp(sp, "0") == 0);
     const char* fz = std::getenv("GLX_FUSED_TRIAL");
-    fused_ok_ = P.method == GLX_PROXGD && comm_ == nullptr && atr_prox_ok(plan_) &&
-                (O.step_type == GLX_STEP_LINE_SEARCH || O.step_type == GLX_STEP_FIXED) &&
-                !(fz && std::strcmp(fz, "0") == 0);
+    const bool fuse_any = comm_ == nullptr && atr_prox_ok(plan_) &&
+                          (O.step_type == GLX_STEP_LINE_SEARCH || O.step_type == GLX_STEP_FIXED) &&
+                          !(fz && std::strcmp(fz, "0") == 0);
+    fused_ok_ = fuse_any && P.method == GLX_PROXGD;
+    fused_fista_ok_ = fuse_any && P.method == GLX_FPROXGD;
     GLX_HIP(hipMemsetAsync(ticket_, 0, kTicketBytes, st_));
     GLX_HIP(hipMemsetAsync(flag_, 0, 256, st_));
     GLX_HIP(hipMemsetAsync(scal_, 0, sizeof(double) * NSCAL, st_));
@@ -450,6 +452,7 @@ class Session : public SessionBase {
       tk_ = O_.alpha0;
       y_ready_ = false;
       spec_ready_ = false;   // y is re-formed from the reset v: its gradient was not speculated
+      spec_trial_ready_ = false;
     }
   }
 
@@ -616,14 +619,34 @@ class Session : public SessionBase {
     if (stop_rule()) { end_phase(); return; }
     const double theta = 2.0 / (double)(inner_ + 1);       // gl_FProxGD_primal.py:138
     const double theta_next = 2.0 / (double)(inner_ + 2);
-    if (!y_ready_) {
-      launch_thr_axpby<T>(X_[ix_], X_[iv_], X_[iy_], nl_, O_.thres, 1.0 - theta, theta, st_);
-      check_launch();
-      residual1(X_[iy_], R_[iry_], S_RG);                 // g(y) and the gradient residual
-      gy_pending_ = true;
+    const bool ls = O_.step_type == GLX_STEP_LINE_SEARCH && O_.ls_maxit > 0;
+    const double t0 = ls ? tk_ : schedule(inner_);
+    const bool fuse = fused_fista_ok_ && !smooth;
+    // first trial: from the previous iteration's speculative fused kernel, fused into this
+    // iteration's A^T r, or (FGD / unfusable plans) the gradient and k_fista_trial
+    std::pair<const T*, int> g{nullptr, 0};
+    bool first_done = false;
+    if (spec_trial_ready_) {   // only ever set after an accepted trial: y and A y - b are ready
+      spec_trial_ready_ = false;
+      use_gset(spec_set_);
+      g = {G_, 1};
+      first_done = spec_trial_mu_ == mu_ && spec_trial_t_ == t0 && spec_trial_theta_ == theta;
+    } else {
+      if (!y_ready_) {
+        launch_thr_axpby<T>(X_[ix_], X_[iv_], X_[iy_], nl_, O_.thres, 1.0 - theta, theta, st_);
+        check_launch();
+        residual1(X_[iy_], R_[iry_], S_RG);               // g(y) and the gradient residual
+        gy_pending_ = true;
+      }
+      if (fuse) {
+        atr_fista(R_[iry_], gset_, X_[iy_], X_[ix_], ic_, ivn_, iyn_, t0, theta, theta_next);
+        g = {G_, 1};
+        first_done = true;
+      } else {
+        g = take_gradient(R_[iry_]);
+      }
     }
     const T* y = X_[iy_];
-    std::pair<const T*, int> g = take_gradient(R_[iry_]);
     if (smooth) {                                         // G = A^T r + mu y / sqrt(|y_i|^2 + d^2)
       launch_fgd_grad<T>(y, g.first, g.second, G_, n_, l_, mu_, O_.delta, red(S_REGY), st_);
       check_launch();
@@ -631,7 +654,7 @@ class Session : public SessionBase {
     }
     const int rc = (iry_ + 1) % kRes, ryn = (iry_ + 2) % kRes;
     double t;
-    bool accepted = false;
+    bool accepted = false, spec_trial = false;
     auto trial = [&](double tt, bool first) {
       launch_fista_trial<T>(!smooth, y, first ? g.first : G_, first ? g.second : 1,
                             (first && g.first != G_) ? G_ : nullptr, X_[ix_], X_[ic_], X_[ivn_],
@@ -640,17 +663,24 @@ class Session : public SessionBase {
       check_launch();
     };
     const int i_rn = smooth ? 3 : 2, i_max = smooth ? 4 : 3;
-    if (O_.step_type == GLX_STEP_LINE_SEARCH && O_.ls_maxit > 0) {
-      t = tk_;
+    if (ls) {
+      t = t0;
       for (int it = 0; it < O_.ls_maxit; ++it) {
-        trial(t, it == 0);
+        if (!(it == 0 && first_done)) trial(t, it == 0);
         const T* xs[3] = {X_[ic_], X_[iyn_], nullptr};
         T* rs[3] = {R_[rc], R_[ryn], nullptr};
         unsigned seq = 0;
         residuals(2, xs, rs, S_RT, X_[ic_], scal_ + S_TR + i_max, nullptr, 0.0, &seq);   // A @ [x | y_next]
         const bool spec = want_spec(it);
         std::pair<const T*, int> sg;
-        if (spec) sg = gradient(R_[ryn], 1 - gset_);   // gradient at the next y
+        if (spec && fuse) {
+          // the next iteration's gradient at y_next and its first trial (t, theta' = theta_next)
+          atr_fista(R_[ryn], 1 - gset_, X_[iyn_], X_[ic_], ff1_, ff2_, ff3_, t, theta_next,
+                    2.0 / (double)(inner_ + 3));
+          spec_trial = true;
+        } else if (spec) {
+          sg = gradient(R_[ryn], 1 - gset_);   // gradient at the next y
+        }
         wait_readback(seq);
         if (gy_pending_) { gy_sq_ = hs_[S_RG]; gy_pending_ = false; }
         double gy = 0.5 * gy_sq_, gxc = 0.5 * hs_[S_RT];
@@ -660,22 +690,35 @@ class Session : public SessionBase {
         }
         if (gxc <= gy + hs_[S_TR + 0] + hs_[S_TR + 1] / (2 * t)) {
           accepted = true;
-          if (spec) { spec_ready_ = true; spec_g_ = sg; spec_set_ = 1 - gset_; }
+          if (spec && !spec_trial) { spec_ready_ = true; spec_g_ = sg; spec_set_ = 1 - gset_; }
           spec_on_ = (it == 0);
           break;
         }
+        spec_trial = false;
         spec_on_ = false;
         t *= O_.ls_coeff;
       }
       if (!accepted) trial(t, false);
     } else {
-      t = O_.step_type == GLX_STEP_LINE_SEARCH ? tk_ : schedule(inner_);
-      trial(t, true);
+      t = t0;
+      if (!first_done) trial(t, true);
     }
     // x_k <- x, v_k <- v (:145, :147), y <- y_next
-    std::swap(ix_, ic_);
-    std::swap(iv_, ivn_);
-    std::swap(iy_, iyn_);
+    if (spec_trial) {   // the speculative outputs become the next iteration's trial buffers
+      const int ox = ix_, ov = iv_, oy = iy_;
+      ix_ = ic_; iv_ = ivn_; iy_ = iyn_;
+      ic_ = ff1_; ivn_ = ff2_; iyn_ = ff3_;
+      ff1_ = ox; ff2_ = ov; ff3_ = oy;
+      spec_trial_ready_ = true;
+      spec_set_ = 1 - gset_;
+      spec_trial_mu_ = mu_;
+      spec_trial_t_ = t;
+      spec_trial_theta_ = theta_next;
+    } else {
+      std::swap(ix_, ic_);
+      std::swap(iv_, ivn_);
+      std::swap(iy_, iyn_);
+    }
     tk_ = t;
     if (accepted) {
       iry_ = ryn;
@@ -688,6 +731,19 @@ class Session : public SessionBase {
       y_ready_ = false;
       f_known_ = false;
     }
+  }
+
+  // A^T r fused with a FISTA trial at y (gradient set `set`; x_k = xk; outputs X_[oc], X_[ov],
+  // X_[oy])
+  void atr_fista(const T* r, int set, const T* yv, const T* xk, int oc, int ov, int oy, double t,
+                 double theta, double theta_next) {
+    hipEvent_t e0 = nullptr, e1 = nullptr;
+    if (O_.profile) { e0 = get_event(); e1 = get_event(); GLX_HIP(hipEventRecord(e0, st_)); }
+    launch_atr_fista<T>(plan_, A_, r, Gs_[set], yv, xk, X_[oc], X_[ov], X_[oy], t, mu_, O_.thres,
+                        theta, theta_next, red(S_TR), st_);
+    check_launch();
+    if (O_.profile) { GLX_HIP(hipEventRecord(e1, st_)); ev_[1].push_back({e0, e1}); }
+    ++atr_calls_;
   }
 
   // ------------------------------------------------------------------ SGD / GD (no syncs)
@@ -733,7 +789,7 @@ class Session : public SessionBase {
   int64_t m_ = 0, n_ = 0, l_ = 0, nl_ = 0, ml_ = 0;
   const T* A_ = nullptr;
   const T* B_ = nullptr;
-  T* X_[kBufs] = {nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr};
+  T* X_[kBufs] = {};
   T* R_[kRes] = {nullptr, nullptr, nullptr, nullptr};
   T *G_ = nullptr, *Gp_ = nullptr, *Pp_ = nullptr;
   T* Gs_[2] = {nullptr, nullptr};
@@ -752,6 +808,7 @@ class Session : public SessionBase {
   int epoch_ = 0;
   // buffer roles
   int ix_ = 0, iv_ = 1, iy_ = 2, ic_ = 3, ivn_ = 4, iyn_ = 5;   // FISTA
+  int ff1_ = 6, ff2_ = 7, ff3_ = 8;                               // FISTA spares (speculation)
   int ixt_ = 1, ip_ = 2, ipt_ = 3, iz_ = 4, if1_ = 5, if2_ = 6;   // ProxGD (+ two spares)
   int irg_ = 0, iry_ = 0;
   bool state_valid_ = false, thr_from_trial_ = false, y_ready_ = false, gy_pending_ = false;
@@ -760,8 +817,8 @@ class Session : public SessionBase {
   bool spec_on_ = true, spec_ready_ = false, spec_off_env_ = false;
   // ProxGD trial fused into A^T r (launch_atr_prox): fused_ok_ = the plan allows it; a
   // speculative fused kernel leaves G and the next iteration's first trial (t, mu) ready
-  bool fused_ok_ = false, spec_trial_ready_ = false;
-  double spec_trial_mu_ = 0, spec_trial_t_ = 0;
+  bool fused_ok_ = false, fused_fista_ok_ = false, spec_trial_ready_ = false;
+  double spec_trial_mu_ = 0, spec_trial_t_ = 0, spec_trial_theta_ = 0;
   std::pair<const T*, int> spec_g_{nullptr, 0};
   double gx_ = 0, gy_sq_ = 0;
   // algorithm state

@@ -1,4 +1,5 @@
-"""The ProxGD trial fused into A^T r (k_atr_prox) and its speculative use.
+"""The line-search trials fused into A^T r (k_atr_prox for ProxGD, k_atr_fista for FProxGD) and
+their speculative use.
 
 At (m, n, l) = (256, 16384, 32) fp64 the planner gives A^T r one K split, so the solver runs
 the first line-search trial of every iteration inside the gradient kernel's epilogue and, after
@@ -25,13 +26,16 @@ def _instance():
     return A, b, x0, mu, numpy_ref.step_size_for(m, n)
 
 
-def _run(monkeypatch, fused, spec, opts):
+METHODS = ["gl_ProxGD_primal", "gl_FProxGD_primal"]
+
+
+def _run(monkeypatch, fused, spec, opts, method="gl_ProxGD_primal"):
     import glx
     monkeypatch.setenv("GLX_FUSED_TRIAL", "1" if fused else "0")
     monkeypatch.setenv("GLX_SPEC_GRAD", "1" if spec else "0")
     A, b, x0, mu, _ = _instance()
     At, bt, xt = (torch.from_numpy(a).cuda() for a in (A, b, x0))
-    s = glx.Session("gl_ProxGD_primal", xt, At, bt, mu, opts)
+    s = glx.Session(method, xt, At, bt, mu, opts)
     s.run(0)
     res = s.finish()
     s.close()
@@ -45,12 +49,13 @@ def test_plan_fuses_at_this_shape():
     assert "atr=k_atr_mfma<WL0" in d and d.rstrip().endswith("S=1"), d
 
 
+@pytest.mark.parametrize("method", METHODS)
 @pytest.mark.parametrize("spec", [False, True])
-def test_fused_trial_bit_identical_iterate(monkeypatch, spec):
+def test_fused_trial_bit_identical_iterate(monkeypatch, spec, method):
     _, _, _, _, alpha0 = _instance()
     opts = {"alpha0": alpha0, "maxit": 40}
-    x_f, r_f = _run(monkeypatch, True, spec, opts)
-    x_u, r_u = _run(monkeypatch, False, False, opts)
+    x_f, r_f = _run(monkeypatch, True, spec, opts, method)
+    x_u, r_u = _run(monkeypatch, False, False, opts, method)
     assert r_f["k"] == r_u["k"]
     assert np.array_equal(x_f, x_u)
     np.testing.assert_allclose(np.asarray(r_f["f_hist"]), np.asarray(r_u["f_hist"]), rtol=1e-13)
@@ -58,12 +63,13 @@ def test_fused_trial_bit_identical_iterate(monkeypatch, spec):
         assert r_f["atr_calls"] >= r_u["atr_calls"]
 
 
-def test_fused_trial_matches_oracle(monkeypatch):
+@pytest.mark.parametrize("method", METHODS)
+def test_fused_trial_matches_oracle(monkeypatch, method):
     from oracle import numpy_ref
     A, b, x0, mu, alpha0 = _instance()
     opts = {"alpha0": alpha0, "maxit": 25}
-    x_g, r_g = _run(monkeypatch, True, True, opts)
-    x_r, k_r, out_r = numpy_ref.gl_ProxGD_primal(x0.copy(), A, b, mu, dict(opts))
+    x_g, r_g = _run(monkeypatch, True, True, opts, method)
+    x_r, k_r, out_r = numpy_ref.SOLVERS[method](x0.copy(), A, b, mu, dict(opts))
     assert r_g["k"] == k_r
     f_g = np.asarray(r_g["f_hist"], dtype=float)
     f_r = np.asarray(out_r["f_hist"], dtype=float)
@@ -71,10 +77,11 @@ def test_fused_trial_matches_oracle(monkeypatch):
     assert abs(float(r_g["fval"]) - float(out_r["fval"])) <= 1e-8 * abs(float(out_r["fval"]))
 
 
-def test_fused_trial_fixed_step(monkeypatch):
+@pytest.mark.parametrize("method", METHODS)
+def test_fused_trial_fixed_step(monkeypatch, method):
     _, _, _, _, alpha0 = _instance()
     opts = {"alpha0": alpha0, "maxit": 20, "step_type": "fixed"}
-    x_f, r_f = _run(monkeypatch, True, True, opts)
-    x_u, r_u = _run(monkeypatch, False, False, opts)
+    x_f, r_f = _run(monkeypatch, True, True, opts, method)
+    x_u, r_u = _run(monkeypatch, False, False, opts, method)
     assert r_f["k"] == r_u["k"]
     assert np.array_equal(x_f, x_u)
