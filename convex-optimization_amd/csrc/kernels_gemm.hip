@@ -1240,7 +1240,8 @@ static int axb_default(int nsrc, int esize) {
 }
 
 static constexpr int kLdsCodes[] = {52224, 52324, 52228, 52328, 52218, 54224, 52214, 54214,
-                                     52428, 62428, 62424, 62418, 72428, 72424, 72828};
+                                     52428, 54228, 54218, 62428, 62424, 62418, 72428, 72424,
+                                     72828};
 static bool lds_code_ok(int c, int64_t n, int64_t l, int esize) {
   bool known = false;
   for (int k : kLdsCodes) known |= (k == c);
@@ -1494,6 +1495,8 @@ static void ax_lds_code(const GemmPlan& p, int code, int S, const T* A, const T*
   }
   switch (code) {
     case 52324: ax_lds_go<T, NT, NSRC, 2, 3, 2, 4>(p, S, A, X, P, gate, epoch, st); break;
+    case 54228: ax_lds_go<T, NT, NSRC, 4, 2, 2, 8>(p, S, A, X, P, gate, epoch, st); break;
+    case 54218: ax_lds_go<T, NT, NSRC, 4, 2, 1, 8>(p, S, A, X, P, gate, epoch, st); break;
     case 52228:
       if constexpr (sizeof(T) == 8 && NT == 2 && NSRC == 2) {
         switch (env_int("GLX_AXL_ABL", 0)) {   // timing ablations (results are wrong)
