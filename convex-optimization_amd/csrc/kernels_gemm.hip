@@ -1250,11 +1250,25 @@ static bool lds_code_ok(int c, int64_t n, int64_t l, int esize) {
   return (l == 16 || l == 32) && n % (4 * E * vpl) == 0;
 }
 // K split of a kind-5 launch: enough blocks for 2 (4-wave) blocks per CU
-static int lds_split(int esize, int64_t m, int64_t n, int code) {
+static int lds_split(int esize, int64_t m, int64_t n, int code, int64_t target = 0) {
   const int E = 16 / esize, mt = (code / 1000) % 10, vpl = (code / 10) % 10, waves = code % 10;
   const int64_t rb = cdiv(m, 16 * mt * waves), chunks = n / (4 * E * vpl);
-  const int64_t target = env_int("GLX_AXL_BLOCKS", waves == 8 ? 256 : 512);
+  if (target <= 0) target = env_int("GLX_AXL_BLOCKS", waves == 8 ? 256 : 512);
   return (int)clampi(cdiv(target, rb), 1, std::max<int64_t>(1, std::min<int64_t>(kMaxSplit, chunks / 8)));
+}
+// A K-split launch writes S partial slabs of m x (nsrc*l) that the finalize kernel reads back.
+// With few rows (the per-rank shards of a multi-GPU run) a 256-block target lets S reach 64 and
+// the slabs rival A itself. When they exceed 1/6 of A, use the 4-wave tile at 256 blocks, which
+// halves them. Shard-shape sweep (profiles/r1_tuning/shard_shapes.txt): at m = 1024 this is
+// +10 % end to end despite a slower A@X; at m >= 2048 the default tile stays ahead.
+static void lds_plan(int esize, int64_t m, int64_t n, int64_t l, int nsrc, int& code, int& S) {
+  S = lds_split(esize, m, n, code);
+  if (std::getenv("GLX_AXL_BLOCKS") || std::getenv("GLX_AXB_VARIANT")) return;
+  if ((double)S * (double)m * nsrc * l * 6.0 <= (double)m * n) return;
+  const int c4 = esize == 8 ? 52224 : 52324;
+  if (!lds_code_ok(c4, n, l, esize)) return;
+  const int S4 = lds_split(esize, m, n, c4, 256);
+  if (S4 < S) { code = c4; S = S4; }
 }
 
 static bool valid_ax_code(int c) {
@@ -1289,12 +1303,13 @@ GemmPlan make_plan(int esize, int64_t m, int64_t n, int64_t l, int ax_variant) {
     const int64_t kunits = n / (64 * (p.ax_vec ? E : 1)); // 64-lane strides per row
     p.ax_S = (int)clampi(cdiv(kTargetWaves, waves), 1, std::max<int64_t>(1, std::min<int64_t>(kMaxSplit, kunits / 4)));
   } else if (lds_code_ok(ax_variant ? ax_variant : (esize == 8 ? kAxDefault : kAxDefault32), n, l, esize)) {
-    const int code = ax_variant ? ax_variant : (esize == 8 ? kAxDefault : kAxDefault32);
+    int code = ax_variant ? ax_variant : (esize == 8 ? kAxDefault : kAxDefault32);
+    if (ax_variant) p.ax_S = lds_split(esize, m, n, code);
+    else lds_plan(esize, m, n, l, 1, code, p.ax_S);
     p.ax_code = code;
     p.ax_kind = 5;
     p.ax_mt = (code / 1000) % 10;
     p.ax_pf = (code / 100) % 10;
-    p.ax_S = lds_split(esize, m, n, code);
   } else {
     int code = valid_ax_code(ax_variant) ? ax_variant : (esize == 8 ? kAxFallback : kAxDefault32);
     int vpl = code / 10000 ? code / 10000 : 1;
@@ -1322,7 +1337,7 @@ GemmPlan make_plan(int esize, int64_t m, int64_t n, int64_t l, int ax_variant) {
     if (p.ax_kind == 3) {
       code = 0;
     } else if (code / 10000 >= 5 && code / 10000 <= 7) {
-      if (lds_code_ok(code, n, l, esize)) S = lds_split(esize, m, n, code);
+      if (lds_code_ok(code, n, l, esize)) lds_plan(esize, m, n, l, ns, code, S);
       else code = ns == 2 ? 1420 : 1220;
     } else if (code >= 10000 && n % (4 * E * (code / 10000)) != 0) {
       code = ns == 2 ? 1420 : 1220;
