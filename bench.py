@@ -16,7 +16,9 @@ iteration):
              sides it is MFMA-bound in fp64 and fp32 (BASELINE.json's metric is the MFMA roofline
              %), with l = 1 (SGD) HBM-bound. achieved = algorithmic flops 2*m*n*l*rhs (or bytes
              s*(m n + (m+n) l rhs)) per launch / average launch time from HIP events recorded on
-             the solver's stream over the timed region. `pair_frac` is the same fraction for the
+             the solver's stream over the timed region, around every 16th A@x / A^T r launch
+             (--profile 16: each timed event pair opens a few-us gap in the queue, 12 % of the
+             iteration at a 1024-row shard when every launch is timed). `pair_frac` is the same fraction for the
              A@x + A^T r pair (the north-star target). `traffic` = HBM bytes per launch from
              rocprofv3 PMC (profiles/pmc_traffic.json, 2*FETCH_SIZE + WRITE_SIZE per the gfx950
              correction) when that file holds the same config, else null;
@@ -135,7 +137,8 @@ def main():
     ap.add_argument("--l", type=int, default=32)
     ap.add_argument("--variant", type=int, default=0)
     ap.add_argument("--exact", type=int, default=0)
-    ap.add_argument("--profile", type=int, default=1, help="HIP events around A@x / A^T r launches")
+    ap.add_argument("--profile", type=int, default=16,
+                    help="HIP events around every k-th A@x / A^T r launch (0 = off)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     args = ap.parse_args()
 
@@ -220,7 +223,8 @@ def main():
                 "unit": unit, "frac": (ach / peak) if ach else None,
                 "traffic": pmc_traffic(cfg_key),
                 "kernel": ax_kernel_name(args.dtype, ml, n, l, nsrc), "flops_per_launch": ax_flops,
-                "bytes_per_launch": ax_bytes, "avg_launch_us": ax_avg_s * 1e6, "launches": ax_n,
+                "bytes_per_launch": ax_bytes, "avg_launch_us": ax_avg_s * 1e6, "launches_timed": ax_n,
+                "timed_every": args.profile,
                 "rhs_per_launch": nsrc, "hbm_GBs": ax_gbs, "hbm_frac": ax_gbs / HBM_PEAK_GBS if ax_n else None,
                 "mfma_tflops": ax_tf, "mfma_frac": ax_tf / peak_tf if ax_n else None,
                 "atr_avg_launch_us": atr_avg_s * 1e6,

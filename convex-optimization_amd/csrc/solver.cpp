@@ -278,6 +278,22 @@ class Session : public SessionBase {
   // ------------------------------------------------------------------ helpers
   Red red(int slot) { return Red{part_, ticket_, scal_ + slot}; }
 
+  // HIP-event timing of A@X (kind 0) / A^T R (kind 1) launches. opts.profile = k > 0 times every
+  // k-th launch of each kind: a timed event pair opens a gap of a few us in the queue, so
+  // sampling keeps the measured run close to an unprofiled one.
+  hipEvent_t prof_begin(int kind) {
+    if (O_.profile <= 0 || (prof_n_[kind]++ % O_.profile) != 0) return nullptr;
+    hipEvent_t e0 = get_event();
+    GLX_HIP(hipEventRecord(e0, st_));
+    return e0;
+  }
+  void prof_end(int kind, hipEvent_t e0) {
+    if (e0 == nullptr) return;
+    hipEvent_t e1 = get_event();
+    GLX_HIP(hipEventRecord(e1, st_));
+    ev_[kind].push_back({e0, e1});
+  }
+
   hipEvent_t get_event() {
     if (ev_pool_.empty()) {   // grow in batches: never create events inside a timed loop's steady state
       for (int i = 0; i < 256; ++i) {
@@ -308,11 +324,10 @@ class Session : public SessionBase {
   void residuals(int nsrc, const T* const* xs, T* const* rs, int slot, const T* cx = nullptr,
                  const double* cmax = nullptr, double* fh = nullptr, double fh_mu = 0.0,
                  unsigned* pub_seq = nullptr) {
-    hipEvent_t e0 = nullptr, e1 = nullptr;
-    if (O_.profile) { e0 = get_event(); e1 = get_event(); GLX_HIP(hipEventRecord(e0, st_)); }
+    hipEvent_t e0 = prof_begin(0);
     launch_ax<T>(plan_, nsrc, A_, xs, Pp_, nullptr, 0, st_);
     check_launch();
-    if (O_.profile) { GLX_HIP(hipEventRecord(e1, st_)); ev_[0].push_back({e0, e1}); }
+    prof_end(0, e0);
     ++ax_calls_;
     ax_cols_ += nsrc;
     launch_finalize_residual<T>(Pp_, ax_split(plan_, nsrc), B_, nsrc, rs, ml_, nullptr, 0, 1, cx,
@@ -341,11 +356,10 @@ class Session : public SessionBase {
     if (set < 0) set = gset_;
     T* G = Gs_[set];
     T* Gp = Gps_[set];
-    hipEvent_t e0 = nullptr, e1 = nullptr;
-    if (O_.profile) { e0 = get_event(); e1 = get_event(); GLX_HIP(hipEventRecord(e0, st_)); }
+    hipEvent_t e0 = prof_begin(1);
     launch_atr<T>(plan_, A_, r, Gp, st_);
     check_launch();
-    if (O_.profile) { GLX_HIP(hipEventRecord(e1, st_)); ev_[1].push_back({e0, e1}); }
+    prof_end(1, e0);
     ++atr_calls_;
     if (!comm_) return {Gp, plan_.atr_S};
     if (plan_.atr_S > 1) {
@@ -596,12 +610,11 @@ class Session : public SessionBase {
 
   // A^T r fused with a ProxGD trial at x (gradient set `set`, outputs X_[op], X_[opt], X_[oz])
   void atr_prox(const T* r, int set, const T* x, int op, int opt, int oz, double t) {
-    hipEvent_t e0 = nullptr, e1 = nullptr;
-    if (O_.profile) { e0 = get_event(); e1 = get_event(); GLX_HIP(hipEventRecord(e0, st_)); }
+    hipEvent_t e0 = prof_begin(1);
     launch_atr_prox<T>(plan_, A_, r, Gs_[set], x, X_[op], X_[opt], X_[oz], t, mu_, O_.thres,
                        red(S_TR), st_);
     check_launch();
-    if (O_.profile) { GLX_HIP(hipEventRecord(e1, st_)); ev_[1].push_back({e0, e1}); }
+    prof_end(1, e0);
     ++atr_calls_;
   }
 
@@ -737,12 +750,11 @@ class Session : public SessionBase {
   // X_[oy])
   void atr_fista(const T* r, int set, const T* yv, const T* xk, int oc, int ov, int oy, double t,
                  double theta, double theta_next) {
-    hipEvent_t e0 = nullptr, e1 = nullptr;
-    if (O_.profile) { e0 = get_event(); e1 = get_event(); GLX_HIP(hipEventRecord(e0, st_)); }
+    hipEvent_t e0 = prof_begin(1);
     launch_atr_fista<T>(plan_, A_, r, Gs_[set], yv, xk, X_[oc], X_[ov], X_[oy], t, mu_, O_.thres,
                         theta, theta_next, red(S_TR), st_);
     check_launch();
-    if (O_.profile) { GLX_HIP(hipEventRecord(e1, st_)); ev_[1].push_back({e0, e1}); }
+    prof_end(1, e0);
     ++atr_calls_;
   }
 
@@ -833,6 +845,7 @@ class Session : public SessionBase {
   int64_t ax_calls_ = 0, ax_cols_ = 0, atr_calls_ = 0, syncs_ = 0;
   double stats_[8] = {0, 0, 0, 0, 0, 0, 0, 0};
   std::vector<std::pair<hipEvent_t, hipEvent_t>> ev_[2];
+  int64_t prof_n_[2] = {0, 0};
   std::vector<hipEvent_t> ev_pool_;
 };
 

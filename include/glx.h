@@ -66,7 +66,7 @@ typedef struct glx_opts {
                                      the reference's evaluation order; 0 = reuse the accepted
                                      line-search residual A@z, z = x - t*G_t (ulp-level
                                      difference, SURVEY.md §8a reuse table)                   */
-  int32_t profile;                /* 1 = time every A@x / A^T r launch with HIP events      */
+  int32_t profile;                /* k > 0: time every k-th A@x / A^T r launch (HIP events) */
   int64_t max_total_iters;        /* stop after this many iterations in total (0 = off)     */
   int32_t ax_variant;             /* A@x kernel variant for A/B tests (0 = auto)            */
   int32_t reserved[7];
@@ -122,8 +122,8 @@ int  glx_session_create(glx_session** out, const glx_problem* prob, const glx_op
                         void* workspace, size_t workspace_bytes, void* stream);
 int  glx_session_run(glx_session* s, int64_t max_steps, int64_t* done, int32_t* finished);
 int  glx_session_finish(glx_session* s, glx_result* res);
-/* average device time (ms) of the A@x (kind 0) / A^T r (kind 1) launches recorded while
- * opts.profile = 1; resets the accumulators. */
+/* launches timed and their total device time (ms) for A@x (kind 0) / A^T r (kind 1), sampled
+ * every opts.profile-th launch; resets the accumulators. */
 int  glx_session_kernel_time(glx_session* s, int kind, int64_t* launches, double* total_ms);
 void glx_session_destroy(glx_session* s);
 

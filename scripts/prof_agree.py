@@ -3,9 +3,9 @@
     python scripts/prof_agree.py --trace DIR --bench bench.json [--out summary.json]
 
 bench.py times the A@X and A^T R launches of the timed region with HIP events on the solver's
-stream; the trace holds every launch of the run (warmup included). The last `launches` A@X
-dispatches of the trace are the timed ones; their mean duration must agree with
-roofline.avg_launch_us (and likewise A^T R).
+stream (every `timed_every`-th launch); the trace holds every launch of the run (warmup
+included). The last launches_timed * timed_every A@X dispatches of the trace are the timed
+region's; their mean duration must agree with roofline.avg_launch_us (and likewise A^T R).
 """
 import argparse
 import csv
@@ -30,7 +30,7 @@ def main():
     out = {"bench_value": bench["value"], "bench_unit": bench["unit"]}
     for kind, key, tag in (("ax", "avg_launch_us", "k_ax_"), ("atr", "atr_avg_launch_us", "k_atr_")):
         durs = [(int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3 for r in rows if tag in r["Kernel_Name"]]
-        n = roof["launches"]
+        n = roof.get("launches_timed", roof.get("launches", 0)) * roof.get("timed_every", 1)
         tail = durs[-n:] if len(durs) >= n else durs
         avg = sum(tail) / max(1, len(tail))
         out[kind] = {"trace_launches": len(durs), "compared": len(tail), "rocprof_avg_us": avg,

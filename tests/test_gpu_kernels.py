@@ -147,3 +147,29 @@ def test_prox_nan_propagates():
     assert torch.isnan(X[5]).all()
     assert not torch.isnan(X[4]).any()
     assert np.isnan(sums[1].item())            # max|x| is NaN like np.max
+
+
+@pytest.mark.parametrize("dtype", ["f64", "f32"])
+@pytest.mark.parametrize("split", [1, 3, 8, 9, 17, 24, 33, 64])
+def test_residual_batch_split_groups(monkeypatch, dtype, split):
+    """Forced K splits: the finalize sums S slabs over G = 1..8 lanes (8 slabs per lane, ragged
+    trailing lanes) and must give the same residual and sum of squares at every S."""
+    k = _glx()
+    monkeypatch.setenv("GLX_AXB_S", str(split))
+    m, n, l = 1000, 8192, 32
+    dt = torch.float64 if dtype == "f64" else torch.float32
+    g = torch.Generator(device="cuda").manual_seed(split)
+    A = torch.randn(m, n, device="cuda", dtype=torch.float64, generator=g).to(dt)
+    Xs = [torch.randn(n, l, device="cuda", dtype=torch.float64, generator=g).to(dt) for _ in range(2)]
+    B = torch.randn(m, l, device="cuda", dtype=torch.float64, generator=g).to(dt)
+    Rs, sq = k.residual_batch(A, Xs, B)
+    Rs2, sq2 = k.residual_batch(A, Xs, B)
+    torch.cuda.synchronize()
+    tol = 1e-13 if dtype == "f64" else 2e-6 * (n ** 0.5)
+    for j, (R, X) in enumerate(zip(Rs, Xs)):
+        ref = A.double() @ X.double() - B.double()
+        mag = A.double().abs() @ X.double().abs() + B.double().abs()
+        assert _rel_err(R, ref, mag) < tol, (j, split)
+        s = float((R.double() ** 2).sum())
+        assert abs(float(sq[j].item()) - s) <= (1e-12 if dtype == "f64" else 1e-6) * s
+        assert torch.equal(R, Rs2[j]) and torch.equal(sq[j], sq2[j])   # deterministic
