@@ -140,6 +140,10 @@ def main():
     ap.add_argument("--profile", type=int, default=16,
                     help="HIP events around every k-th A@x / A^T r launch (0 = off)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--comm", default="rccl", choices=["rccl", "host"],
+                    help="N > 1 transport: rccl (one GPU per rank) or host (all ranks share "
+                         "cuda:0, all-reduces staged through gloo — a one-GPU rehearsal, not a "
+                         "performance number)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -147,6 +151,8 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
         log("note: WORLD_SIZE=%d, --gpus=%d; using WORLD_SIZE" % (world, args.gpus))
+    if args.comm == "host":
+        local = 0
     torch.cuda.set_device(local)
     device = torch.device("cuda", local)
 
@@ -157,7 +163,7 @@ def main():
     if world > 1:
         import torch.distributed as dist
         dist.init_process_group("gloo", rank=rank, world_size=world)
-        comm = Comm.from_torch_distributed()
+        comm = Comm.host_staged() if args.comm == "host" else Comm.from_torch_distributed()
 
     m, n, l = args.m, args.n, args.l
     dtype = torch.float64 if args.dtype == "f64" else torch.float32
@@ -177,6 +183,7 @@ def main():
     s.run(args.warmup)
     s.kernel_time(0)
     s.kernel_time(1)
+    c0 = s.counters()
 
     if dist is not None:
         dist.barrier()
@@ -190,6 +197,8 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
         dist.barrier()
+    c1 = s.counters()
+    work = {k: c1[k] - c0[k] for k in c1}   # executed work of the timed region
     ax_n, ax_ms = s.kernel_time(0)
     atr_n, atr_ms = s.kernel_time(1)
     res = s.finish()
@@ -203,7 +212,7 @@ def main():
         ax_avg_s = (ax_ms / max(1, ax_n)) / 1e3
         atr_avg_s = (atr_ms / max(1, atr_n)) / 1e3
         # right-hand sides batched per A@x launch (e.g. A @ [z | p_thr] for ProxGD)
-        nsrc = res["ax_sources"] / max(1, res["ax_calls"])
+        nsrc = work["ax_sources"] / max(1, work["ax_calls"])
         ax_bytes = es * (ml * n + (ml + n) * l * nsrc)
         atr_bytes = es * (ml * n + (ml + n) * l)
         ax_flops = 2.0 * ml * n * l * nsrc
@@ -232,7 +241,8 @@ def main():
                 "atr_mfma_frac": (atr_flops / atr_avg_s / 1e12) / peak_tf if atr_n else None,
                 "pair_tflops": pair_tf, "pair_frac": pair_tf / peak_tf if pair_tf else None,
                 # all MFMA flops issued in the timed region / its wall time (gaps, prox included)
-                "iter_frac": (ax_n * ax_flops + atr_n * atr_flops) / elapsed / 1e12 / peak_tf}
+                "iter_frac": (2.0 * ml * n * l * work["ax_sources"] + work["atr_calls"] * atr_flops)
+                             / elapsed / 1e12 / peak_tf}
         steps = max(1, done)
         line = {
             "metric": METRIC, "value": steps / elapsed, "unit": "iters/s", "n_gpus": world,
@@ -244,11 +254,13 @@ def main():
             "config": {"workload": "%s %s (m,n,l)=(%d,%d,%d), mu0=1e-2, alpha0=1/(sqrt(m)+sqrt(n))^2"
                                    % (args.method, args.dtype, m, n, l, ),
                        "method": args.method, "m": m, "n": n, "l": l,
-                       "parallelism": "row-shard x%d (RCCL all-reduce of A^T r)" % world if world > 1 else "single GPU",
+                       "parallelism": ("row-shard x%d (%s all-reduce of A^T r)" % (world, "RCCL" if args.comm == "rccl" else "host-staged gloo, ranks sharing one GPU"))
+                                       if world > 1 else "single GPU",
                        "exact_objective": args.exact, "ax_variant": args.variant},
             "roofline": roof,
-            "work": {"ax_per_iter": ax_n / steps, "atr_per_iter": atr_n / steps,
-                     "passes_over_A_per_iter": (ax_n + atr_n) / steps,
+            "work": {"ax_per_iter": work["ax_calls"] / steps, "atr_per_iter": work["atr_calls"] / steps,
+                     "passes_over_A_per_iter": (work["ax_calls"] + work["atr_calls"]) / steps,
+                     "syncs_per_iter": work["syncs"] / steps,
                      "thr_changed_entries_per_step": res["stats"][0] / max(1.0, res["stats"][2]),
                      "thr_changed_rows_per_step": res["stats"][1] / max(1.0, res["stats"][2]),
                      "syncs_total": res["syncs"], "iters_total": res["k"]},

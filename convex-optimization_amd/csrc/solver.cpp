@@ -102,6 +102,7 @@ class SessionBase {
   virtual void run(int64_t max_steps, int64_t* done, int32_t* finished) = 0;
   virtual void finish(glx_result* res) = 0;
   virtual void kernel_time(int kind, int64_t* launches, double* ms) = 0;
+  virtual void counters(int64_t out[4]) const = 0;
 };
 
 template <typename T>
@@ -255,6 +256,13 @@ class Session : public SessionBase {
     y_ready_ = false;
     spec_ready_ = false;
     spec_trial_ready_ = false;
+  }
+
+  void counters(int64_t out[4]) const override {
+    out[0] = ax_calls_;
+    out[1] = ax_cols_;
+    out[2] = atr_calls_;
+    out[3] = syncs_;
   }
 
   void kernel_time(int kind, int64_t* launches, double* ms) override {
@@ -981,6 +989,13 @@ int glx_session_kernel_time(glx_session* s, int kind, int64_t* launches, double*
   return guarded([&] {
     if (!s || !s->impl) throw Error{GLX_E_INVALID, "null session"};
     s->impl->kernel_time(kind, launches, total_ms);
+  });
+}
+
+int glx_session_counters(glx_session* s, int64_t out[4]) {
+  return guarded([&] {
+    if (!s || !s->impl || !out) throw Error{GLX_E_INVALID, "null session/out"};
+    s->impl->counters(out);
   });
 }
 

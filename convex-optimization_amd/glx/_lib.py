@@ -66,6 +66,7 @@ _SIGS = {
     "glx_session_run": (c_int, [c_void_p, c_int64, POINTER(c_int64), POINTER(c_int32)]),
     "glx_session_finish": (c_int, [c_void_p, POINTER(GlxResult)]),
     "glx_session_kernel_time": (c_int, [c_void_p, c_int, POINTER(c_int64), POINTER(c_double)]),
+    "glx_session_counters": (c_int, [c_void_p, POINTER(c_int64)]),
     "glx_session_destroy": (None, [c_void_p]),
     "glx_solve": (c_int, [POINTER(GlxProblem), POINTER(GlxOpts), c_void_p, c_size_t,
                           POINTER(GlxResult), c_void_p]),
@@ -82,11 +83,15 @@ _SIGS = {
     "glx_plan_describe": (c_int, [c_int, c_int64, c_int64, c_int64, c_char_p, c_size_t]),
     "glx_comm_unique_id": (c_int, [POINTER(c_uint8)]),
     "glx_comm_create": (c_int, [POINTER(c_void_p), POINTER(c_uint8), c_int, c_int]),
+    "glx_comm_create_host": (c_int, [POINTER(c_void_p), c_int, c_int, c_void_p, c_void_p]),
     "glx_comm_allreduce": (c_int, [c_void_p, c_void_p, c_int64, c_int, c_void_p]),
     "glx_comm_destroy": (None, [c_void_p]),
 }
 
 EXPORTED = tuple(_SIGS)
+
+# glx_host_allreduce_fn: int (*)(void* host_buf, int64_t count, int dtype, void* user)
+HOST_ALLREDUCE_FN = ctypes.CFUNCTYPE(c_int, c_void_p, c_int64, c_int, c_void_p)
 
 
 def lib():

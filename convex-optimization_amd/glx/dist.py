@@ -26,10 +26,35 @@ def shard_rows(m: int, world: int, rank: int) -> Tuple[int, int]:
 class Comm:
     """An RCCL communicator created from a unique id broadcast over torch.distributed."""
 
-    def __init__(self, handle: ctypes.c_void_p, world: int, rank: int):
+    def __init__(self, handle: ctypes.c_void_p, world: int, rank: int, keep=None):
         self.handle = handle
         self.world = world
         self.rank = rank
+        self._keep = keep   # the host transport's ctypes callback must outlive the handle
+
+    @classmethod
+    def host_staged(cls, group=None) -> "Comm":
+        """A communicator whose all-reduces go through pinned host memory and
+        ``torch.distributed.all_reduce`` on ``group`` (gloo). For several ranks on ONE GPU (tests,
+        one-GPU rehearsal of the sharded solver): RCCL requires one rank per device."""
+        import numpy as np
+        import torch.distributed as dist
+        rank, world = dist.get_rank(group), dist.get_world_size(group)
+
+        def _allreduce(buf, count, dtype, _user):
+            try:
+                ct = ctypes.c_double if dtype == _lib.GLX_F64 else ctypes.c_float
+                arr = np.ctypeslib.as_array(ctypes.cast(buf, ctypes.POINTER(ct)), shape=(int(count),))
+                t = torch.from_numpy(arr)   # shares the pinned staging buffer
+                dist.all_reduce(t, group=group)
+                return 0
+            except Exception:   # never unwind through C
+                return 1
+
+        cb = _lib.HOST_ALLREDUCE_FN(_allreduce)
+        h = ctypes.c_void_p()
+        check(lib().glx_comm_create_host(ctypes.byref(h), world, rank, ctypes.cast(cb, ctypes.c_void_p), None))
+        return cls(h, world, rank, keep=cb)
 
     @classmethod
     def from_torch_distributed(cls, group=None) -> "Comm":

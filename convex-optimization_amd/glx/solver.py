@@ -150,6 +150,12 @@ class Session:
         check(lib().glx_session_kernel_time(self.h, kind, ctypes.byref(cnt), ctypes.byref(ms)))
         return cnt.value, ms.value
 
+    def counters(self) -> Dict[str, int]:
+        """Cumulative executed work: A@x passes, their right-hand sides, A^T r passes, readbacks."""
+        out = (ctypes.c_int64 * 4)()
+        check(lib().glx_session_counters(self.h, out))
+        return {"ax_calls": out[0], "ax_sources": out[1], "atr_calls": out[2], "syncs": out[3]}
+
     def finish(self) -> Dict[str, Any]:
         cap = max(1, 3 * int(self.o.maxit))
         if self.o.max_total_iters > 0:

@@ -125,6 +125,9 @@ int  glx_session_finish(glx_session* s, glx_result* res);
 /* launches timed and their total device time (ms) for A@x (kind 0) / A^T r (kind 1), sampled
  * every opts.profile-th launch; resets the accumulators. */
 int  glx_session_kernel_time(glx_session* s, int kind, int64_t* launches, double* total_ms);
+/* executed-work counters since create: out = {A@x passes, right-hand sides in them, A^T r
+ * passes, host readbacks} (cumulative; the caller differences them around a timed region). */
+int  glx_session_counters(glx_session* s, int64_t out[4]);
 void glx_session_destroy(glx_session* s);
 
 /* One-shot solve: create + run to completion + finish + destroy. */
@@ -159,6 +162,12 @@ int glx_plan_describe(int dtype, int64_t m, int64_t n, int64_t l, char* out, siz
 #define GLX_COMM_ID_BYTES 128
 int  glx_comm_unique_id(uint8_t id[GLX_COMM_ID_BYTES]);
 int  glx_comm_create(glx_comm** out, const uint8_t id[GLX_COMM_ID_BYTES], int nranks, int rank);
+/* Host-staged transport (testing: several ranks sharing one GPU, which RCCL refuses). Each
+ * all-reduce synchronises the stream, copies the buffer to pinned host memory, calls
+ * fn(host_buf, count, dtype, user) — which must sum it in place across ranks and return 0 —
+ * and copies it back. Not a performance path. */
+typedef int (*glx_host_allreduce_fn)(void* host_buf, int64_t count, int dtype, void* user);
+int  glx_comm_create_host(glx_comm** out, int nranks, int rank, glx_host_allreduce_fn fn, void* user);
 /* in-place sum all-reduce of `count` elements of dtype on `stream` (exposed for tests) */
 int  glx_comm_allreduce(glx_comm* c, void* buf, int64_t count, int dtype, void* stream);
 void glx_comm_destroy(glx_comm* c);
