@@ -140,6 +140,9 @@ def main():
     ap.add_argument("--profile", type=int, default=16,
                     help="HIP events around every k-th A@x / A^T r launch (0 = off)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--force-comm", action="store_true",
+                    help="create the communicator even at world size 1 (runs the N-GPU code path "
+                         "with identity all-reduces: a one-GPU model of a rank's schedule)")
     ap.add_argument("--comm", default="rccl", choices=["rccl", "host"],
                     help="N > 1 transport: rccl (one GPU per rank) or host (all ranks share "
                          "cuda:0, all-reduces staged through gloo — a one-GPU rehearsal, not a "
@@ -160,8 +163,10 @@ def main():
     from glx.dist import Comm, shard_rows
     dist = None
     comm = None
-    if world > 1:
+    if world > 1 or args.force_comm:
         import torch.distributed as dist
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        os.environ.setdefault("MASTER_PORT", "29512")
         dist.init_process_group("gloo", rank=rank, world_size=world)
         comm = Comm.host_staged() if args.comm == "host" else Comm.from_torch_distributed()
 

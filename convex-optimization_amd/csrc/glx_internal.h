@@ -155,8 +155,9 @@ void launch_fgd_grad(const T* y, const T* gp, int S, T* g, int64_t n, int64_t l,
 // fh[idx] = 0.5 * s[i_sumsq] + mu * s[i_reg]
 void launch_record_f(const double* s, int i_sumsq, int i_reg, double mu, double* fh, int64_t idx,
                      hipStream_t st);
-// host[0..ns) = s[0..ns), then *host_seq = seq (system-scope release); host memory is mapped
+// host[0..ns) = s[0..ns) except host[off2..off2+n2) = s2[0..n2) when s2 != NULL, then
+// *host_seq = seq (system-scope release); host memory is mapped
 void launch_publish(const double* s, int ns, double* host, unsigned* host_seq, unsigned seq,
-                    hipStream_t st);
+                    hipStream_t st, const double* s2 = nullptr, int off2 = 0, int n2 = 0);
 
 }  // namespace glx

@@ -40,10 +40,12 @@ static inline unsigned grid_for(int64_t work, int per_block) {
 // (profiles/r1_tuning, fused-publish attribution) than a separate launch (~5.5 us).
 constexpr int kPublishMax = 32;
 __device__ inline void publish_packet(const double* s, int ns, double* host, unsigned* host_seq,
-                                      unsigned seq) {
+                                      unsigned seq, const double* s2 = nullptr, int off2 = 0,
+                                      int n2 = 0) {
   double v[kPublishMax];
 #pragma unroll
-  for (int k = 0; k < kPublishMax; ++k) v[k] = k < ns ? s[k] : 0.0;
+  for (int k = 0; k < kPublishMax; ++k)
+    v[k] = (k >= off2 && k < off2 + n2) ? s2[k - off2] : (k < ns ? s[k] : 0.0);
 #pragma unroll
   for (int k = 0; k < kPublishMax; ++k)
     if (k < ns) __hip_atomic_store(host + k, v[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
@@ -425,8 +427,8 @@ __global__ __launch_bounds__(256) void k_thr_axpby(T* __restrict__ xk, const T* 
 
 // publish the scalar packet to host-mapped memory: data, then (system-scope release) seq
 __global__ void k_publish(const double* __restrict__ s, int ns, double* host, unsigned* host_seq,
-                          unsigned seq) {
-  if (threadIdx.x == 0) publish_packet(s, ns, host, host_seq, seq);
+                          unsigned seq, const double* __restrict__ s2, int off2, int n2) {
+  if (threadIdx.x == 0) publish_packet(s, ns, host, host_seq, seq, s2, off2, n2);
 }
 
 template <typename T>
@@ -591,8 +593,9 @@ void launch_record_f(const double* s, int i_sumsq, int i_reg, double mu, double*
   hipLaunchKernelGGL(k_record_f, dim3(1), dim3(64), 0, st, s, i_sumsq, i_reg, mu, fh, idx);
 }
 void launch_publish(const double* s, int ns, double* host, unsigned* host_seq, unsigned seq,
-                    hipStream_t st) {
-  hipLaunchKernelGGL(k_publish, dim3(1), dim3(64), 0, st, s, ns, host, host_seq, seq);
+                    hipStream_t st, const double* s2, int off2, int n2) {
+  hipLaunchKernelGGL(k_publish, dim3(1), dim3(64), 0, st, s, ns, host, host_seq, seq, s2, off2,
+                     s2 ? n2 : 0);
 }
 
 #define GLX_INST(T)                                                                                  \

@@ -76,6 +76,7 @@ static int method_bufs(int method) {
   }
 }
 constexpr int kBufs = 9;
+constexpr int kTailBytes = 64;   // behind each gradient set: scalars that ride its all-reduce
 constexpr int kRes = 4;
 
 static void validate(const glx_problem* P, const glx_opts* O) {
@@ -122,7 +123,7 @@ class Session : public SessionBase {
     T* g[2];
     T* gp[2];
     for (int k = 0; k < 2; ++k) {
-      g[k] = static_cast<T*>(c.take(sizeof(T) * nl));
+      g[k] = static_cast<T*>(c.take(sizeof(T) * nl + kTailBytes));   // + scalar tail (comm)
       gp[k] = plan.atr_S > 1 ? static_cast<T*>(c.take(sizeof(T) * nl * plan.atr_S)) : g[k];
     }
     T* pp = static_cast<T*>(c.take(sizeof(T) * ml * ax_split_max(plan) * 3));   // up to 3 batched sources
@@ -172,7 +173,10 @@ class Session : public SessionBase {
     const char* sp = std::getenv("GLX_SPEC_GRAD");
     spec_off_env_ = (sp && std::strcmp(sp, "0") == 0);
     const char* fz = std::getenv("GLX_FUSED_TRIAL");
-    const bool fuse_any = comm_ == nullptr && atr_prox_ok(plan_) &&
+    // With a communicator the trial cannot live in the A^T r epilogue (the gradient is summed
+    // over ranks first): it runs as A^T r, all-reduce, then k_prox_pgd / k_fista_trial, and is
+    // queued speculatively the same way (see atr_prox).
+    const bool fuse_any = (comm_ != nullptr || atr_prox_ok(plan_)) &&
                           (O.step_type == GLX_STEP_LINE_SEARCH || O.step_type == GLX_STEP_FIXED) &&
                           !(fz && std::strcmp(fz, "0") == 0);
     fused_ok_ = fuse_any && P.method == GLX_PROXGD;
@@ -194,6 +198,7 @@ class Session : public SessionBase {
 
   ~Session() override {
     if (hs_) (void)hipHostFree(hs_);
+    if (rb_event_) (void)hipEventDestroy(rb_event_);
     for (auto& v : ev_)
       for (auto& p : v) { (void)hipEventDestroy(p.first); (void)hipEventDestroy(p.second); }
     for (hipEvent_t e : ev_pool_) (void)hipEventDestroy(e);
@@ -329,9 +334,12 @@ class Session : public SessionBase {
   // pub_seq != NULL: also enqueue the scalar packet for the host once the sums are final
   // (after the all-reduce with a communicator); *pub_seq receives the sequence number to wait
   // for (wait_readback), so more work can be queued before the host blocks.
+  // defer != NULL (communicator, f64): the sums go to `defer` (a gradient set's tail) instead
+  // of scal[slot..], are NOT all-reduced here and nothing is published — they ride the next
+  // gradient all-reduce and publish (atr_prox / atr_fista), saving one all-reduce per iteration.
   void residuals(int nsrc, const T* const* xs, T* const* rs, int slot, const T* cx = nullptr,
                  const double* cmax = nullptr, double* fh = nullptr, double fh_mu = 0.0,
-                 unsigned* pub_seq = nullptr) {
+                 unsigned* pub_seq = nullptr, double* defer = nullptr) {
     hipEvent_t e0 = prof_begin(0);
     launch_ax<T>(plan_, nsrc, A_, xs, Pp_, nullptr, 0, st_);
     check_launch();
@@ -340,8 +348,9 @@ class Session : public SessionBase {
     ax_cols_ += nsrc;
     launch_finalize_residual<T>(Pp_, ax_split(plan_, nsrc), B_, nsrc, rs, ml_, nullptr, 0, 1, cx,
                                 cx ? nl_ : 0, cmax, comm_ ? nullptr : fh, fh_mu, scal_ + S_DRN,
-                                red(slot), st_);
+                                defer ? Red{part_, ticket_, defer} : red(slot), st_);
     check_launch();
+    if (defer) return;
     if (comm_) {
       comm_allreduce(comm_, scal_ + slot, nsrc, GLX_F64, st_);
       if (fh) {
@@ -360,7 +369,9 @@ class Session : public SessionBase {
 
   // G = A^T r as slabs of gradient set `set` (default: the current one); returns (source, S)
   // for the consumer. With a communicator the slabs are summed and all-reduced first (S = 1).
-  std::pair<const T*, int> gradient(const T* r, int set = -1) {
+  // tail_n > 0 (communicator, f64): the all-reduce also sums the first tail_n doubles of the
+  // set's tail (deferred residual sums, see residuals()).
+  std::pair<const T*, int> gradient(const T* r, int set = -1, int tail_n = 0) {
     if (set < 0) set = gset_;
     T* G = Gs_[set];
     T* Gp = Gps_[set];
@@ -374,10 +385,13 @@ class Session : public SessionBase {
       launch_sum_partials<T>(Gp, plan_.atr_S, G, nl_, st_);
       check_launch();
     }
-    comm_allreduce(comm_, G, nl_, P_.dtype, st_);
+    comm_allreduce(comm_, G, nl_ + tail_n, P_.dtype, st_);
     return {G, 1};
   }
   void use_gset(int set) { gset_ = set; G_ = Gs_[set]; Gp_ = Gps_[set]; }
+  double* tail(int set) { return reinterpret_cast<double*>(Gs_[set] + nl_); }
+  // merge a speculated trial's residual sums into the next gradient all-reduce
+  bool merge_tail() const { return comm_ != nullptr && sizeof(T) == 8; }
 
   // Speculative gradient (ProxGD / FISTA with line search). The next iteration's gradient
   // residual is produced by the trial's batched A@X, and the next gradient depends only on
@@ -400,18 +414,24 @@ class Session : public SessionBase {
   // Scalar readback in two halves so that work can be queued between them (the speculative
   // gradient): post_readback enqueues the packet copy behind everything queued so far and
   // returns its sequence number; wait_readback spins on the host-mapped sequence word.
-  unsigned post_readback() {
+  // extra != NULL: the packet's S_RT..S_RT+3 come from extra[0..4) (a gradient set's tail)
+  unsigned post_readback(const double* extra = nullptr) {
     ++syncs_;
-    if (!spin_readback_) return 0;
+    if (!spin_readback_) {   // GLX_READBACK=sync: stream-ordered copies, then an event wait
+      GLX_HIP(hipMemcpyAsync(hs_, scal_, sizeof(double) * NSCAL, hipMemcpyDeviceToHost, st_));
+      if (extra) GLX_HIP(hipMemcpyAsync(hs_ + S_RT, extra, 4 * sizeof(double), hipMemcpyDeviceToHost, st_));
+      if (!rb_event_) GLX_HIP(hipEventCreateWithFlags(&rb_event_, hipEventDisableTiming));
+      GLX_HIP(hipEventRecord(rb_event_, st_));
+      return 0;
+    }
     const unsigned seq = ++seq_;
-    launch_publish(scal_, NSCAL, hs_dev_, hseq_dev_, seq, st_);
+    launch_publish(scal_, NSCAL, hs_dev_, hseq_dev_, seq, st_, extra, S_RT, 4);
     check_launch();
     return seq;
   }
   void wait_readback(unsigned seq) {
     if (!spin_readback_) {
-      GLX_HIP(hipMemcpyAsync(hs_, scal_, sizeof(double) * NSCAL, hipMemcpyDeviceToHost, st_));
-      GLX_HIP(hipStreamSynchronize(st_));
+      GLX_HIP(hipEventSynchronize(rb_event_));
       return;
     }
     // spin on the sequence word the GPU writes after the packet (system-scope release)
@@ -555,14 +575,18 @@ class Session : public SessionBase {
         // one pass: g(z) for the test (:91) + the next iteration's residuals A p_thr (and A p)
         const T* xs[3] = {X_[iz_], X_[ipt_], X_[ip_]};
         T* rs[3] = {R_[rz], R_[rpt], R_[rp]};
+        const int nsrc = exact ? 3 : 2;
         unsigned seq = 0;
-        residuals(exact ? 3 : 2, xs, rs, S_RT, X_[ip_], scal_ + S_TR + 3, nullptr, 0.0, &seq);
         const bool spec = want_spec(it);
+        const bool merge = spec && fused_ok_ && merge_tail();
+        residuals(nsrc, xs, rs, S_RT, X_[ip_], scal_ + S_TR + 3, nullptr, 0.0, merge ? nullptr : &seq,
+                  merge ? tail(1 - gset_) : nullptr);
         std::pair<const T*, int> sg;
         if (spec && fused_ok_) {
           // the next iteration's A^T r and first trial at the candidate p_thr, into the other
           // gradient set and the spare buffers (z is free once this trial's A@X has read it)
-          atr_prox(R_[rpt], 1 - gset_, X_[ipt_], if1_, if2_, iz_, O_.alpha0);
+          atr_prox(R_[rpt], 1 - gset_, X_[ipt_], if1_, if2_, iz_, O_.alpha0, merge ? nsrc : 0,
+                   merge ? &seq : nullptr);
           spec_trial = true;
         } else if (spec) {
           sg = gradient(R_[rpt], 1 - gset_);   // gradient at the candidate p_thr
@@ -616,8 +640,20 @@ class Session : public SessionBase {
     }
   }
 
-  // A^T r fused with a ProxGD trial at x (gradient set `set`, outputs X_[op], X_[opt], X_[oz])
-  void atr_prox(const T* r, int set, const T* x, int op, int opt, int oz, double t) {
+  // A^T r fused with a ProxGD trial at x (gradient set `set`, outputs X_[op], X_[opt], X_[oz]).
+  // With a communicator: A^T r, the all-reduce (also summing tail_n deferred residual sums of
+  // the set's tail), the scalar packet if pub_seq (so the host reads those sums while the trial
+  // runs), then k_prox_pgd — the same arithmetic as the fused epilogue.
+  void atr_prox(const T* r, int set, const T* x, int op, int opt, int oz, double t, int tail_n = 0,
+                unsigned* pub_seq = nullptr) {
+    if (comm_) {
+      const std::pair<const T*, int> g = gradient(r, set, tail_n);
+      if (pub_seq) *pub_seq = post_readback(tail_n ? tail(set) : nullptr);
+      launch_prox_pgd<T>(x, g.first, g.second, nullptr, X_[op], X_[opt], X_[oz], n_, l_, t, mu_,
+                         O_.thres, red(S_TR), st_);
+      check_launch();
+      return;
+    }
     hipEvent_t e0 = prof_begin(1);
     launch_atr_prox<T>(plan_, A_, r, Gs_[set], x, X_[op], X_[opt], X_[oz], t, mu_, O_.thres,
                        red(S_TR), st_);
@@ -691,13 +727,15 @@ class Session : public SessionBase {
         const T* xs[3] = {X_[ic_], X_[iyn_], nullptr};
         T* rs[3] = {R_[rc], R_[ryn], nullptr};
         unsigned seq = 0;
-        residuals(2, xs, rs, S_RT, X_[ic_], scal_ + S_TR + i_max, nullptr, 0.0, &seq);   // A @ [x | y_next]
         const bool spec = want_spec(it);
+        const bool merge = spec && fuse && merge_tail();
+        residuals(2, xs, rs, S_RT, X_[ic_], scal_ + S_TR + i_max, nullptr, 0.0,   // A @ [x | y_next]
+                  merge ? nullptr : &seq, merge ? tail(1 - gset_) : nullptr);
         std::pair<const T*, int> sg;
         if (spec && fuse) {
           // the next iteration's gradient at y_next and its first trial (t, theta' = theta_next)
           atr_fista(R_[ryn], 1 - gset_, X_[iyn_], X_[ic_], ff1_, ff2_, ff3_, t, theta_next,
-                    2.0 / (double)(inner_ + 3));
+                    2.0 / (double)(inner_ + 3), merge ? 2 : 0, merge ? &seq : nullptr);
           spec_trial = true;
         } else if (spec) {
           sg = gradient(R_[ryn], 1 - gset_);   // gradient at the next y
@@ -756,8 +794,17 @@ class Session : public SessionBase {
 
   // A^T r fused with a FISTA trial at y (gradient set `set`; x_k = xk; outputs X_[oc], X_[ov],
   // X_[oy])
+  // (with a communicator: as atr_prox, the trial as k_fista_trial after the all-reduce)
   void atr_fista(const T* r, int set, const T* yv, const T* xk, int oc, int ov, int oy, double t,
-                 double theta, double theta_next) {
+                 double theta, double theta_next, int tail_n = 0, unsigned* pub_seq = nullptr) {
+    if (comm_) {
+      const std::pair<const T*, int> g = gradient(r, set, tail_n);
+      if (pub_seq) *pub_seq = post_readback(tail_n ? tail(set) : nullptr);
+      launch_fista_trial<T>(true, yv, g.first, g.second, nullptr, xk, X_[oc], X_[ov], X_[oy], n_,
+                            l_, t, mu_, O_.thres, theta, theta_next, O_.delta, red(S_TR), st_);
+      check_launch();
+      return;
+    }
     hipEvent_t e0 = prof_begin(1);
     launch_atr_fista<T>(plan_, A_, r, Gs_[set], yv, xk, X_[oc], X_[ov], X_[oy], t, mu_, O_.thres,
                         theta, theta_next, red(S_TR), st_);
@@ -825,6 +872,7 @@ class Session : public SessionBase {
   int method_ = 0;
   bool use_sparsity_ = true, device_hist_ = false, spin_readback_ = true;
   unsigned seq_ = 0;
+  hipEvent_t rb_event_ = nullptr;
   int epoch_ = 0;
   // buffer roles
   int ix_ = 0, iv_ = 1, iy_ = 2, ic_ = 3, ivn_ = 4, iyn_ = 5;   // FISTA
