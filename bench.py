@@ -236,7 +236,9 @@ def main():
         roof = {"bound": "mfma" if mfma_bound else "hbm", "achieved": ach, "peak": peak,
                 "unit": unit, "frac": (ach / peak) if ach else None,
                 "traffic": pmc_traffic(cfg_key),
-                "kernel": ax_kernel_name(args.dtype, ml, n, l, nsrc), "flops_per_launch": ax_flops,
+                "kernel": ("k_gemv_pair_fused: A@[x|thr(x)] and A^T r in ONE pass over A (l = 1)"
+                           if work["atr_calls"] == 0 else ax_kernel_name(args.dtype, ml, n, l, nsrc)),
+                "flops_per_launch": ax_flops,
                 "bytes_per_launch": ax_bytes, "avg_launch_us": ax_avg_s * 1e6, "launches_timed": ax_n,
                 "timed_every": args.profile,
                 "rhs_per_launch": nsrc, "hbm_GBs": ax_gbs, "hbm_frac": ax_gbs / HBM_PEAK_GBS if ax_n else None,

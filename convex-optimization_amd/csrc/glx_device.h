@@ -19,10 +19,21 @@ __device__ inline double nan_max(double a, double b) {
 __device__ inline double combine(int op, double a, double b) { return op == OP_MAX ? nan_max(a, b) : a + b; }
 __device__ inline double identity(int op) { return op == OP_MAX ? -__builtin_inf() : 0.0; }
 
-// Reduce NV per-thread values over the grid; block size must be 256. MAXMASK bit v = max op.
-template <int NV, unsigned MAXMASK>
+// Fixed-order combine of NW per-wave values: ((w0 + w1) + (w2 + w3)) [+ the same for w4..w7].
+template <int NW>
+__device__ inline double waves_combine(int op, const double* w) {
+  double a = combine(op, combine(op, w[0], w[1]), combine(op, w[2], w[3]));
+  if constexpr (NW == 8) a = combine(op, a, combine(op, combine(op, w[4], w[5]), combine(op, w[6], w[7])));
+  return a;
+}
+
+// Reduce NV per-thread values over the grid; block size must be 64 * NW (NW = 4 or 8).
+// MAXMASK bit v = max op.
+template <int NV, unsigned MAXMASK, int NW = 4>
 __device__ bool grid_reduce(double (&v)[NV], const Red& red) {
-  __shared__ double sh[NV][4];
+  static_assert(NW == 4 || NW == 8, "4- or 8-wave blocks");
+  constexpr int NTHR = 64 * NW;
+  __shared__ double sh[NV][NW];
   __shared__ int is_last;
   const int lane = threadIdx.x & 63;
   const int wave = threadIdx.x >> 6;
@@ -43,7 +54,7 @@ __device__ bool grid_reduce(double (&v)[NV], const Red& red) {
 #pragma unroll
     for (int j = 0; j < NV; ++j) {
       const int op = (MAXMASK >> j) & 1;
-      const double bv = combine(op, combine(op, sh[j][0], sh[j][1]), combine(op, sh[j][2], sh[j][3]));
+      const double bv = waves_combine<NW>(op, sh[j]);
       __hip_atomic_store(&red.part[j * kMaxBlocks + blockIdx.x], bv, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -68,13 +79,13 @@ __device__ bool grid_reduce(double (&v)[NV], const Red& red) {
   // every load of the partials is an sc1 load (L1 bypass): no acquire fence needed. All of them
   // are issued before the first is consumed (clamped index, select afterwards), so the last
   // block pays one round trip instead of one per partial.
-  constexpr int PER = kMaxBlocks / 256;
+  constexpr int PER = kMaxBlocks / NTHR;
   double pv[NV][PER];
 #pragma unroll
   for (int j = 0; j < NV; ++j)
 #pragma unroll
     for (int t = 0; t < PER; ++t) {
-      const unsigned b = threadIdx.x + 256u * t;
+      const unsigned b = threadIdx.x + (unsigned)NTHR * t;
       const unsigned bc = b < gridDim.x ? b : gridDim.x - 1;
       pv[j][t] = __hip_atomic_load(&red.part[j * kMaxBlocks + bc], __ATOMIC_RELAXED,
                                    __HIP_MEMORY_SCOPE_AGENT);
@@ -86,7 +97,7 @@ __device__ bool grid_reduce(double (&v)[NV], const Red& red) {
     acc[j] = identity(op);
 #pragma unroll
     for (int t = 0; t < PER; ++t)
-      if (threadIdx.x + 256u * t < gridDim.x) acc[j] = combine(op, acc[j], pv[j][t]);
+      if (threadIdx.x + (unsigned)NTHR * t < gridDim.x) acc[j] = combine(op, acc[j], pv[j][t]);
 #pragma unroll
     for (int off = 32; off > 0; off >>= 1) acc[j] = combine(op, acc[j], __shfl_xor(acc[j], off));
   }
@@ -100,7 +111,7 @@ __device__ bool grid_reduce(double (&v)[NV], const Red& red) {
 #pragma unroll
     for (int j = 0; j < NV; ++j) {
       const int op = (MAXMASK >> j) & 1;
-      red.out[j] = combine(op, combine(op, sh[j][0], sh[j][1]), combine(op, sh[j][2], sh[j][3]));
+      red.out[j] = waves_combine<NW>(op, sh[j]);
     }
     for (int k = 0; k <= kTicketShards; ++k)
       __hip_atomic_store(red.ticket + k * kTicketStride, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);

@@ -155,6 +155,17 @@ void launch_fgd_grad(const T* y, const T* gp, int S, T* g, int64_t n, int64_t l,
 // fh[idx] = 0.5 * s[i_sumsq] + mu * s[i_reg]
 void launch_record_f(const double* s, int i_sumsq, int i_reg, double mu, double* fh, int64_t idx,
                      hipStream_t st);
+// l = 1 descent pass in one sweep of A (kernels_gemv.hip): Gp[blocks][n] = per-workgroup
+// A^T (A xt - b) slabs, red.out[0..1] = sum (A x - b)^2, sum (A xt - b)^2, fh[0] (if non-null)
+// = 0.5 out[0] + fh_mu * rn[0]. gemv_fused_blocks() = workgroups to launch, 0 = not applicable.
+int gemv_fused_blocks(int esize, int64_t m, int64_t n, int64_t l);
+template <typename T>
+void launch_gemv_fused(int blocks, const T* A, const T* x, const T* xt, const T* b, T* Gp, int64_t m,
+                       int64_t n, double* fh, double fh_mu, const double* rn, Red red,
+                       hipStream_t st);
+// G[j] = sum_{s<S} Gp[s][j] (slab order, deterministic)
+template <typename T>
+void launch_sum_cols(const T* Gp, int S, T* G, int64_t n, hipStream_t st);
 // host[0..ns) = s[0..ns) except host[off2..off2+n2) = s2[0..n2) when s2 != NULL, then
 // *host_seq = seq (system-scope release); host memory is mapped
 void launch_publish(const double* s, int ns, double* host, unsigned* host_seq, unsigned seq,

@@ -1222,6 +1222,18 @@ static int env_int(const char* name, int dflt) {
   return (v && *v) ? std::atoi(v) : dflt;
 }
 
+// Occupancy pad (tuning experiment, GLX_AX_LDS_PAD / GLX_ATR_LDS_PAD bytes): unused dynamic
+// LDS added to a launch so that at most one workgroup fits per CU — a 256-workgroup grid can
+// then not double up on some CUs while others idle. 0 = off (the default).
+template <typename K>
+static size_t lds_pad(K kernel, const char* env) {
+  const int pad = env_int(env, 0);
+  if (pad <= 0) return 0;
+  (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kernel),
+                            hipFuncAttributeMaxDynamicSharedMemorySize, pad);
+  return (size_t)pad;
+}
+
 // Defaults chosen by the sweep in scripts/kbench.py on MI355X.
 // ax code: kind*1000 + MT*100 + PF*10 + NTL (kind 1 = direct row loads, 2 = quad + bpermute).
 // kind 5 (X staged in LDS) code: 5 MT PF VPL WAVES. Kind-5 defaults fall back to the register
@@ -1467,8 +1479,9 @@ static void ax_lds_go(const GemmPlan& p, int S, const T* A, const T* const* X, T
   constexpr int E = 16 / sizeof(T);
   const int gx = (int)cdiv(p.m, 16 * MT * WAVES);
   const int xmap = (p.ax_xmap && ax_xmap_ok(S)) ? 1 : 0;
+  static const size_t pad = lds_pad(k_ax_lds<T, MT, NT, NSRC, PF, VPL, WAVES, ABL>, "GLX_AX_LDS_PAD");
   hipLaunchKernelGGL((k_ax_lds<T, MT, NT, NSRC, PF, VPL, WAVES, ABL>), dim3((unsigned)ax_grid(xmap, gx, S)),
-                     dim3(64 * WAVES), 0, st, A, X[0], X[1], X[2], P, p.m, p.n,
+                     dim3(64 * WAVES), pad, st, A, X[0], X[1], X[2], P, p.m, p.n,
                      p.n / (4 * VPL * E), S, gx, xmap, gate, epoch);
 }
 
@@ -1637,7 +1650,8 @@ static void atr_valu_lb(const GemmPlan& p, const T* A, const T* R, T* Gp, hipStr
 template <typename T, int NT, int PF, int WL, bool NTL>
 static void atr_mfma_go(const GemmPlan& p, const T* A, const T* R, T* Gp, hipStream_t st) {
   const dim3 grid((unsigned)(p.n / (WL ? 256 : 64)), (unsigned)p.atr_S);
-  hipLaunchKernelGGL((k_atr_mfma<T, NT, PF, WL, NTL>), grid, dim3(256), 0, st, A, R, Gp, p.m, p.n, p.atr_S);
+  static const size_t pad = lds_pad(k_atr_mfma<T, NT, PF, WL, NTL>, "GLX_ATR_LDS_PAD");
+  hipLaunchKernelGGL((k_atr_mfma<T, NT, PF, WL, NTL>), grid, dim3(256), pad, st, A, R, Gp, p.m, p.n, p.atr_S);
 }
 
 template <typename T, int NT>
@@ -1682,7 +1696,8 @@ bool atr_prox_ok(const GemmPlan& p) {
 template <typename T, int NT, int PF, bool NTL>
 static void atr_prox_go(const GemmPlan& p, const T* A, const T* R, T* G, const T* x, T* pp,
                         T* pthr, T* z, double t, double mu, double thres, Red red, hipStream_t st) {
-  hipLaunchKernelGGL((k_atr_prox<T, NT, PF, NTL>), dim3((unsigned)(p.n / 64)), dim3(256), 0, st, A, R,
+  static const size_t pad = lds_pad(k_atr_prox<T, NT, PF, NTL>, "GLX_ATR_LDS_PAD");
+  hipLaunchKernelGGL((k_atr_prox<T, NT, PF, NTL>), dim3((unsigned)(p.n / 64)), dim3(256), pad, st, A, R,
                      G, p.m, p.n, x, pp, pthr, z, t, t * mu, thres, red);
 }
 template <typename T, int NT>
@@ -1707,7 +1722,8 @@ template <typename T, int NT, int PF, bool NTL>
 static void atr_fista_go(const GemmPlan& p, const T* A, const T* R, T* G, const T* y, const T* xk,
                          T* xc, T* vn, T* yn, double t, double mu, double thres, double theta,
                          double theta_next, Red red, hipStream_t st) {
-  hipLaunchKernelGGL((k_atr_fista<T, NT, PF, NTL>), dim3((unsigned)(p.n / 64)), dim3(256), 0, st, A,
+  static const size_t pad = lds_pad(k_atr_fista<T, NT, PF, NTL>, "GLX_ATR_LDS_PAD");
+  hipLaunchKernelGGL((k_atr_fista<T, NT, PF, NTL>), dim3((unsigned)(p.n / 64)), dim3(256), pad, st, A,
                      R, G, p.m, p.n, y, xk, xc, vn, yn, t, t * mu, thres, theta, 1.0 - theta_next,
                      theta_next, red);
 }

@@ -132,14 +132,27 @@ class Session : public SessionBase {
     unsigned* ticket = static_cast<unsigned*>(c.take(kTicketBytes));
     int* flag = static_cast<int*>(c.take(256));
     double* fh = static_cast<double*>(c.take(sizeof(double) * (fh_cap + 1)));
+    const int gb = gemv_blocks_for(P);
+    T* gs = gb > 0 ? static_cast<T*>(c.take(sizeof(T) * nl * gb)) : nullptr;   // fused l = 1 slabs
     if (s) {
       for (int i = 0; i < kBufs; ++i) s->X_[i] = bufs[i];
       for (int i = 0; i < kRes; ++i) s->R_[i] = res[i];
       for (int k = 0; k < 2; ++k) { s->Gs_[k] = g[k]; s->Gps_[k] = gp[k]; }
       s->G_ = g[0]; s->Gp_ = gp[0]; s->Pp_ = pp;
       s->scal_ = scal; s->part_ = part; s->ticket_ = ticket; s->flag_ = flag; s->fh_dev_ = fh;
+      s->gemv_slabs_ = gs;
+      s->gemv_blocks_ = gb;
     }
     return c.off + 256;
+  }
+
+  // SGD / GD with l = 1: the descent pass reads A once (kernels_gemv.hip); GLX_GEMV_FUSED=0
+  // selects the two-pass path (A @ [x | thr(x)], then A^T r)
+  static int gemv_blocks_for(const glx_problem& P) {
+    if (P.method != GLX_SGD && P.method != GLX_GD) return 0;
+    const char* e = std::getenv("GLX_GEMV_FUSED");
+    if (e && std::strcmp(e, "0") == 0) return 0;
+    return gemv_fused_blocks((int)sizeof(T), P.m, P.n, P.l);
   }
 
   static int64_t fh_capacity(const glx_problem& P, const glx_opts& O) {
@@ -824,6 +837,30 @@ class Session : public SessionBase {
     T* rs[3] = {R_[0], R_[1], nullptr};
     residuals(2, xs, rs, S_RO, nullptr, nullptr, fh_dev_ + k_, descent_mu_obj(phase));
   }
+  // l = 1, one pass over A: the objective of x (recorded at fh[k]) and the slabs of the
+  // gradient A^T (A thr(x) - b) (kernels_gemv.hip)
+  void descent_pass(int64_t phase) {
+    hipEvent_t e0 = prof_begin(0);
+    launch_gemv_fused<T>(gemv_blocks_, A_, X_[0], X_[1], B_, gemv_slabs_, m_, n_,
+                         comm_ ? nullptr : fh_dev_ + k_, descent_mu_obj(phase), scal_ + S_DRN,
+                         red(S_RO), st_);
+    check_launch();
+    prof_end(0, e0);
+    ++ax_calls_;
+    ax_cols_ += 2;
+    if (comm_) {
+      comm_allreduce(comm_, scal_ + S_RO, 2, GLX_F64, st_);
+      launch_record_f(scal_, S_RO, S_DRN, descent_mu_obj(phase), fh_dev_ + k_, 0, st_);
+      check_launch();
+    }
+  }
+  std::pair<const T*, int> descent_gradient() {
+    if (gemv_blocks_ == 0) return gradient(R_[1]);
+    launch_sum_cols<T>(gemv_slabs_, gemv_blocks_, G_, n_, st_);   // l = 1: n x l = n
+    check_launch();
+    if (comm_) comm_allreduce(comm_, G_, nl_, P_.dtype, st_);
+    return {G_, 1};
+  }
   void iter_descent() {
     const bool gd = (method_ == GLX_GD);
     if (!state_valid_) {
@@ -831,19 +868,21 @@ class Session : public SessionBase {
       check_launch();
       launch_threshold<T>(X_[0], X_[1], nl_, O_.thres, flag_, ++epoch_, st_);
       check_launch();
-      descent_residuals(phase_);
+      if (gemv_blocks_) descent_pass(phase_);
+      else descent_residuals(phase_);
       state_valid_ = true;
     }
     ++k_;
     ++inner_;
-    const std::pair<const T*, int> g = gradient(R_[1]);
+    const std::pair<const T*, int> g = descent_gradient();
     const double alpha = (O_.step_type == GLX_STEP_FIXED || mu_ > P_.mu0) ? O_.alpha0 : schedule(inner_);
     launch_descent<T>(X_[0], X_[1], g.first, g.second, n_, l_, alpha, mu_, O_.thres, O_.delta,
                       gd ? 1 : 0, red(S_DRN), st_);
     check_launch();
     // next iteration's objective residual and gradient residual, one pass
     const int64_t next_phase = (inner_ >= O_.maxit) ? phase_ + 1 : phase_;
-    descent_residuals(next_phase);
+    if (gemv_blocks_) descent_pass(next_phase);
+    else descent_residuals(next_phase);
   }
 
  public:
@@ -867,6 +906,8 @@ class Session : public SessionBase {
   unsigned* ticket_ = nullptr;
   int* flag_ = nullptr;
   int64_t fh_cap_ = 0;
+  T* gemv_slabs_ = nullptr;
+  int gemv_blocks_ = 0;
 
  private:
   int method_ = 0;
