@@ -44,7 +44,7 @@ def main():
     write = load(args.write, "WRITE_SIZE")
     summary = {}
     for name in fetch:
-        short = "ax" if "k_ax_" in name else ("atr" if "k_atr_" in name else None)
+        short = "ax" if ("k_ax_" in name or "k_gemv_" in name) else ("atr" if "k_atr_" in name else None)
         if short is None:
             continue
         f = sum(fetch[name]) / len(fetch[name])
