@@ -145,3 +145,31 @@ def test_large_vs_oracle_few_iterations(solver, dtype, shape):
     tol = 1e-8 if dtype == "f64" else 1e-4
     assert _rel(out["fval"], outr["fval"]) < tol
     assert _rel(np.asarray(out["f_hist"], float), np.asarray(outr["f_hist"], float)) < tol
+
+
+@pytest.mark.parametrize("solver,dtype,shape", [
+    ("gl_ProxGD_primal", "f64", (8192, 16384, 32)),     # north-star size (bench.py's workload)
+    ("gl_FProxGD_primal", "f64", (8192, 16384, 32)),
+    ("gl_FProxGD_primal", "f32", (8192, 16384, 32)),    # C3
+    ("gl_SGD_primal", "f64", (65536, 8192, 1)),         # C4 (one-pass l = 1 kernel)
+])
+def test_full_size_vs_oracle(solver, dtype, shape):
+    """BASELINE.json's full sizes: two iterations per continuation phase against the NumPy
+    oracle on the same instance (the oracle runs a few seconds at these sizes on the GPU box's
+    host). Same bars as above: k identical, fval and f_hist within 1e-8 (fp64) / 1e-4 (fp32)."""
+    from oracle import numpy_ref
+    m, n, l = shape
+    A, b, u, x0, mu = numpy_ref.gen_data(m, n, l, 97006855)
+    if dtype == "f32":
+        A, b, x0 = (a.astype(np.float32) for a in (A, b, x0))
+    opts = {"alpha0": numpy_ref.step_size_for(m, n), "maxit": 2}
+    with warnings.catch_warnings():
+        warnings.simplefilter("ignore")
+        xr, kr, outr = numpy_ref.SOLVERS[solver](x0, A, b, mu, dict(opts))
+    import importlib
+    x, k, out = getattr(importlib.import_module(solver), solver)(x0, A, b, mu, dict(opts))
+    assert k == kr
+    tol = 1e-8 if dtype == "f64" else 1e-4
+    assert _rel(out["fval"], outr["fval"]) < tol
+    assert _rel(np.asarray(out["f_hist"], float), np.asarray(outr["f_hist"], float)) < tol
+    assert np.max(np.abs(x.astype(float) - xr.astype(float))) <= (1e-6 if dtype == "f64" else 1e-2) * np.max(np.abs(xr))
