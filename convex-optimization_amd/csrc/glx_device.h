@@ -119,6 +119,44 @@ __device__ bool grid_reduce(double (&v)[NV], const Red& red) {
   return true;
 }
 
+// Hand ns scalars to the host through the mapped, fine-grained (uncached) packet: system-scope
+// stores (sc0 sc1, straight to host memory), drained with vmcnt(0) so every packet store is
+// acknowledged, then the sequence word the host spins on; no L2 writeback is needed for it.
+// All loads are issued before the first store (one latency, not ns). Either its own tiny kernel
+// (k_publish) or the publisher workgroup of the next kernel (publisher_block). Done by the last
+// block of the preceding reduction instead it measured ~15 us slower (profiles/r1_tuning,
+// fused-publish attribution) than a separate launch (~5.5 us).
+constexpr int kPublishMax = 32;
+__device__ inline void publish_packet(const double* s, int ns, double* host, unsigned* host_seq,
+                                      unsigned seq, const double* s2 = nullptr, int off2 = 0,
+                                      int n2 = 0) {
+  double v[kPublishMax];
+#pragma unroll
+  for (int k = 0; k < kPublishMax; ++k)
+    v[k] = (k >= off2 && k < off2 + n2) ? s2[k - off2] : (k < ns ? s[k] : 0.0);
+#pragma unroll
+  for (int k = 0; k < kPublishMax; ++k)
+    if (k < ns) __hip_atomic_store(host + k, v[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __hip_atomic_store(host_seq, seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+// A launch that carries the scalar packet gets one extra (the last) workgroup that writes it and
+// then joins the grid reduction with identity values (the reduction counts every workgroup).
+// The packet then leaves while the kernel's other workgroups work, instead of as a separate
+// k_publish launch in front of the kernel. Returns true in the publisher workgroup.
+template <int NV, unsigned MAXMASK, int NW = 4>
+__device__ inline bool publisher_block(const Pub& pub, const Red& red) {
+  if (pub.host == nullptr || blockIdx.x != gridDim.x - 1) return false;
+  if (threadIdx.x == 0)
+    publish_packet(pub.s, pub.ns, pub.host, pub.host_seq, pub.seq, pub.s2, pub.off2, pub.n2);
+  double v[NV];
+#pragma unroll
+  for (int j = 0; j < NV; ++j) v[j] = identity((MAXMASK >> j) & 1);
+  grid_reduce<NV, MAXMASK, NW>(v, red);
+  return true;
+}
+
 // g = sum_s slabs[s][idx] in slab order (S = 1: a plain load)
 template <typename T>
 __device__ inline T slab_sum(const T* __restrict__ g, int S, int64_t stride, int64_t idx) {

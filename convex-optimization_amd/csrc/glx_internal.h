@@ -35,6 +35,18 @@ struct Red {
   double* out;     // kMaxRedVals consecutive doubles (caller picks the slots)
 };
 
+// A scalar packet for the host (what k_publish writes) carried by a kernel launch as one extra
+// workgroup (publisher_block, glx_device.h); host == NULL: none.
+struct Pub {
+  const double* s = nullptr;
+  int ns = 0;
+  double* host = nullptr;
+  unsigned* host_seq = nullptr;
+  unsigned seq = 0;
+  const double* s2 = nullptr;   // host[off2 .. off2 + n2) come from s2 instead of s
+  int off2 = 0, n2 = 0;
+};
+
 // Launch plan of the two dense products for one (dtype, m, n, l).
 struct GemmPlan {
   int esize;        // 4 or 8
@@ -85,13 +97,13 @@ void launch_atr(const GemmPlan& p, const T* A, const T* R, T* Gp, hipStream_t st
 bool atr_prox_ok(const GemmPlan& p);
 template <typename T>
 void launch_atr_prox(const GemmPlan& p, const T* A, const T* R, T* G, const T* x, T* pp, T* pthr,
-                     T* z, double t, double mu, double thres, Red red, hipStream_t st);
+                     T* z, double t, double mu, double thres, Red red, hipStream_t st, Pub pub = Pub{});
 // FISTA trial fused into A^T R (same plan condition): G = A^T R, then xc, v_next, y_next and the
 // four trial sums of k_fista_trial (PROX) into red.
 template <typename T>
 void launch_atr_fista(const GemmPlan& p, const T* A, const T* R, T* G, const T* y, const T* xk,
                       T* xc, T* vn, T* yn, double t, double mu, double thres, double theta,
-                      double theta_next, Red red, hipStream_t st);
+                      double theta_next, Red red, hipStream_t st, Pub pub = Pub{});
 
 // ---- row / elementwise kernels (kernels_elem.hip) ----
 // Gradient inputs `g` with an `S` argument are S split-K slabs of n*l values summed in slab
@@ -112,7 +124,8 @@ void launch_sum_partials(const T* Gp, int S, T* G, int64_t nl, hipStream_t st);
 // out: [sum g*G_t, sum G_t^2, sum_i ||p_i||, max |p|, #changed by the threshold]
 template <typename T>
 void launch_prox_pgd(const T* x, const T* g, int S, T* gout, T* p, T* pthr, T* z, int64_t n,
-                     int64_t l, double t, double mu, double thres, Red red, hipStream_t st);
+                     int64_t l, double t, double mu, double thres, Red red, hipStream_t st,
+                     Pub pub = Pub{});
 // FISTA (prox = true) / FGD (prox = false: identity) trial fused with the next combine:
 // xc = prox(y - t g, t); vnext = thr(xk) + (xc - thr(xk))/theta;
 // ynext = (1 - theta_next) thr(xc) + theta_next vnext.
@@ -121,7 +134,8 @@ void launch_prox_pgd(const T* x, const T* g, int S, T* gout, T* p, T* pthr, T* z
 template <typename T>
 void launch_fista_trial(bool prox, const T* y, const T* g, int S, T* gout, const T* xk, T* xc,
                         T* vnext, T* ynext, int64_t n, int64_t l, double t, double mu, double thres,
-                        double theta, double theta_next, double delta, Red red, hipStream_t st);
+                        double theta, double theta_next, double delta, Red red, hipStream_t st,
+                        Pub pub = Pub{});
 // plain prox of W (glx_prox): out: [sum ||x_i||, max |x|]
 template <typename T>
 void launch_prox_plain(const T* w, T* x, int64_t n, int64_t l, double t, double mu, double thres,

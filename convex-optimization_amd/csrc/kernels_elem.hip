@@ -32,26 +32,6 @@ static inline unsigned grid_for(int64_t work, int per_block) {
 }
 
 
-// Hand ns scalars to the host through the mapped, fine-grained (uncached) packet: system-scope
-// stores (sc0 sc1, straight to host memory), drained with vmcnt(0) so every packet store is
-// acknowledged, then the sequence word the host spins on; no L2 writeback is needed for it.
-// All loads are issued before the first store (one latency, not ns). Runs as its own tiny
-// kernel: done by the last block of the preceding reduction it measured ~15 us slower
-// (profiles/r1_tuning, fused-publish attribution) than a separate launch (~5.5 us).
-constexpr int kPublishMax = 32;
-__device__ inline void publish_packet(const double* s, int ns, double* host, unsigned* host_seq,
-                                      unsigned seq, const double* s2 = nullptr, int off2 = 0,
-                                      int n2 = 0) {
-  double v[kPublishMax];
-#pragma unroll
-  for (int k = 0; k < kPublishMax; ++k)
-    v[k] = (k >= off2 && k < off2 + n2) ? s2[k - off2] : (k < ns ? s[k] : 0.0);
-#pragma unroll
-  for (int k = 0; k < kPublishMax; ++k)
-    if (k < ns) __hip_atomic_store(host + k, v[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __hip_atomic_store(host_seq, seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-}
 
 // ------------------------------------------------------------------------------------------
 // residual finalize: R = sum_s P[s] - B; out[0] = sum R^2, out[1] = count(|c| > 1e-6 *cmax)
@@ -136,16 +116,18 @@ __global__ __launch_bounds__(256) void k_sum_partials(const T* __restrict__ Gp, 
 }
 
 // Iterate over rows: each group of LPR lanes owns one row per trip.
-#define GLX_ROW_LOOP_BEGIN(LPR)                                                        \
+// NB = the workgroups that share the rows (all but a publisher workgroup, see Pub)
+#define GLX_ROW_LOOP_BEGIN_NB(LPR, NB)                                                 \
   const int sub = threadIdx.x & ((LPR)-1);                                             \
   const int64_t rows_per_block = 256 / (LPR);                                          \
-  const int64_t row_stride = (int64_t)gridDim.x * rows_per_block;                      \
+  const int64_t row_stride = (int64_t)(NB) * rows_per_block;                           \
   const int64_t n_trips = (n + row_stride - 1) / row_stride;                           \
   for (int64_t trip = 0; trip < n_trips; ++trip) {                                     \
     const int64_t row = trip * row_stride + (int64_t)blockIdx.x * rows_per_block +     \
                         (threadIdx.x / (LPR));                                         \
     const bool rv = row < n;                                                           \
     const int64_t base = (rv ? row : 0) * l;
+#define GLX_ROW_LOOP_BEGIN(LPR) GLX_ROW_LOOP_BEGIN_NB(LPR, gridDim.x)
 #define GLX_ROW_LOOP_END }
 
 // ------------------------------------------------------------------------------------------
@@ -160,11 +142,12 @@ __global__ __launch_bounds__(256) void k_prox_pgd(const T* __restrict__ x, const
                                                   int S, T* __restrict__ gout, T* __restrict__ p,
                                                   T* __restrict__ pthr, T* __restrict__ z, int64_t n,
                                                   int64_t l, double t_, double tmu_, double thres_,
-                                                  Red red) {
+                                                  Red red, Pub pub) {
+  if (publisher_block<6, 0x8u>(pub, red)) return;
   const T t = (T)t_, tmu = (T)tmu_, thres = (T)thres_;
   const int64_t nl = n * l;
   double acc[6] = {0.0, 0.0, 0.0, -__builtin_inf(), 0.0, 0.0};
-  GLX_ROW_LOOP_BEGIN(LPR)
+  GLX_ROW_LOOP_BEGIN_NB(LPR, gridDim.x - (pub.host ? 1u : 0u))
   T xv[EPL], gv[EPL], pv[EPL], pth[EPL], zv[EPL];
   bool ok[EPL];
 #pragma unroll
@@ -202,16 +185,17 @@ __global__ __launch_bounds__(256) void k_fista_trial(
     const T* __restrict__ y, const T* __restrict__ g, int S, T* __restrict__ gout,
     const T* __restrict__ xk, T* __restrict__ xc, T* __restrict__ vnext, T* __restrict__ ynext,
     int64_t n, int64_t l, double t_, double tmu_, double thres_, double theta_, double a1_,
-    double b1_, double dd_, double delta_, Red red) {
+    double b1_, double dd_, double delta_, Red red, Pub pub) {
+  constexpr int NV = PROX ? 4 : 5;
+  if (publisher_block<NV, (1u << (NV - 1))>(pub, red)) return;
   const T t = (T)t_, tmu = (T)tmu_, thres = (T)thres_, theta = (T)theta_, a1 = (T)a1_, b1 = (T)b1_;
   const T dd = (T)dd_, delta = (T)delta_;
   const int64_t nl = n * l;
-  constexpr int NV = PROX ? 4 : 5;
   double acc[NV];
 #pragma unroll
   for (int j = 0; j < NV; ++j) acc[j] = 0.0;
   acc[NV - 1] = -__builtin_inf();
-  GLX_ROW_LOOP_BEGIN(LPR)
+  GLX_ROW_LOOP_BEGIN_NB(LPR, gridDim.x - (pub.host ? 1u : 0u))
   T yv[EPL], gv[EPL], xkv[EPL], xcv[EPL], vnv[EPL], ynv[EPL];
   bool ok[EPL];
 #pragma unroll
@@ -474,6 +458,12 @@ static void dispatch_row(int64_t l, F&& f) {
   else dispatch_epl<16>(l, [&](auto epl) { f(std::integral_constant<int, 16>{}, epl); });
 }
 static inline unsigned row_grid(int64_t n, int lpr) { return grid_for(n, 256 / lpr); }
+// + one publisher workgroup when the launch carries the scalar packet (the grid reduction's
+// partials hold at most kMaxBlocks workgroups)
+static inline unsigned row_grid_pub(int64_t n, int lpr, const Pub& pub) {
+  if (pub.host == nullptr) return row_grid(n, lpr);
+  return std::min<unsigned>(row_grid(n, lpr), (unsigned)kMaxBlocks - 1) + 1;
+}
 
 template <typename T>
 void launch_finalize_residual(const T* P, int S, const T* B, int nsrc, T* const* R, int64_t ml,
@@ -507,28 +497,29 @@ void launch_sum_partials(const T* Gp, int S, T* G, int64_t nl, hipStream_t st) {
 }
 template <typename T>
 void launch_prox_pgd(const T* x, const T* g, int S, T* gout, T* p, T* pthr, T* z, int64_t n,
-                     int64_t l, double t, double mu, double thres, Red red, hipStream_t st) {
+                     int64_t l, double t, double mu, double thres, Red red, hipStream_t st, Pub pub) {
   dispatch_row(l, [&](auto lpr, auto epl) {
     hipLaunchKernelGGL((k_prox_pgd<T, decltype(lpr)::value, decltype(epl)::value>),
-                       dim3(row_grid(n, lpr)), dim3(256), 0, st, x, g, S, gout, p, pthr, z, n, l, t,
-                       t * mu, thres, red);
+                       dim3(row_grid_pub(n, lpr, pub)), dim3(256), 0, st, x, g, S, gout, p, pthr, z, n,
+                       l, t, t * mu, thres, red, pub);
   });
 }
 template <typename T>
 void launch_fista_trial(bool prox, const T* y, const T* g, int S, T* gout, const T* xk, T* xc,
                         T* vnext, T* ynext, int64_t n, int64_t l, double t, double mu, double thres,
-                        double theta, double theta_next, double delta, Red red, hipStream_t st) {
+                        double theta, double theta_next, double delta, Red red, hipStream_t st,
+                        Pub pub) {
   dispatch_row(l, [&](auto lpr, auto epl) {
     if (prox)
       hipLaunchKernelGGL((k_fista_trial<T, decltype(lpr)::value, decltype(epl)::value, true>),
-                         dim3(row_grid(n, lpr)), dim3(256), 0, st, y, g, S, gout, xk, xc, vnext, ynext,
-                         n, l, t, t * mu, thres, theta, 1.0 - theta_next, theta_next, delta * delta,
-                         delta, red);
+                         dim3(row_grid_pub(n, lpr, pub)), dim3(256), 0, st, y, g, S, gout, xk, xc,
+                         vnext, ynext, n, l, t, t * mu, thres, theta, 1.0 - theta_next, theta_next,
+                         delta * delta, delta, red, pub);
     else
       hipLaunchKernelGGL((k_fista_trial<T, decltype(lpr)::value, decltype(epl)::value, false>),
-                         dim3(row_grid(n, lpr)), dim3(256), 0, st, y, g, S, gout, xk, xc, vnext, ynext,
-                         n, l, t, t * mu, thres, theta, 1.0 - theta_next, theta_next, delta * delta,
-                         delta, red);
+                         dim3(row_grid_pub(n, lpr, pub)), dim3(256), 0, st, y, g, S, gout, xk, xc,
+                         vnext, ynext, n, l, t, t * mu, thres, theta, 1.0 - theta_next, theta_next,
+                         delta * delta, delta, red, pub);
   });
 }
 template <typename T>
@@ -604,10 +595,10 @@ void launch_publish(const double* s, int ns, double* host, unsigned* host_seq, u
                                             double*, double, const double*, Red, hipStream_t);      \
   template void launch_sum_partials<T>(const T*, int, T*, int64_t, hipStream_t);                    \
   template void launch_prox_pgd<T>(const T*, const T*, int, T*, T*, T*, T*, int64_t, int64_t,       \
-                                   double, double, double, Red, hipStream_t);                       \
+                                   double, double, double, Red, hipStream_t, Pub);                  \
   template void launch_fista_trial<T>(bool, const T*, const T*, int, T*, const T*, T*, T*, T*,      \
                                       int64_t, int64_t, double, double, double, double, double,     \
-                                      double, Red, hipStream_t);                                    \
+                                      double, Red, hipStream_t, Pub);                               \
   template void launch_prox_plain<T>(const T*, T*, int64_t, int64_t, double, double, double, Red,   \
                                      hipStream_t);                                                  \
   template void launch_rownorm_max<T>(const T*, int64_t, int64_t, Red, hipStream_t);                \

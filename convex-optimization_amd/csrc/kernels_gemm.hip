@@ -955,7 +955,9 @@ __global__ __launch_bounds__(256) void k_atr_prox(const T* __restrict__ A, const
                                                   T* __restrict__ G, int64_t m, int64_t n,
                                                   const T* __restrict__ x, T* __restrict__ p,
                                                   T* __restrict__ pthr, T* __restrict__ z,
-                                                  double t_, double tmu_, double thres_, Red red) {
+                                                  double t_, double tmu_, double thres_, Red red,
+                                                  Pub pub) {
+  if (publisher_block<6, 0x8u>(pub, red)) return;   // the extra workgroup (n / 64 + 1 in all)
   typedef MF<T> M;
   constexpr int L = 16 * NT;
   const int lane = threadIdx.x & 63;
@@ -1008,7 +1010,8 @@ __global__ __launch_bounds__(256) void k_atr_fista(const T* __restrict__ A, cons
                                                    T* __restrict__ xc, T* __restrict__ vnext,
                                                    T* __restrict__ ynext, double t_, double tmu_,
                                                    double thres_, double theta_, double a1_,
-                                                   double b1_, Red red) {
+                                                   double b1_, Red red, Pub pub) {
+  if (publisher_block<4, 0x8u>(pub, red)) return;
   typedef MF<T> M;
   constexpr int L = 16 * NT;
   const int lane = threadIdx.x & 63;
@@ -1690,75 +1693,77 @@ template void launch_ax<double>(const GemmPlan&, int, const double*, const doubl
 template void launch_ax<float>(const GemmPlan&, int, const float*, const float* const*, float*, const int*, int, hipStream_t);
 bool atr_prox_ok(const GemmPlan& p) {
   return p.atr_kind == 1 && p.atr_wl == 0 && p.atr_S == 1 && (p.l == 16 || p.l == 32) &&
-         p.n % 64 == 0 && p.n / 64 <= kMaxBlocks;
+         p.n % 64 == 0 && p.n / 64 < kMaxBlocks;   // + a publisher workgroup
 }
 
 template <typename T, int NT, int PF, bool NTL>
 static void atr_prox_go(const GemmPlan& p, const T* A, const T* R, T* G, const T* x, T* pp,
-                        T* pthr, T* z, double t, double mu, double thres, Red red, hipStream_t st) {
+                        T* pthr, T* z, double t, double mu, double thres, Red red, hipStream_t st,
+                        Pub pub) {
   static const size_t pad = lds_pad(k_atr_prox<T, NT, PF, NTL>, "GLX_ATR_LDS_PAD");
-  hipLaunchKernelGGL((k_atr_prox<T, NT, PF, NTL>), dim3((unsigned)(p.n / 64)), dim3(256), pad, st, A, R,
-                     G, p.m, p.n, x, pp, pthr, z, t, t * mu, thres, red);
+  hipLaunchKernelGGL((k_atr_prox<T, NT, PF, NTL>), dim3((unsigned)(p.n / 64 + (pub.host ? 1 : 0))),
+                     dim3(256), pad, st, A, R, G, p.m, p.n, x, pp, pthr, z, t, t * mu, thres, red, pub);
 }
 template <typename T, int NT>
 static void atr_prox_nt(const GemmPlan& p, const T* A, const T* R, T* G, const T* x, T* pp,
-                        T* pthr, T* z, double t, double mu, double thres, Red red, hipStream_t st) {
+                        T* pthr, T* z, double t, double mu, double thres, Red red, hipStream_t st,
+                        Pub pub) {
   switch (p.atr_ntl * 100 + p.atr_pf) {
-    case 4: atr_prox_go<T, NT, 4, false>(p, A, R, G, x, pp, pthr, z, t, mu, thres, red, st); break;
-    case 6: atr_prox_go<T, NT, 6, false>(p, A, R, G, x, pp, pthr, z, t, mu, thres, red, st); break;
-    case 104: atr_prox_go<T, NT, 4, true>(p, A, R, G, x, pp, pthr, z, t, mu, thres, red, st); break;
-    case 108: atr_prox_go<T, NT, 8, true>(p, A, R, G, x, pp, pthr, z, t, mu, thres, red, st); break;
-    default: atr_prox_go<T, NT, 8, false>(p, A, R, G, x, pp, pthr, z, t, mu, thres, red, st); break;
+    case 4: atr_prox_go<T, NT, 4, false>(p, A, R, G, x, pp, pthr, z, t, mu, thres, red, st, pub); break;
+    case 6: atr_prox_go<T, NT, 6, false>(p, A, R, G, x, pp, pthr, z, t, mu, thres, red, st, pub); break;
+    case 104: atr_prox_go<T, NT, 4, true>(p, A, R, G, x, pp, pthr, z, t, mu, thres, red, st, pub); break;
+    case 108: atr_prox_go<T, NT, 8, true>(p, A, R, G, x, pp, pthr, z, t, mu, thres, red, st, pub); break;
+    default: atr_prox_go<T, NT, 8, false>(p, A, R, G, x, pp, pthr, z, t, mu, thres, red, st, pub); break;
   }
 }
 template <typename T>
 void launch_atr_prox(const GemmPlan& p, const T* A, const T* R, T* G, const T* x, T* pp, T* pthr,
-                     T* z, double t, double mu, double thres, Red red, hipStream_t st) {
-  if (p.l == 16) atr_prox_nt<T, 1>(p, A, R, G, x, pp, pthr, z, t, mu, thres, red, st);
-  else atr_prox_nt<T, 2>(p, A, R, G, x, pp, pthr, z, t, mu, thres, red, st);
+                     T* z, double t, double mu, double thres, Red red, hipStream_t st, Pub pub) {
+  if (p.l == 16) atr_prox_nt<T, 1>(p, A, R, G, x, pp, pthr, z, t, mu, thres, red, st, pub);
+  else atr_prox_nt<T, 2>(p, A, R, G, x, pp, pthr, z, t, mu, thres, red, st, pub);
 }
 
 template <typename T, int NT, int PF, bool NTL>
 static void atr_fista_go(const GemmPlan& p, const T* A, const T* R, T* G, const T* y, const T* xk,
                          T* xc, T* vn, T* yn, double t, double mu, double thres, double theta,
-                         double theta_next, Red red, hipStream_t st) {
+                         double theta_next, Red red, hipStream_t st, Pub pub) {
   static const size_t pad = lds_pad(k_atr_fista<T, NT, PF, NTL>, "GLX_ATR_LDS_PAD");
-  hipLaunchKernelGGL((k_atr_fista<T, NT, PF, NTL>), dim3((unsigned)(p.n / 64)), dim3(256), pad, st, A,
-                     R, G, p.m, p.n, y, xk, xc, vn, yn, t, t * mu, thres, theta, 1.0 - theta_next,
-                     theta_next, red);
+  hipLaunchKernelGGL((k_atr_fista<T, NT, PF, NTL>), dim3((unsigned)(p.n / 64 + (pub.host ? 1 : 0))),
+                     dim3(256), pad, st, A, R, G, p.m, p.n, y, xk, xc, vn, yn, t, t * mu, thres, theta,
+                     1.0 - theta_next, theta_next, red, pub);
 }
 template <typename T, int NT>
 static void atr_fista_nt(const GemmPlan& p, const T* A, const T* R, T* G, const T* y, const T* xk,
                          T* xc, T* vn, T* yn, double t, double mu, double thres, double theta,
-                         double theta_next, Red red, hipStream_t st) {
+                         double theta_next, Red red, hipStream_t st, Pub pub) {
   switch (p.atr_ntl * 100 + p.atr_pf) {
-    case 4: atr_fista_go<T, NT, 4, false>(p, A, R, G, y, xk, xc, vn, yn, t, mu, thres, theta, theta_next, red, st); break;
-    case 104: atr_fista_go<T, NT, 4, true>(p, A, R, G, y, xk, xc, vn, yn, t, mu, thres, theta, theta_next, red, st); break;
-    case 108: atr_fista_go<T, NT, 8, true>(p, A, R, G, y, xk, xc, vn, yn, t, mu, thres, theta, theta_next, red, st); break;
-    default: atr_fista_go<T, NT, 8, false>(p, A, R, G, y, xk, xc, vn, yn, t, mu, thres, theta, theta_next, red, st); break;
+    case 4: atr_fista_go<T, NT, 4, false>(p, A, R, G, y, xk, xc, vn, yn, t, mu, thres, theta, theta_next, red, st, pub); break;
+    case 104: atr_fista_go<T, NT, 4, true>(p, A, R, G, y, xk, xc, vn, yn, t, mu, thres, theta, theta_next, red, st, pub); break;
+    case 108: atr_fista_go<T, NT, 8, true>(p, A, R, G, y, xk, xc, vn, yn, t, mu, thres, theta, theta_next, red, st, pub); break;
+    default: atr_fista_go<T, NT, 8, false>(p, A, R, G, y, xk, xc, vn, yn, t, mu, thres, theta, theta_next, red, st, pub); break;
   }
 }
 template <typename T>
 void launch_atr_fista(const GemmPlan& p, const T* A, const T* R, T* G, const T* y, const T* xk,
                       T* xc, T* vn, T* yn, double t, double mu, double thres, double theta,
-                      double theta_next, Red red, hipStream_t st) {
-  if (p.l == 16) atr_fista_nt<T, 1>(p, A, R, G, y, xk, xc, vn, yn, t, mu, thres, theta, theta_next, red, st);
-  else atr_fista_nt<T, 2>(p, A, R, G, y, xk, xc, vn, yn, t, mu, thres, theta, theta_next, red, st);
+                      double theta_next, Red red, hipStream_t st, Pub pub) {
+  if (p.l == 16) atr_fista_nt<T, 1>(p, A, R, G, y, xk, xc, vn, yn, t, mu, thres, theta, theta_next, red, st, pub);
+  else atr_fista_nt<T, 2>(p, A, R, G, y, xk, xc, vn, yn, t, mu, thres, theta, theta_next, red, st, pub);
 }
 
 template void launch_atr<double>(const GemmPlan&, const double*, const double*, double*, hipStream_t);
 template void launch_atr_fista<double>(const GemmPlan&, const double*, const double*, double*,
                                        const double*, const double*, double*, double*, double*,
-                                       double, double, double, double, double, Red, hipStream_t);
+                                       double, double, double, double, double, Red, hipStream_t, Pub);
 template void launch_atr_fista<float>(const GemmPlan&, const float*, const float*, float*,
                                       const float*, const float*, float*, float*, float*, double,
-                                      double, double, double, double, Red, hipStream_t);
+                                      double, double, double, double, Red, hipStream_t, Pub);
 template void launch_atr_prox<double>(const GemmPlan&, const double*, const double*, double*,
                                       const double*, double*, double*, double*, double, double,
-                                      double, Red, hipStream_t);
+                                      double, Red, hipStream_t, Pub);
 template void launch_atr_prox<float>(const GemmPlan&, const float*, const float*, float*,
                                      const float*, float*, float*, float*, double, double, double,
-                                     Red, hipStream_t);
+                                     Red, hipStream_t, Pub);
 template void launch_atr<float>(const GemmPlan&, const float*, const float*, float*, hipStream_t);
 
 }  // namespace glx

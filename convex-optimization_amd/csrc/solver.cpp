@@ -183,6 +183,10 @@ class Session : public SessionBase {
     hseq_dev_ = reinterpret_cast<unsigned*>(hs_dev_ + NSCAL + 2);
     const char* rb = std::getenv("GLX_READBACK");
     spin_readback_ = !(rb && std::strcmp(rb, "sync") == 0);
+    // the scalar packet rides the speculative kernel queued right behind it (one extra
+    // workgroup, publisher_block) instead of a k_publish launch in front of it
+    const char* ap = std::getenv("GLX_ATTACH_PUB");
+    attach_ok_ = spin_readback_ && !(ap && std::strcmp(ap, "0") == 0);
     const char* sp = std::getenv("GLX_SPEC_GRAD");
     spec_off_env_ = (sp && std::strcmp(sp, "0") == 0);
     const char* fz = std::getenv("GLX_FUSED_TRIAL");
@@ -442,6 +446,21 @@ class Session : public SessionBase {
     check_launch();
     return seq;
   }
+  // The packet as a Pub for the next launch to carry (attach_ok_); *seq_out = its number.
+  Pub make_pub(const double* extra, unsigned* seq_out) {
+    ++syncs_;
+    Pub pb;
+    pb.s = scal_;
+    pb.ns = NSCAL;
+    pb.host = hs_dev_;
+    pb.host_seq = hseq_dev_;
+    pb.seq = ++seq_;
+    pb.s2 = extra;
+    pb.off2 = S_RT;
+    pb.n2 = extra ? 4 : 0;
+    *seq_out = pb.seq;
+    return pb;
+  }
   void wait_readback(unsigned seq) {
     if (!spin_readback_) {
       GLX_HIP(hipEventSynchronize(rb_event_));
@@ -592,14 +611,16 @@ class Session : public SessionBase {
         unsigned seq = 0;
         const bool spec = want_spec(it);
         const bool merge = spec && fused_ok_ && merge_tail();
-        residuals(nsrc, xs, rs, S_RT, X_[ip_], scal_ + S_TR + 3, nullptr, 0.0, merge ? nullptr : &seq,
-                  merge ? tail(1 - gset_) : nullptr);
+        // the packet rides the speculative kernel (no communicator; with one only when merged)
+        const bool late_pub = merge || (spec && fused_ok_ && attach_ok_ && comm_ == nullptr);
+        residuals(nsrc, xs, rs, S_RT, X_[ip_], scal_ + S_TR + 3, nullptr, 0.0,
+                  late_pub ? nullptr : &seq, merge ? tail(1 - gset_) : nullptr);
         std::pair<const T*, int> sg;
         if (spec && fused_ok_) {
           // the next iteration's A^T r and first trial at the candidate p_thr, into the other
           // gradient set and the spare buffers (z is free once this trial's A@X has read it)
           atr_prox(R_[rpt], 1 - gset_, X_[ipt_], if1_, if2_, iz_, O_.alpha0, merge ? nsrc : 0,
-                   merge ? &seq : nullptr);
+                   late_pub ? &seq : nullptr);
           spec_trial = true;
         } else if (spec) {
           sg = gradient(R_[rpt], 1 - gset_);   // gradient at the candidate p_thr
@@ -659,17 +680,22 @@ class Session : public SessionBase {
   // runs), then k_prox_pgd — the same arithmetic as the fused epilogue.
   void atr_prox(const T* r, int set, const T* x, int op, int opt, int oz, double t, int tail_n = 0,
                 unsigned* pub_seq = nullptr) {
+    const double* extra = tail_n ? tail(set) : nullptr;
     if (comm_) {
       const std::pair<const T*, int> g = gradient(r, set, tail_n);
-      if (pub_seq) *pub_seq = post_readback(tail_n ? tail(set) : nullptr);
+      Pub pb;
+      if (pub_seq && attach_ok_) pb = make_pub(extra, pub_seq);
+      else if (pub_seq) *pub_seq = post_readback(extra);
       launch_prox_pgd<T>(x, g.first, g.second, nullptr, X_[op], X_[opt], X_[oz], n_, l_, t, mu_,
-                         O_.thres, red(S_TR), st_);
+                         O_.thres, red(S_TR), st_, pb);
       check_launch();
       return;
     }
+    Pub pb;   // without a communicator pub_seq is only passed when attaching
+    if (pub_seq) pb = make_pub(extra, pub_seq);
     hipEvent_t e0 = prof_begin(1);
     launch_atr_prox<T>(plan_, A_, r, Gs_[set], x, X_[op], X_[opt], X_[oz], t, mu_, O_.thres,
-                       red(S_TR), st_);
+                       red(S_TR), st_, pb);
     check_launch();
     prof_end(1, e0);
     ++atr_calls_;
@@ -742,13 +768,14 @@ class Session : public SessionBase {
         unsigned seq = 0;
         const bool spec = want_spec(it);
         const bool merge = spec && fuse && merge_tail();
+        const bool late_pub = merge || (spec && fuse && attach_ok_ && comm_ == nullptr);
         residuals(2, xs, rs, S_RT, X_[ic_], scal_ + S_TR + i_max, nullptr, 0.0,   // A @ [x | y_next]
-                  merge ? nullptr : &seq, merge ? tail(1 - gset_) : nullptr);
+                  late_pub ? nullptr : &seq, merge ? tail(1 - gset_) : nullptr);
         std::pair<const T*, int> sg;
         if (spec && fuse) {
           // the next iteration's gradient at y_next and its first trial (t, theta' = theta_next)
           atr_fista(R_[ryn], 1 - gset_, X_[iyn_], X_[ic_], ff1_, ff2_, ff3_, t, theta_next,
-                    2.0 / (double)(inner_ + 3), merge ? 2 : 0, merge ? &seq : nullptr);
+                    2.0 / (double)(inner_ + 3), merge ? 2 : 0, late_pub ? &seq : nullptr);
           spec_trial = true;
         } else if (spec) {
           sg = gradient(R_[ryn], 1 - gset_);   // gradient at the next y
@@ -810,17 +837,22 @@ class Session : public SessionBase {
   // (with a communicator: as atr_prox, the trial as k_fista_trial after the all-reduce)
   void atr_fista(const T* r, int set, const T* yv, const T* xk, int oc, int ov, int oy, double t,
                  double theta, double theta_next, int tail_n = 0, unsigned* pub_seq = nullptr) {
+    const double* extra = tail_n ? tail(set) : nullptr;
     if (comm_) {
       const std::pair<const T*, int> g = gradient(r, set, tail_n);
-      if (pub_seq) *pub_seq = post_readback(tail_n ? tail(set) : nullptr);
+      Pub pb;
+      if (pub_seq && attach_ok_) pb = make_pub(extra, pub_seq);
+      else if (pub_seq) *pub_seq = post_readback(extra);
       launch_fista_trial<T>(true, yv, g.first, g.second, nullptr, xk, X_[oc], X_[ov], X_[oy], n_,
-                            l_, t, mu_, O_.thres, theta, theta_next, O_.delta, red(S_TR), st_);
+                            l_, t, mu_, O_.thres, theta, theta_next, O_.delta, red(S_TR), st_, pb);
       check_launch();
       return;
     }
+    Pub pb;
+    if (pub_seq) pb = make_pub(extra, pub_seq);
     hipEvent_t e0 = prof_begin(1);
     launch_atr_fista<T>(plan_, A_, r, Gs_[set], yv, xk, X_[oc], X_[ov], X_[oy], t, mu_, O_.thres,
-                        theta, theta_next, red(S_TR), st_);
+                        theta, theta_next, red(S_TR), st_, pb);
     check_launch();
     prof_end(1, e0);
     ++atr_calls_;
@@ -913,6 +945,7 @@ class Session : public SessionBase {
   int method_ = 0;
   bool use_sparsity_ = true, device_hist_ = false, spin_readback_ = true;
   unsigned seq_ = 0;
+  bool attach_ok_ = true;
   hipEvent_t rb_event_ = nullptr;
   int epoch_ = 0;
   // buffer roles
