@@ -85,11 +85,15 @@ def workspace(problem: GlxProblem, o: GlxOpts, device) -> torch.Tensor:
     return torch.empty(int(nbytes.value), dtype=torch.uint8, device=device)
 
 
-def _lambda_max(A: torch.Tensor) -> float:
+def _lambda_max(A: torch.Tensor, comm=None) -> float:
     """``np.max(LA.eigvals(A.T @ A))`` (gl_SGD_primal.py:35-37) for the optional
-    continuous_subgradient_flag, evaluated on the device."""
+    continuous_subgradient_flag, evaluated on the device. With row-sharded A the Gram matrix is
+    the sum of the shards' (all-reduced once, before the solve)."""
     a = A.to(torch.float64)
-    return float(torch.linalg.eigvalsh(a.T @ a).max().item())
+    gram = a.T @ a
+    if comm is not None:
+        comm.allreduce_(gram)
+    return float(torch.linalg.eigvalsh(gram).max().item())
 
 
 class Session:
@@ -115,7 +119,7 @@ class Session:
                 raise ValueError("A, b, x must be contiguous device tensors")
         self.o = make_opts(method, opts)
         if method in (_lib.GLX_SGD, _lib.GLX_GD) and opts.get("continuous_subgradient_flag"):
-            self.o.alpha0 = 1.0 / _lambda_max(A)
+            self.o.alpha0 = 1.0 / _lambda_max(A, comm)
         self.refs = (A, b, x)
         self.p = GlxProblem(dtype=_lib.GLX_F64 if A.dtype == torch.float64 else _lib.GLX_F32,
                             method=method, m=m, n=n, l=x.shape[1], A=A.data_ptr(), b=b.data_ptr(),

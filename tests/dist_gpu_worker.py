@@ -31,6 +31,7 @@ def main():
     ap.add_argument("--dtype", default="f64")
     ap.add_argument("--maxit", type=int, default=20)
     ap.add_argument("--transport", default="host", choices=["host", "rccl"])
+    ap.add_argument("--csf", action="store_true", help="continuous_subgradient_flag (SGD/GD)")
     ap.add_argument("--out", required=True)
     a = ap.parse_args()
 
@@ -49,6 +50,8 @@ def main():
         A, b, x0 = (v.astype(np.float32) for v in (A, b, x0))
     r0, r1 = shard_rows(a.m, world, rank)
     opts = {"alpha0": numpy_ref.step_size_for(a.m, a.n), "maxit": a.maxit}
+    if a.csf:
+        opts["continuous_subgradient_flag"] = True
     x, k, out = glx.solve(a.solver, x0, A[r0:r1], b[r0:r1], mu, dict(opts), comm=comm)
     digest = hashlib.sha256(np.ascontiguousarray(x).tobytes()).hexdigest()
     mine = {"rank": rank, "k": int(k), "fval": float(out["fval"]), "x_sha": digest,

@@ -28,13 +28,13 @@ def _free_port():
     return p
 
 
-def run_sharded(tmp_path, world, solver, m, n, l, dtype="f64", maxit=20):
+def run_sharded(tmp_path, world, solver, m, n, l, dtype="f64", maxit=20, extra=()):
     out = tmp_path / ("verdict_%s_%d.json" % (solver, world))
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes", "1",
            "--nproc-per-node", str(world), "--master-addr", "127.0.0.1",
            "--master-port", str(_free_port()), os.path.join(ROOT, "tests", "dist_gpu_worker.py"),
            "--solver", solver, "--rows", str(m), "--cols", str(n), "--groups-l", str(l), "--dtype", dtype,
-           "--maxit", str(maxit), "--out", str(out)]
+           "--maxit", str(maxit), "--out", str(out)] + list(extra)
     env = dict(os.environ, OMP_NUM_THREADS="1")
     p = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=110)
     assert p.returncode == 0, p.stdout[-3000:] + p.stderr[-3000:]
@@ -69,3 +69,12 @@ def test_sharded_fp32(tmp_path):
     ranks = v["ranks"]
     assert ranks[0]["x_sha"] == ranks[1]["x_sha"]
     assert abs(ranks[0]["fval"] - v["oracle_fval"]) / abs(v["oracle_fval"]) < 1e-4
+
+
+def test_sharded_continuous_subgradient(tmp_path):
+    # alpha0 = 1 / max eig(sum_g A_g^T A_g): the Gram matrix is all-reduced across the shards
+    v = run_sharded(tmp_path, 2, "gl_SGD_primal", 301, 256, 2, extra=["--csf"])
+    ranks = v["ranks"]
+    assert ranks[0]["x_sha"] == ranks[1]["x_sha"]
+    assert ranks[0]["k"] == v["oracle_k"]
+    assert abs(ranks[0]["fval"] - v["oracle_fval"]) / abs(v["oracle_fval"]) < 1e-8

@@ -173,3 +173,21 @@ def test_full_size_vs_oracle(solver, dtype, shape):
     assert _rel(out["fval"], outr["fval"]) < tol
     assert _rel(np.asarray(out["f_hist"], float), np.asarray(outr["f_hist"], float)) < tol
     assert np.max(np.abs(x.astype(float) - xr.astype(float))) <= (1e-6 if dtype == "f64" else 1e-2) * np.max(np.abs(xr))
+
+
+@pytest.mark.parametrize("solver", ["gl_SGD_primal", "gl_GD_primal"])
+def test_continuous_subgradient_flag(solver):
+    """opts['continuous_subgradient_flag'] (gl_SGD_primal.py:35-37, gl_GD_primal.py:43-45):
+    alpha0 = 1 / max eig(A^T A). The build takes the eigenvalue with a symmetric solver on the
+    device, the oracle with np.linalg.eigvals as the reference does: alpha0 agrees to rounding."""
+    from oracle import numpy_ref
+    A, b, u, x0, mu = numpy_ref.gen_data(300, 256, 2, 31)
+    opts = {"continuous_subgradient_flag": True, "maxit": 30}
+    with warnings.catch_warnings():
+        warnings.simplefilter("ignore")
+        xr, kr, outr = numpy_ref.SOLVERS[solver](x0, A, b, mu, dict(opts))
+    import importlib
+    x, k, out = getattr(importlib.import_module(solver), solver)(x0, A, b, mu, dict(opts))
+    assert k == kr
+    assert _rel(out["fval"], outr["fval"]) < 1e-8
+    assert _rel(np.asarray(out["f_hist"], float), np.asarray(outr["f_hist"], float)) < 1e-8
