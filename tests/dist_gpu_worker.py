@@ -32,6 +32,8 @@ def main():
     ap.add_argument("--maxit", type=int, default=20)
     ap.add_argument("--transport", default="host", choices=["host", "rccl"])
     ap.add_argument("--csf", action="store_true", help="continuous_subgradient_flag (SGD/GD)")
+    ap.add_argument("--alpha-scale", type=float, default=1.0,
+                    help="alpha0 = scale / (sqrt(m) + sqrt(n))^2 (> 1: line-search rejections)")
     ap.add_argument("--out", required=True)
     a = ap.parse_args()
 
@@ -49,7 +51,7 @@ def main():
     if a.dtype == "f32":
         A, b, x0 = (v.astype(np.float32) for v in (A, b, x0))
     r0, r1 = shard_rows(a.m, world, rank)
-    opts = {"alpha0": numpy_ref.step_size_for(a.m, a.n), "maxit": a.maxit}
+    opts = {"alpha0": a.alpha_scale * numpy_ref.step_size_for(a.m, a.n), "maxit": a.maxit}
     if a.csf:
         opts["continuous_subgradient_flag"] = True
     x, k, out = glx.solve(a.solver, x0, A[r0:r1], b[r0:r1], mu, dict(opts), comm=comm)
