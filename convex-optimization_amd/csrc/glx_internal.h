@@ -92,18 +92,23 @@ void launch_ax(const GemmPlan& p, int nsrc, const T* A, const T* const* X, T* P,
                int epoch, hipStream_t st);
 template <typename T>
 void launch_atr(const GemmPlan& p, const T* A, const T* R, T* Gp, hipStream_t st);
-// ProxGD trial fused into A^T R (needs atr_prox_ok: MFMA panels, WL 0, one K split):
+// ProxGD trial fused into A^T R (needs atr_prox_ok: MFMA panels, WL 0, at most 8 K splits):
 // G = A^T R, then p = prox(x - t G), p_thr, z and the six trial sums of k_prox_pgd into red.
+// With S = atr_S > 1 K splits the blocks write slabs Gp[S][n][l] and the last block of each
+// 64-row panel (counter pcnt[panel], zero before the first launch, reset by that block) sums
+// them in slab order and runs the trial.
 bool atr_prox_ok(const GemmPlan& p);
 template <typename T>
 void launch_atr_prox(const GemmPlan& p, const T* A, const T* R, T* G, const T* x, T* pp, T* pthr,
-                     T* z, double t, double mu, double thres, Red red, hipStream_t st, Pub pub = Pub{});
+                     T* z, double t, double mu, double thres, Red red, hipStream_t st, Pub pub = Pub{},
+                     T* Gp = nullptr, unsigned* pcnt = nullptr);
 // FISTA trial fused into A^T R (same plan condition): G = A^T R, then xc, v_next, y_next and the
 // four trial sums of k_fista_trial (PROX) into red.
 template <typename T>
 void launch_atr_fista(const GemmPlan& p, const T* A, const T* R, T* G, const T* y, const T* xk,
                       T* xc, T* vn, T* yn, double t, double mu, double thres, double theta,
-                      double theta_next, Red red, hipStream_t st, Pub pub = Pub{});
+                      double theta_next, Red red, hipStream_t st, Pub pub = Pub{},
+                      T* Gp = nullptr, unsigned* pcnt = nullptr);
 
 // ---- row / elementwise kernels (kernels_elem.hip) ----
 // Gradient inputs `g` with an `S` argument are S split-K slabs of n*l values summed in slab

@@ -32,6 +32,7 @@
 #include <cstdlib>
 #include <string>
 
+#include "glx.h"
 #include "glx_device.h"
 
 namespace glx {
@@ -844,9 +845,11 @@ template <bool NTL> struct Load4<float, NTL> {
 // block's four waves split the rows (K) and are summed through LDS in the fixed order
 // ((w0 + w1) + w2) + w3; afterwards wave w holds the complete sum for e == w in acc[w][*]
 // (the other e of a wave are partial and unused), so the four waves share the epilogue.
+// (pbx, pby) = (panel, K split) of this block: (blockIdx.x, blockIdx.y) for k_atr_mfma.
 template <typename T, int NT, int PF, int WL, bool NTL>
 __device__ inline int64_t atr_panel(const T* __restrict__ A, const T* __restrict__ R, int64_t m,
-                                    int64_t n, int S, typename MF<T>::acc_t (&acc)[4][NT]) {
+                                    int64_t n, int S, typename MF<T>::acc_t (&acc)[4][NT],
+                                    int64_t pbx, int64_t pby) {
   typedef MF<T> M;
   typedef typename M::acc_t C;
   constexpr int L = 16 * NT;
@@ -855,10 +858,10 @@ __device__ inline int64_t atr_panel(const T* __restrict__ A, const T* __restrict
   const int lane = threadIdx.x & 63;
   const int wave = threadIdx.x >> 6;
   const int i = lane & 15, q = lane >> 4;
-  const int64_t col0 = WL == 0 ? (int64_t)blockIdx.x * 64 : (int64_t)blockIdx.x * 256 + wave * 64;
+  const int64_t col0 = WL == 0 ? pbx * 64 : pbx * 256 + wave * 64;
   const int64_t steps = m / 4;
   const int64_t W = WL == 0 ? (int64_t)S * 4 : (int64_t)S;
-  const int64_t w = WL == 0 ? (int64_t)blockIdx.y * 4 + wave : (int64_t)blockIdx.y;
+  const int64_t w = WL == 0 ? pby * 4 + wave : pby;
   const int64_t sb = steps * w / W, se = steps * (w + 1) / W;
 
   const T* ap = A + (sb * 4 + q) * n + col0 + 4 * i;
@@ -922,6 +925,64 @@ __device__ inline int64_t atr_panel(const T* __restrict__ A, const T* __restrict
   return col0;
 }
 
+// K splits of a fused A^T R (WL 0, S > 1): a 1-D grid of n/64 panels x S splits (+ the
+// publisher). Every block stores its panel rows (wave w: rows e == w) into slab `split` of Gp;
+// the block that arrives last on its panel's counter sums the S slabs in slab order (the
+// order of slab_sum, so G is bit-identical to the unfused path) and runs the trial epilogue.
+// Hand-off: sc1 (agent-scope) stores, vmcnt(0), a workgroup barrier, one agent-scope add per
+// block; the last arriver loads with sc1 after a barrier (MI355X_MICROARCH.md "Valid forms",
+// row 1). Returns false in the blocks that are not last (they only join the grid reduction).
+template <typename T, int NT>
+__device__ inline bool atr_split_combine(typename MF<T>::acc_t (&acc)[4][NT], T* __restrict__ Gp,
+                                         int64_t n, int S, int64_t panel, int64_t split,
+                                         unsigned* __restrict__ pcnt) {
+  typedef MF<T> M;
+  constexpr int L = 16 * NT;
+  __shared__ int last;
+  const int lane = threadIdx.x & 63;
+  const int wave = threadIdx.x >> 6;
+  const int i = lane & 15;
+  const int64_t col0 = panel * 64;
+  const int64_t nl = n * L;
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    if (e != wave) continue;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int64_t row = col0 + 4 * M::row(lane, r) + e;
+#pragma unroll
+      for (int nt = 0; nt < NT; ++nt)
+        __hip_atomic_store(Gp + split * nl + row * L + nt * 16 + i, acc[e][nt][r], __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0)
+    last = __hip_atomic_fetch_add(pcnt + panel, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
+           (unsigned)S - 1;
+  __syncthreads();
+  if (!last) return false;
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    if (e != wave) continue;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int64_t row = col0 + 4 * M::row(lane, r) + e;
+#pragma unroll
+      for (int nt = 0; nt < NT; ++nt) {
+        const T* g = Gp + row * L + nt * 16 + i;
+        T v = __hip_atomic_load(g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        for (int k = 1; k < S; ++k)
+          v = v + __hip_atomic_load(g + (int64_t)k * nl, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        acc[e][nt][r] = v;
+      }
+    }
+  }
+  if (threadIdx.x == 0) __hip_atomic_store(pcnt + panel, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  return true;
+}
+
 template <typename T, int NT, int PF, int WL, bool NTL>
 __global__ __launch_bounds__(256) void k_atr_mfma(const T* __restrict__ A, const T* __restrict__ R,
                                                   T* __restrict__ Gp, int64_t m, int64_t n, int S) {
@@ -931,7 +992,7 @@ __global__ __launch_bounds__(256) void k_atr_mfma(const T* __restrict__ A, const
   const int wave = threadIdx.x >> 6;
   const int i = lane & 15;
   typename M::acc_t acc[4][NT];
-  const int64_t col0 = atr_panel<T, NT, PF, WL, NTL>(A, R, m, n, S, acc);
+  const int64_t col0 = atr_panel<T, NT, PF, WL, NTL>(A, R, m, n, S, acc, blockIdx.x, blockIdx.y);
   T* gout = Gp + (int64_t)blockIdx.y * n * L;
 #pragma unroll
   for (int e = 0; e < 4; ++e) {
@@ -956,16 +1017,22 @@ __global__ __launch_bounds__(256) void k_atr_prox(const T* __restrict__ A, const
                                                   const T* __restrict__ x, T* __restrict__ p,
                                                   T* __restrict__ pthr, T* __restrict__ z,
                                                   double t_, double tmu_, double thres_, Red red,
-                                                  Pub pub) {
-  if (publisher_block<6, 0x8u>(pub, red)) return;   // the extra workgroup (n / 64 + 1 in all)
+                                                  Pub pub, int S, T* __restrict__ Gp,
+                                                  unsigned* __restrict__ pcnt) {
+  if (publisher_block<6, 0x8u>(pub, red)) return;   // the extra workgroup (n / 64 * S + 1 in all)
   typedef MF<T> M;
   constexpr int L = 16 * NT;
   const int lane = threadIdx.x & 63;
   const int wave = threadIdx.x >> 6;
   const int i = lane & 15;
   typename M::acc_t acc[4][NT];
-  const int64_t col0 = atr_panel<T, NT, PF, 0, NTL>(A, R, m, n, 1, acc);
+  const int64_t panel = blockIdx.x / S, split = blockIdx.x % S;
+  const int64_t col0 = atr_panel<T, NT, PF, 0, NTL>(A, R, m, n, S, acc, panel, split);
   double accr[6] = {0.0, 0.0, 0.0, -__builtin_inf(), 0.0, 0.0};
+  if (S > 1 && !atr_split_combine<T, NT>(acc, Gp, n, S, panel, split, pcnt)) {
+    grid_reduce<6, 0x8u>(accr, red);
+    return;
+  }
   const T t = (T)t_, tmu = (T)tmu_, thres = (T)thres_;
 #pragma unroll
   for (int e = 0; e < 4; ++e) {
@@ -1010,7 +1077,8 @@ __global__ __launch_bounds__(256) void k_atr_fista(const T* __restrict__ A, cons
                                                    T* __restrict__ xc, T* __restrict__ vnext,
                                                    T* __restrict__ ynext, double t_, double tmu_,
                                                    double thres_, double theta_, double a1_,
-                                                   double b1_, Red red, Pub pub) {
+                                                   double b1_, Red red, Pub pub, int S,
+                                                   T* __restrict__ Gp, unsigned* __restrict__ pcnt) {
   if (publisher_block<4, 0x8u>(pub, red)) return;
   typedef MF<T> M;
   constexpr int L = 16 * NT;
@@ -1018,8 +1086,13 @@ __global__ __launch_bounds__(256) void k_atr_fista(const T* __restrict__ A, cons
   const int wave = threadIdx.x >> 6;
   const int i = lane & 15;
   typename M::acc_t acc[4][NT];
-  const int64_t col0 = atr_panel<T, NT, PF, 0, NTL>(A, R, m, n, 1, acc);
+  const int64_t panel = blockIdx.x / S, split = blockIdx.x % S;
+  const int64_t col0 = atr_panel<T, NT, PF, 0, NTL>(A, R, m, n, S, acc, panel, split);
   double accr[4] = {0.0, 0.0, 0.0, -__builtin_inf()};
+  if (S > 1 && !atr_split_combine<T, NT>(acc, Gp, n, S, panel, split, pcnt)) {
+    grid_reduce<4, 0x8u>(accr, red);
+    return;
+  }
   const T t = (T)t_, tmu = (T)tmu_, thres = (T)thres_, theta = (T)theta_, a1 = (T)a1_, b1 = (T)b1_;
 #pragma unroll
   for (int e = 0; e < 4; ++e) {
@@ -1692,78 +1765,89 @@ void launch_atr(const GemmPlan& p, const T* A, const T* R, T* Gp, hipStream_t st
 template void launch_ax<double>(const GemmPlan&, int, const double*, const double* const*, double*, const int*, int, hipStream_t);
 template void launch_ax<float>(const GemmPlan&, int, const float*, const float* const*, float*, const int*, int, hipStream_t);
 bool atr_prox_ok(const GemmPlan& p) {
-  return p.atr_kind == 1 && p.atr_wl == 0 && p.atr_S == 1 && (p.l == 16 || p.l == 32) &&
-         p.n % 64 == 0 && p.n / 64 < kMaxBlocks;   // + a publisher workgroup
+  return p.atr_kind == 1 && p.atr_wl == 0 && p.atr_S >= 1 && p.atr_S <= 8 &&
+         (p.l == 16 || p.l == 32) && p.n % 64 == 0 &&
+         (p.n / 64) * p.atr_S < kMaxBlocks &&   // + a publisher workgroup
+         (p.atr_S == 1 || env_int("GLX_ATR_FUSE_SPLIT", 1) != 0);
 }
 
 template <typename T, int NT, int PF, bool NTL>
 static void atr_prox_go(const GemmPlan& p, const T* A, const T* R, T* G, const T* x, T* pp,
                         T* pthr, T* z, double t, double mu, double thres, Red red, hipStream_t st,
-                        Pub pub) {
+                        Pub pub, T* Gp, unsigned* pcnt) {
   static const size_t pad = lds_pad(k_atr_prox<T, NT, PF, NTL>, "GLX_ATR_LDS_PAD");
-  hipLaunchKernelGGL((k_atr_prox<T, NT, PF, NTL>), dim3((unsigned)(p.n / 64 + (pub.host ? 1 : 0))),
-                     dim3(256), pad, st, A, R, G, p.m, p.n, x, pp, pthr, z, t, t * mu, thres, red, pub);
+  hipLaunchKernelGGL((k_atr_prox<T, NT, PF, NTL>),
+                     dim3((unsigned)(p.n / 64 * p.atr_S + (pub.host ? 1 : 0))), dim3(256), pad, st,
+                     A, R, G, p.m, p.n, x, pp, pthr, z, t, t * mu, thres, red, pub, p.atr_S, Gp, pcnt);
 }
 template <typename T, int NT>
 static void atr_prox_nt(const GemmPlan& p, const T* A, const T* R, T* G, const T* x, T* pp,
                         T* pthr, T* z, double t, double mu, double thres, Red red, hipStream_t st,
-                        Pub pub) {
+                        Pub pub, T* Gp, unsigned* pcnt) {
   switch (p.atr_ntl * 100 + p.atr_pf) {
-    case 4: atr_prox_go<T, NT, 4, false>(p, A, R, G, x, pp, pthr, z, t, mu, thres, red, st, pub); break;
-    case 6: atr_prox_go<T, NT, 6, false>(p, A, R, G, x, pp, pthr, z, t, mu, thres, red, st, pub); break;
-    case 104: atr_prox_go<T, NT, 4, true>(p, A, R, G, x, pp, pthr, z, t, mu, thres, red, st, pub); break;
-    case 108: atr_prox_go<T, NT, 8, true>(p, A, R, G, x, pp, pthr, z, t, mu, thres, red, st, pub); break;
-    default: atr_prox_go<T, NT, 8, false>(p, A, R, G, x, pp, pthr, z, t, mu, thres, red, st, pub); break;
+    case 4: atr_prox_go<T, NT, 4, false>(p, A, R, G, x, pp, pthr, z, t, mu, thres, red, st, pub, Gp, pcnt); break;
+    case 6: atr_prox_go<T, NT, 6, false>(p, A, R, G, x, pp, pthr, z, t, mu, thres, red, st, pub, Gp, pcnt); break;
+    case 104: atr_prox_go<T, NT, 4, true>(p, A, R, G, x, pp, pthr, z, t, mu, thres, red, st, pub, Gp, pcnt); break;
+    case 108: atr_prox_go<T, NT, 8, true>(p, A, R, G, x, pp, pthr, z, t, mu, thres, red, st, pub, Gp, pcnt); break;
+    default: atr_prox_go<T, NT, 8, false>(p, A, R, G, x, pp, pthr, z, t, mu, thres, red, st, pub, Gp, pcnt); break;
   }
 }
 template <typename T>
 void launch_atr_prox(const GemmPlan& p, const T* A, const T* R, T* G, const T* x, T* pp, T* pthr,
-                     T* z, double t, double mu, double thres, Red red, hipStream_t st, Pub pub) {
-  if (p.l == 16) atr_prox_nt<T, 1>(p, A, R, G, x, pp, pthr, z, t, mu, thres, red, st, pub);
-  else atr_prox_nt<T, 2>(p, A, R, G, x, pp, pthr, z, t, mu, thres, red, st, pub);
+                     T* z, double t, double mu, double thres, Red red, hipStream_t st, Pub pub,
+                     T* Gp, unsigned* pcnt) {
+  if (p.atr_S > 1 && (Gp == nullptr || pcnt == nullptr))
+    throw Error{GLX_E_INVALID, "fused A^T R with K splits needs slab and counter buffers"};
+  if (p.l == 16) atr_prox_nt<T, 1>(p, A, R, G, x, pp, pthr, z, t, mu, thres, red, st, pub, Gp, pcnt);
+  else atr_prox_nt<T, 2>(p, A, R, G, x, pp, pthr, z, t, mu, thres, red, st, pub, Gp, pcnt);
 }
 
 template <typename T, int NT, int PF, bool NTL>
 static void atr_fista_go(const GemmPlan& p, const T* A, const T* R, T* G, const T* y, const T* xk,
                          T* xc, T* vn, T* yn, double t, double mu, double thres, double theta,
-                         double theta_next, Red red, hipStream_t st, Pub pub) {
+                         double theta_next, Red red, hipStream_t st, Pub pub, T* Gp, unsigned* pcnt) {
   static const size_t pad = lds_pad(k_atr_fista<T, NT, PF, NTL>, "GLX_ATR_LDS_PAD");
-  hipLaunchKernelGGL((k_atr_fista<T, NT, PF, NTL>), dim3((unsigned)(p.n / 64 + (pub.host ? 1 : 0))),
-                     dim3(256), pad, st, A, R, G, p.m, p.n, y, xk, xc, vn, yn, t, t * mu, thres, theta,
-                     1.0 - theta_next, theta_next, red, pub);
+  hipLaunchKernelGGL((k_atr_fista<T, NT, PF, NTL>),
+                     dim3((unsigned)(p.n / 64 * p.atr_S + (pub.host ? 1 : 0))), dim3(256), pad, st,
+                     A, R, G, p.m, p.n, y, xk, xc, vn, yn, t, t * mu, thres, theta, 1.0 - theta_next,
+                     theta_next, red, pub, p.atr_S, Gp, pcnt);
 }
 template <typename T, int NT>
 static void atr_fista_nt(const GemmPlan& p, const T* A, const T* R, T* G, const T* y, const T* xk,
                          T* xc, T* vn, T* yn, double t, double mu, double thres, double theta,
-                         double theta_next, Red red, hipStream_t st, Pub pub) {
+                         double theta_next, Red red, hipStream_t st, Pub pub, T* Gp, unsigned* pcnt) {
   switch (p.atr_ntl * 100 + p.atr_pf) {
-    case 4: atr_fista_go<T, NT, 4, false>(p, A, R, G, y, xk, xc, vn, yn, t, mu, thres, theta, theta_next, red, st, pub); break;
-    case 104: atr_fista_go<T, NT, 4, true>(p, A, R, G, y, xk, xc, vn, yn, t, mu, thres, theta, theta_next, red, st, pub); break;
-    case 108: atr_fista_go<T, NT, 8, true>(p, A, R, G, y, xk, xc, vn, yn, t, mu, thres, theta, theta_next, red, st, pub); break;
-    default: atr_fista_go<T, NT, 8, false>(p, A, R, G, y, xk, xc, vn, yn, t, mu, thres, theta, theta_next, red, st, pub); break;
+    case 4: atr_fista_go<T, NT, 4, false>(p, A, R, G, y, xk, xc, vn, yn, t, mu, thres, theta, theta_next, red, st, pub, Gp, pcnt); break;
+    case 104: atr_fista_go<T, NT, 4, true>(p, A, R, G, y, xk, xc, vn, yn, t, mu, thres, theta, theta_next, red, st, pub, Gp, pcnt); break;
+    case 108: atr_fista_go<T, NT, 8, true>(p, A, R, G, y, xk, xc, vn, yn, t, mu, thres, theta, theta_next, red, st, pub, Gp, pcnt); break;
+    default: atr_fista_go<T, NT, 8, false>(p, A, R, G, y, xk, xc, vn, yn, t, mu, thres, theta, theta_next, red, st, pub, Gp, pcnt); break;
   }
 }
 template <typename T>
 void launch_atr_fista(const GemmPlan& p, const T* A, const T* R, T* G, const T* y, const T* xk,
                       T* xc, T* vn, T* yn, double t, double mu, double thres, double theta,
-                      double theta_next, Red red, hipStream_t st, Pub pub) {
-  if (p.l == 16) atr_fista_nt<T, 1>(p, A, R, G, y, xk, xc, vn, yn, t, mu, thres, theta, theta_next, red, st, pub);
-  else atr_fista_nt<T, 2>(p, A, R, G, y, xk, xc, vn, yn, t, mu, thres, theta, theta_next, red, st, pub);
+                      double theta_next, Red red, hipStream_t st, Pub pub, T* Gp, unsigned* pcnt) {
+  if (p.atr_S > 1 && (Gp == nullptr || pcnt == nullptr))
+    throw Error{GLX_E_INVALID, "fused A^T R with K splits needs slab and counter buffers"};
+  if (p.l == 16) atr_fista_nt<T, 1>(p, A, R, G, y, xk, xc, vn, yn, t, mu, thres, theta, theta_next, red, st, pub, Gp, pcnt);
+  else atr_fista_nt<T, 2>(p, A, R, G, y, xk, xc, vn, yn, t, mu, thres, theta, theta_next, red, st, pub, Gp, pcnt);
 }
 
 template void launch_atr<double>(const GemmPlan&, const double*, const double*, double*, hipStream_t);
 template void launch_atr_fista<double>(const GemmPlan&, const double*, const double*, double*,
                                        const double*, const double*, double*, double*, double*,
-                                       double, double, double, double, double, Red, hipStream_t, Pub);
+                                       double, double, double, double, double, Red, hipStream_t, Pub,
+                                       double*, unsigned*);
 template void launch_atr_fista<float>(const GemmPlan&, const float*, const float*, float*,
                                       const float*, const float*, float*, float*, float*, double,
-                                      double, double, double, double, Red, hipStream_t, Pub);
+                                      double, double, double, double, Red, hipStream_t, Pub,
+                                      float*, unsigned*);
 template void launch_atr_prox<double>(const GemmPlan&, const double*, const double*, double*,
                                       const double*, double*, double*, double*, double, double,
-                                      double, Red, hipStream_t, Pub);
+                                      double, Red, hipStream_t, Pub, double*, unsigned*);
 template void launch_atr_prox<float>(const GemmPlan&, const float*, const float*, float*,
                                      const float*, float*, float*, float*, double, double, double,
-                                     Red, hipStream_t, Pub);
+                                     Red, hipStream_t, Pub, float*, unsigned*);
 template void launch_atr<float>(const GemmPlan&, const float*, const float*, float*, hipStream_t);
 
 }  // namespace glx

@@ -130,6 +130,8 @@ class Session : public SessionBase {
     double* scal = static_cast<double*>(c.take(sizeof(double) * NSCAL));
     double* part = static_cast<double*>(c.take(sizeof(double) * kMaxRedVals * kMaxBlocks));
     unsigned* ticket = static_cast<unsigned*>(c.take(kTicketBytes));
+    // per-panel arrival counters of the fused A^T R with K splits (atr_split_combine)
+    unsigned* pcnt = static_cast<unsigned*>(c.take(sizeof(unsigned) * (P.n / 64 + 64)));
     int* flag = static_cast<int*>(c.take(256));
     double* fh = static_cast<double*>(c.take(sizeof(double) * (fh_cap + 1)));
     const int gb = gemv_blocks_for(P);
@@ -140,6 +142,7 @@ class Session : public SessionBase {
       for (int k = 0; k < 2; ++k) { s->Gs_[k] = g[k]; s->Gps_[k] = gp[k]; }
       s->G_ = g[0]; s->Gp_ = gp[0]; s->Pp_ = pp;
       s->scal_ = scal; s->part_ = part; s->ticket_ = ticket; s->flag_ = flag; s->fh_dev_ = fh;
+      s->pcnt_ = pcnt;
       s->gemv_slabs_ = gs;
       s->gemv_blocks_ = gb;
     }
@@ -199,6 +202,7 @@ class Session : public SessionBase {
     fused_ok_ = fuse_any && P.method == GLX_PROXGD;
     fused_fista_ok_ = fuse_any && P.method == GLX_FPROXGD;
     GLX_HIP(hipMemsetAsync(ticket_, 0, kTicketBytes, st_));
+    GLX_HIP(hipMemsetAsync(pcnt_, 0, sizeof(unsigned) * (P.n / 64 + 64), st_));
     GLX_HIP(hipMemsetAsync(flag_, 0, 256, st_));
     GLX_HIP(hipMemsetAsync(scal_, 0, sizeof(double) * NSCAL, st_));
     mus_[0] = 100 * P.mu0;
@@ -695,7 +699,7 @@ class Session : public SessionBase {
     if (pub_seq) pb = make_pub(extra, pub_seq);
     hipEvent_t e0 = prof_begin(1);
     launch_atr_prox<T>(plan_, A_, r, Gs_[set], x, X_[op], X_[opt], X_[oz], t, mu_, O_.thres,
-                       red(S_TR), st_, pb);
+                       red(S_TR), st_, pb, Gps_[set], pcnt_);
     check_launch();
     prof_end(1, e0);
     ++atr_calls_;
@@ -852,7 +856,7 @@ class Session : public SessionBase {
     if (pub_seq) pb = make_pub(extra, pub_seq);
     hipEvent_t e0 = prof_begin(1);
     launch_atr_fista<T>(plan_, A_, r, Gs_[set], yv, xk, X_[oc], X_[ov], X_[oy], t, mu_, O_.thres,
-                        theta, theta_next, red(S_TR), st_, pb);
+                        theta, theta_next, red(S_TR), st_, pb, Gps_[set], pcnt_);
     check_launch();
     prof_end(1, e0);
     ++atr_calls_;
@@ -936,6 +940,7 @@ class Session : public SessionBase {
   double *hs_ = nullptr, *hs_dev_ = nullptr;
   unsigned *hseq_ = nullptr, *hseq_dev_ = nullptr;
   unsigned* ticket_ = nullptr;
+  unsigned* pcnt_ = nullptr;   // per-panel counters (fused A^T R with K splits)
   int* flag_ = nullptr;
   int64_t fh_cap_ = 0;
   T* gemv_slabs_ = nullptr;

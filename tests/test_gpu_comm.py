@@ -4,7 +4,8 @@ With a communicator, the solver sums the A^T r slabs, all-reduces the gradient a
 squared-residual sum over RCCL, and feeds S = 1 arrays to the row kernels — the exact code path
 every rank runs at N GPUs. With one rank the all-reduce is an identity, so the result must be
 bit-identical to the communicator-free run (which sums the slabs inside the prox kernel, in the
-same slab order). N > 1 is covered by tests/test_dist_cpu.py (gloo) and the driver's 8-GPU run.
+same slab order; GLX_ATR_FUSE_SPLIT=0 keeps that run off the fused A^T R + trial kernel, whose
+trial sums are added in another order). N > 1 is covered by tests/test_dist_cpu.py (gloo) and the driver's 8-GPU run.
 """
 import os
 import socket
@@ -52,8 +53,9 @@ def test_allreduce_identity_world1(comm):
     ("gl_SGD_primal", (1024, 256, 1), torch.float64),
     ("gl_FProxGD_primal", (512, 1024, 32), torch.float32),
 ])
-def test_comm_path_bit_identical_world1(comm, solver, shape, dtype):
+def test_comm_path_bit_identical_world1(comm, monkeypatch, solver, shape, dtype):
     import glx
+    monkeypatch.setenv("GLX_ATR_FUSE_SPLIT", "0")
     from oracle import numpy_ref
     m, n, l = shape
     A, b, u, x0, mu = numpy_ref.gen_data(m, n, l, 7)
