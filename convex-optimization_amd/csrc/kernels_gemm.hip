@@ -290,9 +290,7 @@ __device__ inline void lds_put(T* dst, typename MF<T>::vec_t v) {
   }
 }
 
-// ABL (timing ablation, never used for results; GLX_AXL_ABL): 1 = no barriers, 2 = no X
-// staging or LDS reads (constant B operand), 3 = no A loads (constant A operand), 4 = 3 + 1.
-template <typename T, int MT, int NT, int NSRC, int PF, int VPL, int WAVES, int ABL = 0>
+template <typename T, int MT, int NT, int NSRC, int PF, int VPL, int WAVES>
 __global__ __launch_bounds__(64 * WAVES) void k_ax_lds(const T* __restrict__ A,
                                                       const T* __restrict__ X0,
                                                       const T* __restrict__ X1,
@@ -376,8 +374,7 @@ __global__ __launch_bounds__(64 * WAVES) void k_ax_lds(const T* __restrict__ A,
     for (int mt = 0; mt < MT; ++mt)
 #pragma unroll
       for (int v = 0; v < VPL; ++v)
-        dst[mt][v] = (ABL == 3 || ABL == 4) ? V{} + (T)(lane + mt)
-                                           : load_vec<T, false>(ap[mt] + off * CK + v * E);
+        dst[mt][v] = load_vec<T, false>(ap[mt] + off * CK + v * E);
   };
   auto put_x = [&](int slot, const V (&src)[XPT]) {
 #pragma unroll
@@ -391,7 +388,7 @@ __global__ __launch_bounds__(64 * WAVES) void k_ax_lds(const T* __restrict__ A,
       const int src = cc / NT, nt = cc % NT;
       const T* xp = &xs[slot][src * CK * LP + q * EL * LP + nt * 16 + i];
 #pragma unroll
-      for (int e = 0; e < EL; ++e) xv[cc][e] = (ABL == 2) ? (T)(cc + e + i) : xp[e * LP];
+      for (int e = 0; e < EL; ++e) xv[cc][e] = xp[e * LP];
     }
   };
   // MFMAs of row tile mt for one chunk
@@ -422,21 +419,19 @@ __global__ __launch_bounds__(64 * WAVES) void k_ax_lds(const T* __restrict__ A,
     for (int p = 0; p < PF; ++p) {
       const int64_t c = c0 + p;
       const int slot = (int)(c & 1);
-      if (ABL != 2) put_x(slot ^ 1, xr[(p + 1) % PF]);   // X(c+1), loaded PF-1 chunks ago
+      put_x(slot ^ 1, xr[(p + 1) % PF]);   // X(c+1), loaded PF-1 chunks ago
       load_x(xr[p], c + PF);       // xr[p] (X(c)) has been in LDS since chunk c-1
       T xv[NC][EL];
       read_x(slot, xv);
 #pragma unroll
       for (int mt = 0; mt < MT; ++mt) {
         mma_tile(mt, a[p][mt], xv);
-        if (ABL != 3 && ABL != 4) {
-          int64_t off = c + PF;
-          off = off < nch ? off : nch - 1;
+        int64_t off = c + PF;
+        off = off < nch ? off : nch - 1;
 #pragma unroll
-          for (int v = 0; v < VPL; ++v) a[p][mt][v] = load_vec<T, false>(ap[mt] + off * CK + v * E);
-        }
+        for (int v = 0; v < VPL; ++v) a[p][mt][v] = load_vec<T, false>(ap[mt] + off * CK + v * E);
       }
-      if (ABL != 1 && ABL != 2 && ABL != 4) __syncthreads();
+      __syncthreads();
     }
   }
   // tail: fewer than PF chunks left (their data is already in the ring)
@@ -445,12 +440,12 @@ __global__ __launch_bounds__(64 * WAVES) void k_ax_lds(const T* __restrict__ A,
     const int64_t c = c0 + p;
     if (c < nch) {
       const int slot = (int)(c & 1);
-      if (c + 1 < nch && ABL != 2) put_x(slot ^ 1, xr[(p + 1) % PF]);
+      if (c + 1 < nch) put_x(slot ^ 1, xr[(p + 1) % PF]);
       T xv[NC][EL];
       read_x(slot, xv);
 #pragma unroll
       for (int mt = 0; mt < MT; ++mt) mma_tile(mt, a[p][mt], xv);
-      if (ABL != 1 && ABL != 2 && ABL != 4) __syncthreads();
+      __syncthreads();
     }
   }
 
@@ -1328,6 +1323,7 @@ static int axb_default(int nsrc, int esize) {
 }
 
 static constexpr int kLdsCodes[] = {52224, 52324, 52228, 52328, 52218, 54224, 52214, 54214,
+                                     51228, 51328, 51224,
                                      52428, 54228, 54218, 62428, 62424, 62418, 72428, 72424,
                                      72828};
 static bool lds_code_ok(int c, int64_t n, int64_t l, int esize) {
@@ -1549,14 +1545,14 @@ static void ax_mfma_go(const GemmPlan& p, const T* A, const T* const* X, T* P, c
                      epoch);
 }
 
-template <typename T, int NT, int NSRC, int MT, int PF, int VPL, int WAVES, int ABL = 0>
+template <typename T, int NT, int NSRC, int MT, int PF, int VPL, int WAVES>
 static void ax_lds_go(const GemmPlan& p, int S, const T* A, const T* const* X, T* P,
                       const int* gate, int epoch, hipStream_t st) {
   constexpr int E = 16 / sizeof(T);
   const int gx = (int)cdiv(p.m, 16 * MT * WAVES);
   const int xmap = (p.ax_xmap && ax_xmap_ok(S)) ? 1 : 0;
-  static const size_t pad = lds_pad(k_ax_lds<T, MT, NT, NSRC, PF, VPL, WAVES, ABL>, "GLX_AX_LDS_PAD");
-  hipLaunchKernelGGL((k_ax_lds<T, MT, NT, NSRC, PF, VPL, WAVES, ABL>), dim3((unsigned)ax_grid(xmap, gx, S)),
+  static const size_t pad = lds_pad(k_ax_lds<T, MT, NT, NSRC, PF, VPL, WAVES>, "GLX_AX_LDS_PAD");
+  hipLaunchKernelGGL((k_ax_lds<T, MT, NT, NSRC, PF, VPL, WAVES>), dim3((unsigned)ax_grid(xmap, gx, S)),
                      dim3(64 * WAVES), pad, st, A, X[0], X[1], X[2], P, p.m, p.n,
                      p.n / (4 * VPL * E), S, gx, xmap, gate, epoch);
 }
@@ -1601,32 +1597,17 @@ static void ax_lds_code(const GemmPlan& p, int code, int S, const T* A, const T*
     case 52324: ax_lds_go<T, NT, NSRC, 2, 3, 2, 4>(p, S, A, X, P, gate, epoch, st); break;
     case 54228: ax_lds_go<T, NT, NSRC, 4, 2, 2, 8>(p, S, A, X, P, gate, epoch, st); break;
     case 54218: ax_lds_go<T, NT, NSRC, 4, 2, 1, 8>(p, S, A, X, P, gate, epoch, st); break;
-    case 52228:
-      if constexpr (sizeof(T) == 8 && NT == 2 && NSRC == 2) {
-        switch (env_int("GLX_AXL_ABL", 0)) {   // timing ablations (results are wrong)
-          case 1: ax_lds_go<T, NT, NSRC, 2, 2, 2, 8, 1>(p, S, A, X, P, gate, epoch, st); return;
-          case 2: ax_lds_go<T, NT, NSRC, 2, 2, 2, 8, 2>(p, S, A, X, P, gate, epoch, st); return;
-          case 3: ax_lds_go<T, NT, NSRC, 2, 2, 2, 8, 3>(p, S, A, X, P, gate, epoch, st); return;
-          default: break;
-        }
-      }
-      ax_lds_go<T, NT, NSRC, 2, 2, 2, 8>(p, S, A, X, P, gate, epoch, st);
-      break;
+    case 52228: ax_lds_go<T, NT, NSRC, 2, 2, 2, 8>(p, S, A, X, P, gate, epoch, st); break;
+    // one 16-row tile per wave: twice the row tiles, half the K splits and partial slabs
+    case 51228: ax_lds_go<T, NT, NSRC, 1, 2, 2, 8>(p, S, A, X, P, gate, epoch, st); break;
+    case 51328: ax_lds_go<T, NT, NSRC, 1, 3, 2, 8>(p, S, A, X, P, gate, epoch, st); break;
+    case 51224: ax_lds_go<T, NT, NSRC, 1, 2, 2, 4>(p, S, A, X, P, gate, epoch, st); break;
     case 52328: ax_lds_go<T, NT, NSRC, 2, 3, 2, 8>(p, S, A, X, P, gate, epoch, st); break;
     case 52218: ax_lds_go<T, NT, NSRC, 2, 2, 1, 8>(p, S, A, X, P, gate, epoch, st); break;
     case 54224: ax_lds_go<T, NT, NSRC, 4, 2, 2, 4>(p, S, A, X, P, gate, epoch, st); break;
     case 52214: ax_lds_go<T, NT, NSRC, 2, 2, 1, 4>(p, S, A, X, P, gate, epoch, st); break;
     case 54214: ax_lds_go<T, NT, NSRC, 4, 2, 1, 4>(p, S, A, X, P, gate, epoch, st); break;
     default:   // 52224
-      if constexpr (sizeof(T) == 8 && NT == 2 && NSRC == 2) {
-        switch (env_int("GLX_AXL_ABL", 0)) {   // timing ablations (results are wrong)
-          case 1: ax_lds_go<T, NT, NSRC, 2, 2, 2, 4, 1>(p, S, A, X, P, gate, epoch, st); return;
-          case 2: ax_lds_go<T, NT, NSRC, 2, 2, 2, 4, 2>(p, S, A, X, P, gate, epoch, st); return;
-          case 3: ax_lds_go<T, NT, NSRC, 2, 2, 2, 4, 3>(p, S, A, X, P, gate, epoch, st); return;
-          case 4: ax_lds_go<T, NT, NSRC, 2, 2, 2, 4, 4>(p, S, A, X, P, gate, epoch, st); return;
-          default: break;
-        }
-      }
       ax_lds_go<T, NT, NSRC, 2, 2, 2, 4>(p, S, A, X, P, gate, epoch, st);
       break;
   }
