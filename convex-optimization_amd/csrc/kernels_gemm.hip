@@ -1345,9 +1345,22 @@ static int lds_split(int esize, int64_t m, int64_t n, int code, int64_t target =
 // the slabs rival A itself. When they exceed 1/6 of A, use the 4-wave tile at 256 blocks, which
 // halves them. Shard-shape sweep (profiles/r1_tuning/shard_shapes.txt): at m = 1024 this is
 // +10 % end to end despite a slower A@X; at m >= 2048 the default tile stays ahead.
+//
+// Per-rank shards at l = 32 (m <= 2048: the 4- and 8-GPU runs of the north-star size) take the
+// 8-wave tile with ONE 16-row tile per wave and a 3-deep ring (51328): at these row counts the
+// K splits are short, and two waves per SIMD with half the rows per block keep the slab volume
+// of the 4-wave tile. Measured end to end with the communicator path
+// (profiles/r1_tuning/small_kernels/ax_shard_tile.log): +4.7 % at m = 1024, +3 % at 2048,
+// neutral at 4096; at m = 8192 the default tile stays ahead (A@X 290 vs 306 us).
 static void lds_plan(int esize, int64_t m, int64_t n, int64_t l, int nsrc, int& code, int& S) {
   S = lds_split(esize, m, n, code);
   if (std::getenv("GLX_AXL_BLOCKS") || std::getenv("GLX_AXB_VARIANT")) return;
+  if (esize == 8 && nsrc == 2 && l == 32 && m <= 2048 && code == 52228 &&
+      lds_code_ok(51328, n, l, esize) && env_int("GLX_SHARD_TILE", 1) != 0) {
+    code = 51328;
+    S = lds_split(esize, m, n, code);
+    return;
+  }
   if ((double)S * (double)m * nsrc * l * 6.0 <= (double)m * n) return;
   const int c4 = esize == 8 ? 52224 : 52324;
   if (!lds_code_ok(c4, n, l, esize)) return;
