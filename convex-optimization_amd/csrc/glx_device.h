@@ -157,6 +157,22 @@ __device__ inline bool publisher_block(const Pub& pub, const Red& red) {
   return true;
 }
 
+// The same for the FIRST workgroup of the launch (the other workgroups index themselves with
+// blockIdx.x - 1). Workgroups are dispatched in index order, so the packet leaves at the start
+// of the launch even when only one workgroup fits per CU and a last-index publisher would wait
+// for the kernel's first workgroups to retire.
+template <int NV, unsigned MAXMASK, int NW = 4>
+__device__ inline bool publisher_first(const Pub& pub, const Red& red) {
+  if (pub.host == nullptr || blockIdx.x != 0) return false;
+  if (threadIdx.x == 0)
+    publish_packet(pub.s, pub.ns, pub.host, pub.host_seq, pub.seq, pub.s2, pub.off2, pub.n2);
+  double v[NV];
+#pragma unroll
+  for (int j = 0; j < NV; ++j) v[j] = identity((MAXMASK >> j) & 1);
+  grid_reduce<NV, MAXMASK, NW>(v, red);
+  return true;
+}
+
 // g = sum_s slabs[s][idx] in slab order (S = 1: a plain load)
 template <typename T>
 __device__ inline T slab_sum(const T* __restrict__ g, int S, int64_t stride, int64_t idx) {

@@ -1006,7 +1006,7 @@ __global__ __launch_bounds__(256) void k_atr_mfma(const T* __restrict__ A, const
 // columns i and 16 + i of 4 rows, exactly the 16-lanes-per-row layout of k_prox_pgd — every
 // wave writes its rows of G and runs the trial on them (prox_pgd_row, the same arithmetic as
 // k_prox_pgd) with x = the thresholded iterate; the six trial sums are reduced over the grid.
-template <typename T, int NT, int PF, bool NTL>
+template <typename T, int NT, int PF, bool NTL, bool SPLIT>
 __global__ __launch_bounds__(256) void k_atr_prox(const T* __restrict__ A, const T* __restrict__ R,
                                                   T* __restrict__ G, int64_t m, int64_t n,
                                                   const T* __restrict__ x, T* __restrict__ p,
@@ -1014,19 +1014,22 @@ __global__ __launch_bounds__(256) void k_atr_prox(const T* __restrict__ A, const
                                                   double t_, double tmu_, double thres_, Red red,
                                                   Pub pub, int S, T* __restrict__ Gp,
                                                   unsigned* __restrict__ pcnt) {
-  if (publisher_block<6, 0x8u>(pub, red)) return;   // the extra workgroup (n / 64 * S + 1 in all)
+  if (publisher_first<6, 0x8u>(pub, red)) return;   // the extra workgroup (n / 64 * S + 1 in all)
   typedef MF<T> M;
   constexpr int L = 16 * NT;
   const int lane = threadIdx.x & 63;
   const int wave = threadIdx.x >> 6;
   const int i = lane & 15;
   typename M::acc_t acc[4][NT];
-  const int64_t panel = blockIdx.x / S, split = blockIdx.x % S;
-  const int64_t col0 = atr_panel<T, NT, PF, 0, NTL>(A, R, m, n, S, acc, panel, split);
+  const int64_t bid = (int64_t)blockIdx.x - (pub.host ? 1 : 0);
+  const int64_t panel = SPLIT ? bid / S : bid, split = SPLIT ? bid % S : 0;
+  const int64_t col0 = atr_panel<T, NT, PF, 0, NTL>(A, R, m, n, SPLIT ? S : 1, acc, panel, split);
   double accr[6] = {0.0, 0.0, 0.0, -__builtin_inf(), 0.0, 0.0};
-  if (S > 1 && !atr_split_combine<T, NT>(acc, Gp, n, S, panel, split, pcnt)) {
-    grid_reduce<6, 0x8u>(accr, red);
-    return;
+  if constexpr (SPLIT) {   // a separate instantiation: the S = 1 kernel keeps 2 blocks per CU
+    if (!atr_split_combine<T, NT>(acc, Gp, n, S, panel, split, pcnt)) {
+      grid_reduce<6, 0x8u>(accr, red);
+      return;
+    }
   }
   const T t = (T)t_, tmu = (T)tmu_, thres = (T)thres_;
 #pragma unroll
@@ -1065,7 +1068,7 @@ __global__ __launch_bounds__(256) void k_atr_prox(const T* __restrict__ A, const
 // FISTA's backtracking trial fused into A^T R the same way (WL 0, one K split): each wave runs
 // fista_row (the arithmetic of k_fista_trial) on its 16 gradient rows, with y the extrapolated
 // point and xk the current iterate; writes G, xc, v_next, y_next and reduces the four sums.
-template <typename T, int NT, int PF, bool NTL>
+template <typename T, int NT, int PF, bool NTL, bool SPLIT>
 __global__ __launch_bounds__(256) void k_atr_fista(const T* __restrict__ A, const T* __restrict__ R,
                                                    T* __restrict__ G, int64_t m, int64_t n,
                                                    const T* __restrict__ y, const T* __restrict__ xk,
@@ -1074,19 +1077,22 @@ __global__ __launch_bounds__(256) void k_atr_fista(const T* __restrict__ A, cons
                                                    double thres_, double theta_, double a1_,
                                                    double b1_, Red red, Pub pub, int S,
                                                    T* __restrict__ Gp, unsigned* __restrict__ pcnt) {
-  if (publisher_block<4, 0x8u>(pub, red)) return;
+  if (publisher_first<4, 0x8u>(pub, red)) return;
   typedef MF<T> M;
   constexpr int L = 16 * NT;
   const int lane = threadIdx.x & 63;
   const int wave = threadIdx.x >> 6;
   const int i = lane & 15;
   typename M::acc_t acc[4][NT];
-  const int64_t panel = blockIdx.x / S, split = blockIdx.x % S;
-  const int64_t col0 = atr_panel<T, NT, PF, 0, NTL>(A, R, m, n, S, acc, panel, split);
+  const int64_t bid = (int64_t)blockIdx.x - (pub.host ? 1 : 0);
+  const int64_t panel = SPLIT ? bid / S : bid, split = SPLIT ? bid % S : 0;
+  const int64_t col0 = atr_panel<T, NT, PF, 0, NTL>(A, R, m, n, SPLIT ? S : 1, acc, panel, split);
   double accr[4] = {0.0, 0.0, 0.0, -__builtin_inf()};
-  if (S > 1 && !atr_split_combine<T, NT>(acc, Gp, n, S, panel, split, pcnt)) {
-    grid_reduce<4, 0x8u>(accr, red);
-    return;
+  if constexpr (SPLIT) {
+    if (!atr_split_combine<T, NT>(acc, Gp, n, S, panel, split, pcnt)) {
+      grid_reduce<4, 0x8u>(accr, red);
+      return;
+    }
   }
   const T t = (T)t_, tmu = (T)tmu_, thres = (T)thres_, theta = (T)theta_, a1 = (T)a1_, b1 = (T)b1_;
 #pragma unroll
@@ -1769,10 +1775,15 @@ template <typename T, int NT, int PF, bool NTL>
 static void atr_prox_go(const GemmPlan& p, const T* A, const T* R, T* G, const T* x, T* pp,
                         T* pthr, T* z, double t, double mu, double thres, Red red, hipStream_t st,
                         Pub pub, T* Gp, unsigned* pcnt) {
-  static const size_t pad = lds_pad(k_atr_prox<T, NT, PF, NTL>, "GLX_ATR_LDS_PAD");
-  hipLaunchKernelGGL((k_atr_prox<T, NT, PF, NTL>),
-                     dim3((unsigned)(p.n / 64 * p.atr_S + (pub.host ? 1 : 0))), dim3(256), pad, st,
-                     A, R, G, p.m, p.n, x, pp, pthr, z, t, t * mu, thres, red, pub, p.atr_S, Gp, pcnt);
+  const dim3 grid((unsigned)(p.n / 64 * p.atr_S + (pub.host ? 1 : 0)));
+  if (p.atr_S > 1) {
+    hipLaunchKernelGGL((k_atr_prox<T, NT, PF, NTL, true>), grid, dim3(256), 0, st, A, R, G, p.m,
+                       p.n, x, pp, pthr, z, t, t * mu, thres, red, pub, p.atr_S, Gp, pcnt);
+    return;
+  }
+  static const size_t pad = lds_pad(k_atr_prox<T, NT, PF, NTL, false>, "GLX_ATR_LDS_PAD");
+  hipLaunchKernelGGL((k_atr_prox<T, NT, PF, NTL, false>), grid, dim3(256), pad, st, A, R, G, p.m,
+                     p.n, x, pp, pthr, z, t, t * mu, thres, red, pub, 1, Gp, pcnt);
 }
 template <typename T, int NT>
 static void atr_prox_nt(const GemmPlan& p, const T* A, const T* R, T* G, const T* x, T* pp,
@@ -1800,11 +1811,17 @@ template <typename T, int NT, int PF, bool NTL>
 static void atr_fista_go(const GemmPlan& p, const T* A, const T* R, T* G, const T* y, const T* xk,
                          T* xc, T* vn, T* yn, double t, double mu, double thres, double theta,
                          double theta_next, Red red, hipStream_t st, Pub pub, T* Gp, unsigned* pcnt) {
-  static const size_t pad = lds_pad(k_atr_fista<T, NT, PF, NTL>, "GLX_ATR_LDS_PAD");
-  hipLaunchKernelGGL((k_atr_fista<T, NT, PF, NTL>),
-                     dim3((unsigned)(p.n / 64 * p.atr_S + (pub.host ? 1 : 0))), dim3(256), pad, st,
-                     A, R, G, p.m, p.n, y, xk, xc, vn, yn, t, t * mu, thres, theta, 1.0 - theta_next,
-                     theta_next, red, pub, p.atr_S, Gp, pcnt);
+  const dim3 grid((unsigned)(p.n / 64 * p.atr_S + (pub.host ? 1 : 0)));
+  if (p.atr_S > 1) {
+    hipLaunchKernelGGL((k_atr_fista<T, NT, PF, NTL, true>), grid, dim3(256), 0, st, A, R, G, p.m,
+                       p.n, y, xk, xc, vn, yn, t, t * mu, thres, theta, 1.0 - theta_next,
+                       theta_next, red, pub, p.atr_S, Gp, pcnt);
+    return;
+  }
+  static const size_t pad = lds_pad(k_atr_fista<T, NT, PF, NTL, false>, "GLX_ATR_LDS_PAD");
+  hipLaunchKernelGGL((k_atr_fista<T, NT, PF, NTL, false>), grid, dim3(256), pad, st, A, R, G, p.m,
+                     p.n, y, xk, xc, vn, yn, t, t * mu, thres, theta, 1.0 - theta_next, theta_next,
+                     red, pub, 1, Gp, pcnt);
 }
 template <typename T, int NT>
 static void atr_fista_nt(const GemmPlan& p, const T* A, const T* R, T* G, const T* y, const T* xk,
