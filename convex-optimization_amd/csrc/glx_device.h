@@ -28,9 +28,11 @@ __device__ inline double waves_combine(int op, const double* w) {
 }
 
 // Reduce NV per-thread values over the grid; block size must be 64 * NW (NW = 4 or 8).
-// MAXMASK bit v = max op.
+// MAXMASK bit v = max op. slot = this block's partials slot (default blockIdx.x): a launch
+// whose first workgroup is a publisher (publisher_first) puts that one last and the others at
+// blockIdx.x - 1, so the sums come out bit-identical with and without the packet.
 template <int NV, unsigned MAXMASK, int NW = 4>
-__device__ bool grid_reduce(double (&v)[NV], const Red& red) {
+__device__ bool grid_reduce(double (&v)[NV], const Red& red, int slot = -1) {
   static_assert(NW == 4 || NW == 8, "4- or 8-wave blocks");
   constexpr int NTHR = 64 * NW;
   __shared__ double sh[NV][NW];
@@ -55,7 +57,8 @@ __device__ bool grid_reduce(double (&v)[NV], const Red& red) {
     for (int j = 0; j < NV; ++j) {
       const int op = (MAXMASK >> j) & 1;
       const double bv = waves_combine<NW>(op, sh[j]);
-      __hip_atomic_store(&red.part[j * kMaxBlocks + blockIdx.x], bv, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(&red.part[j * kMaxBlocks + (slot < 0 ? (int)blockIdx.x : slot)], bv,
+                         __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     // Two-level arrival: one device-scope counter costs ~12 ns per arriving block
@@ -123,7 +126,7 @@ __device__ bool grid_reduce(double (&v)[NV], const Red& red) {
 // stores (sc0 sc1, straight to host memory), drained with vmcnt(0) so every packet store is
 // acknowledged, then the sequence word the host spins on; no L2 writeback is needed for it.
 // All loads are issued before the first store (one latency, not ns). Either its own tiny kernel
-// (k_publish) or the publisher workgroup of the next kernel (publisher_block). Done by the last
+// (k_publish) or the publisher workgroup of the next kernel (publisher_first). Done by the last
 // block of the preceding reduction instead it measured ~15 us slower (profiles/r1_tuning,
 // fused-publish attribution) than a separate launch (~5.5 us).
 constexpr int kPublishMax = 32;
@@ -141,29 +144,34 @@ __device__ inline void publish_packet(const double* s, int ns, double* host, uns
   __hip_atomic_store(host_seq, seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
-// A launch that carries the scalar packet gets one extra (the last) workgroup that writes it and
-// then joins the grid reduction with identity values (the reduction counts every workgroup).
-// The packet then leaves while the kernel's other workgroups work, instead of as a separate
-// k_publish launch in front of the kernel. Returns true in the publisher workgroup.
+// A launch that carries the scalar packet gets one extra workgroup, the FIRST (blockIdx.x 0;
+// the other workgroups index themselves with blockIdx.x - 1), that writes it and then joins the
+// grid reduction with identity values (the reduction counts every workgroup). Workgroups are
+// dispatched in index order, so the packet leaves at the start of the launch, while the
+// kernel's other workgroups work, instead of as a separate k_publish launch in front of it —
+// also when only one workgroup fits per CU (a last-index publisher then waited for the first
+// workgroups to retire: a 4 us gap before the next kernel). Returns true in the publisher.
 template <int NV, unsigned MAXMASK, int NW = 4>
-__device__ inline bool publisher_block(const Pub& pub, const Red& red) {
-  if (pub.host == nullptr || blockIdx.x != gridDim.x - 1) return false;
+__device__ inline bool publisher_first(const Pub& pub, const Red& red) {
+  if (pub.host == nullptr || blockIdx.x != 0) return false;
   if (threadIdx.x == 0)
     publish_packet(pub.s, pub.ns, pub.host, pub.host_seq, pub.seq, pub.s2, pub.off2, pub.n2);
   double v[NV];
 #pragma unroll
   for (int j = 0; j < NV; ++j) v[j] = identity((MAXMASK >> j) & 1);
-  grid_reduce<NV, MAXMASK, NW>(v, red);
+  grid_reduce<NV, MAXMASK, NW>(v, red, (int)gridDim.x - 1);
   return true;
 }
+// partials slot of a non-publisher workgroup of such a launch
+__device__ inline int work_slot(const Pub& pub) { return (int)blockIdx.x - (pub.host ? 1 : 0); }
 
-// The same for the FIRST workgroup of the launch (the other workgroups index themselves with
-// blockIdx.x - 1). Workgroups are dispatched in index order, so the packet leaves at the start
-// of the launch even when only one workgroup fits per CU and a last-index publisher would wait
-// for the kernel's first workgroups to retire.
+// The row kernels (k_prox_pgd, k_fista_trial: at N > 1 the speculative kernel that carries the
+// packet) keep the publisher as their LAST workgroup: they fit many workgroups per CU, so it
+// starts at once anyway, and a first-index publisher measured 2-5 % slower end to end on the
+// multi-GPU shards (profiles/r1_tuning/small_kernels/publisher_first_rows.log).
 template <int NV, unsigned MAXMASK, int NW = 4>
-__device__ inline bool publisher_first(const Pub& pub, const Red& red) {
-  if (pub.host == nullptr || blockIdx.x != 0) return false;
+__device__ inline bool publisher_last(const Pub& pub, const Red& red) {
+  if (pub.host == nullptr || blockIdx.x != gridDim.x - 1) return false;
   if (threadIdx.x == 0)
     publish_packet(pub.s, pub.ns, pub.host, pub.host_seq, pub.seq, pub.s2, pub.off2, pub.n2);
   double v[NV];

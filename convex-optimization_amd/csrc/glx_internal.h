@@ -36,7 +36,7 @@ struct Red {
 };
 
 // A scalar packet for the host (what k_publish writes) carried by a kernel launch as one extra
-// workgroup (publisher_block, glx_device.h); host == NULL: none.
+// workgroup (publisher_first, glx_device.h); host == NULL: none.
 struct Pub {
   const double* s = nullptr;
   int ns = 0;

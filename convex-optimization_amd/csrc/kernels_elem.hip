@@ -116,17 +116,19 @@ __global__ __launch_bounds__(256) void k_sum_partials(const T* __restrict__ Gp, 
 }
 
 // Iterate over rows: each group of LPR lanes owns one row per trip.
-// NB = the workgroups that share the rows (all but a publisher workgroup, see Pub)
-#define GLX_ROW_LOOP_BEGIN_NB(LPR, NB)                                                 \
+// NB = the workgroups that share the rows, BI = this workgroup's index among them (all but a
+// publisher workgroup, see Pub)
+#define GLX_ROW_LOOP_BEGIN_NBI(LPR, NB, BI)                                            \
   const int sub = threadIdx.x & ((LPR)-1);                                             \
   const int64_t rows_per_block = 256 / (LPR);                                          \
   const int64_t row_stride = (int64_t)(NB) * rows_per_block;                           \
   const int64_t n_trips = (n + row_stride - 1) / row_stride;                           \
   for (int64_t trip = 0; trip < n_trips; ++trip) {                                     \
-    const int64_t row = trip * row_stride + (int64_t)blockIdx.x * rows_per_block +     \
+    const int64_t row = trip * row_stride + (int64_t)(BI) * rows_per_block +           \
                         (threadIdx.x / (LPR));                                         \
     const bool rv = row < n;                                                           \
     const int64_t base = (rv ? row : 0) * l;
+#define GLX_ROW_LOOP_BEGIN_NB(LPR, NB) GLX_ROW_LOOP_BEGIN_NBI(LPR, NB, blockIdx.x)
 #define GLX_ROW_LOOP_BEGIN(LPR) GLX_ROW_LOOP_BEGIN_NB(LPR, gridDim.x)
 #define GLX_ROW_LOOP_END }
 
@@ -143,7 +145,7 @@ __global__ __launch_bounds__(256) void k_prox_pgd(const T* __restrict__ x, const
                                                   T* __restrict__ pthr, T* __restrict__ z, int64_t n,
                                                   int64_t l, double t_, double tmu_, double thres_,
                                                   Red red, Pub pub) {
-  if (publisher_block<6, 0x8u>(pub, red)) return;
+  if (publisher_last<6, 0x8u>(pub, red)) return;
   const T t = (T)t_, tmu = (T)tmu_, thres = (T)thres_;
   const int64_t nl = n * l;
   double acc[6] = {0.0, 0.0, 0.0, -__builtin_inf(), 0.0, 0.0};
@@ -187,7 +189,7 @@ __global__ __launch_bounds__(256) void k_fista_trial(
     int64_t n, int64_t l, double t_, double tmu_, double thres_, double theta_, double a1_,
     double b1_, double dd_, double delta_, Red red, Pub pub) {
   constexpr int NV = PROX ? 4 : 5;
-  if (publisher_block<NV, (1u << (NV - 1))>(pub, red)) return;
+  if (publisher_last<NV, (1u << (NV - 1))>(pub, red)) return;
   const T t = (T)t_, tmu = (T)tmu_, thres = (T)thres_, theta = (T)theta_, a1 = (T)a1_, b1 = (T)b1_;
   const T dd = (T)dd_, delta = (T)delta_;
   const int64_t nl = n * l;

@@ -1027,7 +1027,7 @@ __global__ __launch_bounds__(256) void k_atr_prox(const T* __restrict__ A, const
   double accr[6] = {0.0, 0.0, 0.0, -__builtin_inf(), 0.0, 0.0};
   if constexpr (SPLIT) {   // a separate instantiation: the S = 1 kernel keeps 2 blocks per CU
     if (!atr_split_combine<T, NT>(acc, Gp, n, S, panel, split, pcnt)) {
-      grid_reduce<6, 0x8u>(accr, red);
+      grid_reduce<6, 0x8u>(accr, red, work_slot(pub));
       return;
     }
   }
@@ -1062,7 +1062,7 @@ __global__ __launch_bounds__(256) void k_atr_prox(const T* __restrict__ A, const
       }
     }
   }
-  grid_reduce<6, 0x8u>(accr, red);
+  grid_reduce<6, 0x8u>(accr, red, work_slot(pub));
 }
 
 // FISTA's backtracking trial fused into A^T R the same way (WL 0, one K split): each wave runs
@@ -1090,7 +1090,7 @@ __global__ __launch_bounds__(256) void k_atr_fista(const T* __restrict__ A, cons
   double accr[4] = {0.0, 0.0, 0.0, -__builtin_inf()};
   if constexpr (SPLIT) {
     if (!atr_split_combine<T, NT>(acc, Gp, n, S, panel, split, pcnt)) {
-      grid_reduce<4, 0x8u>(accr, red);
+      grid_reduce<4, 0x8u>(accr, red, work_slot(pub));
       return;
     }
   }
@@ -1129,7 +1129,7 @@ __global__ __launch_bounds__(256) void k_atr_fista(const T* __restrict__ A, cons
       }
     }
   }
-  grid_reduce<4, 0x8u>(accr, red);
+  grid_reduce<4, 0x8u>(accr, red, work_slot(pub));
 }
 
 // ------------------------------------------------------------------------------------------

@@ -187,7 +187,7 @@ class Session : public SessionBase {
     const char* rb = std::getenv("GLX_READBACK");
     spin_readback_ = !(rb && std::strcmp(rb, "sync") == 0);
     // the scalar packet rides the speculative kernel queued right behind it (one extra
-    // workgroup, publisher_block) instead of a k_publish launch in front of it
+    // workgroup, publisher_first) instead of a k_publish launch in front of it
     const char* ap = std::getenv("GLX_ATTACH_PUB");
     attach_ok_ = spin_readback_ && !(ap && std::strcmp(ap, "0") == 0);
     const char* sp = std::getenv("GLX_SPEC_GRAD");
