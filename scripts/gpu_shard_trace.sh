@@ -8,7 +8,7 @@ tag=m${m}${c:+_comm}
 timeout -k 10 300 rocprofv3 --kernel-trace --output-format csv -d $O/$tag -o run -- python bench.py --no-cpu-baseline --steps 300 --warmup 30 --m $m $c > $O/$tag.json 2> $O/$tag.err; rc=$?; echo "$tag rc=$rc" >> $O/status.txt
 [ $rc -eq 0 ] || exit 1
 python -c "
-import json; d=json.load(open('$O/$tag.json')); print('$tag %.1f it/s' % d['value'])"
+import json; d=json.loads(open('$O/$tag.json').read().strip().splitlines()[-1]); print('$tag %.1f it/s' % d['value'])"
 python scripts/trace_gaps.py $(find $O/$tag -name "*kernel_trace.csv" | head -1) --last 2000
 done; done
 cat $O/status.txt | tr '\n' ' '
