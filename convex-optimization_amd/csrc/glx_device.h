@@ -132,11 +132,13 @@ __device__ bool grid_reduce(double (&v)[NV], const Red& red, int slot = -1) {
 constexpr int kPublishMax = 32;
 __device__ inline void publish_packet(const double* s, int ns, double* host, unsigned* host_seq,
                                       unsigned seq, const double* s2 = nullptr, int off2 = 0,
-                                      int n2 = 0) {
+                                      int n2 = 0, const double* s3 = nullptr, int off3 = 0,
+                                      int n3 = 0) {
   double v[kPublishMax];
 #pragma unroll
   for (int k = 0; k < kPublishMax; ++k)
-    v[k] = (k >= off2 && k < off2 + n2) ? s2[k - off2] : (k < ns ? s[k] : 0.0);
+    v[k] = (k >= off3 && k < off3 + n3) ? s3[k - off3]
+                                        : ((k >= off2 && k < off2 + n2) ? s2[k - off2] : (k < ns ? s[k] : 0.0));
 #pragma unroll
   for (int k = 0; k < kPublishMax; ++k)
     if (k < ns) __hip_atomic_store(host + k, v[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
@@ -155,7 +157,8 @@ template <int NV, unsigned MAXMASK, int NW = 4>
 __device__ inline bool publisher_first(const Pub& pub, const Red& red) {
   if (pub.host == nullptr || blockIdx.x != 0) return false;
   if (threadIdx.x == 0)
-    publish_packet(pub.s, pub.ns, pub.host, pub.host_seq, pub.seq, pub.s2, pub.off2, pub.n2);
+    publish_packet(pub.s, pub.ns, pub.host, pub.host_seq, pub.seq, pub.s2, pub.off2, pub.n2,
+                   pub.s3, pub.off3, pub.n3);
   double v[NV];
 #pragma unroll
   for (int j = 0; j < NV; ++j) v[j] = identity((MAXMASK >> j) & 1);
@@ -173,7 +176,8 @@ template <int NV, unsigned MAXMASK, int NW = 4>
 __device__ inline bool publisher_last(const Pub& pub, const Red& red) {
   if (pub.host == nullptr || blockIdx.x != gridDim.x - 1) return false;
   if (threadIdx.x == 0)
-    publish_packet(pub.s, pub.ns, pub.host, pub.host_seq, pub.seq, pub.s2, pub.off2, pub.n2);
+    publish_packet(pub.s, pub.ns, pub.host, pub.host_seq, pub.seq, pub.s2, pub.off2, pub.n2,
+                   pub.s3, pub.off3, pub.n3);
   double v[NV];
 #pragma unroll
   for (int j = 0; j < NV; ++j) v[j] = identity((MAXMASK >> j) & 1);

@@ -45,6 +45,8 @@ struct Pub {
   unsigned seq = 0;
   const double* s2 = nullptr;   // host[off2 .. off2 + n2) come from s2 instead of s
   int off2 = 0, n2 = 0;
+  const double* s3 = nullptr;   // host[off3 .. off3 + n3) come from s3 (a snapshot)
+  int off3 = 0, n3 = 0;
 };
 
 // Launch plan of the two dense products for one (dtype, m, n, l).
@@ -87,9 +89,12 @@ std::string describe_plan(const GemmPlan& p);
 // ---- dense products (kernels_gemm.hip) ----
 // A @ [X[0] | .. | X[nsrc-1]] (nsrc <= 3, each n x l) in one pass over A: partial slabs
 // P[src][ax_split(p, nsrc)][m][l]; skipped entirely unless gate == NULL or *gate == epoch.
+// pub.host != NULL: the launch also hands that scalar packet to the host from its first
+// workgroup (needs ax_pub_ok: the kind-5 LDS tile for nsrc).
+bool ax_pub_ok(const GemmPlan& p, int nsrc);
 template <typename T>
 void launch_ax(const GemmPlan& p, int nsrc, const T* A, const T* const* X, T* P, const int* gate,
-               int epoch, hipStream_t st);
+               int epoch, hipStream_t st, Pub pub = Pub{});
 template <typename T>
 void launch_atr(const GemmPlan& p, const T* A, const T* R, T* Gp, hipStream_t st);
 // ProxGD trial fused into A^T R (needs atr_prox_ok: MFMA panels, WL 0, at most 8 K splits):
@@ -122,7 +127,8 @@ template <typename T>
 void launch_finalize_residual(const T* P, int S, const T* B, int nsrc, T* const* R, int64_t ml,
                               const int* gate, int epoch, int gate_mode, const T* cx, int64_t cn,
                               const double* cmax, double* fh, double fh_mu, const double* fh_rn,
-                              Red red, hipStream_t st);
+                              Red red, hipStream_t st, const double* snap_src = nullptr,
+                              double* snap_dst = nullptr, int nsnap = 0);
 template <typename T>
 void launch_sum_partials(const T* Gp, int S, T* G, int64_t nl, hipStream_t st);
 // ProxGD trial: p = prox(x - t g, t), G_t = (x - p)/t, z = x - t G_t, pthr = p thresholded.

@@ -76,7 +76,8 @@ __global__ __launch_bounds__(256) void k_finalize_residual(
     const T* __restrict__ P, int S, const T* __restrict__ B, T* __restrict__ R0, T* __restrict__ R1,
     T* __restrict__ R2, int64_t ml, const int* __restrict__ gate, int epoch, int gate_mode,
     const T* __restrict__ cx, int64_t cn, const double* __restrict__ cmax, double* __restrict__ fh,
-    double fh_mu, const double* __restrict__ fh_rn, Red red) {
+    double fh_mu, const double* __restrict__ fh_rn, Red red, const double* __restrict__ snap_src,
+    double* __restrict__ snap_dst, int nsnap) {
   const bool live = (gate == nullptr) || (*gate == epoch);
   if (!live && gate_mode == 0) return;  // uniform over the grid: nobody touches the ticket
   double v[4] = {0.0, 0.0, 0.0, 0.0};
@@ -105,6 +106,9 @@ __global__ __launch_bounds__(256) void k_finalize_residual(
     for (int64_t idx = tid; idx < cn; idx += stride) v[3] += (tabs(cx[idx]) > thr) ? 1.0 : 0.0;
   const bool last = grid_reduce<4, 0u>(v, red);
   if (last && fh != nullptr && threadIdx.x == 0) *fh = 0.5 * red.out[0] + fh_mu * (*fh_rn);
+  // snapshot of the preceding trial's sums for a packet published after the next trial has
+  // overwritten them (the A@X-carried packet of the multi-GPU path)
+  if (last && (int)threadIdx.x < nsnap) snap_dst[threadIdx.x] = snap_src[threadIdx.x];
 }
 
 template <typename T>
@@ -471,7 +475,8 @@ template <typename T>
 void launch_finalize_residual(const T* P, int S, const T* B, int nsrc, T* const* R, int64_t ml,
                               const int* gate, int epoch, int gate_mode, const T* cx, int64_t cn,
                               const double* cmax, double* fh, double fh_mu, const double* fh_rn,
-                              Red red, hipStream_t st) {
+                              Red red, hipStream_t st, const double* snap_src, double* snap_dst,
+                              int nsnap) {
   const int G = finalize_groups(S);
   if (G > 8) throw Error{GLX_E_INVALID, "finalize: more than 64 K-split slabs"};
   const int64_t work = ml * G > cn ? ml * G : cn;
@@ -481,7 +486,7 @@ void launch_finalize_residual(const T* P, int S, const T* B, int nsrc, T* const*
   auto go = [&](auto ns, auto g) {
     hipLaunchKernelGGL((k_finalize_residual<T, decltype(ns)::value, decltype(g)::value>), grid,
                        dim3(256), 0, st, P, S, B, R[0], r1, r2, ml, gate, epoch, gate_mode, cx, cn,
-                       cmax, fh, fh_mu, fh_rn, red);
+                       cmax, fh, fh_mu, fh_rn, red, snap_src, snap_dst, nsnap);
   };
   auto by_g = [&](auto ns) {
     if (G == 1) go(ns, std::integral_constant<int, 1>{});
@@ -594,7 +599,8 @@ void launch_publish(const double* s, int ns, double* host, unsigned* host_seq, u
 #define GLX_INST(T)                                                                                  \
   template void launch_finalize_residual<T>(const T*, int, const T*, int, T* const*, int64_t,       \
                                             const int*, int, int, const T*, int64_t, const double*, \
-                                            double*, double, const double*, Red, hipStream_t);      \
+                                            double*, double, const double*, Red, hipStream_t,       \
+                                            const double*, double*, int);                           \
   template void launch_sum_partials<T>(const T*, int, T*, int64_t, hipStream_t);                    \
   template void launch_prox_pgd<T>(const T*, const T*, int, T*, T*, T*, T*, int64_t, int64_t,       \
                                    double, double, double, Red, hipStream_t, Pub);                  \

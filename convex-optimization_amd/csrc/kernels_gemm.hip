@@ -95,8 +95,8 @@ __device__ inline typename MF<T>::vec_t load_vec(const T* p) {
 // given to XCD group s (S | 8: 8/S XCDs per split; 8 | S: S/8 splits per XCD). Each XCD's L2
 // then holds only its own slice of X instead of all of it. Placement is a speed matter only:
 // any other placement computes the same result.
-__device__ inline bool ax_block(int xmap, int gx, int S, int& bx, int& by) {
-  const int lin = blockIdx.x;
+__device__ inline bool ax_block(int xmap, int gx, int S, int& bx, int& by, int shift = 0) {
+  const int lin = (int)blockIdx.x - shift;   // shift 1: workgroup 0 carries the scalar packet
   if (xmap) {
     const int xcd = lin & 7, slot = lin >> 3;
     if (S <= 8) {
@@ -297,7 +297,8 @@ __global__ __launch_bounds__(64 * WAVES) void k_ax_lds(const T* __restrict__ A,
                                                       const T* __restrict__ X2,
                                                       T* __restrict__ P, int64_t m, int64_t n,
                                                       int64_t chunks, int S, int gx, int xmap,
-                                                      const int* __restrict__ gate, int epoch) {
+                                                      const int* __restrict__ gate, int epoch,
+                                                      Pub pub) {
   typedef MF<T> M;
   typedef typename M::vec_t V;
   typedef typename M::acc_t C;
@@ -316,9 +317,18 @@ __global__ __launch_bounds__(64 * WAVES) void k_ax_lds(const T* __restrict__ A,
   constexpr int VPR = L / E;              // vectors per X row
   static_assert(PF >= 2, "X(c+1) must sit in another ring slot than X(c + PF)");
   __shared__ __attribute__((aligned(16))) T xs[2][XCH];
+  // pub.host: workgroup 0 hands the scalar packet to the host (no reduction to join here) while
+  // the others run; with a short kernel in front (the N > 1 trial) a packet carried by THAT
+  // kernel held up this launch by ~4 us (profiles/r1_tuning/small_kernels/ax_publisher.log)
+  if (pub.host != nullptr && blockIdx.x == 0) {
+    if (threadIdx.x == 0)
+      publish_packet(pub.s, pub.ns, pub.host, pub.host_seq, pub.seq, pub.s2, pub.off2, pub.n2,
+                     pub.s3, pub.off3, pub.n3);
+    return;
+  }
   if (!gate_live(gate, epoch)) return;
   int bx, by;
-  if (!ax_block(xmap, gx, S, bx, by)) return;
+  if (!ax_block(xmap, gx, S, bx, by, pub.host != nullptr ? 1 : 0)) return;
 
   const int lane = threadIdx.x & 63;
   const int wave = threadIdx.x >> 6;
@@ -1566,14 +1576,15 @@ static void ax_mfma_go(const GemmPlan& p, const T* A, const T* const* X, T* P, c
 
 template <typename T, int NT, int NSRC, int MT, int PF, int VPL, int WAVES>
 static void ax_lds_go(const GemmPlan& p, int S, const T* A, const T* const* X, T* P,
-                      const int* gate, int epoch, hipStream_t st) {
+                      const int* gate, int epoch, hipStream_t st, Pub pub = Pub{}) {
   constexpr int E = 16 / sizeof(T);
   const int gx = (int)cdiv(p.m, 16 * MT * WAVES);
   const int xmap = (p.ax_xmap && ax_xmap_ok(S)) ? 1 : 0;
   static const size_t pad = lds_pad(k_ax_lds<T, MT, NT, NSRC, PF, VPL, WAVES>, "GLX_AX_LDS_PAD");
-  hipLaunchKernelGGL((k_ax_lds<T, MT, NT, NSRC, PF, VPL, WAVES>), dim3((unsigned)ax_grid(xmap, gx, S)),
+  hipLaunchKernelGGL((k_ax_lds<T, MT, NT, NSRC, PF, VPL, WAVES>),
+                     dim3((unsigned)ax_grid(xmap, gx, S) + (pub.host ? 1u : 0u)),
                      dim3(64 * WAVES), pad, st, A, X[0], X[1], X[2], P, p.m, p.n,
-                     p.n / (4 * VPL * E), S, gx, xmap, gate, epoch);
+                     p.n / (4 * VPL * E), S, gx, xmap, gate, epoch, pub);
 }
 
 template <typename T, int NT, int NSRC, int MT, int PF, int VPL, int WAVES, int BAR>
@@ -1601,7 +1612,9 @@ static void ax_lds2_go(const GemmPlan& p, int S, const T* A, const T* const* X, 
 // kind 5 codes: 5 MT PF VPL WAVES; kind 6 (pipelined X): 6 MT PF VPL WAVES
 template <typename T, int NT, int NSRC>
 static void ax_lds_code(const GemmPlan& p, int code, int S, const T* A, const T* const* X, T* P,
-                        const int* gate, int epoch, hipStream_t st) {
+                        const int* gate, int epoch, hipStream_t st, Pub pub) {
+  if (pub.host != nullptr && code / 10000 != 5)
+    throw Error{GLX_E_INVALID, "A@X: only the kind-5 LDS tile carries the scalar packet"};
   switch (code) {
     case 62428: ax_lds2_go<T, NT, NSRC, 2, 4, 2, 8>(p, S, A, X, P, gate, epoch, st); return;
     case 62424: ax_lds2_go<T, NT, NSRC, 2, 4, 2, 4>(p, S, A, X, P, gate, epoch, st); return;
@@ -1609,25 +1622,25 @@ static void ax_lds_code(const GemmPlan& p, int code, int S, const T* A, const T*
     case 72428: ax_lds3_go<T, NT, NSRC, 2, 4, 2, 8, 2>(p, S, A, X, P, gate, epoch, st); return;   // barrier / 2
     case 72424: ax_lds3_go<T, NT, NSRC, 2, 4, 2, 4, 2>(p, S, A, X, P, gate, epoch, st); return;
     case 72828: ax_lds3_go<T, NT, NSRC, 2, 8, 2, 8, 4>(p, S, A, X, P, gate, epoch, st); return;   // barrier / 4
-    case 52428: ax_lds_go<T, NT, NSRC, 2, 4, 2, 8>(p, S, A, X, P, gate, epoch, st); return;
+    case 52428: ax_lds_go<T, NT, NSRC, 2, 4, 2, 8>(p, S, A, X, P, gate, epoch, st, pub); return;
     default: break;
   }
   switch (code) {
-    case 52324: ax_lds_go<T, NT, NSRC, 2, 3, 2, 4>(p, S, A, X, P, gate, epoch, st); break;
-    case 54228: ax_lds_go<T, NT, NSRC, 4, 2, 2, 8>(p, S, A, X, P, gate, epoch, st); break;
-    case 54218: ax_lds_go<T, NT, NSRC, 4, 2, 1, 8>(p, S, A, X, P, gate, epoch, st); break;
-    case 52228: ax_lds_go<T, NT, NSRC, 2, 2, 2, 8>(p, S, A, X, P, gate, epoch, st); break;
+    case 52324: ax_lds_go<T, NT, NSRC, 2, 3, 2, 4>(p, S, A, X, P, gate, epoch, st, pub); break;
+    case 54228: ax_lds_go<T, NT, NSRC, 4, 2, 2, 8>(p, S, A, X, P, gate, epoch, st, pub); break;
+    case 54218: ax_lds_go<T, NT, NSRC, 4, 2, 1, 8>(p, S, A, X, P, gate, epoch, st, pub); break;
+    case 52228: ax_lds_go<T, NT, NSRC, 2, 2, 2, 8>(p, S, A, X, P, gate, epoch, st, pub); break;
     // one 16-row tile per wave: twice the row tiles, half the K splits and partial slabs
-    case 51228: ax_lds_go<T, NT, NSRC, 1, 2, 2, 8>(p, S, A, X, P, gate, epoch, st); break;
-    case 51328: ax_lds_go<T, NT, NSRC, 1, 3, 2, 8>(p, S, A, X, P, gate, epoch, st); break;
-    case 51224: ax_lds_go<T, NT, NSRC, 1, 2, 2, 4>(p, S, A, X, P, gate, epoch, st); break;
-    case 52328: ax_lds_go<T, NT, NSRC, 2, 3, 2, 8>(p, S, A, X, P, gate, epoch, st); break;
-    case 52218: ax_lds_go<T, NT, NSRC, 2, 2, 1, 8>(p, S, A, X, P, gate, epoch, st); break;
-    case 54224: ax_lds_go<T, NT, NSRC, 4, 2, 2, 4>(p, S, A, X, P, gate, epoch, st); break;
-    case 52214: ax_lds_go<T, NT, NSRC, 2, 2, 1, 4>(p, S, A, X, P, gate, epoch, st); break;
-    case 54214: ax_lds_go<T, NT, NSRC, 4, 2, 1, 4>(p, S, A, X, P, gate, epoch, st); break;
+    case 51228: ax_lds_go<T, NT, NSRC, 1, 2, 2, 8>(p, S, A, X, P, gate, epoch, st, pub); break;
+    case 51328: ax_lds_go<T, NT, NSRC, 1, 3, 2, 8>(p, S, A, X, P, gate, epoch, st, pub); break;
+    case 51224: ax_lds_go<T, NT, NSRC, 1, 2, 2, 4>(p, S, A, X, P, gate, epoch, st, pub); break;
+    case 52328: ax_lds_go<T, NT, NSRC, 2, 3, 2, 8>(p, S, A, X, P, gate, epoch, st, pub); break;
+    case 52218: ax_lds_go<T, NT, NSRC, 2, 2, 1, 8>(p, S, A, X, P, gate, epoch, st, pub); break;
+    case 54224: ax_lds_go<T, NT, NSRC, 4, 2, 2, 4>(p, S, A, X, P, gate, epoch, st, pub); break;
+    case 52214: ax_lds_go<T, NT, NSRC, 2, 2, 1, 4>(p, S, A, X, P, gate, epoch, st, pub); break;
+    case 54214: ax_lds_go<T, NT, NSRC, 4, 2, 1, 4>(p, S, A, X, P, gate, epoch, st, pub); break;
     default:   // 52224
-      ax_lds_go<T, NT, NSRC, 2, 2, 2, 4>(p, S, A, X, P, gate, epoch, st);
+      ax_lds_go<T, NT, NSRC, 2, 2, 2, 4>(p, S, A, X, P, gate, epoch, st, pub);
       break;
   }
 }
@@ -1635,14 +1648,15 @@ static void ax_lds_code(const GemmPlan& p, int code, int S, const T* A, const T*
 // One source: the swept variant. Batched sources (2, 3) use fixed register-feasible tiles.
 template <typename T, int NT>
 static void ax_mfma_nt(const GemmPlan& p, int nsrc, const T* A, const T* const* X, T* P,
-                       const int* gate, int epoch, hipStream_t st) {
+                       const int* gate, int epoch, hipStream_t st, Pub pub) {
   const int code = p.axb_code[nsrc];
   if (code / 10000 >= 5 && code / 10000 <= 7) {
-    if (nsrc == 1) ax_lds_code<T, NT, 1>(p, code, p.axb_S[1], A, X, P, gate, epoch, st);
-    else if (nsrc == 2) ax_lds_code<T, NT, 2>(p, code, p.axb_S[2], A, X, P, gate, epoch, st);
-    else ax_lds_code<T, NT, 3>(p, code, p.axb_S[3], A, X, P, gate, epoch, st);
+    if (nsrc == 1) ax_lds_code<T, NT, 1>(p, code, p.axb_S[1], A, X, P, gate, epoch, st, pub);
+    else if (nsrc == 2) ax_lds_code<T, NT, 2>(p, code, p.axb_S[2], A, X, P, gate, epoch, st, pub);
+    else ax_lds_code<T, NT, 3>(p, code, p.axb_S[3], A, X, P, gate, epoch, st, pub);
     return;
   }
+  if (pub.host != nullptr) throw Error{GLX_E_INVALID, "A@X: this tile cannot carry the scalar packet"};
   if (nsrc == 2) {
     switch (code) {
       case 1220: ax_mfma_go<T, NT, 2, 2, 2, false, false>(p, A, X, P, gate, epoch, st); break;
@@ -1695,17 +1709,24 @@ static void ax_mfma_nt(const GemmPlan& p, int nsrc, const T* A, const T* const* 
   }
 }
 
+bool ax_pub_ok(const GemmPlan& p, int nsrc) {
+  return p.ax_kind != 3 && (p.l == 16 || p.l == 32) && nsrc >= 1 && nsrc <= 3 &&
+         p.axb_code[nsrc] / 10000 == 5;
+}
+
 template <typename T>
 void launch_ax(const GemmPlan& p, int nsrc, const T* A, const T* const* X, T* P, const int* gate,
-               int epoch, hipStream_t st) {
+               int epoch, hipStream_t st, Pub pub) {
+  if (pub.host != nullptr && !ax_pub_ok(p, nsrc))
+    throw Error{GLX_E_INVALID, "A@X: this plan cannot carry the scalar packet"};
   if (p.ax_kind == 3) {
     if (nsrc == 1) ax_valu_src<T, 1>(p, A, X, P, gate, epoch, st);
     else if (nsrc == 2) ax_valu_src<T, 2>(p, A, X, P, gate, epoch, st);
     else ax_valu_src<T, 3>(p, A, X, P, gate, epoch, st);
     return;
   }
-  if (p.l == 16) ax_mfma_nt<T, 1>(p, nsrc, A, X, P, gate, epoch, st);
-  else ax_mfma_nt<T, 2>(p, nsrc, A, X, P, gate, epoch, st);
+  if (p.l == 16) ax_mfma_nt<T, 1>(p, nsrc, A, X, P, gate, epoch, st, pub);
+  else ax_mfma_nt<T, 2>(p, nsrc, A, X, P, gate, epoch, st, pub);
 }
 
 template <typename T, int LB>
@@ -1762,8 +1783,8 @@ void launch_atr(const GemmPlan& p, const T* A, const T* R, T* Gp, hipStream_t st
   else atr_mfma_nt<T, 2>(p, A, R, Gp, st);
 }
 
-template void launch_ax<double>(const GemmPlan&, int, const double*, const double* const*, double*, const int*, int, hipStream_t);
-template void launch_ax<float>(const GemmPlan&, int, const float*, const float* const*, float*, const int*, int, hipStream_t);
+template void launch_ax<double>(const GemmPlan&, int, const double*, const double* const*, double*, const int*, int, hipStream_t, Pub);
+template void launch_ax<float>(const GemmPlan&, int, const float*, const float* const*, float*, const int*, int, hipStream_t, Pub);
 bool atr_prox_ok(const GemmPlan& p) {
   return p.atr_kind == 1 && p.atr_wl == 0 && p.atr_S >= 1 && p.atr_S <= 8 &&
          (p.l == 16 || p.l == 32) && p.n % 64 == 0 &&

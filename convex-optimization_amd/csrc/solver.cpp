@@ -52,7 +52,9 @@ enum {
   S_RG = 16,    // standalone residual finalize (FISTA y): [sum r^2, ...]
   S_REGY = 20,  // FGD smooth regulariser at y
   S_DRN = 21,   // row-norm sum written by the SGD/GD step (+1: max)
-  NSCAL = 24
+  NSCAL = 24,   // the host packet copies slots [0, NSCAL)
+  S_SNAP = 24,  // snapshot of S_TR..S_TR+5 taken by a finalize (packet remap, not copied itself)
+  NSCAL_DEV = 32
 };
 
 struct Carver {
@@ -127,7 +129,7 @@ class Session : public SessionBase {
       gp[k] = plan.atr_S > 1 ? static_cast<T*>(c.take(sizeof(T) * nl * plan.atr_S)) : g[k];
     }
     T* pp = static_cast<T*>(c.take(sizeof(T) * ml * ax_split_max(plan) * 3));   // up to 3 batched sources
-    double* scal = static_cast<double*>(c.take(sizeof(double) * NSCAL));
+    double* scal = static_cast<double*>(c.take(sizeof(double) * NSCAL_DEV));
     double* part = static_cast<double*>(c.take(sizeof(double) * kMaxRedVals * kMaxBlocks));
     unsigned* ticket = static_cast<unsigned*>(c.take(kTicketBytes));
     // per-panel arrival counters of the fused A^T R with K splits (atr_split_combine)
@@ -192,6 +194,8 @@ class Session : public SessionBase {
     attach_ok_ = spin_readback_ && !(ap && std::strcmp(ap, "0") == 0);
     const char* sp = std::getenv("GLX_SPEC_GRAD");
     spec_off_env_ = (sp && std::strcmp(sp, "0") == 0);
+    const char* sa = std::getenv("GLX_SPEC_AX_PUB");
+    spec_ax_pub_ = !(sa && std::strcmp(sa, "0") == 0);
     const char* fz = std::getenv("GLX_FUSED_TRIAL");
     // With a communicator the trial cannot live in the A^T r epilogue (the gradient is summed
     // over ranks first): it runs as A^T r, all-reduce, then k_prox_pgd / k_fista_trial, and is
@@ -204,7 +208,7 @@ class Session : public SessionBase {
     GLX_HIP(hipMemsetAsync(ticket_, 0, kTicketBytes, st_));
     GLX_HIP(hipMemsetAsync(pcnt_, 0, sizeof(unsigned) * (P.n / 64 + 64), st_));
     GLX_HIP(hipMemsetAsync(flag_, 0, 256, st_));
-    GLX_HIP(hipMemsetAsync(scal_, 0, sizeof(double) * NSCAL, st_));
+    GLX_HIP(hipMemsetAsync(scal_, 0, sizeof(double) * NSCAL_DEV, st_));
     mus_[0] = 100 * P.mu0;
     mus_[1] = 10 * P.mu0;
     mus_[2] = P.mu0;
@@ -282,6 +286,7 @@ class Session : public SessionBase {
     y_ready_ = false;
     spec_ready_ = false;
     spec_trial_ready_ = false;
+    ax_queued_ = false;
   }
 
   void counters(int64_t out[4]) const override {
@@ -358,18 +363,18 @@ class Session : public SessionBase {
   // defer != NULL (communicator, f64): the sums go to `defer` (a gradient set's tail) instead
   // of scal[slot..], are NOT all-reduced here and nothing is published — they ride the next
   // gradient all-reduce and publish (atr_prox / atr_fista), saving one all-reduce per iteration.
+  // skip_ax: the slabs are already in Pp_ (queued speculatively with the trial, spec_ax);
+  // only the finalize runs.
   void residuals(int nsrc, const T* const* xs, T* const* rs, int slot, const T* cx = nullptr,
                  const double* cmax = nullptr, double* fh = nullptr, double fh_mu = 0.0,
-                 unsigned* pub_seq = nullptr, double* defer = nullptr) {
-    hipEvent_t e0 = prof_begin(0);
-    launch_ax<T>(plan_, nsrc, A_, xs, Pp_, nullptr, 0, st_);
-    check_launch();
-    prof_end(0, e0);
-    ++ax_calls_;
-    ax_cols_ += nsrc;
+                 unsigned* pub_seq = nullptr, double* defer = nullptr, bool skip_ax = false,
+                 bool snap_trial = false) {
+    if (!skip_ax) spec_ax(nsrc, xs);
     launch_finalize_residual<T>(Pp_, ax_split(plan_, nsrc), B_, nsrc, rs, ml_, nullptr, 0, 1, cx,
                                 cx ? nl_ : 0, cmax, comm_ ? nullptr : fh, fh_mu, scal_ + S_DRN,
-                                defer ? Red{part_, ticket_, defer} : red(slot), st_);
+                                defer ? Red{part_, ticket_, defer} : red(slot), st_,
+                                snap_trial ? scal_ + S_TR : nullptr,
+                                snap_trial ? scal_ + S_SNAP : nullptr, snap_trial ? 6 : 0);
     check_launch();
     if (defer) return;
     if (comm_) {
@@ -380,6 +385,15 @@ class Session : public SessionBase {
       }
     }
     if (pub_seq != nullptr) *pub_seq = post_readback();
+  }
+  // A @ [xs] into the slabs Pp_; pb: the launch also carries that scalar packet (ax_pub_ok)
+  void spec_ax(int nsrc, const T* const* xs, Pub pb = Pub{}) {
+    hipEvent_t e0 = prof_begin(0);
+    launch_ax<T>(plan_, nsrc, A_, xs, Pp_, nullptr, 0, st_, pb);
+    check_launch();
+    prof_end(0, e0);
+    ++ax_calls_;
+    ax_cols_ += nsrc;
   }
   void residual1(const T* x, T* r, int slot, const T* cx = nullptr, const double* cmax = nullptr,
                  unsigned* pub_seq = nullptr) {
@@ -551,6 +565,7 @@ class Session : public SessionBase {
   void proxgd_prologue(bool have_thr) {
     spec_ready_ = false;   // the gradient is recomputed from the rebuilt residual
     spec_trial_ready_ = false;
+    ax_queued_ = false;
     if (!have_thr) {
       launch_threshold<T>(X_[ix_], X_[ixt_], nl_, O_.thres, flag_, ++epoch_, st_);
       check_launch();
@@ -585,6 +600,7 @@ class Session : public SessionBase {
       use_gset(spec_set_);
       g = {G_, 1};
       first_done = (spec_trial_mu_ == mu_ && spec_trial_t_ == t0);   // else: a phase change
+      if (!first_done) ax_queued_ = false;
     } else if (fused_ok_) {
       atr_prox(R_[irg_], gset_, X_[ixt_], ip_, ipt_, iz_, t0);
       g = {G_, 1};
@@ -617,15 +633,31 @@ class Session : public SessionBase {
         const bool merge = spec && fused_ok_ && merge_tail();
         // the packet rides the speculative kernel (no communicator; with one only when merged)
         const bool late_pub = merge || (spec && fused_ok_ && attach_ok_ && comm_ == nullptr);
+        const bool skip_ax = it == 0 && first_done && ax_queued_;   // queued with the trial
+        ax_queued_ = false;
+        // with a communicator the speculative next trial is a short k_prox_pgd: its A@X is
+        // queued right behind it and carries this trial's packet, whose trial sums (which
+        // that k_prox_pgd overwrites) come from a snapshot this finalize takes
+        const bool axp = spec && fused_ok_ && comm_ != nullptr && late_pub && attach_ok_ &&
+                         spec_ax_pub_ && ax_pub_ok(plan_, nsrc);
         residuals(nsrc, xs, rs, S_RT, X_[ip_], scal_ + S_TR + 3, nullptr, 0.0,
-                  late_pub ? nullptr : &seq, merge ? tail(1 - gset_) : nullptr);
+                  late_pub ? nullptr : &seq, merge ? tail(1 - gset_) : nullptr, skip_ax, axp);
         std::pair<const T*, int> sg;
         if (spec && fused_ok_) {
           // the next iteration's A^T r and first trial at the candidate p_thr, into the other
           // gradient set and the spare buffers (z is free once this trial's A@X has read it)
+          Pub pbx;
           atr_prox(R_[rpt], 1 - gset_, X_[ipt_], if1_, if2_, iz_, O_.alpha0, merge ? nsrc : 0,
-                   late_pub ? &seq : nullptr);
+                   late_pub ? &seq : nullptr, axp ? &pbx : nullptr);
           spec_trial = true;
+          if (axp) {
+            pbx.s3 = scal_ + S_SNAP;
+            pbx.off3 = S_TR;
+            pbx.n3 = 6;
+            const T* sx[3] = {X_[iz_], X_[if2_], X_[if1_]};   // [z | p_thr | p] of that trial
+            spec_ax(nsrc, sx, pbx);
+            ax_queued_ = true;
+          }
         } else if (spec) {
           sg = gradient(R_[rpt], 1 - gset_);   // gradient at the candidate p_thr
         }
@@ -639,6 +671,7 @@ class Session : public SessionBase {
         }
         spec_trial = false;
         spec_on_ = false;
+        ax_queued_ = false;   // the speculated trial and its A@X are dropped
         t *= O_.ls_coeff;
       }
       // after ls_maxit failures the reference returns alpha0*coeff^maxit untested (:99)
@@ -682,13 +715,16 @@ class Session : public SessionBase {
   // With a communicator: A^T r, the all-reduce (also summing tail_n deferred residual sums of
   // the set's tail), the scalar packet if pub_seq (so the host reads those sums while the trial
   // runs), then k_prox_pgd — the same arithmetic as the fused epilogue.
+  // pub_out (communicator): the packet is returned for the caller's next launch to carry
+  // instead of riding k_prox_pgd.
   void atr_prox(const T* r, int set, const T* x, int op, int opt, int oz, double t, int tail_n = 0,
-                unsigned* pub_seq = nullptr) {
+                unsigned* pub_seq = nullptr, Pub* pub_out = nullptr) {
     const double* extra = tail_n ? tail(set) : nullptr;
     if (comm_) {
       const std::pair<const T*, int> g = gradient(r, set, tail_n);
       Pub pb;
-      if (pub_seq && attach_ok_) pb = make_pub(extra, pub_seq);
+      if (pub_seq && pub_out) *pub_out = make_pub(extra, pub_seq);
+      else if (pub_seq && attach_ok_) pb = make_pub(extra, pub_seq);
       else if (pub_seq) *pub_seq = post_readback(extra);
       launch_prox_pgd<T>(x, g.first, g.second, nullptr, X_[op], X_[opt], X_[oz], n_, l_, t, mu_,
                          O_.thres, red(S_TR), st_, pb);
@@ -928,6 +964,8 @@ class Session : public SessionBase {
   hipStream_t st_;
   GemmPlan plan_{};
   glx_comm* comm_ = nullptr;
+  bool ax_queued_ = false;     // the pending first trial's A@X is already queued (spec_ax)
+  bool spec_ax_pub_ = true;    // GLX_SPEC_AX_PUB=0: the packet rides k_prox_pgd instead
   int64_t m_ = 0, n_ = 0, l_ = 0, nl_ = 0, ml_ = 0;
   const T* A_ = nullptr;
   const T* B_ = nullptr;
