@@ -99,6 +99,31 @@ static void validate(const glx_problem* P, const glx_opts* O) {
 }
 
 // ------------------------------------------------------------------------------------------
+// The solver's plan: the shape's GEMM plan, plus one method-level choice. fp32 ProxGD/FProxGD
+// on one GPU take the 4-wave panel AᵀR with 2 K splits (code 1104) instead of the 4-panel
+// tile (1114), so that the line-search trial fuses into it (atr_split_combine): the AᵀR pass
+// is ≈13 µs slower but the trial launch and its boundary go. Same box: C3 (8192,16384,32)
+// FProxGD 3669–3691 → 3743–3749 it/s, ProxGD 3654–3657 → 3744–3752, FProxGD at (4096,8192,16)
+// 11 362–11 366 → 13 200–13 215 (profiles/r1_tuning/small_kernels/atr_f32_fused.log).
+static GemmPlan session_plan(const glx_problem& P, const glx_opts& O) {
+  const int es = P.dtype == GLX_F64 ? 8 : 4;
+  GemmPlan p = make_plan(es, P.m, P.n, P.l, O.ax_variant);
+  const bool trial_method = (P.method == GLX_PROXGD || P.method == GLX_FPROXGD) &&
+                            (O.step_type == GLX_STEP_LINE_SEARCH || O.step_type == GLX_STEP_FIXED);
+  if (es == 4 && P.comm == nullptr && trial_method && p.atr_kind == 1 &&
+      (P.l == 16 || P.l == 32) && P.n % 64 == 0 && P.m >= 128 && (P.n / 64) * 2 < kMaxBlocks &&
+      !std::getenv("GLX_ATR_VARIANT") && !std::getenv("GLX_ATR_S") &&
+      !std::getenv("GLX_FUSED_TRIAL")) {
+    GemmPlan f = p;
+    f.atr_wl = 0;
+    f.atr_ntl = 1;
+    f.atr_pf = 4;
+    f.atr_S = 2;
+    if (atr_prox_ok(f)) return f;   // only where the trial actually fuses (GLX_ATR_FUSE_SPLIT)
+  }
+  return p;
+}
+
 class SessionBase {
  public:
   virtual ~SessionBase() {}
@@ -170,7 +195,7 @@ class Session : public SessionBase {
       : P_(P), O_(O), st_(st) {
     m_ = P.m; n_ = P.n; l_ = P.l;
     nl_ = n_ * l_; ml_ = m_ * l_;
-    plan_ = make_plan(sizeof(T), m_, n_, l_, O.ax_variant);
+    plan_ = session_plan(P, O);
     comm_ = static_cast<glx_comm*>(P.comm);
     fh_cap_ = fh_capacity(P, O);
     const size_t need = carve(P, plan_, fh_cap_, nullptr, nullptr);
@@ -1023,8 +1048,7 @@ class Session : public SessionBase {
 };
 
 static size_t session_bytes(const glx_problem& P, const glx_opts& O) {
-  const int es = P.dtype == GLX_F64 ? 8 : 4;
-  const GemmPlan plan = make_plan(es, P.m, P.n, P.l, O.ax_variant);
+  const GemmPlan plan = session_plan(P, O);
   if (P.dtype == GLX_F64)
     return Session<double>::carve(P, plan, Session<double>::fh_capacity(P, O), nullptr, nullptr);
   return Session<float>::carve(P, plan, Session<float>::fh_capacity(P, O), nullptr, nullptr);
