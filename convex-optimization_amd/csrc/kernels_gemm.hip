@@ -1017,7 +1017,7 @@ __global__ __launch_bounds__(256) void k_atr_mfma(const T* __restrict__ A, const
 // wave writes its rows of G and runs the trial on them (prox_pgd_row, the same arithmetic as
 // k_prox_pgd) with x = the thresholded iterate; the six trial sums are reduced over the grid.
 template <typename T, int NT, int PF, bool NTL, bool SPLIT>
-__global__ __launch_bounds__(256) void k_atr_prox(const T* __restrict__ A, const T* __restrict__ R,
+__global__ __launch_bounds__(256, sizeof(T) == 8 ? 2 : 1) void k_atr_prox(const T* __restrict__ A, const T* __restrict__ R,
                                                   T* __restrict__ G, int64_t m, int64_t n,
                                                   const T* __restrict__ x, T* __restrict__ p,
                                                   T* __restrict__ pthr, T* __restrict__ z,
@@ -1079,7 +1079,7 @@ __global__ __launch_bounds__(256) void k_atr_prox(const T* __restrict__ A, const
 // fista_row (the arithmetic of k_fista_trial) on its 16 gradient rows, with y the extrapolated
 // point and xk the current iterate; writes G, xc, v_next, y_next and reduces the four sums.
 template <typename T, int NT, int PF, bool NTL, bool SPLIT>
-__global__ __launch_bounds__(256) void k_atr_fista(const T* __restrict__ A, const T* __restrict__ R,
+__global__ __launch_bounds__(256, sizeof(T) == 8 ? 2 : 1) void k_atr_fista(const T* __restrict__ A, const T* __restrict__ R,
                                                    T* __restrict__ G, int64_t m, int64_t n,
                                                    const T* __restrict__ y, const T* __restrict__ xk,
                                                    T* __restrict__ xc, T* __restrict__ vnext,
