@@ -5,9 +5,20 @@
 
 One step = one recorded iteration of the solver (objective, stop rule, threshold, A^T(Ax-b),
 line search, prox) on one synthetic instance whose A, b, x live in HBM before timing starts.
-N > 1 (launched by torch.distributed.run, one process per GPU): A and b are row-sharded, the
-gradient is summed with RCCL, and the same global problem is solved (strong scaling); the
-reported value is iterations/s of the whole job (max of the per-rank times).
+N > 1 (one process per GPU): A and b are row-sharded, the gradient is summed with RCCL, and
+the same global problem is solved (strong scaling); the reported value is iterations/s of the
+whole job (max of the per-rank times). Launched either by torch.distributed.run (RANK /
+WORLD_SIZE set), or as plain `python bench.py --gpus N`: then this process touches no GPU, starts
+`torch.distributed.run --nproc-per-node N` on itself as a child and exits with its code (rank 0
+prints the JSON line). Fewer than N visible devices, or a launcher world size that differs
+from --gpus, is an error (exit 2), never a silent one-rank measurement.
+
+Pre-warm (outside the timed region, declared in the line as `prewarm`): before the W warmup
+steps every rank runs a throwaway solver session on the same instance for --prewarm-s seconds
+(default 0.5). After ~1 s idle the MI355X's power management lets the first ~2 ms of fp64 MFMA
+load run fast, then throttles (A@X 290 -> 400+ us) and recovers over ~30 ms
+(profiles/r2_power_probe.jsonl); a 20-step run would otherwise time that transient, not the
+solver. The timed session restarts from x0, so the iterations timed are the same ones.
 
 Also reported, for the dominant kernel (A@x with its batched right-hand sides, ~55-60% of the
 iteration):
@@ -114,15 +125,53 @@ def ax_kernel_name(dtype, m, n, l, nsrc):
     return desc
 
 
+PMC_FILE = "profiles/pmc_traffic.json"
+
+
 def pmc_traffic(cfg_key):
-    path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    """(bytes per A@X launch, source) from the committed rocprofv3 PMC summary of a separate run
+    of this same configuration (FETCH_SIZE / WRITE_SIZE passes cannot share the timed run);
+    (None, None) when that file holds no entry for this configuration."""
     try:
-        with open(path) as fh:
+        with open(os.path.join(ROOT, PMC_FILE)) as fh:
             d = json.load(fh)
         e = d.get(cfg_key)
-        return None if e is None else float(e["bytes_per_launch"])
+        if e is None:
+            return None, None
+        return float(e["bytes_per_launch"]), "%s[%s] (%s)" % (PMC_FILE, cfg_key, e.get("source", "committed PMC run"))
     except Exception:
-        return None
+        return None, None
+
+
+def launch_ranks(args):
+    """`bench.py --gpus N` without a launcher: run torch.distributed.run with N processes on this
+    script (one rank per GPU) as a CHILD process and return its exit code. Called before any GPU
+    call; torch.cuda.device_count() does not initialise the GPU."""
+    import socket
+    import subprocess
+    visible = torch.cuda.device_count()
+    with socket.socket() as sk:          # a free rendezvous port on the loopback interface
+        sk.bind(("127.0.0.1", 0))
+        port = sk.getsockname()[1]
+    argv = [a for a in sys.argv[1:] if a != "--dry-run-launch"]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+           "--nproc-per-node", str(args.gpus), "--master-addr", "127.0.0.1",
+           "--master-port", str(port), os.path.abspath(__file__)] + argv
+    ok = visible >= args.gpus or args.comm == "host"
+    if args.dry_run_launch:
+        print(json.dumps({"launch": cmd, "nproc": args.gpus, "visible_devices": visible, "ok": ok}))
+        return 0
+    if not ok:
+        log("error: --gpus %d but only %d GPU(s) visible; refusing to measure fewer ranks" %
+            (args.gpus, visible))
+        return 2
+    log("launching %d ranks: %s" % (args.gpus, " ".join(cmd)))
+    return subprocess.call(cmd)
+
+
+def glx_env():
+    """Every GLX_* knob set in the environment (empty at the measured defaults)."""
+    return {k: v for k, v in sorted(os.environ.items()) if k.startswith("GLX_")}
 
 
 def main():
@@ -137,8 +186,13 @@ def main():
     ap.add_argument("--l", type=int, default=32)
     ap.add_argument("--variant", type=int, default=0)
     ap.add_argument("--exact", type=int, default=0)
-    ap.add_argument("--profile", type=int, default=16,
-                    help="HIP events around every k-th A@x / A^T r launch (0 = off)")
+    ap.add_argument("--profile", type=int, default=None,
+                    help="HIP events around every k-th A@x / A^T r launch (0 = off; default: "
+                         "min(16, steps // 8), so at least 8 launches of each are timed)")
+    ap.add_argument("--prewarm-s", type=float, default=0.5,
+                    help="seconds of a throwaway solver session before the warmup (0 = off)")
+    ap.add_argument("--dry-run-launch", action="store_true",
+                    help="print the launcher decision (child command, visible devices) and exit")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--force-comm", action="store_true",
                     help="create the communicator even at world size 1 (runs the N-GPU code path "
@@ -148,14 +202,22 @@ def main():
                          "cuda:0, all-reduces staged through gloo — a one-GPU rehearsal, not a "
                          "performance number)")
     args = ap.parse_args()
+    if args.profile is None:
+        args.profile = max(1, min(16, args.steps // 8))
 
+    if "WORLD_SIZE" not in os.environ and (args.gpus > 1 or args.dry_run_launch):
+        sys.exit(launch_ranks(args))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
-        log("note: WORLD_SIZE=%d, --gpus=%d; using WORLD_SIZE" % (world, args.gpus))
+        log("error: the launcher started WORLD_SIZE=%d ranks but --gpus=%d" % (world, args.gpus))
+        sys.exit(2)
     if args.comm == "host":
         local = 0
+    elif local >= torch.cuda.device_count():
+        log("error: LOCAL_RANK %d but only %d GPU(s) visible" % (local, torch.cuda.device_count()))
+        sys.exit(2)
     torch.cuda.set_device(local)
     device = torch.device("cuda", local)
 
@@ -183,6 +245,24 @@ def main():
     total = args.warmup + args.steps
     opts = {"alpha0": alpha0, "maxit": max(total + 1, 2500), "max_total_iters": total,
             "profile": args.profile, "ax_variant": args.variant, "exact_objective": args.exact}
+    prewarm = None
+    if args.prewarm_s > 0:
+        prewarm = {"seconds": args.prewarm_s, "iters": 0,
+                   "what": "throwaway session of the same solver on the same instance before the "
+                           "warmup; the timed session restarts from x0"}
+        xw = x0.clone()
+        pw = glx.Session(args.method, xw, A, b, mu, dict(opts, profile=0, max_total_iters=0),
+                         comm=comm)
+        t_pw = time.perf_counter()
+        while time.perf_counter() - t_pw < args.prewarm_s:
+            got = pw.run(16)
+            prewarm["iters"] += got
+            if pw.finished or got == 0:
+                break
+        pw.close()
+        del pw, xw
+        torch.cuda.synchronize()
+        prewarm["seconds"] = round(time.perf_counter() - t_pw, 3)
     x = x0.clone()
     s = glx.Session(args.method, x, A, b, mu, opts, comm=comm)
     s.run(args.warmup)
@@ -229,13 +309,17 @@ def main():
         ax_tf = ax_flops / ax_avg_s / 1e12 if ax_n else None
         ax_gbs = ax_bytes / ax_avg_s / 1e9 if ax_n else None
         pair_tf = ((ax_flops + atr_flops) / (ax_avg_s + atr_avg_s) / 1e12) if (ax_n and atr_n) else None
+        # SURVEY §8d's literal pair: one A@x (l right-hand sides) + one A^T r = 4 m n l flops over
+        # the same two launches (the batched second right-hand side is not counted)
+        pair4_tf = ((4.0 * ml * n * l) / (ax_avg_s + atr_avg_s) / 1e12) if (ax_n and atr_n) else None
+        traffic, traffic_src = pmc_traffic(cfg_key)
         if mfma_bound:
             ach, peak, unit = ax_tf, peak_tf, "TFLOP/s"
         else:
             ach, peak, unit = ax_gbs, HBM_PEAK_GBS, "GB/s"
         roof = {"bound": "mfma" if mfma_bound else "hbm", "achieved": ach, "peak": peak,
                 "unit": unit, "frac": (ach / peak) if ach else None,
-                "traffic": pmc_traffic(cfg_key),
+                "traffic": traffic, "traffic_source": traffic_src,
                 "kernel": ("k_gemv_pair_fused: A@[x|thr(x)] and A^T r in ONE pass over A (l = 1)"
                            if work["atr_calls"] == 0 else ax_kernel_name(args.dtype, ml, n, l, nsrc)),
                 "flops_per_launch": ax_flops,
@@ -247,6 +331,12 @@ def main():
                 "atr_GBs": atr_bytes / atr_avg_s / 1e9 if atr_n else None,
                 "atr_mfma_frac": (atr_flops / atr_avg_s / 1e12) / peak_tf if atr_n else None,
                 "pair_tflops": pair_tf, "pair_frac": pair_tf / peak_tf if pair_tf else None,
+                "pair_definition": "pair_frac: executed MFMA flops of the A@X launch (2 m n l per "
+                                   "right-hand side, all of which the reference also computes) + "
+                                   "A^T r (2 m n l), over the two launches' time; the north-star "
+                                   "60 % target is read on this one. pair4_frac: SURVEY §8d's "
+                                   "literal 4 m n l over the same time",
+                "pair4_tflops": pair4_tf, "pair4_frac": pair4_tf / peak_tf if pair4_tf else None,
                 # all MFMA flops issued in the timed region / its wall time (gaps, prox included)
                 "iter_frac": (2.0 * ml * n * l * work["ax_sources"] + work["atr_calls"] * atr_flops)
                              / elapsed / 1e12 / peak_tf}
@@ -265,6 +355,8 @@ def main():
                                        if world > 1 else "single GPU",
                        "exact_objective": args.exact, "ax_variant": args.variant},
             "roofline": roof,
+            "prewarm": prewarm,
+            "env": glx_env(),
             "work": {"ax_per_iter": work["ax_calls"] / steps, "atr_per_iter": work["atr_calls"] / steps,
                      "passes_over_A_per_iter": (work["ax_calls"] + work["atr_calls"]) / steps,
                      "syncs_per_iter": work["syncs"] / steps,

@@ -54,6 +54,7 @@ enum {
   S_DRN = 21,   // row-norm sum written by the SGD/GD step (+1: max)
   NSCAL = 24,   // the host packet copies slots [0, NSCAL)
   S_SNAP = 24,  // snapshot of S_TR..S_TR+5 taken by a finalize (packet remap, not copied itself)
+  S_SPX = 30,   // SGD/GD log sparsity every 100 iterations: [sum ||x_i||, max |x|] of the new x
   NSCAL_DEV = 32
 };
 
@@ -131,6 +132,7 @@ class SessionBase {
   virtual void finish(glx_result* res) = 0;
   virtual void kernel_time(int kind, int64_t* launches, double* ms) = 0;
   virtual void counters(int64_t out[4]) const = 0;
+  virtual void trace(double* sp_after, int64_t cap, int64_t* n, int64_t phase_info[6]) const = 0;
 };
 
 template <typename T>
@@ -161,6 +163,7 @@ class Session : public SessionBase {
     unsigned* pcnt = static_cast<unsigned*>(c.take(sizeof(unsigned) * (P.n / 64 + 64)));
     int* flag = static_cast<int*>(c.take(256));
     double* fh = static_cast<double*>(c.take(sizeof(double) * (fh_cap + 1)));
+    double* sp100 = static_cast<double*>(c.take(sizeof(double) * (fh_cap / 100 + 2)));
     const int gb = gemv_blocks_for(P);
     T* gs = gb > 0 ? static_cast<T*>(c.take(sizeof(T) * nl * gb)) : nullptr;   // fused l = 1 slabs
     if (s) {
@@ -170,6 +173,7 @@ class Session : public SessionBase {
       s->G_ = g[0]; s->Gp_ = gp[0]; s->Pp_ = pp;
       s->scal_ = scal; s->part_ = part; s->ticket_ = ticket; s->flag_ = flag; s->fh_dev_ = fh;
       s->pcnt_ = pcnt;
+      s->sp100_ = sp100;
       s->gemv_slabs_ = gs;
       s->gemv_blocks_ = gb;
     }
@@ -244,6 +248,7 @@ class Session : public SessionBase {
     use_sparsity_ = (method_ == GLX_PROXGD || method_ == GLX_FPROXGD || method_ == GLX_FGD);
     device_hist_ = (method_ == GLX_SGD || method_ == GLX_GD);
     if (method_ == GLX_FPROXGD || method_ == GLX_FGD) copy_x(iv_, ix_);  // v_k = copy(x_k)
+    phase_start_[0] = 0;
   }
 
   ~Session() override {
@@ -281,12 +286,27 @@ class Session : public SessionBase {
     const double mu_obj = (method_ == GLX_SGD) ? mu_ : P_.mu0;
     objective_of(X_[ix_]);
     res->fval = 0.5 * hs_[S_RO] + mu_obj * hs_[S_XRN];
+    const double final_sp = hs_[S_RO + 3] / (double)nl_;   // count(x) when use_sparsity_
     if (ix_ != 0) copy_buf(X_[0], X_[ix_]);
     if (device_hist_ && k_ > 0) {
       fh_.resize(k_);
       GLX_HIP(hipMemcpyAsync(fh_.data(), fh_dev_, sizeof(double) * k_, hipMemcpyDeviceToHost, st_));
     }
+    std::vector<double> sp100;
+    if (device_hist_ && k_ >= 100) {
+      sp100.resize(k_ / 100 + 1);
+      GLX_HIP(hipMemcpyAsync(sp100.data(), sp100_, sizeof(double) * sp100.size(), hipMemcpyDeviceToHost, st_));
+    }
     GLX_HIP(hipStreamSynchronize(st_));
+    // sparsity of the iterate after iteration i's update (the reference's 100-iteration debug
+    // line, gl_ProxGD_primal.py:134-136): the next recorded sparsity, the returned x's for the
+    // last one; SGD/GD record it on the device at every 100th iteration only (NaN elsewhere)
+    trace_sp_.assign(k_, NAN);
+    for (int64_t i = 0; i < k_; ++i) {
+      if (use_sparsity_) trace_sp_[i] = (i + 1 < (int64_t)sp_hist_.size()) ? sp_hist_[i + 1] : final_sp;
+      else if ((i + 1) % 100 == 0 && (size_t)((i + 1) / 100) < sp100.size())
+        trace_sp_[i] = sp100[(i + 1) / 100] / (double)nl_;
+    }
     if (device_hist_) {
       fhb_.resize(fh_.size());
       double best = INFINITY;
@@ -312,6 +332,14 @@ class Session : public SessionBase {
     spec_ready_ = false;
     spec_trial_ready_ = false;
     ax_queued_ = false;
+  }
+
+  void trace(double* sp_after, int64_t cap, int64_t* n, int64_t phase_info[6]) const override {
+    const int64_t cnt = std::min<int64_t>(cap, (int64_t)trace_sp_.size());
+    if (sp_after && cnt > 0) std::memcpy(sp_after, trace_sp_.data(), sizeof(double) * cnt);
+    if (n) *n = sp_after ? cnt : (int64_t)trace_sp_.size();
+    if (phase_info)
+      for (int p = 0; p < 3; ++p) { phase_info[p] = phase_start_[p]; phase_info[3 + p] = phase_break_[p]; }
   }
 
   void counters(int64_t out[4]) const override {
@@ -541,7 +569,7 @@ class Session : public SessionBase {
     fh_.push_back(f);
     if (f < fbest_) fbest_ = f;   // Python min(f_best, f): NaN never becomes the best
     fhb_.push_back(fbest_);
-    if (use_sparsity_) { sp_prev_ = sp_cur_; sp_cur_ = s; }
+    if (use_sparsity_) { sp_prev_ = sp_cur_; sp_cur_ = s; sp_hist_.push_back(s); }
     ++k_;
     ++inner_;
   }
@@ -558,11 +586,13 @@ class Session : public SessionBase {
     return stable_ > O_.stable_len_threshold;
   }
 
-  void end_phase() {
+  void end_phase(bool by_stop_rule = false) {
+    if (phase_ < 3) phase_break_[phase_] = by_stop_rule ? 1 : 0;
     ++phase_;
     inner_ = 0;
     stable_ = 0;
     if (phase_ >= 3) { finished_ = true; return; }
+    phase_start_[phase_] = k_;
     mu_ = mus_[phase_];
     if (method_ == GLX_FPROXGD || method_ == GLX_FGD) {  // gl_FProxGD_primal.py:68-69
       copy_x(iv_, ix_);
@@ -615,7 +645,7 @@ class Session : public SessionBase {
   void iter_proxgd() {
     if (!state_valid_) proxgd_prologue(thr_from_trial_);
     record(f_cur_, s_cur_);
-    if (stop_rule()) { end_phase(); return; }
+    if (stop_rule()) { end_phase(true); return; }
     const bool ls = O_.step_type == GLX_STEP_LINE_SEARCH && O_.ls_maxit > 0;
     const double t0 = ls ? O_.alpha0 : schedule(inner_);
     std::pair<const T*, int> g{nullptr, 0};
@@ -777,7 +807,7 @@ class Session : public SessionBase {
       f_known_ = true;
     }
     record(f_cur_, s_cur_);
-    if (stop_rule()) { end_phase(); return; }
+    if (stop_rule()) { end_phase(true); return; }
     const double theta = 2.0 / (double)(inner_ + 1);       // gl_FProxGD_primal.py:138
     const double theta_next = 2.0 / (double)(inner_ + 2);
     const bool ls = O_.step_type == GLX_STEP_LINE_SEARCH && O_.ls_maxit > 0;
@@ -976,6 +1006,12 @@ class Session : public SessionBase {
     launch_descent<T>(X_[0], X_[1], g.first, g.second, n_, l_, alpha, mu_, O_.thres, O_.delta,
                       gd ? 1 : 0, red(S_DRN), st_);
     check_launch();
+    if (k_ % 100 == 0 && k_ / 100 <= fh_cap_ / 100 + 1) {   // sparsity_func(x) of the debug line (:99)
+      launch_rownorm_max<T>(X_[0], n_, l_, red(S_SPX), st_);
+      check_launch();
+      launch_count_above<T>(X_[0], nl_, scal_ + S_SPX + 1, Red{part_, ticket_, sp100_ + k_ / 100}, st_);
+      check_launch();
+    }
     // next iteration's objective residual and gradient residual, one pass
     const int64_t next_phase = (inner_ >= O_.maxit) ? phase_ + 1 : phase_;
     if (gemv_blocks_) descent_pass(next_phase);
@@ -1006,6 +1042,7 @@ class Session : public SessionBase {
   unsigned* pcnt_ = nullptr;   // per-panel counters (fused A^T R with K splits)
   int* flag_ = nullptr;
   int64_t fh_cap_ = 0;
+  double* sp100_ = nullptr;   // SGD/GD: count(|x| > 1e-6 max|x|) after every 100th iteration
   T* gemv_slabs_ = nullptr;
   int gemv_blocks_ = 0;
 
@@ -1038,7 +1075,9 @@ class Session : public SessionBase {
   bool finished_ = false, f_known_ = false, rn_known_ = false;
   double mus_[3] = {0, 0, 0}, mu_ = 0, tk_ = 0;
   double f_cur_ = 0, s_cur_ = 0, fbest_ = 0, sp_cur_ = 0, sp_prev_ = 0;
-  std::vector<double> fh_, fhb_;
+  std::vector<double> fh_, fhb_, sp_hist_, trace_sp_;
+  int64_t phase_start_[3] = {-1, -1, -1};
+  int64_t phase_break_[3] = {0, 0, 0};
   double tt_ = 0;
   int64_t ax_calls_ = 0, ax_cols_ = 0, atr_calls_ = 0, syncs_ = 0;
   double stats_[8] = {0, 0, 0, 0, 0, 0, 0, 0};
@@ -1185,6 +1224,14 @@ int glx_session_counters(glx_session* s, int64_t out[4]) {
   return guarded([&] {
     if (!s || !s->impl || !out) throw Error{GLX_E_INVALID, "null session/out"};
     s->impl->counters(out);
+  });
+}
+
+int glx_session_trace(glx_session* s, double* sparsity_after, int64_t cap, int64_t* n,
+                      int64_t phase_info[6]) {
+  return guarded([&] {
+    if (!s || !s->impl) throw Error{GLX_E_INVALID, "null session"};
+    s->impl->trace(sparsity_after, cap, n, phase_info);
   });
 }
 

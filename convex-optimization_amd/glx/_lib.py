@@ -67,6 +67,8 @@ _SIGS = {
     "glx_session_finish": (c_int, [c_void_p, POINTER(GlxResult)]),
     "glx_session_kernel_time": (c_int, [c_void_p, c_int, POINTER(c_int64), POINTER(c_double)]),
     "glx_session_counters": (c_int, [c_void_p, POINTER(c_int64)]),
+    "glx_session_trace": (c_int, [c_void_p, POINTER(c_double), c_int64, POINTER(c_int64),
+                                  POINTER(c_int64)]),
     "glx_session_destroy": (None, [c_void_p]),
     "glx_solve": (c_int, [POINTER(GlxProblem), POINTER(GlxOpts), c_void_p, c_size_t,
                           POINTER(GlxResult), c_void_p]),

@@ -21,7 +21,7 @@ from __future__ import annotations
 
 import ctypes
 import logging
-from typing import Any, Dict, Optional, Tuple
+from typing import Any, Dict, List, Optional, Tuple
 
 import numpy as np
 import torch
@@ -70,8 +70,10 @@ def make_opts(method: int, opts: Dict[str, Any]) -> GlxOpts:
 
 
 def _as_device(a, device, dtype) -> torch.Tensor:
-    t = torch.as_tensor(a)
-    return t.to(device=device, dtype=dtype).contiguous()
+    t = torch.as_tensor(a).to(device=device, dtype=dtype).contiguous()
+    if t.data_ptr() % 16:   # e.g. a view A[1:] with odd n: libglx needs 16-byte aligned rows
+        t = t.clone()
+    return t
 
 
 def _dtype_of(A) -> torch.dtype:
@@ -94,6 +96,27 @@ def _lambda_max(A: torch.Tensor, comm=None) -> float:
     if comm is not None:
         comm.allreduce_(gram)
     return float(torch.linalg.eigvalsh(gram).max().item())
+
+
+def _replay_log(s: "Session", res: Dict[str, Any], mu_0: float) -> None:
+    """The reference's debug lines, replayed from the recorded history after the solve so the
+    hot loop never formats or syncs for them: ``new mu=`` at each phase start
+    (gl_ProxGD_primal.py:54) and every 100th iteration ``iter= k, objective= f_hist[k-1],
+    sparsity= <of the updated x>`` (:134-136), skipping the iteration where the stop rule broke
+    (it does no update, :124-125). SGD/GD's sparsity is recorded at those iterations only."""
+    sp, starts, breaks = s.trace()
+    f_hist = res["f_hist"]
+    k = len(f_hist)
+    for p, mu in enumerate((100 * mu_0, 10 * mu_0, mu_0)):
+        if starts[p] < 0:
+            break
+        logger.debug("new mu= {:10E}".format(mu))
+        end = starts[p + 1] if p < 2 and starts[p + 1] >= 0 else k
+        for it in range(starts[p] + 1, end + 1):
+            if it % 100 or it > k or (breaks[p] and it == end):
+                continue
+            logger.debug("iter= {:5}, objective= {:10E}, sparsity= {:3f}".format(
+                it, float(f_hist[it - 1]), float(sp[it - 1]) if it - 1 < len(sp) else float("nan")))
 
 
 class Session:
@@ -160,6 +183,18 @@ class Session:
         check(lib().glx_session_counters(self.h, out))
         return {"ax_calls": out[0], "ax_sources": out[1], "atr_calls": out[2], "syncs": out[3]}
 
+    def trace(self) -> Tuple[np.ndarray, List[int], List[int]]:
+        """(sparsity after each iteration's update, phase start k's, phases ended by the stop rule)
+        — see glx_session_trace; valid after finish()."""
+        n = ctypes.c_int64(0)
+        info = (ctypes.c_int64 * 6)()
+        check(lib().glx_session_trace(self.h, None, 0, ctypes.byref(n), info))
+        sp = np.full(int(n.value), np.nan)
+        if n.value:
+            check(lib().glx_session_trace(self.h, sp.ctypes.data_as(ctypes.POINTER(ctypes.c_double)),
+                                          int(n.value), ctypes.byref(n), info))
+        return sp, [int(v) for v in info[:3]], [int(v) for v in info[3:]]
+
     def finish(self) -> Dict[str, Any]:
         cap = max(1, 3 * int(self.o.maxit))
         if self.o.max_total_iters > 0:
@@ -208,6 +243,8 @@ def solve(name: str, x0, A, b, mu_0, opts: Optional[Dict[str, Any]] = None, comm
     try:
         s.run(0)
         res = s.finish()
+        if logger.isEnabledFor(logging.DEBUG):
+            _replay_log(s, res, float(mu_0))
     finally:
         s.close()
     torch.cuda.synchronize(device)

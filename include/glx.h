@@ -128,6 +128,16 @@ int  glx_session_kernel_time(glx_session* s, int kind, int64_t* launches, double
 /* executed-work counters since create: out = {A@x passes, right-hand sides in them, A^T r
  * passes, host readbacks} (cumulative; the caller differences them around a timed region). */
 int  glx_session_counters(glx_session* s, int64_t out[4]);
+/* After glx_session_finish: what the reference's 'opt' logger prints, so a host can replay it
+ * without touching the hot loop (gl_ProxGD_primal.py:54 `new mu=` per phase, :134-136 the line
+ * every 100 iterations; same in gl_FProxGD_primal.py:56,149-151 and gl_SGD_primal.py:49,98-99).
+ * sparsity_after[i] = sparsity of the iterate after iteration i+1's update (NaN where not
+ * recorded: SGD/GD record it at every 100th iteration only); *n = entries written (with
+ * sparsity_after == NULL: entries available). phase_info[p] = k at the start of phase p (-1 if
+ * never entered), phase_info[3 + p] = 1 if the stop rule ended phase p (that iteration logs
+ * nothing, :118-125). */
+int  glx_session_trace(glx_session* s, double* sparsity_after, int64_t cap, int64_t* n,
+                       int64_t phase_info[6]);
 void glx_session_destroy(glx_session* s);
 
 /* One-shot solve: create + run to completion + finish + destroy. */

@@ -1,0 +1,12 @@
+#!/bin/bash
+# Round 2: GPU test suite + smoke + driver-form bench (with prewarm) + fp32 parity margins.
+cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
+O=gpurun_out/r2_check; rm -rf $O; mkdir -p $O
+timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 150 --timeout-method thread > $O/pytest.log 2>&1; rc=$?
+echo "pytest rc=$rc" >> $O/status.txt
+[ $rc -eq 0 ] || exit 1
+timeout -k 10 120 python3 -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1 || exit 1
+timeout -k 10 200 python3 bench.py --gpus 1 --steps 20 --warmup 5 > $O/driver.json 2> $O/driver.err || exit 1
+timeout -k 10 200 python3 bench.py --gpus 1 --steps 20 --warmup 5 --no-cpu-baseline > $O/driver2.json 2> $O/driver2.err || exit 1
+timeout -k 10 300 python3 scripts/fp32_parity_probe.py > $O/fp32.jsonl 2> $O/fp32.err || exit 1
+echo done

@@ -4,6 +4,7 @@ The fixtures were produced by running the reference solvers (tests/golden/make_g
 the oracle must reproduce them bit-for-bit on this NumPy build (≤1e-13 relative is
 accepted to tolerate a different BLAS on another host).
 """
+import os
 import warnings
 
 import numpy as np
@@ -66,3 +67,29 @@ def test_unknown_step_type_raises():
     A, b, u, x0, mu = numpy_ref.gen_data(16, 32, 2, 1)
     with pytest.raises(ValueError):
         numpy_ref.gl_ProxGD_primal(x0, A, b, mu, {"step_type": "bogus"})
+
+
+def test_oracle_log_lines_match_reference():
+    """The oracle's restated 'opt' debug lines (alpha0=, new mu= per phase, every 100th
+    iteration) equal the reference's own, recorded in tests/golden/logs.json."""
+    import json
+    import logging
+    from conftest import GOLDEN
+    from oracle import numpy_ref
+    logs = json.load(open(os.path.join(GOLDEN, "logs.json")))
+    lg = logging.getLogger("oracle.opt")
+    for name, case in logs.items():
+        lines = []
+        h = logging.Handler(logging.DEBUG)
+        h.emit = lambda rec: lines.append(rec.getMessage())
+        lg.addHandler(h)
+        old = lg.level
+        lg.setLevel(logging.DEBUG)
+        try:
+            A, b, u, x0, mu = numpy_ref.gen_data(case["m"], case["n"], case["l"], case["seed"])
+            with np.errstate(all="ignore"):
+                numpy_ref.SOLVERS[case["solver"]](x0, A, b, mu, {})
+        finally:
+            lg.removeHandler(h)
+            lg.setLevel(old)
+        assert lines == case["lines"], name
