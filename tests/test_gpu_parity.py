@@ -3,7 +3,12 @@ and vs the CPU oracle on larger instances.
 
 Bar (BASELINE north star): fp64 — identical iteration count k, final objective within 1e-8
 relative (f_hist elementwise within 1e-8 relative as well), iterate within 1e-6 relative;
-fp32 — objective within 1e-4 relative (the trajectory may diverge in fp32).
+fp32 — final objective within 1e-6 relative, f_hist elementwise within 2e-5
+where k agrees. Measured on MI355X (profiles/r2_fp32_parity_margins.jsonl): fval 3e-8..7.3e-7
+on every fp32 golden case, f_hist up to 9.4e-6 mid-trajectory (fp32 summation-order noise,
+amplified over 120 iterations, shrinking again as the run converges). One exception bar: a
+40-iteration-per-phase fp32 ProxGD run that stops far from convergence measured 3.3e-6 on fval
+(FP32_UNCONVERGED_BAR).
 """
 import warnings
 
@@ -22,6 +27,9 @@ CASES = sorted(golden_index())
 # entries flip with rounding — the report's own run (NumPy 1.19) took 2037 iterations where
 # NumPy 2.2 takes 2034. Bar for these: k within 0.5 %, objective within 1e-6.
 ULP_SENSITIVE_K = {"default_gl_FGD_primal"}
+FP32_FVAL_BAR = 1e-6
+FP32_FHIST_BAR = 2e-5
+FP32_UNCONVERGED_BAR = 1e-5
 
 
 def _solve(meta, A, b, x0, mu, extra=None):
@@ -70,9 +78,9 @@ def test_solver_matches_reference_golden(name):
         xg = gold["x"]
         assert np.max(np.abs(x - xg)) <= 1e-6 * max(1.0, np.max(np.abs(xg)))
     else:
-        assert _rel(out["fval"], gold["fval"]) < 1e-4
+        assert _rel(out["fval"], gold["fval"]) < FP32_FVAL_BAR
         if k == int(gold["k"]):
-            assert _rel(f_hist[:10], gold["f_hist"][:10]) < 1e-4
+            assert _rel(f_hist, gold["f_hist"]) < FP32_FHIST_BAR
 
 
 @pytest.mark.parametrize("name", ["default_gl_ProxGD_primal", "seed114514_gl_ProxGD_primal",
@@ -142,9 +150,10 @@ def test_large_vs_oracle_few_iterations(solver, dtype, shape):
     import importlib
     x, k, out = getattr(importlib.import_module(solver), solver)(x0, A, b, mu, dict(opts))
     assert k == kr
-    tol = 1e-8 if dtype == "f64" else 1e-4
+    tol = 1e-8 if dtype == "f64" else FP32_FVAL_BAR
     assert _rel(out["fval"], outr["fval"]) < tol
-    assert _rel(np.asarray(out["f_hist"], float), np.asarray(outr["f_hist"], float)) < tol
+    assert _rel(np.asarray(out["f_hist"], float), np.asarray(outr["f_hist"], float)) < \
+        (tol if dtype == "f64" else FP32_FHIST_BAR)
 
 
 @pytest.mark.parametrize("solver,dtype,shape", [
@@ -156,7 +165,7 @@ def test_large_vs_oracle_few_iterations(solver, dtype, shape):
 def test_full_size_vs_oracle(solver, dtype, shape):
     """BASELINE.json's full sizes: two iterations per continuation phase against the NumPy
     oracle on the same instance (the oracle runs a few seconds at these sizes on the GPU box's
-    host). Same bars as above: k identical, fval and f_hist within 1e-8 (fp64) / 1e-4 (fp32)."""
+    host). Same bars as above: k identical, fval and f_hist within 1e-8 (fp64) / FP32_*_BAR."""
     from oracle import numpy_ref
     m, n, l = shape
     A, b, u, x0, mu = numpy_ref.gen_data(m, n, l, 97006855)
@@ -169,9 +178,10 @@ def test_full_size_vs_oracle(solver, dtype, shape):
     import importlib
     x, k, out = getattr(importlib.import_module(solver), solver)(x0, A, b, mu, dict(opts))
     assert k == kr
-    tol = 1e-8 if dtype == "f64" else 1e-4
+    tol = 1e-8 if dtype == "f64" else FP32_FVAL_BAR
     assert _rel(out["fval"], outr["fval"]) < tol
-    assert _rel(np.asarray(out["f_hist"], float), np.asarray(outr["f_hist"], float)) < tol
+    assert _rel(np.asarray(out["f_hist"], float), np.asarray(outr["f_hist"], float)) < \
+        (tol if dtype == "f64" else FP32_FHIST_BAR)
     assert np.max(np.abs(x.astype(float) - xr.astype(float))) <= (1e-6 if dtype == "f64" else 1e-2) * np.max(np.abs(xr))
 
 
@@ -191,3 +201,31 @@ def test_continuous_subgradient_flag(solver):
     assert k == kr
     assert _rel(out["fval"], outr["fval"]) < 1e-8
     assert _rel(np.asarray(out["f_hist"], float), np.asarray(outr["f_hist"], float)) < 1e-8
+
+
+@pytest.mark.parametrize("solver,alpha_scale", [
+    ("gl_ProxGD_primal", 1.0),
+    ("gl_FProxGD_primal", 1.0),
+    ("gl_ProxGD_primal", 2.5),      # alpha0 above 1/L: line-search rejections (and 5-trial fallbacks)
+])
+def test_full_size_long_trajectory_vs_oracle(solver, alpha_scale):
+    """North-star size (8192,16384,32) fp64, 40 iterations per continuation phase (120 in all,
+    both phase boundaries crossed) against the oracle on the same instance: k identical, the
+    whole f_hist within 1e-8 relative, the iterate within 1e-6 of max|x|. With alpha0 = 2.5/L
+    the ProxGD line search rejects trials, so the retry path (k_prox_pgd from the stored
+    gradient, dropped speculation) is compared over a real trajectory too."""
+    from oracle import numpy_ref
+    m, n, l = 8192, 16384, 32
+    A, b, u, x0, mu = numpy_ref.gen_data(m, n, l, 97006855)
+    opts = {"alpha0": alpha_scale * numpy_ref.step_size_for(m, n), "maxit": 40}
+    with warnings.catch_warnings():
+        warnings.simplefilter("ignore")
+        xr, kr, outr = numpy_ref.SOLVERS[solver](x0, A, b, mu, dict(opts))
+    import importlib
+    x, k, out = getattr(importlib.import_module(solver), solver)(x0, A, b, mu, dict(opts))
+    assert k == kr == 120
+    assert _rel(out["fval"], outr["fval"]) < 1e-8
+    assert _rel(np.asarray(out["f_hist"], float), np.asarray(outr["f_hist"], float)) < 1e-8
+    assert np.max(np.abs(x - xr)) <= 1e-6 * np.max(np.abs(xr))
+    if alpha_scale > 1:
+        assert out["glx"]["syncs"] > k   # more than one readback per iteration: trials were retried
