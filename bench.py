@@ -296,14 +296,24 @@ def main():
         ml = r1 - r0
         ax_avg_s = (ax_ms / max(1, ax_n)) / 1e3
         atr_avg_s = (atr_ms / max(1, atr_n)) / 1e3
-        # right-hand sides batched per A@x launch (e.g. A @ [z | p_thr] for ProxGD)
+        # dense right-hand sides batched per A@x launch (e.g. A @ [z | p_thr | p] in exact mode).
+        # ProxGD's split-candidate mode batches [e | p_thr]: e = p - p_thr is nonzero only in the
+        # rows the hard threshold touched, its MFMAs run on flagged K chunks only, and it is not
+        # counted as a dense source; its algorithmic work is 2 m l flops per such row.
+        # Gather form (default): A e reads the flagged rows of a transposed copy of A (m values
+        # each) on top of the dense pass; the "sp" form skips unflagged K chunks in the tile.
         nsrc = work["ax_sources"] / max(1, work["ax_calls"])
-        ax_bytes = es * (ml * n + (ml + n) * l * nsrc)
+        split_env = os.environ.get("GLX_SPLIT_CAND", "1")
+        split_cand = (args.method == "gl_ProxGD_primal" and not args.exact and split_env != "0")
+        sparse_rows = res["stats"][1] / max(1.0, res["stats"][2]) if split_cand else 0.0
+        gather_rows = sparse_rows if (split_cand and split_env != "sp") else 0.0
+        ax_bytes = es * (ml * n + (ml + n) * l * nsrc + (n * l if split_cand else 0) + ml * gather_rows)
         atr_bytes = es * (ml * n + (ml + n) * l)
-        ax_flops = 2.0 * ml * n * l * nsrc
+        ax_flops = 2.0 * ml * n * l * nsrc + 2.0 * ml * l * sparse_rows
         atr_flops = 2.0 * ml * n * l
         ach = ax_bytes / ax_avg_s / 1e9 if ax_n else None
-        cfg_key = "%s_%s_%dx%dx%d_g%d" % (args.method, args.dtype, m, n, l, world)
+        cfg_key = "%s_%s_%dx%dx%d_g%d%s" % (args.method, args.dtype, m, n, l, world,
+                                            "_sc" if split_cand else "")
         peak_tf = MFMA_PEAK_TFS[args.dtype]
         mfma_bound = ax_flops / (peak_tf * 1e12) >= ax_bytes / (HBM_PEAK_GBS * 1e9)
         ax_tf = ax_flops / ax_avg_s / 1e12 if ax_n else None
@@ -325,20 +335,24 @@ def main():
                 "flops_per_launch": ax_flops,
                 "bytes_per_launch": ax_bytes, "avg_launch_us": ax_avg_s * 1e6, "launches_timed": ax_n,
                 "timed_every": args.profile,
-                "rhs_per_launch": nsrc, "hbm_GBs": ax_gbs, "hbm_frac": ax_gbs / HBM_PEAK_GBS if ax_n else None,
+                "rhs_per_launch": nsrc,
+                "split_candidate": ("gather" if gather_rows or (split_cand and split_env != "sp") else
+                                    ("sp" if split_cand else False)),
+                "sparse_rows_per_launch": sparse_rows, "hbm_GBs": ax_gbs, "hbm_frac": ax_gbs / HBM_PEAK_GBS if ax_n else None,
                 "mfma_tflops": ax_tf, "mfma_frac": ax_tf / peak_tf if ax_n else None,
                 "atr_avg_launch_us": atr_avg_s * 1e6,
                 "atr_GBs": atr_bytes / atr_avg_s / 1e9 if atr_n else None,
                 "atr_mfma_frac": (atr_flops / atr_avg_s / 1e12) / peak_tf if atr_n else None,
                 "pair_tflops": pair_tf, "pair_frac": pair_tf / peak_tf if pair_tf else None,
-                "pair_definition": "pair_frac: executed MFMA flops of the A@X launch (2 m n l per "
-                                   "right-hand side, all of which the reference also computes) + "
+                "pair_definition": "pair_frac: algorithmic MFMA flops of the A@X launch (2 m n l "
+                                   "per dense right-hand side, 2 m l per flagged row of e) + "
                                    "A^T r (2 m n l), over the two launches' time; the north-star "
                                    "60 % target is read on this one. pair4_frac: SURVEY §8d's "
                                    "literal 4 m n l over the same time",
                 "pair4_tflops": pair4_tf, "pair4_frac": pair4_tf / peak_tf if pair4_tf else None,
                 # all MFMA flops issued in the timed region / its wall time (gaps, prox included)
-                "iter_frac": (2.0 * ml * n * l * work["ax_sources"] + work["atr_calls"] * atr_flops)
+                "iter_frac": (2.0 * ml * n * l * work["ax_sources"] + work["atr_calls"] * atr_flops
+                              + 2.0 * ml * l * sparse_rows * work["ax_calls"])
                              / elapsed / 1e12 / peak_tf}
         steps = max(1, done)
         line = {

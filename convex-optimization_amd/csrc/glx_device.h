@@ -220,11 +220,18 @@ __device__ inline float row_allsum(float v) {
 // p_thr = p with |p| < thres zeroed. acc (per thread, reduced over the grid by the caller):
 // [sum g*G_t, sum G_t^2, sum_i ||p_i||, max |p|, #{p changed by the threshold},
 //  #{rows of p changed by the threshold}]. rv = the row exists (all LPR lanes call this).
+//
+// emode (the split-candidate form of the fast objective mode, see solver.cpp iter_proxgd):
+// instead of z the third output is e = p - p_thr, i.e. p where the threshold zeroed it and 0
+// elsewhere (exact: p_thr is either p or 0, and NaN is never "small"), so A p = A p_thr + A e
+// with e nonzero only in the rows the threshold touched. Returns whether this row of e is
+// nonzero (every lane of the row gets the same answer).
 // ------------------------------------------------------------------------------------------
 template <typename T, int LPR, int EPL>
-__device__ inline void prox_pgd_row(const T (&xv)[EPL], const T (&gv)[EPL], const bool (&ok)[EPL],
+__device__ inline bool prox_pgd_row(const T (&xv)[EPL], const T (&gv)[EPL], const bool (&ok)[EPL],
                                     bool rv, int sub, T t, T tmu, T thres, T (&pv)[EPL],
-                                    T (&pth)[EPL], T (&zv)[EPL], double (&acc)[6]) {
+                                    T (&pth)[EPL], T (&zv)[EPL], double (&acc)[6],
+                                    bool emode = false) {
   T w[EPL];
   T sq = T(0);
 #pragma unroll
@@ -242,9 +249,9 @@ __device__ inline void prox_pgd_row(const T (&xv)[EPL], const T (&gv)[EPL], cons
   for (int e = 0; e < EPL; ++e) {
     pv[e] = (w[e] * c) / d;
     const T G = (xv[e] - pv[e]) / t;
-    zv[e] = xv[e] - t * G;
     const bool small = tabs(pv[e]) < thres;
     pth[e] = small ? T(0) : pv[e];
+    zv[e] = emode ? (small ? pv[e] : T(0)) : xv[e] - t * G;
     if (ok[e]) {
       acc[0] += (double)(gv[e] * G);
       acc[1] += (double)(G * G);
@@ -261,6 +268,7 @@ __device__ inline void prox_pgd_row(const T (&xv)[EPL], const T (&gv)[EPL], cons
     acc[2] += (double)pn;
     acc[5] += rowch > 0.0 ? 1.0 : 0.0;
   }
+  return rowch > 0.0;
 }
 
 // ------------------------------------------------------------------------------------------

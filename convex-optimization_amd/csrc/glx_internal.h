@@ -91,14 +91,18 @@ std::string describe_plan(const GemmPlan& p);
 // P[src][ax_split(p, nsrc)][m][l]; skipped entirely unless gate == NULL or *gate == epoch.
 // pub.host != NULL: the launch also hands that scalar packet to the host from its first
 // workgroup (needs ax_pub_ok: the kind-5 LDS tile for nsrc).
+// sf != NULL: n row flags of X[0] (sf[k] == 0 => row k of X[0] is exactly zero); the kind-5
+// tile then skips the MFMAs of X[0] on K chunks without a flagged row (same result: the
+// skipped products are exact zeros). Other tiles ignore it.
 bool ax_pub_ok(const GemmPlan& p, int nsrc);
 template <typename T>
 void launch_ax(const GemmPlan& p, int nsrc, const T* A, const T* const* X, T* P, const int* gate,
-               int epoch, hipStream_t st, Pub pub = Pub{});
+               int epoch, hipStream_t st, Pub pub = Pub{}, const uint8_t* sf = nullptr);
 template <typename T>
 void launch_atr(const GemmPlan& p, const T* A, const T* R, T* Gp, hipStream_t st);
 // ProxGD trial fused into A^T R (needs atr_prox_ok: MFMA panels, WL 0, at most 8 K splits):
-// G = A^T R, then p = prox(x - t G), p_thr, z and the six trial sums of k_prox_pgd into red.
+// G = A^T R, then p = prox(x - t G), p_thr, z and the six trial sums of k_prox_pgd into red
+// (zf != NULL: z = e = p - p_thr and its row flags, as launch_prox_pgd).
 // With S = atr_S > 1 K splits the blocks write slabs Gp[S][n][l] and the last block of each
 // 64-row panel (counter pcnt[panel], zero before the first launch, reset by that block) sums
 // them in slab order and runs the trial.
@@ -106,7 +110,7 @@ bool atr_prox_ok(const GemmPlan& p);
 template <typename T>
 void launch_atr_prox(const GemmPlan& p, const T* A, const T* R, T* G, const T* x, T* pp, T* pthr,
                      T* z, double t, double mu, double thres, Red red, hipStream_t st, Pub pub = Pub{},
-                     T* Gp = nullptr, unsigned* pcnt = nullptr);
+                     T* Gp = nullptr, unsigned* pcnt = nullptr, uint8_t* zf = nullptr);
 // FISTA trial fused into A^T R (same plan condition): G = A^T R, then xc, v_next, y_next and the
 // four trial sums of k_fista_trial (PROX) into red.
 template <typename T>
@@ -114,6 +118,19 @@ void launch_atr_fista(const GemmPlan& p, const T* A, const T* R, T* G, const T* 
                       T* xc, T* vn, T* yn, double t, double mu, double thres, double theta,
                       double theta_next, Red red, hipStream_t st, Pub pub = Pub{},
                       T* Gp = nullptr, unsigned* pcnt = nullptr);
+
+// ---- split-candidate A e from a transposed copy of A (kernels_gather.hip) ----
+// gather_ok: the shape supports it (l in {16, 32}, n < 65536); gather_split: K splits of the
+// flagged-row list for m output rows (slabs P[S][m][l]).
+bool gather_ok(int64_t n, int64_t l);
+int gather_split(int64_t m);
+// At (n x m) = A^T
+template <typename T>
+void launch_transpose(const T* A, T* At, int64_t m, int64_t n, hipStream_t st);
+// P[s][r][c] = sum over the flagged rows k of e (zf[k] != 0) in list split s of At[k][r] E[k][c]
+template <typename T>
+void launch_at_gather(const T* At, const T* E, const uint8_t* zf, int64_t m, int64_t n, int64_t l,
+                      T* P, int S, hipStream_t st);
 
 // ---- row / elementwise kernels (kernels_elem.hip) ----
 // Gradient inputs `g` with an `S` argument are S split-K slabs of n*l values summed in slab
@@ -123,20 +140,25 @@ void launch_atr_fista(const GemmPlan& p, const T* A, const T* R, T* G, const T* 
 // out[src] = sum R[src]^2 (out[0..2]), out[3] = count(|cx| > 1e-6 * (*cmax)) when cx != NULL;
 // fh != NULL: *fh = 0.5 out[0] + fh_mu * (*fh_rn) (device-side objective history).
 // gate_mode: when gated off, 0 = do nothing, 1 = recompute out[0] from R[0] (nsrc = 1).
+// chain (nsrc = 2, split-candidate mode): source 0 is a correction on top of source 1,
+// R[0] = (sum_s P[1][s] - B) + sum_s P[0][s]; R[0] may then be NULL (only its sum is kept).
+// With chain, source 0 has S0 slabs (0: S) at P and source 1 has S slabs at P + S0 * ml.
 template <typename T>
 void launch_finalize_residual(const T* P, int S, const T* B, int nsrc, T* const* R, int64_t ml,
                               const int* gate, int epoch, int gate_mode, const T* cx, int64_t cn,
                               const double* cmax, double* fh, double fh_mu, const double* fh_rn,
                               Red red, hipStream_t st, const double* snap_src = nullptr,
-                              double* snap_dst = nullptr, int nsnap = 0);
+                              double* snap_dst = nullptr, int nsnap = 0, int chain = 0, int S0 = 0);
 template <typename T>
 void launch_sum_partials(const T* Gp, int S, T* G, int64_t nl, hipStream_t st);
 // ProxGD trial: p = prox(x - t g, t), G_t = (x - p)/t, z = x - t G_t, pthr = p thresholded.
 // out: [sum g*G_t, sum G_t^2, sum_i ||p_i||, max |p|, #changed by the threshold]
+// zf != NULL (split-candidate mode): z receives e = p - p_thr instead and zf[i] (n bytes) = row
+// i of e is nonzero.
 template <typename T>
 void launch_prox_pgd(const T* x, const T* g, int S, T* gout, T* p, T* pthr, T* z, int64_t n,
                      int64_t l, double t, double mu, double thres, Red red, hipStream_t st,
-                     Pub pub = Pub{});
+                     Pub pub = Pub{}, uint8_t* zf = nullptr);
 // FISTA (prox = true) / FGD (prox = false: identity) trial fused with the next combine:
 // xc = prox(y - t g, t); vnext = thr(xk) + (xc - thr(xk))/theta;
 // ynext = (1 - theta_next) thr(xc) + theta_next vnext.

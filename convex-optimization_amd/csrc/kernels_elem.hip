@@ -77,7 +77,7 @@ __global__ __launch_bounds__(256) void k_finalize_residual(
     T* __restrict__ R2, int64_t ml, const int* __restrict__ gate, int epoch, int gate_mode,
     const T* __restrict__ cx, int64_t cn, const double* __restrict__ cmax, double* __restrict__ fh,
     double fh_mu, const double* __restrict__ fh_rn, Red red, const double* __restrict__ snap_src,
-    double* __restrict__ snap_dst, int nsnap) {
+    double* __restrict__ snap_dst, int nsnap, int chain, const T* __restrict__ P0, int S0) {
   const bool live = (gate == nullptr) || (*gate == epoch);
   if (!live && gate_mode == 0) return;  // uniform over the grid: nobody touches the ticket
   double v[4] = {0.0, 0.0, 0.0, 0.0};
@@ -90,6 +90,17 @@ __global__ __launch_bounds__(256) void k_finalize_residual(
   // leave the loop together and the butterfly only reads active partners
   for (int64_t idx = tid / G; idx < ml; idx += stride / G) {
     const T bv = B[idx];
+    if (NSRC == 2 && chain) {   // split-candidate: R0 = (A p_thr - b) + A e (always live)
+      const T r1 = group_slab_sum<T, G>(P + (int64_t)S0 * ml, S, ml, idx, sub) - bv;
+      const T r0 = r1 + group_slab_sum<T, G>(P0, S0, ml, idx, sub);
+      if (sub == 1 % G) rs[1][idx] = r1;
+      if (R0 != nullptr && sub == 0) rs[0][idx] = r0;
+      if (sub == 0) {
+        v[0] += (double)(r0 * r0);
+        v[1] += (double)(r1 * r1);
+      }
+      continue;
+    }
 #pragma unroll
     for (int sr = 0; sr < NSRC; ++sr) {
       T r;
@@ -146,7 +157,8 @@ __global__ __launch_bounds__(256) void k_sum_partials(const T* __restrict__ Gp, 
 template <typename T, int LPR, int EPL>
 __global__ __launch_bounds__(256) void k_prox_pgd(const T* __restrict__ x, const T* __restrict__ g,
                                                   int S, T* __restrict__ gout, T* __restrict__ p,
-                                                  T* __restrict__ pthr, T* __restrict__ z, int64_t n,
+                                                  T* __restrict__ pthr, T* __restrict__ z,
+                                                  uint8_t* __restrict__ zf, int64_t n,
                                                   int64_t l, double t_, double tmu_, double thres_,
                                                   Red red, Pub pub) {
   if (publisher_last<6, 0x8u>(pub, red)) return;
@@ -164,7 +176,9 @@ __global__ __launch_bounds__(256) void k_prox_pgd(const T* __restrict__ x, const
     gv[e] = ok[e] ? slab_sum(g, S, nl, base + j) : T(0);
     if (ok[e] && gout != nullptr) gout[base + j] = gv[e];
   }
-  prox_pgd_row<T, LPR, EPL>(xv, gv, ok, rv, sub, t, tmu, thres, pv, pth, zv, acc);
+  const bool rowe = prox_pgd_row<T, LPR, EPL>(xv, gv, ok, rv, sub, t, tmu, thres, pv, pth, zv, acc,
+                                              zf != nullptr);
+  if (zf != nullptr && rv && sub == 0) zf[row] = rowe ? 1 : 0;
 #pragma unroll
   for (int e = 0; e < EPL; ++e) {
     const int64_t j = sub + (int64_t)e * LPR;
@@ -476,8 +490,10 @@ void launch_finalize_residual(const T* P, int S, const T* B, int nsrc, T* const*
                               const int* gate, int epoch, int gate_mode, const T* cx, int64_t cn,
                               const double* cmax, double* fh, double fh_mu, const double* fh_rn,
                               Red red, hipStream_t st, const double* snap_src, double* snap_dst,
-                              int nsnap) {
-  const int G = finalize_groups(S);
+                              int nsnap, int chain, int S0) {
+  if (chain && (nsrc != 2 || gate != nullptr)) throw Error{GLX_E_INVALID, "finalize: chain needs 2 ungated sources"};
+  if (S0 <= 0) S0 = S;
+  const int G = finalize_groups(S > S0 ? S : S0);
   if (G > 8) throw Error{GLX_E_INVALID, "finalize: more than 64 K-split slabs"};
   const int64_t work = ml * G > cn ? ml * G : cn;
   const dim3 grid(grid_for(work, 256 * 2));
@@ -486,7 +502,7 @@ void launch_finalize_residual(const T* P, int S, const T* B, int nsrc, T* const*
   auto go = [&](auto ns, auto g) {
     hipLaunchKernelGGL((k_finalize_residual<T, decltype(ns)::value, decltype(g)::value>), grid,
                        dim3(256), 0, st, P, S, B, R[0], r1, r2, ml, gate, epoch, gate_mode, cx, cn,
-                       cmax, fh, fh_mu, fh_rn, red, snap_src, snap_dst, nsnap);
+                       cmax, fh, fh_mu, fh_rn, red, snap_src, snap_dst, nsnap, chain, P, S0);
   };
   auto by_g = [&](auto ns) {
     if (G == 1) go(ns, std::integral_constant<int, 1>{});
@@ -504,11 +520,12 @@ void launch_sum_partials(const T* Gp, int S, T* G, int64_t nl, hipStream_t st) {
 }
 template <typename T>
 void launch_prox_pgd(const T* x, const T* g, int S, T* gout, T* p, T* pthr, T* z, int64_t n,
-                     int64_t l, double t, double mu, double thres, Red red, hipStream_t st, Pub pub) {
+                     int64_t l, double t, double mu, double thres, Red red, hipStream_t st, Pub pub,
+                     uint8_t* zf) {
   dispatch_row(l, [&](auto lpr, auto epl) {
     hipLaunchKernelGGL((k_prox_pgd<T, decltype(lpr)::value, decltype(epl)::value>),
-                       dim3(row_grid_pub(n, lpr, pub)), dim3(256), 0, st, x, g, S, gout, p, pthr, z, n,
-                       l, t, t * mu, thres, red, pub);
+                       dim3(row_grid_pub(n, lpr, pub)), dim3(256), 0, st, x, g, S, gout, p, pthr, z, zf,
+                       n, l, t, t * mu, thres, red, pub);
   });
 }
 template <typename T>
@@ -600,10 +617,10 @@ void launch_publish(const double* s, int ns, double* host, unsigned* host_seq, u
   template void launch_finalize_residual<T>(const T*, int, const T*, int, T* const*, int64_t,       \
                                             const int*, int, int, const T*, int64_t, const double*, \
                                             double*, double, const double*, Red, hipStream_t,       \
-                                            const double*, double*, int);                           \
+                                            const double*, double*, int, int, int);                 \
   template void launch_sum_partials<T>(const T*, int, T*, int64_t, hipStream_t);                    \
   template void launch_prox_pgd<T>(const T*, const T*, int, T*, T*, T*, T*, int64_t, int64_t,       \
-                                   double, double, double, Red, hipStream_t, Pub);                  \
+                                   double, double, double, Red, hipStream_t, Pub, uint8_t*);        \
   template void launch_fista_trial<T>(bool, const T*, const T*, int, T*, const T*, T*, T*, T*,      \
                                       int64_t, int64_t, double, double, double, double, double,     \
                                       double, Red, hipStream_t, Pub);                               \

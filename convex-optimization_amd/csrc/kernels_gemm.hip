@@ -290,7 +290,12 @@ __device__ inline void lds_put(T* dst, typename MF<T>::vec_t v) {
   }
 }
 
-template <typename T, int MT, int NT, int NSRC, int PF, int VPL, int WAVES>
+//
+// SP (split-candidate mode, NSRC = 2): X0 = e is zero except in the rows sf flags, so the MFMAs
+// of source 0 run only on chunks with a flagged row (one uniform branch per chunk; the flags
+// of chunk c + PF are fetched with its A refill). Skipped chunks contribute exact zeros, so the
+// partials equal the dense product's.
+template <typename T, int MT, int NT, int NSRC, int PF, int VPL, int WAVES, bool SP = false>
 __global__ __launch_bounds__(64 * WAVES) void k_ax_lds(const T* __restrict__ A,
                                                       const T* __restrict__ X0,
                                                       const T* __restrict__ X1,
@@ -298,7 +303,8 @@ __global__ __launch_bounds__(64 * WAVES) void k_ax_lds(const T* __restrict__ A,
                                                       T* __restrict__ P, int64_t m, int64_t n,
                                                       int64_t chunks, int S, int gx, int xmap,
                                                       const int* __restrict__ gate, int epoch,
-                                                      Pub pub) {
+                                                      Pub pub, const uint8_t* __restrict__ sf) {
+  static_assert(!SP || NSRC == 2, "split-candidate mode has two sources");
   typedef MF<T> M;
   typedef typename M::vec_t V;
   typedef typename M::acc_t C;
@@ -401,21 +407,35 @@ __global__ __launch_bounds__(64 * WAVES) void k_ax_lds(const T* __restrict__ A,
       for (int e = 0; e < EL; ++e) xv[cc][e] = xp[e * LP];
     }
   };
-  // MFMAs of row tile mt for one chunk
-  auto mma_tile = [&](int mt, const V (&av)[VPL], const T (&xv)[NC][EL]) {
+  // MFMAs of row tile mt for one chunk, column tiles [C0, C1)
+  auto mma_cols = [&](int mt, const V (&av)[VPL], const T (&xv)[NC][EL], int c0, int c1) {
 #pragma unroll
     for (int v = 0; v < VPL; ++v)
 #pragma unroll
       for (int e = 0; e < E; ++e)
 #pragma unroll
         for (int cc = 0; cc < NC; ++cc)
-          acc[mt][cc] = M::mma(av[v][e], xv[cc][v * E + e], acc[mt][cc]);
+          if (cc >= c0 && cc < c1) acc[mt][cc] = M::mma(av[v][e], xv[cc][v * E + e], acc[mt][cc]);
   };
+  auto mma_tile = [&](int mt, const V (&av)[VPL], const T (&xv)[NC][EL]) {
+    mma_cols(mt, av, xv, SP ? NT : 0, NC);
+  };
+  // SP: does chunk `off` hold a flagged row of X0 (CK flag bytes, OR-ed as words)?
+  auto flag_of = [&](int64_t off) -> unsigned {
+    off = off < nch ? off : nch - 1;
+    const unsigned* fp = reinterpret_cast<const unsigned*>(sf + (cb + off) * CK);
+    unsigned f = 0;
+#pragma unroll
+    for (int j = 0; j < CK / 4; ++j) f |= fp[j];
+    return __builtin_amdgcn_readfirstlane(f);
+  };
+  unsigned fl[PF];
 
 #pragma unroll
   for (int p = 0; p < PF; ++p) {   // X first, then A, in every ring step (see header)
     load_x(xr[p], p);
     load_a(a[p], p);
+    if constexpr (SP) fl[p] = flag_of(p);
   }
   put_x(0, xr[0]);                 // chunk 0 -> slot 0
   __syncthreads();
@@ -433,13 +453,33 @@ __global__ __launch_bounds__(64 * WAVES) void k_ax_lds(const T* __restrict__ A,
       load_x(xr[p], c + PF);       // xr[p] (X(c)) has been in LDS since chunk c-1
       T xv[NC][EL];
       read_x(slot, xv);
+      int64_t off = c + PF;
+      off = off < nch ? off : nch - 1;
+      if constexpr (SP) {
+        // two straight-line bodies, so an active chunk runs exactly the dense schedule
+        if (fl[p] != 0) {
 #pragma unroll
-      for (int mt = 0; mt < MT; ++mt) {
-        mma_tile(mt, a[p][mt], xv);
-        int64_t off = c + PF;
-        off = off < nch ? off : nch - 1;
+          for (int mt = 0; mt < MT; ++mt) {
+            mma_cols(mt, a[p][mt], xv, 0, NC);
 #pragma unroll
-        for (int v = 0; v < VPL; ++v) a[p][mt][v] = load_vec<T, false>(ap[mt] + off * CK + v * E);
+            for (int v = 0; v < VPL; ++v) a[p][mt][v] = load_vec<T, false>(ap[mt] + off * CK + v * E);
+          }
+        } else {
+#pragma unroll
+          for (int mt = 0; mt < MT; ++mt) {
+            mma_cols(mt, a[p][mt], xv, NT, NC);
+#pragma unroll
+            for (int v = 0; v < VPL; ++v) a[p][mt][v] = load_vec<T, false>(ap[mt] + off * CK + v * E);
+          }
+        }
+        fl[p] = flag_of(c + PF);
+      } else {
+#pragma unroll
+        for (int mt = 0; mt < MT; ++mt) {
+          mma_tile(mt, a[p][mt], xv);
+#pragma unroll
+          for (int v = 0; v < VPL; ++v) a[p][mt][v] = load_vec<T, false>(ap[mt] + off * CK + v * E);
+        }
       }
       __syncthreads();
     }
@@ -455,6 +495,12 @@ __global__ __launch_bounds__(64 * WAVES) void k_ax_lds(const T* __restrict__ A,
       read_x(slot, xv);
 #pragma unroll
       for (int mt = 0; mt < MT; ++mt) mma_tile(mt, a[p][mt], xv);
+      if constexpr (SP) {
+        if (fl[p] != 0) {
+#pragma unroll
+          for (int mt = 0; mt < MT; ++mt) mma_cols(mt, a[p][mt], xv, 0, NT);
+        }
+      }
       __syncthreads();
     }
   }
@@ -1023,7 +1069,8 @@ __global__ __launch_bounds__(256, sizeof(T) == 8 ? 2 : 1) void k_atr_prox(const 
                                                   T* __restrict__ pthr, T* __restrict__ z,
                                                   double t_, double tmu_, double thres_, Red red,
                                                   Pub pub, int S, T* __restrict__ Gp,
-                                                  unsigned* __restrict__ pcnt) {
+                                                  unsigned* __restrict__ pcnt,
+                                                  uint8_t* __restrict__ zf) {
   if (publisher_first<6, 0x8u>(pub, red)) return;   // the extra workgroup (n / 64 * S + 1 in all)
   typedef MF<T> M;
   constexpr int L = 16 * NT;
@@ -1063,7 +1110,9 @@ __global__ __launch_bounds__(256, sizeof(T) == 8 ? 2 : 1) void k_atr_prox(const 
         ok[nt] = true;
         G[row * L + nt * 16 + i] = gv[nt];
       }
-      prox_pgd_row<T, 16, NT>(xa[r], gv, ok, true, i, t, tmu, thres, pv, pth, zv, accr);
+      const bool rowe =
+          prox_pgd_row<T, 16, NT>(xa[r], gv, ok, true, i, t, tmu, thres, pv, pth, zv, accr, zf != nullptr);
+      if (zf != nullptr && i == 0) zf[row] = rowe ? 1 : 0;
 #pragma unroll
       for (int nt = 0; nt < NT; ++nt) {
         p[row * L + nt * 16 + i] = pv[nt];
@@ -1576,15 +1625,24 @@ static void ax_mfma_go(const GemmPlan& p, const T* A, const T* const* X, T* P, c
 
 template <typename T, int NT, int NSRC, int MT, int PF, int VPL, int WAVES>
 static void ax_lds_go(const GemmPlan& p, int S, const T* A, const T* const* X, T* P,
-                      const int* gate, int epoch, hipStream_t st, Pub pub = Pub{}) {
+                      const int* gate, int epoch, hipStream_t st, Pub pub = Pub{},
+                      const uint8_t* sf = nullptr) {
   constexpr int E = 16 / sizeof(T);
   const int gx = (int)cdiv(p.m, 16 * MT * WAVES);
   const int xmap = (p.ax_xmap && ax_xmap_ok(S)) ? 1 : 0;
+  const dim3 grid((unsigned)ax_grid(xmap, gx, S) + (pub.host ? 1u : 0u));
+  if constexpr (NSRC == 2) {
+    if (sf != nullptr) {
+      hipLaunchKernelGGL((k_ax_lds<T, MT, NT, NSRC, PF, VPL, WAVES, true>), grid, dim3(64 * WAVES), 0,
+                         st, A, X[0], X[1], X[2], P, p.m, p.n, p.n / (4 * VPL * E), S, gx, xmap,
+                         gate, epoch, pub, sf);
+      return;
+    }
+  }
   static const size_t pad = lds_pad(k_ax_lds<T, MT, NT, NSRC, PF, VPL, WAVES>, "GLX_AX_LDS_PAD");
-  hipLaunchKernelGGL((k_ax_lds<T, MT, NT, NSRC, PF, VPL, WAVES>),
-                     dim3((unsigned)ax_grid(xmap, gx, S) + (pub.host ? 1u : 0u)),
+  hipLaunchKernelGGL((k_ax_lds<T, MT, NT, NSRC, PF, VPL, WAVES>), grid,
                      dim3(64 * WAVES), pad, st, A, X[0], X[1], X[2], P, p.m, p.n,
-                     p.n / (4 * VPL * E), S, gx, xmap, gate, epoch, pub);
+                     p.n / (4 * VPL * E), S, gx, xmap, gate, epoch, pub, nullptr);
 }
 
 template <typename T, int NT, int NSRC, int MT, int PF, int VPL, int WAVES, int BAR>
@@ -1612,7 +1670,8 @@ static void ax_lds2_go(const GemmPlan& p, int S, const T* A, const T* const* X, 
 // kind 5 codes: 5 MT PF VPL WAVES; kind 6 (pipelined X): 6 MT PF VPL WAVES
 template <typename T, int NT, int NSRC>
 static void ax_lds_code(const GemmPlan& p, int code, int S, const T* A, const T* const* X, T* P,
-                        const int* gate, int epoch, hipStream_t st, Pub pub) {
+                        const int* gate, int epoch, hipStream_t st, Pub pub,
+                        const uint8_t* sf) {
   if (pub.host != nullptr && code / 10000 != 5)
     throw Error{GLX_E_INVALID, "A@X: only the kind-5 LDS tile carries the scalar packet"};
   switch (code) {
@@ -1622,25 +1681,25 @@ static void ax_lds_code(const GemmPlan& p, int code, int S, const T* A, const T*
     case 72428: ax_lds3_go<T, NT, NSRC, 2, 4, 2, 8, 2>(p, S, A, X, P, gate, epoch, st); return;   // barrier / 2
     case 72424: ax_lds3_go<T, NT, NSRC, 2, 4, 2, 4, 2>(p, S, A, X, P, gate, epoch, st); return;
     case 72828: ax_lds3_go<T, NT, NSRC, 2, 8, 2, 8, 4>(p, S, A, X, P, gate, epoch, st); return;   // barrier / 4
-    case 52428: ax_lds_go<T, NT, NSRC, 2, 4, 2, 8>(p, S, A, X, P, gate, epoch, st, pub); return;
+    case 52428: ax_lds_go<T, NT, NSRC, 2, 4, 2, 8>(p, S, A, X, P, gate, epoch, st, pub, sf); return;
     default: break;
   }
   switch (code) {
-    case 52324: ax_lds_go<T, NT, NSRC, 2, 3, 2, 4>(p, S, A, X, P, gate, epoch, st, pub); break;
-    case 54228: ax_lds_go<T, NT, NSRC, 4, 2, 2, 8>(p, S, A, X, P, gate, epoch, st, pub); break;
-    case 54218: ax_lds_go<T, NT, NSRC, 4, 2, 1, 8>(p, S, A, X, P, gate, epoch, st, pub); break;
-    case 52228: ax_lds_go<T, NT, NSRC, 2, 2, 2, 8>(p, S, A, X, P, gate, epoch, st, pub); break;
+    case 52324: ax_lds_go<T, NT, NSRC, 2, 3, 2, 4>(p, S, A, X, P, gate, epoch, st, pub, sf); break;
+    case 54228: ax_lds_go<T, NT, NSRC, 4, 2, 2, 8>(p, S, A, X, P, gate, epoch, st, pub, sf); break;
+    case 54218: ax_lds_go<T, NT, NSRC, 4, 2, 1, 8>(p, S, A, X, P, gate, epoch, st, pub, sf); break;
+    case 52228: ax_lds_go<T, NT, NSRC, 2, 2, 2, 8>(p, S, A, X, P, gate, epoch, st, pub, sf); break;
     // one 16-row tile per wave: twice the row tiles, half the K splits and partial slabs
-    case 51228: ax_lds_go<T, NT, NSRC, 1, 2, 2, 8>(p, S, A, X, P, gate, epoch, st, pub); break;
-    case 51328: ax_lds_go<T, NT, NSRC, 1, 3, 2, 8>(p, S, A, X, P, gate, epoch, st, pub); break;
-    case 51224: ax_lds_go<T, NT, NSRC, 1, 2, 2, 4>(p, S, A, X, P, gate, epoch, st, pub); break;
-    case 52328: ax_lds_go<T, NT, NSRC, 2, 3, 2, 8>(p, S, A, X, P, gate, epoch, st, pub); break;
-    case 52218: ax_lds_go<T, NT, NSRC, 2, 2, 1, 8>(p, S, A, X, P, gate, epoch, st, pub); break;
-    case 54224: ax_lds_go<T, NT, NSRC, 4, 2, 2, 4>(p, S, A, X, P, gate, epoch, st, pub); break;
-    case 52214: ax_lds_go<T, NT, NSRC, 2, 2, 1, 4>(p, S, A, X, P, gate, epoch, st, pub); break;
-    case 54214: ax_lds_go<T, NT, NSRC, 4, 2, 1, 4>(p, S, A, X, P, gate, epoch, st, pub); break;
+    case 51228: ax_lds_go<T, NT, NSRC, 1, 2, 2, 8>(p, S, A, X, P, gate, epoch, st, pub, sf); break;
+    case 51328: ax_lds_go<T, NT, NSRC, 1, 3, 2, 8>(p, S, A, X, P, gate, epoch, st, pub, sf); break;
+    case 51224: ax_lds_go<T, NT, NSRC, 1, 2, 2, 4>(p, S, A, X, P, gate, epoch, st, pub, sf); break;
+    case 52328: ax_lds_go<T, NT, NSRC, 2, 3, 2, 8>(p, S, A, X, P, gate, epoch, st, pub, sf); break;
+    case 52218: ax_lds_go<T, NT, NSRC, 2, 2, 1, 8>(p, S, A, X, P, gate, epoch, st, pub, sf); break;
+    case 54224: ax_lds_go<T, NT, NSRC, 4, 2, 2, 4>(p, S, A, X, P, gate, epoch, st, pub, sf); break;
+    case 52214: ax_lds_go<T, NT, NSRC, 2, 2, 1, 4>(p, S, A, X, P, gate, epoch, st, pub, sf); break;
+    case 54214: ax_lds_go<T, NT, NSRC, 4, 2, 1, 4>(p, S, A, X, P, gate, epoch, st, pub, sf); break;
     default:   // 52224
-      ax_lds_go<T, NT, NSRC, 2, 2, 2, 4>(p, S, A, X, P, gate, epoch, st, pub);
+      ax_lds_go<T, NT, NSRC, 2, 2, 2, 4>(p, S, A, X, P, gate, epoch, st, pub, sf);
       break;
   }
 }
@@ -1648,12 +1707,12 @@ static void ax_lds_code(const GemmPlan& p, int code, int S, const T* A, const T*
 // One source: the swept variant. Batched sources (2, 3) use fixed register-feasible tiles.
 template <typename T, int NT>
 static void ax_mfma_nt(const GemmPlan& p, int nsrc, const T* A, const T* const* X, T* P,
-                       const int* gate, int epoch, hipStream_t st, Pub pub) {
+                       const int* gate, int epoch, hipStream_t st, Pub pub, const uint8_t* sf) {
   const int code = p.axb_code[nsrc];
   if (code / 10000 >= 5 && code / 10000 <= 7) {
-    if (nsrc == 1) ax_lds_code<T, NT, 1>(p, code, p.axb_S[1], A, X, P, gate, epoch, st, pub);
-    else if (nsrc == 2) ax_lds_code<T, NT, 2>(p, code, p.axb_S[2], A, X, P, gate, epoch, st, pub);
-    else ax_lds_code<T, NT, 3>(p, code, p.axb_S[3], A, X, P, gate, epoch, st, pub);
+    if (nsrc == 1) ax_lds_code<T, NT, 1>(p, code, p.axb_S[1], A, X, P, gate, epoch, st, pub, nullptr);
+    else if (nsrc == 2) ax_lds_code<T, NT, 2>(p, code, p.axb_S[2], A, X, P, gate, epoch, st, pub, sf);
+    else ax_lds_code<T, NT, 3>(p, code, p.axb_S[3], A, X, P, gate, epoch, st, pub, nullptr);
     return;
   }
   if (pub.host != nullptr) throw Error{GLX_E_INVALID, "A@X: this tile cannot carry the scalar packet"};
@@ -1716,7 +1775,7 @@ bool ax_pub_ok(const GemmPlan& p, int nsrc) {
 
 template <typename T>
 void launch_ax(const GemmPlan& p, int nsrc, const T* A, const T* const* X, T* P, const int* gate,
-               int epoch, hipStream_t st, Pub pub) {
+               int epoch, hipStream_t st, Pub pub, const uint8_t* sf) {
   if (pub.host != nullptr && !ax_pub_ok(p, nsrc))
     throw Error{GLX_E_INVALID, "A@X: this plan cannot carry the scalar packet"};
   if (p.ax_kind == 3) {
@@ -1725,8 +1784,8 @@ void launch_ax(const GemmPlan& p, int nsrc, const T* A, const T* const* X, T* P,
     else ax_valu_src<T, 3>(p, A, X, P, gate, epoch, st);
     return;
   }
-  if (p.l == 16) ax_mfma_nt<T, 1>(p, nsrc, A, X, P, gate, epoch, st, pub);
-  else ax_mfma_nt<T, 2>(p, nsrc, A, X, P, gate, epoch, st, pub);
+  if (p.l == 16) ax_mfma_nt<T, 1>(p, nsrc, A, X, P, gate, epoch, st, pub, sf);
+  else ax_mfma_nt<T, 2>(p, nsrc, A, X, P, gate, epoch, st, pub, sf);
 }
 
 template <typename T, int LB>
@@ -1783,8 +1842,8 @@ void launch_atr(const GemmPlan& p, const T* A, const T* R, T* Gp, hipStream_t st
   else atr_mfma_nt<T, 2>(p, A, R, Gp, st);
 }
 
-template void launch_ax<double>(const GemmPlan&, int, const double*, const double* const*, double*, const int*, int, hipStream_t, Pub);
-template void launch_ax<float>(const GemmPlan&, int, const float*, const float* const*, float*, const int*, int, hipStream_t, Pub);
+template void launch_ax<double>(const GemmPlan&, int, const double*, const double* const*, double*, const int*, int, hipStream_t, Pub, const uint8_t*);
+template void launch_ax<float>(const GemmPlan&, int, const float*, const float* const*, float*, const int*, int, hipStream_t, Pub, const uint8_t*);
 bool atr_prox_ok(const GemmPlan& p) {
   return p.atr_kind == 1 && p.atr_wl == 0 && p.atr_S >= 1 && p.atr_S <= 8 &&
          (p.l == 16 || p.l == 32) && p.n % 64 == 0 &&
@@ -1795,37 +1854,37 @@ bool atr_prox_ok(const GemmPlan& p) {
 template <typename T, int NT, int PF, bool NTL>
 static void atr_prox_go(const GemmPlan& p, const T* A, const T* R, T* G, const T* x, T* pp,
                         T* pthr, T* z, double t, double mu, double thres, Red red, hipStream_t st,
-                        Pub pub, T* Gp, unsigned* pcnt) {
+                        Pub pub, T* Gp, unsigned* pcnt, uint8_t* zf) {
   const dim3 grid((unsigned)(p.n / 64 * p.atr_S + (pub.host ? 1 : 0)));
   if (p.atr_S > 1) {
     hipLaunchKernelGGL((k_atr_prox<T, NT, PF, NTL, true>), grid, dim3(256), 0, st, A, R, G, p.m,
-                       p.n, x, pp, pthr, z, t, t * mu, thres, red, pub, p.atr_S, Gp, pcnt);
+                       p.n, x, pp, pthr, z, t, t * mu, thres, red, pub, p.atr_S, Gp, pcnt, zf);
     return;
   }
   static const size_t pad = lds_pad(k_atr_prox<T, NT, PF, NTL, false>, "GLX_ATR_LDS_PAD");
   hipLaunchKernelGGL((k_atr_prox<T, NT, PF, NTL, false>), grid, dim3(256), pad, st, A, R, G, p.m,
-                     p.n, x, pp, pthr, z, t, t * mu, thres, red, pub, 1, Gp, pcnt);
+                     p.n, x, pp, pthr, z, t, t * mu, thres, red, pub, 1, Gp, pcnt, zf);
 }
 template <typename T, int NT>
 static void atr_prox_nt(const GemmPlan& p, const T* A, const T* R, T* G, const T* x, T* pp,
                         T* pthr, T* z, double t, double mu, double thres, Red red, hipStream_t st,
-                        Pub pub, T* Gp, unsigned* pcnt) {
+                        Pub pub, T* Gp, unsigned* pcnt, uint8_t* zf) {
   switch (p.atr_ntl * 100 + p.atr_pf) {
-    case 4: atr_prox_go<T, NT, 4, false>(p, A, R, G, x, pp, pthr, z, t, mu, thres, red, st, pub, Gp, pcnt); break;
-    case 6: atr_prox_go<T, NT, 6, false>(p, A, R, G, x, pp, pthr, z, t, mu, thres, red, st, pub, Gp, pcnt); break;
-    case 104: atr_prox_go<T, NT, 4, true>(p, A, R, G, x, pp, pthr, z, t, mu, thres, red, st, pub, Gp, pcnt); break;
-    case 108: atr_prox_go<T, NT, 8, true>(p, A, R, G, x, pp, pthr, z, t, mu, thres, red, st, pub, Gp, pcnt); break;
-    default: atr_prox_go<T, NT, 8, false>(p, A, R, G, x, pp, pthr, z, t, mu, thres, red, st, pub, Gp, pcnt); break;
+    case 4: atr_prox_go<T, NT, 4, false>(p, A, R, G, x, pp, pthr, z, t, mu, thres, red, st, pub, Gp, pcnt, zf); break;
+    case 6: atr_prox_go<T, NT, 6, false>(p, A, R, G, x, pp, pthr, z, t, mu, thres, red, st, pub, Gp, pcnt, zf); break;
+    case 104: atr_prox_go<T, NT, 4, true>(p, A, R, G, x, pp, pthr, z, t, mu, thres, red, st, pub, Gp, pcnt, zf); break;
+    case 108: atr_prox_go<T, NT, 8, true>(p, A, R, G, x, pp, pthr, z, t, mu, thres, red, st, pub, Gp, pcnt, zf); break;
+    default: atr_prox_go<T, NT, 8, false>(p, A, R, G, x, pp, pthr, z, t, mu, thres, red, st, pub, Gp, pcnt, zf); break;
   }
 }
 template <typename T>
 void launch_atr_prox(const GemmPlan& p, const T* A, const T* R, T* G, const T* x, T* pp, T* pthr,
                      T* z, double t, double mu, double thres, Red red, hipStream_t st, Pub pub,
-                     T* Gp, unsigned* pcnt) {
+                     T* Gp, unsigned* pcnt, uint8_t* zf) {
   if (p.atr_S > 1 && (Gp == nullptr || pcnt == nullptr))
     throw Error{GLX_E_INVALID, "fused A^T R with K splits needs slab and counter buffers"};
-  if (p.l == 16) atr_prox_nt<T, 1>(p, A, R, G, x, pp, pthr, z, t, mu, thres, red, st, pub, Gp, pcnt);
-  else atr_prox_nt<T, 2>(p, A, R, G, x, pp, pthr, z, t, mu, thres, red, st, pub, Gp, pcnt);
+  if (p.l == 16) atr_prox_nt<T, 1>(p, A, R, G, x, pp, pthr, z, t, mu, thres, red, st, pub, Gp, pcnt, zf);
+  else atr_prox_nt<T, 2>(p, A, R, G, x, pp, pthr, z, t, mu, thres, red, st, pub, Gp, pcnt, zf);
 }
 
 template <typename T, int NT, int PF, bool NTL>
@@ -1876,10 +1935,10 @@ template void launch_atr_fista<float>(const GemmPlan&, const float*, const float
                                       float*, unsigned*);
 template void launch_atr_prox<double>(const GemmPlan&, const double*, const double*, double*,
                                       const double*, double*, double*, double*, double, double,
-                                      double, Red, hipStream_t, Pub, double*, unsigned*);
+                                      double, Red, hipStream_t, Pub, double*, unsigned*, uint8_t*);
 template void launch_atr_prox<float>(const GemmPlan&, const float*, const float*, float*,
                                      const float*, float*, float*, float*, double, double, double,
-                                     Red, hipStream_t, Pub, float*, unsigned*);
+                                     Red, hipStream_t, Pub, float*, unsigned*, uint8_t*);
 template void launch_atr<float>(const GemmPlan&, const float*, const float*, float*, hipStream_t);
 
 }  // namespace glx

@@ -8,7 +8,8 @@
 // history is recorded on the device.
 //
 // Work per iteration (passes over A; reference counts from SURVEY §3):
-//   ProxGD  reference 5.7 A@x + 1 A^T r;  here 1 A@z per trial + 1 A^T r
+//   ProxGD  reference 5.7 A@x + 1 A^T r;  here 1 A@[e | p_thr] per trial + 1 A^T r (e: the
+//           entries the threshold zeroed, MFMAs on flagged K chunks only)
 //           (+1 A@x when the hard threshold changed x, +1 A@x in exact_objective mode)
 //   FProxGD reference 4 A@x + 1 A^T r;    here 1 A@y + 1 A@x per trial + 1 A^T r
 //   SGD/GD  reference 2 A@x + 1 A^T r;    here 1 A@x (+1 when the threshold changed x) + 1 A^T r
@@ -106,6 +107,21 @@ static void validate(const glx_problem* P, const glx_opts* O) {
 // is ≈13 µs slower but the trial launch and its boundary go. Same box: C3 (8192,16384,32)
 // FProxGD 3669–3691 → 3743–3749 it/s, ProxGD 3654–3657 → 3744–3752, FProxGD at (4096,8192,16)
 // 11 362–11 366 → 13 200–13 215 (profiles/r1_tuning/small_kernels/atr_f32_fused.log).
+// Split-candidate ProxGD (the fast objective mode, see iter_proxgd): 0 = off (exact mode, other
+// methods, or GLX_SPLIT_CAND=0: the dense [z | p_thr] batch of round 1); 1 = A e from the
+// transposed copy of A (kernels_gather.hip, the default); 2 = A e by skipping unflagged K
+// chunks inside the batched A@X tile (GLX_SPLIT_CAND=sp).
+// fp64 only: in fp32 the regrouped sum (A p_thr - b) + A e moves f by ~1e-6 relative on short
+// unconverged runs (measured 1.5e-6 on mid_384x640x16 against the 1e-6 fp32 bar), and no fp32
+// ProxGD configuration is on the benchmark path.
+static int split_mode(const glx_problem& P, const glx_opts& O) {
+  if (P.method != GLX_PROXGD || O.exact_objective != 0 || P.dtype != GLX_F64) return 0;
+  const char* sc = std::getenv("GLX_SPLIT_CAND");
+  if (sc && std::strcmp(sc, "0") == 0) return 0;
+  if (sc && std::strcmp(sc, "sp") == 0) return 2;
+  return gather_ok(P.n, P.l) ? 1 : 2;
+}
+
 static GemmPlan session_plan(const glx_problem& P, const glx_opts& O) {
   const int es = P.dtype == GLX_F64 ? 8 : 4;
   GemmPlan p = make_plan(es, P.m, P.n, P.l, O.ax_variant);
@@ -139,8 +155,8 @@ template <typename T>
 class Session : public SessionBase {
  public:
   // workspace layout; with ws == nullptr only computes the size
-  static size_t carve(const glx_problem& P, const GemmPlan& plan, int64_t fh_cap, void* ws,
-                      Session* s) {
+  static size_t carve(const glx_problem& P, const GemmPlan& plan, int64_t fh_cap, int smode,
+                      void* ws, Session* s) {
     Carver c(ws);
     const int64_t nl = P.n * P.l, ml = P.m * P.l;
     const int nb = method_bufs(P.method);
@@ -155,13 +171,19 @@ class Session : public SessionBase {
       g[k] = static_cast<T*>(c.take(sizeof(T) * nl + kTailBytes));   // + scalar tail (comm)
       gp[k] = plan.atr_S > 1 ? static_cast<T*>(c.take(sizeof(T) * nl * plan.atr_S)) : g[k];
     }
-    T* pp = static_cast<T*>(c.take(sizeof(T) * ml * ax_split_max(plan) * 3));   // up to 3 batched sources
+    // A@X slabs of up to 3 batched sources; split-candidate gather: the A e slabs + A p_thr's
+    const int64_t pslabs = std::max<int64_t>((int64_t)ax_split_max(plan) * 3,
+                                             smode == 1 ? gather_split(P.m) + ax_split(plan, 1) : 0);
+    T* pp = static_cast<T*>(c.take(sizeof(T) * ml * pslabs));
+    T* at = smode == 1 ? static_cast<T*>(c.take(sizeof(T) * P.m * P.n)) : nullptr;   // A^T
     double* scal = static_cast<double*>(c.take(sizeof(double) * NSCAL_DEV));
     double* part = static_cast<double*>(c.take(sizeof(double) * kMaxRedVals * kMaxBlocks));
     unsigned* ticket = static_cast<unsigned*>(c.take(kTicketBytes));
     // per-panel arrival counters of the fused A^T R with K splits (atr_split_combine)
     unsigned* pcnt = static_cast<unsigned*>(c.take(sizeof(unsigned) * (P.n / 64 + 64)));
     int* flag = static_cast<int*>(c.take(256));
+    // split-candidate mode: row flags of e = p - p_thr (z's buffer), read in chunks of up to 32
+    uint8_t* zf = static_cast<uint8_t*>(c.take((size_t)((P.n + 255) / 256) * 256));
     double* fh = static_cast<double*>(c.take(sizeof(double) * (fh_cap + 1)));
     double* sp100 = static_cast<double*>(c.take(sizeof(double) * (fh_cap / 100 + 2)));
     const int gb = gemv_blocks_for(P);
@@ -170,9 +192,10 @@ class Session : public SessionBase {
       for (int i = 0; i < kBufs; ++i) s->X_[i] = bufs[i];
       for (int i = 0; i < kRes; ++i) s->R_[i] = res[i];
       for (int k = 0; k < 2; ++k) { s->Gs_[k] = g[k]; s->Gps_[k] = gp[k]; }
-      s->G_ = g[0]; s->Gp_ = gp[0]; s->Pp_ = pp;
+      s->G_ = g[0]; s->Gp_ = gp[0]; s->Pp_ = pp; s->At_ = at;
       s->scal_ = scal; s->part_ = part; s->ticket_ = ticket; s->flag_ = flag; s->fh_dev_ = fh;
       s->pcnt_ = pcnt;
+      s->zf_ = zf;
       s->sp100_ = sp100;
       s->gemv_slabs_ = gs;
       s->gemv_blocks_ = gb;
@@ -202,10 +225,11 @@ class Session : public SessionBase {
     plan_ = session_plan(P, O);
     comm_ = static_cast<glx_comm*>(P.comm);
     fh_cap_ = fh_capacity(P, O);
-    const size_t need = carve(P, plan_, fh_cap_, nullptr, nullptr);
+    smode_ = split_mode(P, O);
+    const size_t need = carve(P, plan_, fh_cap_, smode_, nullptr, nullptr);
     if (!ws || ws_bytes < need) throw Error{GLX_E_WORKSPACE, "workspace too small: need " + std::to_string(need) + " bytes"};
     if (reinterpret_cast<uintptr_t>(ws) & 255) throw Error{GLX_E_WORKSPACE, "workspace must be 256-byte aligned"};
-    carve(P, plan_, fh_cap_, ws, this);
+    carve(P, plan_, fh_cap_, smode_, ws, this);
     A_ = static_cast<const T*>(P.A);
     B_ = static_cast<const T*>(P.b);
     // scalar packet: host-mapped, coherent memory the GPU writes directly (k_publish)
@@ -233,6 +257,11 @@ class Session : public SessionBase {
                           (O.step_type == GLX_STEP_LINE_SEARCH || O.step_type == GLX_STEP_FIXED) &&
                           !(fz && std::strcmp(fz, "0") == 0);
     fused_ok_ = fuse_any && P.method == GLX_PROXGD;
+    // ProxGD's fast objective mode evaluates the candidate as A p = A p_thr + A e, e = p - p_thr
+    // nonzero only where the hard threshold zeroed p (see iter_proxgd, split_mode)
+    emode_ = smode_ != 0;
+    gsplit_ = gather_split(m_);
+    if (smode_ == 1) launch_transpose<T>(static_cast<const T*>(P.A), At_, m_, n_, st_);   // once
     fused_fista_ok_ = fuse_any && P.method == GLX_FPROXGD;
     GLX_HIP(hipMemsetAsync(ticket_, 0, kTicketBytes, st_));
     GLX_HIP(hipMemsetAsync(pcnt_, 0, sizeof(unsigned) * (P.n / 64 + 64), st_));
@@ -418,16 +447,25 @@ class Session : public SessionBase {
   // gradient all-reduce and publish (atr_prox / atr_fista), saving one all-reduce per iteration.
   // skip_ax: the slabs are already in Pp_ (queued speculatively with the trial, spec_ax);
   // only the finalize runs.
+  // chain (split-candidate ProxGD trial, nsrc = 2): xs = [e | p_thr] with e flagged by zf_;
+  // the finalize forms A p - b = (A p_thr - b) + A e and keeps only its sum (rs[0] unused).
   void residuals(int nsrc, const T* const* xs, T* const* rs, int slot, const T* cx = nullptr,
                  const double* cmax = nullptr, double* fh = nullptr, double fh_mu = 0.0,
                  unsigned* pub_seq = nullptr, double* defer = nullptr, bool skip_ax = false,
-                 bool snap_trial = false) {
-    if (!skip_ax) spec_ax(nsrc, xs);
-    launch_finalize_residual<T>(Pp_, ax_split(plan_, nsrc), B_, nsrc, rs, ml_, nullptr, 0, 1, cx,
+                 bool snap_trial = false, bool chain = false) {
+    const bool gat = chain && smode_ == 1;
+    if (!skip_ax) {
+      if (gat) cand_ax(xs);
+      else spec_ax(nsrc, xs, Pub{}, chain ? zf_ : nullptr);
+    }
+    T* rsc[3] = {chain ? nullptr : rs[0], rs[1], rs[2]};
+    launch_finalize_residual<T>(Pp_, gat ? ax_split(plan_, 1) : ax_split(plan_, nsrc), B_, nsrc, rsc,
+                                ml_, nullptr, 0, 1, cx,
                                 cx ? nl_ : 0, cmax, comm_ ? nullptr : fh, fh_mu, scal_ + S_DRN,
                                 defer ? Red{part_, ticket_, defer} : red(slot), st_,
                                 snap_trial ? scal_ + S_TR : nullptr,
-                                snap_trial ? scal_ + S_SNAP : nullptr, snap_trial ? 6 : 0);
+                                snap_trial ? scal_ + S_SNAP : nullptr, snap_trial ? 6 : 0,
+                                chain ? 1 : 0, gat ? gsplit_ : 0);
     check_launch();
     if (defer) return;
     if (comm_) {
@@ -440,13 +478,27 @@ class Session : public SessionBase {
     if (pub_seq != nullptr) *pub_seq = post_readback();
   }
   // A @ [xs] into the slabs Pp_; pb: the launch also carries that scalar packet (ax_pub_ok)
-  void spec_ax(int nsrc, const T* const* xs, Pub pb = Pub{}) {
+  void spec_ax(int nsrc, const T* const* xs, Pub pb = Pub{}, const uint8_t* sf = nullptr) {
     hipEvent_t e0 = prof_begin(0);
-    launch_ax<T>(plan_, nsrc, A_, xs, Pp_, nullptr, 0, st_, pb);
+    launch_ax<T>(plan_, nsrc, A_, xs, Pp_, nullptr, 0, st_, pb, sf);
     check_launch();
     prof_end(0, e0);
     ++ax_calls_;
-    ax_cols_ += nsrc;
+    ax_cols_ += sf ? nsrc - 1 : nsrc;   // dense right-hand sides (the flagged e is counted apart)
+  }
+  // Split-candidate trial, gather form: A p_thr (one dense source, slabs behind the A e slabs)
+  // and A e from the transposed copy (gsplit_ slabs at Pp_); xs = [e | p_thr]. Timed as one
+  // A@X (kind 0). pb: the dense launch carries that scalar packet.
+  void cand_ax(const T* const* xs, Pub pb = Pub{}) {
+    hipEvent_t e0 = prof_begin(0);
+    const T* xd[3] = {xs[1], nullptr, nullptr};
+    launch_ax<T>(plan_, 1, A_, xd, Pp_ + (size_t)gsplit_ * ml_, nullptr, 0, st_, pb);
+    check_launch();
+    launch_at_gather<T>(At_, xs[0], zf_, m_, n_, l_, Pp_, gsplit_, st_);
+    check_launch();
+    prof_end(0, e0);
+    ++ax_calls_;
+    ax_cols_ += 1;
   }
   void residual1(const T* x, T* r, int slot, const T* cx = nullptr, const double* cmax = nullptr,
                  unsigned* pub_seq = nullptr) {
@@ -672,14 +724,20 @@ class Session : public SessionBase {
     auto trial = [&](double tt, bool first) {
       launch_prox_pgd<T>(xt, first ? g.first : G_, first ? g.second : 1,
                          (first && g.first != G_) ? G_ : nullptr, X_[ip_], X_[ipt_], X_[iz_], n_,
-                         l_, tt, mu_, O_.thres, red(S_TR), st_);
+                         l_, tt, mu_, O_.thres, red(S_TR), st_, Pub{}, ezf());
       check_launch();
     };
     if (ls) {
       t = t0;
       for (int it = 0; it < O_.ls_maxit; ++it) {
         if (!(it == 0 && first_done)) trial(t, it == 0);
-        // one pass: g(z) for the test (:91) + the next iteration's residuals A p_thr (and A p)
+        // one pass: the candidate's g for the test (:91) + the next iteration's residual
+        // A p_thr (exact mode: g(z) and A p as a third source). Split-candidate mode (emode_,
+        // the default fast mode): the batch is [e | p_thr], e = p - p_thr, and the test and the
+        // next objective use g(p) = 1/2 ||(A p_thr - b) + A e||^2. z = x - t G_t equals p up to
+        // the rounding of x - t((x - p)/t), the same order as the GEMMs' own summation-order
+        // differences, while e is nonzero only in the rows the hard threshold touched, so A e
+        // costs MFMAs only on those K chunks (k_ax_lds SP) instead of a second dense source.
         const T* xs[3] = {X_[iz_], X_[ipt_], X_[ip_]};
         T* rs[3] = {R_[rz], R_[rpt], R_[rp]};
         const int nsrc = exact ? 3 : 2;
@@ -694,9 +752,9 @@ class Session : public SessionBase {
         // queued right behind it and carries this trial's packet, whose trial sums (which
         // that k_prox_pgd overwrites) come from a snapshot this finalize takes
         const bool axp = spec && fused_ok_ && comm_ != nullptr && late_pub && attach_ok_ &&
-                         spec_ax_pub_ && ax_pub_ok(plan_, nsrc);
+                         spec_ax_pub_ && ax_pub_ok(plan_, smode_ == 1 ? 1 : nsrc);
         residuals(nsrc, xs, rs, S_RT, X_[ip_], scal_ + S_TR + 3, nullptr, 0.0,
-                  late_pub ? nullptr : &seq, merge ? tail(1 - gset_) : nullptr, skip_ax, axp);
+                  late_pub ? nullptr : &seq, merge ? tail(1 - gset_) : nullptr, skip_ax, axp, emode_);
         std::pair<const T*, int> sg;
         if (spec && fused_ok_) {
           // the next iteration's A^T r and first trial at the candidate p_thr, into the other
@@ -710,7 +768,8 @@ class Session : public SessionBase {
             pbx.off3 = S_TR;
             pbx.n3 = 6;
             const T* sx[3] = {X_[iz_], X_[if2_], X_[if1_]};   // [z | p_thr | p] of that trial
-            spec_ax(nsrc, sx, pbx);
+            if (smode_ == 1) cand_ax(sx, pbx);
+            else spec_ax(nsrc, sx, pbx, ezf());
             ax_queued_ = true;
           }
         } else if (spec) {
@@ -741,9 +800,11 @@ class Session : public SessionBase {
       stats_[2] += 1;
       irg_ = rpt;
       gx_ = 0.5 * hs_[S_RT + 1];
-      // exact: A p from the batch; fast: A z - b (z = x - t G_t is ulp-close to p) unless the
+      // exact: A p from the batch; split-candidate: A p - b = (A p_thr - b) + A e; dense z
+      // batch (GLX_SPLIT_CAND=0): A z - b (z = x - t G_t is ulp-close to p) unless the
       // threshold changed nothing, in which case A p_thr - b == A p - b exactly
-      const double sq_x = exact ? hs_[S_RT + 2] : (hs_[S_TR + 4] == 0 ? hs_[S_RT + 1] : hs_[S_RT]);
+      const double sq_x = exact ? hs_[S_RT + 2]
+                                : ((emode_ || hs_[S_TR + 4] != 0) ? hs_[S_RT] : hs_[S_RT + 1]);
       f_cur_ = 0.5 * sq_x + P_.mu0 * hs_[S_TR + 2];
       s_cur_ = hs_[S_RT + 3] / (double)nl_;
       state_valid_ = true;
@@ -782,7 +843,7 @@ class Session : public SessionBase {
       else if (pub_seq && attach_ok_) pb = make_pub(extra, pub_seq);
       else if (pub_seq) *pub_seq = post_readback(extra);
       launch_prox_pgd<T>(x, g.first, g.second, nullptr, X_[op], X_[opt], X_[oz], n_, l_, t, mu_,
-                         O_.thres, red(S_TR), st_, pb);
+                         O_.thres, red(S_TR), st_, pb, ezf());
       check_launch();
       return;
     }
@@ -790,7 +851,7 @@ class Session : public SessionBase {
     if (pub_seq) pb = make_pub(extra, pub_seq);
     hipEvent_t e0 = prof_begin(1);
     launch_atr_prox<T>(plan_, A_, r, Gs_[set], x, X_[op], X_[opt], X_[oz], t, mu_, O_.thres,
-                       red(S_TR), st_, pb, Gps_[set], pcnt_);
+                       red(S_TR), st_, pb, Gps_[set], pcnt_, ezf());
     check_launch();
     prof_end(1, e0);
     ++atr_calls_;
@@ -1040,6 +1101,11 @@ class Session : public SessionBase {
   unsigned *hseq_ = nullptr, *hseq_dev_ = nullptr;
   unsigned* ticket_ = nullptr;
   unsigned* pcnt_ = nullptr;   // per-panel counters (fused A^T R with K splits)
+  uint8_t* zf_ = nullptr;      // row flags of e (split-candidate ProxGD)
+  T* At_ = nullptr;            // A^T (split-candidate gather form)
+  int smode_ = 0, gsplit_ = 1;
+  bool emode_ = false;         // split-candidate ProxGD: trials write e = p - p_thr, not z
+  uint8_t* ezf() const { return emode_ ? zf_ : nullptr; }
   int* flag_ = nullptr;
   int64_t fh_cap_ = 0;
   double* sp100_ = nullptr;   // SGD/GD: count(|x| > 1e-6 max|x|) after every 100th iteration
@@ -1088,9 +1154,10 @@ class Session : public SessionBase {
 
 static size_t session_bytes(const glx_problem& P, const glx_opts& O) {
   const GemmPlan plan = session_plan(P, O);
+  const int sm = split_mode(P, O);
   if (P.dtype == GLX_F64)
-    return Session<double>::carve(P, plan, Session<double>::fh_capacity(P, O), nullptr, nullptr);
-  return Session<float>::carve(P, plan, Session<float>::fh_capacity(P, O), nullptr, nullptr);
+    return Session<double>::carve(P, plan, Session<double>::fh_capacity(P, O), sm, nullptr, nullptr);
+  return Session<float>::carve(P, plan, Session<float>::fh_capacity(P, O), sm, nullptr, nullptr);
 }
 
 template <typename F>
