@@ -132,6 +132,19 @@ template <typename T>
 void launch_at_gather(const T* At, const T* E, const uint8_t* zf, int64_t m, int64_t n, int64_t l,
                       T* P, int S, hipStream_t st);
 
+// ---- fused residual + gradient in one pass over A (kernels_fused.hip) ----
+// Sraw = A X (m x 32) and Gs[RG][n][32] with G = A^T (A X - B) = sum of the RG slabs in order.
+// resgrad_shape_ok: fp64, l = 32, n % 512 == 0, m % (16 RG) == 0; resgrad_device_ok: all 256
+// workgroups can be resident (>= 256 CUs). ws: resgrad_ws_bytes; its counters must be zeroed
+// (resgrad_reset) before launch_count 1, and launch_count must grow by one per launch.
+bool resgrad_shape_ok(int esize, int64_t m, int64_t n, int64_t l);
+bool resgrad_device_ok();
+int resgrad_groups(int64_t n);
+size_t resgrad_ws_bytes(int64_t m, int64_t n);
+void resgrad_reset(void* ws, int64_t m, int64_t n, hipStream_t st);
+void launch_resgrad(const double* A, const double* X, const double* B, double* Sraw, double* Gs,
+                    void* ws, unsigned launch_count, int64_t m, int64_t n, int* err, hipStream_t st);
+
 // ---- row / elementwise kernels (kernels_elem.hip) ----
 // Gradient inputs `g` with an `S` argument are S split-K slabs of n*l values summed in slab
 // order on the fly (S = 1: an already-summed array).

@@ -20,6 +20,8 @@
 // finalize kernel, which forms A p - b = (A p_thr - b) + sum_s P[s].
 #include <hip/hip_runtime.h>
 
+#include <cstdlib>
+
 #include "glx.h"
 #include "glx_device.h"
 
@@ -47,7 +49,6 @@ template <> struct GM<float> {
 constexpr int kGW = 4;                  // waves per workgroup
 constexpr int kGThreads = 64 * kGW;
 constexpr int kGMT = 4;                 // 16-row tiles per wave (64 output rows)
-constexpr int kGPF = 4;                 // k-steps in flight per wave
 constexpr int kGRows = 16 * kGMT * kGW; // output rows per workgroup
 }  // namespace
 
@@ -74,7 +75,8 @@ __global__ __launch_bounds__(256) void k_transpose(const T* __restrict__ A, T* _
 }
 
 // grid: gx row blocks x S splits of the flagged-row list (blockIdx.x = split * gx + row block)
-template <typename T, int NT>
+// PF k-steps in flight per wave (2 KiB of At each at l = 32, f64)
+template <typename T, int NT, int kGPF>
 __global__ __launch_bounds__(kGThreads) void k_at_gather(const T* __restrict__ At,
                                                          const T* __restrict__ E,
                                                          const uint8_t* __restrict__ zf,
@@ -188,11 +190,18 @@ __global__ __launch_bounds__(kGThreads) void k_at_gather(const T* __restrict__ A
     }
 }
 
+static int genv(const char* name, int dflt) {
+  const char* v = std::getenv(name);
+  return (v && *v) ? std::atoi(v) : dflt;
+}
+
+// K splits of the flagged-row list: about kGatherBlocks workgroups (GLX_GATHER_BLOCKS)
+static constexpr int kGatherBlocks = 512;
 int gather_split(int64_t m) {
   const int64_t gx = (m + kGRows - 1) / kGRows;
-  int64_t s = 256 / gx;
+  int64_t s = genv("GLX_GATHER_BLOCKS", kGatherBlocks) / gx;
   if (s < 1) s = 1;
-  if (s > 16) s = 16;
+  if (s > 32) s = 32;
   return (int)s;
 }
 
@@ -210,20 +219,24 @@ void launch_at_gather(const T* At, const T* E, const uint8_t* zf, int64_t m, int
   if (!gather_ok(n, l)) throw Error{GLX_E_INVALID, "A e gather: needs l in {16, 32} and n < 65536"};
   const int gx = (int)((m + kGRows - 1) / kGRows);
   const size_t lds = sizeof(unsigned short) * (size_t)n;
-  static bool attr = false;
-  if (!attr) {   // the list can exceed the default 64 KiB dynamic LDS limit only past n = 32768
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(k_at_gather<T, 2>),
-                              hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024 - 64);
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(k_at_gather<T, 1>),
-                              hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024 - 64);
-    attr = true;
+  static const int pf = genv("GLX_GATHER_PF", 8);
+  auto go = [&](auto kern) {
+    static bool attr = false;
+    if (!attr) {   // the list exceeds the default 64 KiB dynamic LDS limit only past n = 32768
+      (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kern),
+                                hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024 - 64);
+      attr = true;
+    }
+    hipLaunchKernelGGL(kern, dim3((unsigned)(gx * S)), dim3(kGThreads), lds, st, At, E, zf, m, n, P,
+                       S, gx);
+  };
+  if (l == 32) {
+    if (pf == 4) go(k_at_gather<T, 2, 4>);
+    else go(k_at_gather<T, 2, 8>);
+  } else {
+    if (pf == 4) go(k_at_gather<T, 1, 4>);
+    else go(k_at_gather<T, 1, 8>);
   }
-  if (l == 32)
-    hipLaunchKernelGGL((k_at_gather<T, 2>), dim3((unsigned)(gx * S)), dim3(kGThreads), lds, st, At, E,
-                       zf, m, n, P, S, gx);
-  else
-    hipLaunchKernelGGL((k_at_gather<T, 1>), dim3((unsigned)(gx * S)), dim3(kGThreads), lds, st, At, E,
-                       zf, m, n, P, S, gx);
 }
 
 template void launch_transpose<double>(const double*, double*, int64_t, int64_t, hipStream_t);

@@ -1180,6 +1180,7 @@ static int guarded(F&& f) {
 // ---- single-kernel workspace: P slabs + Gp slabs + reduction scratch
 struct KernelWs {
   void* pp; void* gp; double* part; unsigned* ticket; double* scal;
+  void* rg_ws; double* rg_s; double* rg_g; int* rg_err;   // fused residual-gradient pass
 };
 static size_t kernel_ws(int es, const GemmPlan& p, void* base, KernelWs* out) {
   Carver c(base);
@@ -1193,7 +1194,16 @@ static size_t kernel_ws(int es, const GemmPlan& p, void* base, KernelWs* out) {
   double* part = static_cast<double*>(c.take(sizeof(double) * kMaxRedVals * kMaxBlocks));
   unsigned* ticket = static_cast<unsigned*>(c.take(kTicketBytes));
   double* scal = static_cast<double*>(c.take(sizeof(double) * NSCAL));
-  if (out) *out = KernelWs{pp, gp, part, ticket, scal};
+  void* rg_ws = nullptr;
+  double *rg_s = nullptr, *rg_g = nullptr;
+  int* rg_err = nullptr;
+  if (resgrad_shape_ok(es, p.m, p.n, p.l)) {
+    rg_ws = c.take(resgrad_ws_bytes(p.m, p.n));
+    rg_s = static_cast<double*>(c.take(sizeof(double) * p.m * p.l));
+    rg_g = static_cast<double*>(c.take(sizeof(double) * p.n * p.l * resgrad_groups(p.n)));
+    rg_err = static_cast<int*>(c.take(256));
+  }
+  if (out) *out = KernelWs{pp, gp, part, ticket, scal, rg_ws, rg_s, rg_g, rg_err};
   return c.off + 256;
 }
 
@@ -1416,6 +1426,55 @@ int glx_gradient(int dtype, int64_t m, int64_t n, int64_t l, const void* A, cons
       launch_atr<double>(p, (const double*)A, (const double*)R, gp, st);
       if (p.atr_S > 1) launch_sum_partials<double>(gp, p.atr_S, (double*)G, n * l, st);
     } else {
+      float* gp = p.atr_S > 1 ? (float*)k.gp : (float*)G;
+      launch_atr<float>(p, (const float*)A, (const float*)R, gp, st);
+      if (p.atr_S > 1) launch_sum_partials<float>(gp, p.atr_S, (float*)G, n * l, st);
+    }
+    check_launch();
+  });
+}
+
+int glx_residual_gradient(int dtype, int64_t m, int64_t n, int64_t l, const void* A, const void* X,
+                          const void* B, void* R, void* G, void* ws, size_t wsb, int one_pass,
+                          int* fused_out, void* stream) {
+  return guarded([&] {
+    hipStream_t st = static_cast<hipStream_t>(stream);
+    GemmPlan p;
+    KernelWs k = kernel_setup(dtype, m, n, l, ws, wsb, 0, st, &p);
+    const bool fused = one_pass != 0 && dtype == GLX_F64 && k.rg_ws != nullptr && resgrad_device_ok();
+    if (fused_out) *fused_out = fused ? 1 : 0;
+    if (fused) {
+      resgrad_reset(k.rg_ws, m, n, st);
+      GLX_HIP(hipMemsetAsync(k.rg_err, 0, sizeof(int), st));
+      launch_resgrad((const double*)A, (const double*)X, (const double*)B, k.rg_s, k.rg_g, k.rg_ws, 1,
+                     m, n, k.rg_err, st);
+      double* rs[3] = {(double*)R, nullptr, nullptr};
+      launch_finalize_residual<double>(k.rg_s, 1, (const double*)B, 1, rs, m * l, nullptr, 0, 1,
+                                       nullptr, 0, nullptr, nullptr, 0.0, nullptr,
+                                       Red{k.part, k.ticket, k.scal}, st);
+      launch_sum_partials<double>(k.rg_g, resgrad_groups(n), (double*)G, n * l, st);
+      check_launch();
+      return;
+    }
+    const int es = dtype == GLX_F64 ? 8 : 4;
+    (void)es;
+    if (dtype == GLX_F64) {
+      const double* xs[3] = {(const double*)X, nullptr, nullptr};
+      double* rs[3] = {(double*)R, nullptr, nullptr};
+      launch_ax<double>(p, 1, (const double*)A, xs, (double*)k.pp, nullptr, 0, st);
+      launch_finalize_residual<double>((const double*)k.pp, p.ax_S, (const double*)B, 1, rs, m * l,
+                                       nullptr, 0, 1, nullptr, 0, nullptr, nullptr, 0.0, nullptr,
+                                       Red{k.part, k.ticket, k.scal}, st);
+      double* gp = p.atr_S > 1 ? (double*)k.gp : (double*)G;
+      launch_atr<double>(p, (const double*)A, (const double*)R, gp, st);
+      if (p.atr_S > 1) launch_sum_partials<double>(gp, p.atr_S, (double*)G, n * l, st);
+    } else {
+      const float* xs[3] = {(const float*)X, nullptr, nullptr};
+      float* rs[3] = {(float*)R, nullptr, nullptr};
+      launch_ax<float>(p, 1, (const float*)A, xs, (float*)k.pp, nullptr, 0, st);
+      launch_finalize_residual<float>((const float*)k.pp, p.ax_S, (const float*)B, 1, rs, m * l,
+                                      nullptr, 0, 1, nullptr, 0, nullptr, nullptr, 0.0, nullptr,
+                                      Red{k.part, k.ticket, k.scal}, st);
       float* gp = p.atr_S > 1 ? (float*)k.gp : (float*)G;
       launch_atr<float>(p, (const float*)A, (const float*)R, gp, st);
       if (p.atr_S > 1) launch_sum_partials<float>(gp, p.atr_S, (float*)G, n * l, st);

@@ -1,4 +1,5 @@
-"""Single-kernel entry points of libglx (``glx_residual`` / ``glx_gradient`` / ``glx_prox``).
+"""Single-kernel entry points of libglx (``glx_residual`` / ``glx_gradient`` / ``glx_prox`` /
+``glx_residual_gradient``).
 
 These are the dense products and the group prox of the reference iteration exposed one at a
 time — ``A @ x - b`` (gl_ProxGD_primal.py:25,61), ``A.T @ r`` (:129) and ``prox_th``
@@ -75,6 +76,24 @@ def gradient(A: torch.Tensor, R: torch.Tensor) -> torch.Tensor:
     check(lib().glx_gradient(dt, m, n, l, A.data_ptr(), R.data_ptr(), G.data_ptr(), ws.data_ptr(),
                              ws.numel(), _stream(A.device)))
     return G
+
+
+def residual_gradient(A: torch.Tensor, X: torch.Tensor, B: torch.Tensor, one_pass: bool = False
+                      ) -> Tuple[torch.Tensor, torch.Tensor, bool]:
+    """R = A X - B and G = A^T R: two passes over A (the faster path), or with one_pass=True
+    the fused kernel that reads A from HBM once, where the shape and device allow it.
+    Returns (R, G, one_pass_ran)."""
+    m, n = A.shape
+    l = X.shape[1]
+    dt = _dt(A)
+    R = torch.empty((m, l), dtype=A.dtype, device=A.device)
+    G = torch.empty((n, l), dtype=A.dtype, device=A.device)
+    ws = _ws(dt, m, n, l, A.device)
+    fused = ctypes.c_int(0)
+    check(lib().glx_residual_gradient(dt, m, n, l, A.data_ptr(), X.data_ptr(), B.data_ptr(),
+                                      R.data_ptr(), G.data_ptr(), ws.data_ptr(), ws.numel(),
+                                      1 if one_pass else 0, ctypes.byref(fused), _stream(A.device)))
+    return R, G, bool(fused.value)
 
 
 def prox(W: torch.Tensor, t: float, mu: float, thres: float = 1e-3

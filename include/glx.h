@@ -162,6 +162,15 @@ int glx_gradient(int dtype, int64_t m, int64_t n, int64_t l, const void* A, cons
  * sums_dev[1] = max |X_out| (device doubles). */
 int glx_prox(int dtype, int64_t n, int64_t l, const void* W, double t, double mu, double thres,
              void* X_out, void* sums_dev, void* workspace, size_t workspace_bytes, void* stream);
+/* R = A X - B (m x l) and G = A^T R (n x l) (reference gl_ProxGD_primal.py:129
+ * `A.T @ (A @ x - b)`). one_pass = 0: A @ X, then A^T R (two passes over A, the faster path on
+ * MI355X); one_pass = 1: the fused residual-gradient kernel reads A from HBM once
+ *  where the shape and device allow it (fp64, l = 32, n = 512 P with P a power
+ * of two in 2..128, m a multiple of 16 * 256 / P, >= 256 CUs), else two passes.
+ * *one_pass_ran (may be NULL) = 1 when the fused kernel ran. */
+int glx_residual_gradient(int dtype, int64_t m, int64_t n, int64_t l, const void* A, const void* X,
+                          const void* B, void* R, void* G, void* workspace, size_t workspace_bytes,
+                          int one_pass, int* one_pass_ran, void* stream);
 /* Workspace bytes for the single-kernel entry points above. */
 int glx_kernel_workspace_bytes(int dtype, int64_t m, int64_t n, int64_t l, size_t* bytes);
 /* One-line description of the kernels (tile, split) the planner picks for this shape, for

@@ -123,6 +123,22 @@ def test_torch_tensors_in_torch_out():
     assert _rel(out["fval"], gold["fval"]) < 1e-8
 
 
+def test_misaligned_device_views():
+    """A torch view whose data pointer is not 16-byte aligned (a row-offset view of an odd-width
+    buffer) is copied to an aligned tensor instead of being rejected."""
+    from gl_ProxGD_primal import gl_ProxGD_primal
+    meta, gold = golden_case("short5_gl_ProxGD_primal")
+    A, b, u, x0, mu = golden_inputs(meta)
+    m, n = A.shape
+    big = torch.zeros(m * n + 1, dtype=torch.float64, device="cuda")
+    Av = big[1:].view(m, n)                       # 8-byte offset: not 16-byte aligned
+    Av.copy_(torch.from_numpy(A))
+    assert Av.data_ptr() % 16 != 0
+    x, k, out = gl_ProxGD_primal(x0, Av, b, mu, dict(meta["opts"]))
+    assert k == int(gold["k"])
+    assert _rel(out["fval"], gold["fval"]) < 1e-8
+
+
 def test_bad_step_type_raises():
     from gl_ProxGD_primal import gl_ProxGD_primal
     A = np.zeros((8, 16))

@@ -104,8 +104,10 @@ def test_workspace_planning_host_only():
         nb = ctypes.c_size_t(0)
         _lib.check(_lib.lib().glx_workspace_bytes(ctypes.byref(p), ctypes.byref(make_opts(0, {})), ctypes.byref(nb)))
         es = 8 if dt == 1 else 4
-        assert nb.value >= es * (2 * n * l + 2 * m * l)       # x-buffers + residuals at least
-        assert nb.value < es * (m * n) // 4 + (64 << 20)        # never close to the size of A
+        # fp64 ProxGD's split-candidate trial keeps a transposed copy of A (kernels_gather.hip)
+        at = es * m * n if (dt == 1 and l in (16, 32)) else 0
+        assert nb.value >= es * (2 * n * l + 2 * m * l) + at  # x-buffers + residuals at least
+        assert nb.value < at + es * (m * n) // 4 + (64 << 20)   # else never close to the size of A
 
 
 def test_invalid_problem_rejected_on_host():
