@@ -127,10 +127,15 @@ int gather_split(int64_t m);
 // At (n x m) = A^T
 template <typename T>
 void launch_transpose(const T* A, T* At, int64_t m, int64_t n, hipStream_t st);
-// P[s][r][c] = sum over the flagged rows k of e (zf[k] != 0) in list split s of At[k][r] E[k][c]
+// launch_e_lists: per column c the ascending k with zf[k] != 0 and E[k][c] != 0, into lists_ws
+// (gather_lists_bytes(n)); launch_at_gather: P[r][c] = sum over column c's list of
+// At[k][r] E[k][c] (one slab)
+size_t gather_lists_bytes(int64_t n);
 template <typename T>
-void launch_at_gather(const T* At, const T* E, const uint8_t* zf, int64_t m, int64_t n, int64_t l,
-                      T* P, int S, hipStream_t st);
+void launch_e_lists(const T* E, const uint8_t* zf, int64_t n, int64_t l, void* lists_ws, hipStream_t st);
+template <typename T>
+void launch_at_gather(const T* At, const T* E, int64_t m, int64_t n, int64_t l, T* P, void* lists_ws,
+                      hipStream_t st);
 
 // ---- fused residual + gradient in one pass over A (kernels_fused.hip) ----
 // Sraw = A X (m x 32) and Gs[RG][n][32] with G = A^T (A X - B) = sum of the RG slabs in order.

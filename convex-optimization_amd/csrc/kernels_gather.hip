@@ -9,15 +9,13 @@
 // with one right-hand side, HBM-bound); A e needs column k of A for every flagged row k of e,
 // which is row k of At = A^T (n x m, one contiguous m-vector), built once per session:
 //
-//   P[s][r][c] = sum over the flagged rows k of split s (ascending):  At[k][r] * e[k][c]
+//   P[r][c] = sum over the k with e[k][c] != 0 (ascending):  At[k][r] * e[k][c]
 //
-// Every workgroup compacts the n row flags (zf[k] != 0, written by the trial kernel) into an
-// ascending index list in LDS (a 256-thread scan; the order is fixed, so the sums are
-// deterministic), takes its share s of the list, and runs a 16x16x4 MFMA loop whose K index
-// walks the list: lane (i, q) loads At[k_q][r0 + 16 mt + i] (16 lanes = 128 contiguous bytes of
-// one At row) and e[k_q][16 nt + i]. Reads |flagged| * m * s bytes of At: ≈ 190 MiB at 3 000
-// rows instead of a second dense pass (1 GiB of MFMA-bound work). Partial slabs go to the
-// finalize kernel, which forms A p - b = (A p_thr - b) + sum_s P[s].
+// e has about one nonzero per flagged row, so A e is computed column by column on the VALU
+// (k_at_gather below), reading At only for the nonzeros: ≈ 230 MB at 3 500 nonzeros instead of a
+// second dense pass (1 GiB of MFMA-bound work). The result goes to the finalize kernel, which
+// forms A p - b = (A p_thr - b) + A e. (A 16x16x4 MFMA form over the flagged rows measured 72 us
+// a trial at NS, round 2: its flops were ~97 % zeros.)
 #include <hip/hip_runtime.h>
 
 #include <cstdlib>
@@ -28,28 +26,8 @@
 namespace glx {
 
 namespace {
-typedef double gd4 __attribute__((ext_vector_type(4)));
-typedef float gf4 __attribute__((ext_vector_type(4)));
-template <typename T> struct GM;
-template <> struct GM<double> {
-  typedef gd4 acc_t;
-  __device__ static inline acc_t mma(double a, double b, acc_t c) {
-    return __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, c, 0, 0, 0);
-  }
-  __device__ static inline int row(int lane, int r) { return (lane >> 4) + 4 * r; }
-};
-template <> struct GM<float> {
-  typedef gf4 acc_t;
-  __device__ static inline acc_t mma(float a, float b, acc_t c) {
-    return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
-  }
-  __device__ static inline int row(int lane, int r) { return ((lane >> 4) << 2) + r; }
-};
-
 constexpr int kGW = 4;                  // waves per workgroup
 constexpr int kGThreads = 64 * kGW;
-constexpr int kGMT = 4;                 // 16-row tiles per wave (64 output rows)
-constexpr int kGRows = 16 * kGMT * kGW; // output rows per workgroup
 }  // namespace
 
 // At = A^T through 64 x 64 LDS tiles (padded rows: conflict-free transposed reads)
@@ -74,135 +52,134 @@ __global__ __launch_bounds__(256) void k_transpose(const T* __restrict__ A, T* _
   }
 }
 
-// grid: gx row blocks x S splits of the flagged-row list (blockIdx.x = split * gx + row block)
-// PF k-steps in flight per wave (2 KiB of At each at l = 32, f64)
-template <typename T, int NT, int kGPF>
-__global__ __launch_bounds__(kGThreads) void k_at_gather(const T* __restrict__ At,
-                                                         const T* __restrict__ E,
-                                                         const uint8_t* __restrict__ zf,
-                                                         int64_t m, int64_t n, T* __restrict__ P,
-                                                         int S, int gx) {
-  typedef GM<T> M;
-  typedef typename M::acc_t C;
-  constexpr int L = 16 * NT;
-  extern __shared__ unsigned short lst[];            // n entries (worst case: every row flagged)
+// Column lists of e (one workgroup per column c): the ascending k with zf[k] != 0 and
+// e[k][c] != 0 -> lists[c * n ...], counts[c]. First the flagged rows (a 256-thread scan of the
+// n flags into LDS), then their e[k][c] (loads issued 16 at a time), then a second scan.
+template <typename T, int L>
+__global__ __launch_bounds__(kGThreads) void k_e_lists(const T* __restrict__ E,
+                                                       const uint8_t* __restrict__ zf, int64_t n,
+                                                       unsigned short* __restrict__ lists,
+                                                       unsigned* __restrict__ counts) {
+  extern __shared__ unsigned short fl[];             // the flagged rows (n entries worst case)
   __shared__ unsigned wsum[kGW];
   const int tid = threadIdx.x;
   const int lane = tid & 63, wave = tid >> 6;
-  const int i = lane & 15, q = lane >> 4;
-  const int bx = (int)blockIdx.x % gx, split = (int)blockIdx.x / gx;
-
-  // ---- compaction: thread t owns flags [t * per, (t + 1) * per), per a multiple of 16, read
-  // as 16-B vectors (the flag buffer is padded to 256 B; bytes at k >= n are ignored)
+  const int c = (int)blockIdx.x;
+  auto scan = [&](unsigned cntl, unsigned& base, unsigned& total) {
+    unsigned inc = cntl;
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+      const unsigned v = __shfl_up(inc, off);
+      if (lane >= off) inc += v;
+    }
+    __syncthreads();
+    if (lane == 63) wsum[wave] = inc;
+    __syncthreads();
+    base = 0;
+    total = 0;
+#pragma unroll
+    for (int w = 0; w < kGW; ++w) {
+      if (w < wave) base += wsum[w];
+      total += wsum[w];
+    }
+    base += inc - cntl;
+  };
+  // 1. flagged rows: thread t owns flags [t * per, (t + 1) * per) (16-B vectors; the buffer is
+  //    padded to 256 B, bytes at k >= n are ignored)
   const int64_t per = (((n + kGThreads - 1) / kGThreads) + 15) & ~int64_t(15);
   const int64_t f0 = tid * per;
   const int64_t f1 = (f0 + per < n) ? f0 + per : (f0 < n ? n : f0);
-  auto flagged = [&](int64_t k) -> bool { return zf[k] != 0; };
-  unsigned cntl = 0;
+  unsigned cnt1 = 0;
   for (int64_t k = f0; k < f1; k += 16) {
     const uint4 v = *reinterpret_cast<const uint4*>(zf + k);
     const unsigned w[4] = {v.x, v.y, v.z, v.w};
 #pragma unroll
     for (int j = 0; j < 16; ++j)
-      if (k + j < f1 && ((w[j >> 2] >> (8 * (j & 3))) & 0xffu) != 0) ++cntl;
+      if (k + j < f1 && ((w[j >> 2] >> (8 * (j & 3))) & 0xffu) != 0) ++cnt1;
   }
-  // inclusive scan over the wave, then over the waves
-  unsigned inc = cntl;
+  unsigned pos, nf;
+  scan(cnt1, pos, nf);
+  if (cnt1 != 0)
+    for (int64_t k = f0; k < f1; k += 16) {   // the same 16-B vectors again (L1/L2 hits)
+      const uint4 v = *reinterpret_cast<const uint4*>(zf + k);
+      const unsigned w[4] = {v.x, v.y, v.z, v.w};
 #pragma unroll
-  for (int off = 1; off < 64; off <<= 1) {
-    const unsigned v = __shfl_up(inc, off);
-    if (lane >= off) inc += v;
-  }
-  if (lane == 63) wsum[wave] = inc;
+      for (int j = 0; j < 16; ++j)
+        if (k + j < f1 && ((w[j >> 2] >> (8 * (j & 3))) & 0xffu) != 0) fl[pos++] = (unsigned short)(k + j);
+    }
   __syncthreads();
-  unsigned wbase = 0, total = 0;
+  // 2. thread t takes flagged entries [t * q, (t + 1) * q) in order, so the list stays ascending
+  const unsigned q = (nf + kGThreads - 1) / kGThreads;
+  const unsigned g0 = tid * q, g1 = (g0 + q < nf) ? g0 + q : (g0 < nf ? nf : g0);
+  // nonzero bits of this thread's entries, 64 at a time (q <= 64 when n <= 16384; larger n
+  // takes a second round of loads in the write pass)
+  unsigned cnt2 = 0;
+  unsigned long long nzb = 0;
+  for (unsigned g = g0; g < g1; g += 16) {
+    T ev[16];
 #pragma unroll
-  for (int w = 0; w < kGW; ++w) {
-    if (w < wave) wbase += wsum[w];
-    total += wsum[w];
-  }
-  unsigned pos = wbase + inc - cntl;
-  if (cntl != 0)
-    for (int64_t k = f0; k < f1; ++k)
-      if (flagged(k)) lst[pos++] = (unsigned short)k;
-  __syncthreads();
-
-  const int64_t beg = (int64_t)total * split / S, end = (int64_t)total * (split + 1) / S;
-  const int64_t row0 = (int64_t)bx * kGRows + (int64_t)wave * (16 * kGMT);
-  C acc[kGMT][NT];
+    for (int u = 0; u < 16; ++u) ev[u] = (g + u < g1) ? E[(int64_t)fl[g + u] * L + c] : T(0);
 #pragma unroll
-  for (int mt = 0; mt < kGMT; ++mt)
-#pragma unroll
-    for (int nt = 0; nt < NT; ++nt) acc[mt][nt] = C{};
-
-  if (end > beg) {
-    int64_t rr[kGMT];
-#pragma unroll
-    for (int mt = 0; mt < kGMT; ++mt) {
-      const int64_t r = row0 + 16 * mt + i;
-      rr[mt] = r < m ? r : m - 1;
-    }
-    const int64_t nsteps = (end - beg + 3) / 4;
-    T a[kGPF][kGMT], e[kGPF][NT];
-    // step s, lane group q: list position beg + 4 s + q (past the end: a zero e row)
-    auto ld = [&](int p, int64_t s) {
-      s = s < nsteps ? s : nsteps - 1;
-      const int64_t ps = beg + 4 * s + q;
-      const bool ok = ps < end;
-      const int64_t k = lst[ok ? ps : beg];
-#pragma unroll
-      for (int mt = 0; mt < kGMT; ++mt) a[p][mt] = At[k * m + rr[mt]];
-#pragma unroll
-      for (int nt = 0; nt < NT; ++nt) e[p][nt] = ok ? E[k * L + 16 * nt + i] : T(0);
-    };
-#pragma unroll
-    for (int p = 0; p < kGPF; ++p) ld(p, p);
-    int64_t s0 = 0;
-    for (; s0 + kGPF <= nsteps; s0 += kGPF) {
-#pragma unroll
-      for (int p = 0; p < kGPF; ++p) {
-#pragma unroll
-        for (int mt = 0; mt < kGMT; ++mt)
-#pragma unroll
-          for (int nt = 0; nt < NT; ++nt) acc[mt][nt] = M::mma(a[p][mt], e[p][nt], acc[mt][nt]);
-        ld(p, s0 + p + kGPF);
-      }
-    }
-#pragma unroll
-    for (int p = 0; p < kGPF - 1; ++p)
-      if (s0 + p < nsteps) {
-#pragma unroll
-        for (int mt = 0; mt < kGMT; ++mt)
-#pragma unroll
-          for (int nt = 0; nt < NT; ++nt) acc[mt][nt] = M::mma(a[p][mt], e[p][nt], acc[mt][nt]);
+    for (int u = 0; u < 16; ++u)
+      if (ev[u] != T(0)) {
+        ++cnt2;
+        if (g - g0 + u < 64) nzb |= 1ull << (g - g0 + u);
       }
   }
-  T* out = P + (int64_t)split * m * L;
-#pragma unroll
-  for (int mt = 0; mt < kGMT; ++mt)
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const int64_t row = row0 + 16 * mt + M::row(lane, r);
-      if (row < m) {
-#pragma unroll
-        for (int nt = 0; nt < NT; ++nt) out[row * L + 16 * nt + i] = acc[mt][nt][r];
-      }
-    }
+  unsigned p2, nc;
+  scan(cnt2, p2, nc);
+  unsigned short* out = lists + (int64_t)c * n;
+  for (unsigned g = g0; g < g1; ++g) {
+    const unsigned o = g - g0;
+    const bool nz = o < 64 ? ((nzb >> o) & 1ull) != 0 : E[(int64_t)fl[g] * L + c] != T(0);
+    if (nz) out[p2++] = fl[g];
+  }
+  if (tid == 0) counts[c] = nc;
 }
 
-static int genv(const char* name, int dflt) {
-  const char* v = std::getenv(name);
-  return (v && *v) ? std::atoi(v) : dflt;
+// One workgroup per (256-row block, column c) of A e. e has few nonzeros per flagged row (about
+// one of the 32 columns at the north-star size), so a dense 16x16x4 MFMA over all 32 columns
+// would spend ~97 % of its flops on zeros: here every output element is a fp64 VALU dot product
+// over column c's list (k_e_lists) in its ascending order (deterministic); thread t (row
+// r = 256 rb + t) keeps 8 loads in flight and the 64 lanes of a wave read 512 contiguous bytes
+// of one At row. out[r][c] = the sum (one slab: no K split).
+template <typename T, int L>
+__global__ __launch_bounds__(kGThreads) void k_at_gather(const T* __restrict__ At,
+                                                         const T* __restrict__ E,
+                                                         const unsigned short* __restrict__ lists,
+                                                         const unsigned* __restrict__ counts,
+                                                         int64_t m, int64_t n, T* __restrict__ P,
+                                                         int gx) {
+  const int rb = (int)blockIdx.x % gx, c = (int)blockIdx.x / gx;
+  const int total = (int)counts[c];
+  const unsigned short* lst = lists + (int64_t)c * n;
+  const int64_t r = (int64_t)rb * kGThreads + threadIdx.x;
+  const int64_t rr = r < m ? r : m - 1;
+  constexpr int U = 8;
+  T acc = T(0);
+  int idx = 0;
+  for (; idx + U <= total; idx += U) {
+    T a[U], ev[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int64_t k = lst[idx + u];
+      a[u] = At[k * m + rr];
+      ev[u] = E[k * L + c];
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) acc = acc + a[u] * ev[u];
+  }
+  for (; idx < total; ++idx) {
+    const int64_t k = lst[idx];
+    acc = acc + At[k * m + rr] * E[k * L + c];
+  }
+  if (r < m) P[r * L + c] = acc;
 }
 
-// K splits of the flagged-row list: about kGatherBlocks workgroups (GLX_GATHER_BLOCKS)
-static constexpr int kGatherBlocks = 512;
+// A e is written as ONE slab (no K split)
 int gather_split(int64_t m) {
-  const int64_t gx = (m + kGRows - 1) / kGRows;
-  int64_t s = genv("GLX_GATHER_BLOCKS", kGatherBlocks) / gx;
-  if (s < 1) s = 1;
-  if (s > 32) s = 32;
-  return (int)s;
+  (void)m;
+  return 1;
 }
 
 bool gather_ok(int64_t n, int64_t l) { return (l == 16 || l == 32) && n <= 65535; }
@@ -213,37 +190,54 @@ void launch_transpose(const T* A, T* At, int64_t m, int64_t n, hipStream_t st) {
   hipLaunchKernelGGL(k_transpose<T>, grid, dim3(256), 0, st, A, At, m, n);
 }
 
+size_t gather_lists_bytes(int64_t n);
+
+static unsigned* list_counts(void* lists_ws, int64_t n) {
+  return reinterpret_cast<unsigned*>(static_cast<char*>(lists_ws) + gather_lists_bytes(n) - 256);
+}
+
 template <typename T>
-void launch_at_gather(const T* At, const T* E, const uint8_t* zf, int64_t m, int64_t n, int64_t l,
-                      T* P, int S, hipStream_t st) {
-  if (!gather_ok(n, l)) throw Error{GLX_E_INVALID, "A e gather: needs l in {16, 32} and n < 65536"};
-  const int gx = (int)((m + kGRows - 1) / kGRows);
+void launch_e_lists(const T* E, const uint8_t* zf, int64_t n, int64_t l, void* lists_ws, hipStream_t st) {
+  if (!gather_ok(n, l)) throw Error{GLX_E_INVALID, "A e gather: needs l in {16, 32}, n < 65536"};
   const size_t lds = sizeof(unsigned short) * (size_t)n;
-  static const int pf = genv("GLX_GATHER_PF", 8);
   auto go = [&](auto kern) {
     static bool attr = false;
-    if (!attr) {   // the list exceeds the default 64 KiB dynamic LDS limit only past n = 32768
+    if (!attr) {   // the flagged-row list exceeds the default 64 KiB dynamic LDS only past n = 32768
       (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kern),
                                 hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024 - 64);
       attr = true;
     }
-    hipLaunchKernelGGL(kern, dim3((unsigned)(gx * S)), dim3(kGThreads), lds, st, At, E, zf, m, n, P,
-                       S, gx);
+    hipLaunchKernelGGL(kern, dim3((unsigned)l), dim3(kGThreads), lds, st, E, zf, n,
+                       static_cast<unsigned short*>(lists_ws), list_counts(lists_ws, n));
   };
-  if (l == 32) {
-    if (pf == 4) go(k_at_gather<T, 2, 4>);
-    else go(k_at_gather<T, 2, 8>);
-  } else {
-    if (pf == 4) go(k_at_gather<T, 1, 4>);
-    else go(k_at_gather<T, 1, 8>);
-  }
+  if (l == 32) go(k_e_lists<T, 32>);
+  else go(k_e_lists<T, 16>);
 }
+
+template <typename T>
+void launch_at_gather(const T* At, const T* E, int64_t m, int64_t n, int64_t l, T* P, void* lists_ws,
+                      hipStream_t st) {
+  if (!gather_ok(n, l)) throw Error{GLX_E_INVALID, "A e gather: needs l in {16, 32}, n < 65536"};
+  const int gx = (int)((m + kGThreads - 1) / kGThreads);
+  const unsigned short* lists = static_cast<const unsigned short*>(lists_ws);
+  if (l == 32)
+    hipLaunchKernelGGL((k_at_gather<T, 32>), dim3((unsigned)(gx * l)), dim3(kGThreads), 0, st, At, E,
+                       lists, list_counts(lists_ws, n), m, n, P, gx);
+  else
+    hipLaunchKernelGGL((k_at_gather<T, 16>), dim3((unsigned)(gx * l)), dim3(kGThreads), 0, st, At, E,
+                       lists, list_counts(lists_ws, n), m, n, P, gx);
+}
+
+// workspace of the column lists: l * n indices + 256 B of counts
+size_t gather_lists_bytes(int64_t n) { return (((size_t)32 * n * 2 + 255) & ~size_t(255)) + 256; }
 
 template void launch_transpose<double>(const double*, double*, int64_t, int64_t, hipStream_t);
 template void launch_transpose<float>(const float*, float*, int64_t, int64_t, hipStream_t);
-template void launch_at_gather<double>(const double*, const double*, const uint8_t*, int64_t, int64_t,
-                                       int64_t, double*, int, hipStream_t);
-template void launch_at_gather<float>(const float*, const float*, const uint8_t*, int64_t, int64_t,
-                                      int64_t, float*, int, hipStream_t);
+template void launch_e_lists<double>(const double*, const uint8_t*, int64_t, int64_t, void*, hipStream_t);
+template void launch_e_lists<float>(const float*, const uint8_t*, int64_t, int64_t, void*, hipStream_t);
+template void launch_at_gather<double>(const double*, const double*, int64_t, int64_t, int64_t, double*,
+                                       void*, hipStream_t);
+template void launch_at_gather<float>(const float*, const float*, int64_t, int64_t, int64_t, float*,
+                                      void*, hipStream_t);
 
 }  // namespace glx

@@ -176,6 +176,7 @@ class Session : public SessionBase {
                                              smode == 1 ? gather_split(P.m) + ax_split(plan, 1) : 0);
     T* pp = static_cast<T*>(c.take(sizeof(T) * ml * pslabs));
     T* at = smode == 1 ? static_cast<T*>(c.take(sizeof(T) * P.m * P.n)) : nullptr;   // A^T
+    void* glists = smode == 1 ? c.take(gather_lists_bytes(P.n)) : nullptr;
     double* scal = static_cast<double*>(c.take(sizeof(double) * NSCAL_DEV));
     double* part = static_cast<double*>(c.take(sizeof(double) * kMaxRedVals * kMaxBlocks));
     unsigned* ticket = static_cast<unsigned*>(c.take(kTicketBytes));
@@ -192,7 +193,7 @@ class Session : public SessionBase {
       for (int i = 0; i < kBufs; ++i) s->X_[i] = bufs[i];
       for (int i = 0; i < kRes; ++i) s->R_[i] = res[i];
       for (int k = 0; k < 2; ++k) { s->Gs_[k] = g[k]; s->Gps_[k] = gp[k]; }
-      s->G_ = g[0]; s->Gp_ = gp[0]; s->Pp_ = pp; s->At_ = at;
+      s->G_ = g[0]; s->Gp_ = gp[0]; s->Pp_ = pp; s->At_ = at; s->glists_ = glists;
       s->scal_ = scal; s->part_ = part; s->ticket_ = ticket; s->flag_ = flag; s->fh_dev_ = fh;
       s->pcnt_ = pcnt;
       s->zf_ = zf;
@@ -261,7 +262,12 @@ class Session : public SessionBase {
     // nonzero only where the hard threshold zeroed p (see iter_proxgd, split_mode)
     emode_ = smode_ != 0;
     gsplit_ = gather_split(m_);
-    if (smode_ == 1) launch_transpose<T>(static_cast<const T*>(P.A), At_, m_, n_, st_);   // once
+    if (smode_ == 1) {
+      launch_transpose<T>(static_cast<const T*>(P.A), At_, m_, n_, st_);   // once
+      GLX_HIP(hipStreamCreateWithFlags(&st2_, hipStreamNonBlocking));
+      GLX_HIP(hipEventCreateWithFlags(&ev_trial_, hipEventDisableTiming));
+      GLX_HIP(hipEventCreateWithFlags(&ev_lists_, hipEventDisableTiming));
+    }
     fused_fista_ok_ = fuse_any && P.method == GLX_FPROXGD;
     GLX_HIP(hipMemsetAsync(ticket_, 0, kTicketBytes, st_));
     GLX_HIP(hipMemsetAsync(pcnt_, 0, sizeof(unsigned) * (P.n / 64 + 64), st_));
@@ -281,6 +287,12 @@ class Session : public SessionBase {
   }
 
   ~Session() override {
+    if (st2_) {
+      (void)hipStreamSynchronize(st2_);
+      (void)hipStreamDestroy(st2_);
+    }
+    if (ev_trial_) (void)hipEventDestroy(ev_trial_);
+    if (ev_lists_) (void)hipEventDestroy(ev_lists_);
     if (hs_) (void)hipHostFree(hs_);
     if (rb_event_) (void)hipEventDestroy(rb_event_);
     for (auto& v : ev_)
@@ -486,15 +498,22 @@ class Session : public SessionBase {
     ++ax_calls_;
     ax_cols_ += sf ? nsrc - 1 : nsrc;   // dense right-hand sides (the flagged e is counted apart)
   }
-  // Split-candidate trial, gather form: A p_thr (one dense source, slabs behind the A e slabs)
-  // and A e from the transposed copy (gsplit_ slabs at Pp_); xs = [e | p_thr]. Timed as one
-  // A@X (kind 0). pb: the dense launch carries that scalar packet.
+  // Split-candidate trial, gather form: A p_thr (one dense source, slabs behind the A e slab)
+  // and A e from the transposed copy (one slab at Pp_); xs = [e | p_thr]. The column lists of e
+  // are built on a side stream while the dense pass runs. Timed as one A@X (kind 0). pb: the
+  // dense launch carries that scalar packet.
   void cand_ax(const T* const* xs, Pub pb = Pub{}) {
     hipEvent_t e0 = prof_begin(0);
     const T* xd[3] = {xs[1], nullptr, nullptr};
+    GLX_HIP(hipEventRecord(ev_trial_, st_));
+    GLX_HIP(hipStreamWaitEvent(st2_, ev_trial_, 0));
+    launch_e_lists<T>(xs[0], zf_, n_, l_, glists_, st2_);
+    check_launch();
+    GLX_HIP(hipEventRecord(ev_lists_, st2_));
     launch_ax<T>(plan_, 1, A_, xd, Pp_ + (size_t)gsplit_ * ml_, nullptr, 0, st_, pb);
     check_launch();
-    launch_at_gather<T>(At_, xs[0], zf_, m_, n_, l_, Pp_, gsplit_, st_);
+    GLX_HIP(hipStreamWaitEvent(st_, ev_lists_, 0));
+    launch_at_gather<T>(At_, xs[0], m_, n_, l_, Pp_, glists_, st_);
     check_launch();
     prof_end(0, e0);
     ++ax_calls_;
@@ -1103,6 +1122,9 @@ class Session : public SessionBase {
   unsigned* pcnt_ = nullptr;   // per-panel counters (fused A^T R with K splits)
   uint8_t* zf_ = nullptr;      // row flags of e (split-candidate ProxGD)
   T* At_ = nullptr;            // A^T (split-candidate gather form)
+  void* glists_ = nullptr;     // its per-column index lists of e
+  hipStream_t st2_ = nullptr;  // side stream: the lists, beside the dense A@X
+  hipEvent_t ev_trial_ = nullptr, ev_lists_ = nullptr;
   int smode_ = 0, gsplit_ = 1;
   bool emode_ = false;         // split-candidate ProxGD: trials write e = p - p_thr, not z
   uint8_t* ezf() const { return emode_ ? zf_ : nullptr; }
