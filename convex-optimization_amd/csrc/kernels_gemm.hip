@@ -1417,9 +1417,19 @@ static int lds_split(int esize, int64_t m, int64_t n, int code, int64_t target =
 // of the 4-wave tile. Measured end to end with the communicator path
 // (profiles/r1_tuning/small_kernels/ax_shard_tile.log): +4.7 % at m = 1024, +3 % at 2048,
 // neutral at 4096; at m = 8192 the default tile stays ahead (A@X 290 vs 306 us).
+//
+// One right-hand side at l = 32, f64 (round 2: the split-candidate trial's dense pass A p_thr is
+// HBM-bound): 51328 with its 4 K splits, A@X 246-250 vs 252-254 us incl. the A e gather, NS
+// ProxGD 2266-2269 vs 2231-2232 it/s on one box (profiles/r2_axtile/).
 static void lds_plan(int esize, int64_t m, int64_t n, int64_t l, int nsrc, int& code, int& S) {
   S = lds_split(esize, m, n, code);
   if (std::getenv("GLX_AXL_BLOCKS") || std::getenv("GLX_AXB_VARIANT")) return;
+  if (esize == 8 && nsrc == 1 && l == 32 && code == 52228 && lds_code_ok(51328, n, l, esize) &&
+      !std::getenv("GLX_AX_VARIANT")) {
+    code = 51328;
+    S = lds_split(esize, m, n, code);
+    return;
+  }
   if (esize == 8 && nsrc == 2 && l == 32 && m <= 2048 && code == 52228 &&
       lds_code_ok(51328, n, l, esize) && env_int("GLX_SHARD_TILE", 1) != 0) {
     code = 51328;
