@@ -278,11 +278,14 @@ __device__ inline bool prox_pgd_row(const T (&xv)[EPL], const T (&gv)[EPL], cons
 // acc: PROX [sum g*(xc-y), sum (xc-y)^2, sum ||xc_i||, max |xc|];
 //      FGD  [sum g*(xc-y), sum (xc-y)^2, sum (sqrt(||xc_i||^2+d^2)-d), sum ||xc_i||, max |xc|].
 // ------------------------------------------------------------------------------------------
+// ecv (split form, when non-null): e_c = xc - thr(xc), i.e. xc where the threshold zeroes it and
+// 0 elsewhere; returns whether this row of e_c is nonzero (same answer on every lane of the row).
 template <typename T, int LPR, int EPL, bool PROX>
-__device__ inline void fista_row(const T (&yv)[EPL], const T (&gv)[EPL], const T (&xkv)[EPL],
+__device__ inline bool fista_row(const T (&yv)[EPL], const T (&gv)[EPL], const T (&xkv)[EPL],
                                  const bool (&ok)[EPL], bool rv, int sub, T t, T tmu, T thres,
                                  T theta, T a1, T b1, T dd, T delta, T (&xcv)[EPL],
-                                 T (&vnv)[EPL], T (&ynv)[EPL], double (&acc)[PROX ? 4 : 5]) {
+                                 T (&vnv)[EPL], T (&ynv)[EPL], double (&acc)[PROX ? 4 : 5],
+                                 T* ecv = nullptr) {
   constexpr int NV = PROX ? 4 : 5;
   T w[EPL];
   T sq = T(0);
@@ -299,6 +302,7 @@ __device__ inline void fista_row(const T (&yv)[EPL], const T (&gv)[EPL], const T
     d = ((nrm < thres) ? T(1) : T(0)) + nrm;
   }
   T psq = T(0);
+  bool rch = false;
 #pragma unroll
   for (int e = 0; e < EPL; ++e) {
     const T pv = PROX ? (w[e] * c) / d : w[e];
@@ -306,10 +310,15 @@ __device__ inline void fista_row(const T (&yv)[EPL], const T (&gv)[EPL], const T
     T xo = xkv[e];
     if (tabs(xo) < thres) xo = T(0);
     const T vn = xo + (pv - xo) / theta;
-    const T pt = (tabs(pv) < thres) ? T(0) : pv;
+    const bool small = tabs(pv) < thres;
+    const T pt = small ? T(0) : pv;
     xcv[e] = pv;
     vnv[e] = vn;
     ynv[e] = a1 * pt + b1 * vn;
+    if (ecv != nullptr) {
+      ecv[e] = small ? pv : T(0);
+      if (ok[e] && small && pv != T(0)) rch = true;
+    }
     if (ok[e]) {
       acc[0] += (double)(gv[e] * dl);
       acc[1] += (double)(dl * dl);
@@ -326,6 +335,7 @@ __device__ inline void fista_row(const T (&yv)[EPL], const T (&gv)[EPL], const T
       acc[3] += (double)__builtin_sqrt(ps);
     }
   }
+  return ecv != nullptr && row_allsum<LPR>(rch ? 1.0 : 0.0) > 0.0;
 }
 
 }  // namespace glx

@@ -112,12 +112,13 @@ void launch_atr_prox(const GemmPlan& p, const T* A, const T* R, T* G, const T* x
                      T* z, double t, double mu, double thres, Red red, hipStream_t st, Pub pub = Pub{},
                      T* Gp = nullptr, unsigned* pcnt = nullptr, uint8_t* zf = nullptr);
 // FISTA trial fused into A^T R (same plan condition): G = A^T R, then xc, v_next, y_next and the
-// four trial sums of k_fista_trial (PROX) into red.
+// four trial sums of k_fista_trial (PROX) into red (ec, zf: as launch_fista_trial).
 template <typename T>
 void launch_atr_fista(const GemmPlan& p, const T* A, const T* R, T* G, const T* y, const T* xk,
                       T* xc, T* vn, T* yn, double t, double mu, double thres, double theta,
                       double theta_next, Red red, hipStream_t st, Pub pub = Pub{},
-                      T* Gp = nullptr, unsigned* pcnt = nullptr);
+                      T* Gp = nullptr, unsigned* pcnt = nullptr, T* ec = nullptr,
+                      uint8_t* zf = nullptr);
 
 // ---- split-candidate A e from a transposed copy of A (kernels_gather.hip) ----
 // gather_ok: the shape supports it (l in {16, 32}, n < 65536); gather_split: K splits of the
@@ -131,6 +132,8 @@ void launch_transpose(const T* A, T* At, int64_t m, int64_t n, hipStream_t st);
 // (gather_lists_bytes(n)); launch_at_gather: P[r][c] = sum over column c's list of
 // At[k][r] E[k][c] (one slab)
 size_t gather_lists_bytes(int64_t n);
+// the l per-column list lengths inside lists_ws (device)
+const unsigned* gather_counts(const void* lists_ws, int64_t n);
 template <typename T>
 void launch_e_lists(const T* E, const uint8_t* zf, int64_t n, int64_t l, void* lists_ws, hipStream_t st);
 template <typename T>
@@ -182,11 +185,21 @@ void launch_prox_pgd(const T* x, const T* g, int S, T* gout, T* p, T* pthr, T* z
 // ynext = (1 - theta_next) thr(xc) + theta_next vnext.
 // out: prox: [sum g*(xc-y), sum (xc-y)^2, sum ||xc_i||, max |xc|]
 //      FGD : [sum g*(xc-y), sum (xc-y)^2, sum (sqrt(||xc_i||^2+d^2)-d), sum ||xc_i||, max |xc|]
+// ec != NULL (split-candidate mode): ec = xc - thr(xc) and zf[i] (n bytes) = row i of ec is nonzero.
 template <typename T>
 void launch_fista_trial(bool prox, const T* y, const T* g, int S, T* gout, const T* xk, T* xc,
                         T* vnext, T* ynext, int64_t n, int64_t l, double t, double mu, double thres,
                         double theta, double theta_next, double delta, Red red, hipStream_t st,
-                        Pub pub = Pub{});
+                        Pub pub = Pub{}, T* ec = nullptr, uint8_t* zf = nullptr);
+// split-candidate FISTA batch finalize (k_finalize_fista): P = S slabs of A xc, Pe = S0 slabs of
+// A e_c, sxo = A thr(xk); Ry = A y_next - b with y_next = a1 thr(xc) + b1 (thr(xk) + (xc -
+// thr(xk)) / theta), sxo_out = A thr(xc). out: [sum (A xc - b)^2, sum Ry^2,
+// sum counts[0..nl) (nnz of e_c, gather_counts), count as above].
+template <typename T>
+void launch_finalize_fista(const T* P, int S, const T* Pe, int S0, const T* B, T* Ry, const T* sxo,
+                           T* sxo_out, int64_t ml, double a1, double b1, double theta, const T* cx,
+                           int64_t cn, const double* cmax, const unsigned* counts, int nl, Red red,
+                           hipStream_t st);
 // plain prox of W (glx_prox): out: [sum ||x_i||, max |x|]
 template <typename T>
 void launch_prox_plain(const T* w, T* x, int64_t n, int64_t l, double t, double mu, double thres,

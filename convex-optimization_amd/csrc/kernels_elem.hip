@@ -122,6 +122,46 @@ __global__ __launch_bounds__(256) void k_finalize_residual(
   if (last && (int)threadIdx.x < nsnap) snap_dst[threadIdx.x] = snap_src[threadIdx.x];
 }
 
+// Split-candidate FISTA batch (solver.cpp iter_fista): the dense source is A xc (S slabs at P),
+// the gather slab(s) hold A e_c (S0 at Pe), and A y_next follows from the linearity of
+// y_next = a1 thr(xc) + b1 (thr(xk) + (xc - thr(xk)) / theta)   (fista_row):
+//   A thr(xc) = A xc - A e_c,   A y_next = a1 A thr(xc) + b1 (A thr(xk) + (A xc - A thr(xk)) / theta)
+// with A thr(xk) (sxo) kept from the previous accepted trial. Writes R_y = A y_next - b and
+// sxo_out = A thr(xc); out: [sum (A xc - b)^2, sum R_y^2, nnz(e_c) = sum of the nl list
+// lengths `counts` (k_e_lists), count(|cx| > 1e-6 *cmax)].
+template <typename T, int G>
+__global__ __launch_bounds__(256) void k_finalize_fista(
+    const T* __restrict__ P, int S, const T* __restrict__ Pe, int S0, const T* __restrict__ B,
+    T* __restrict__ Ry, const T* __restrict__ sxo, T* __restrict__ sxo_out, int64_t ml, double a1_,
+    double b1_, double theta_, const T* __restrict__ cx, int64_t cn, const double* __restrict__ cmax,
+    const unsigned* __restrict__ counts, int nl, Red red) {
+  const T a1 = (T)a1_, b1 = (T)b1_, theta = (T)theta_;
+  double v[4] = {0.0, 0.0, 0.0, 0.0};
+  if (blockIdx.x == 0 && (int)threadIdx.x < nl) v[2] = (double)counts[threadIdx.x];
+  const T thr = cx != nullptr ? (T)1e-6 * (T)(*cmax) : T(0);
+  const int sub = threadIdx.x % G;
+  const int64_t tid = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  const int64_t stride = (int64_t)gridDim.x * 256;
+  for (int64_t idx = tid / G; idx < ml; idx += stride / G) {
+    const T bv = B[idx];
+    const T sx = group_slab_sum<T, G>(P, S, ml, idx, sub);
+    const T apt = sx - group_slab_sum<T, G>(Pe, S0, ml, idx, sub);
+    const T so = sxo[idx];
+    const T avn = so + (sx - so) / theta;
+    const T ry = (a1 * apt + b1 * avn) - bv;
+    const T rx = sx - bv;
+    if (sub == 0) {
+      Ry[idx] = ry;
+      sxo_out[idx] = apt;
+      v[0] += (double)(rx * rx);
+      v[1] += (double)(ry * ry);
+    }
+  }
+  if (cx != nullptr)
+    for (int64_t idx = tid; idx < cn; idx += stride) v[3] += (tabs(cx[idx]) > thr) ? 1.0 : 0.0;
+  grid_reduce<4, 0u>(v, red);
+}
+
 template <typename T>
 __global__ __launch_bounds__(256) void k_sum_partials(const T* __restrict__ Gp, int S, T* __restrict__ G,
                                                       int64_t nl) {
@@ -205,7 +245,8 @@ __global__ __launch_bounds__(256) void k_fista_trial(
     const T* __restrict__ y, const T* __restrict__ g, int S, T* __restrict__ gout,
     const T* __restrict__ xk, T* __restrict__ xc, T* __restrict__ vnext, T* __restrict__ ynext,
     int64_t n, int64_t l, double t_, double tmu_, double thres_, double theta_, double a1_,
-    double b1_, double dd_, double delta_, Red red, Pub pub) {
+    double b1_, double dd_, double delta_, Red red, Pub pub, T* __restrict__ ec,
+    uint8_t* __restrict__ zf) {
   constexpr int NV = PROX ? 4 : 5;
   if (publisher_last<NV, (1u << (NV - 1))>(pub, red)) return;
   const T t = (T)t_, tmu = (T)tmu_, thres = (T)thres_, theta = (T)theta_, a1 = (T)a1_, b1 = (T)b1_;
@@ -216,7 +257,7 @@ __global__ __launch_bounds__(256) void k_fista_trial(
   for (int j = 0; j < NV; ++j) acc[j] = 0.0;
   acc[NV - 1] = -__builtin_inf();
   GLX_ROW_LOOP_BEGIN_NB(LPR, gridDim.x - (pub.host ? 1u : 0u))
-  T yv[EPL], gv[EPL], xkv[EPL], xcv[EPL], vnv[EPL], ynv[EPL];
+  T yv[EPL], gv[EPL], xkv[EPL], xcv[EPL], vnv[EPL], ynv[EPL], ecv[EPL];
   bool ok[EPL];
 #pragma unroll
   for (int e = 0; e < EPL; ++e) {
@@ -227,8 +268,10 @@ __global__ __launch_bounds__(256) void k_fista_trial(
     xkv[e] = ok[e] ? xk[base + j] : T(0);
     if (ok[e] && gout != nullptr) gout[base + j] = gv[e];
   }
-  fista_row<T, LPR, EPL, PROX>(yv, gv, xkv, ok, rv, sub, t, tmu, thres, theta, a1, b1, dd, delta,
-                               xcv, vnv, ynv, acc);
+  const bool rowe = fista_row<T, LPR, EPL, PROX>(yv, gv, xkv, ok, rv, sub, t, tmu, thres, theta, a1,
+                                                  b1, dd, delta, xcv, vnv, ynv, acc,
+                                                  ec != nullptr ? ecv : nullptr);
+  if (zf != nullptr && rv && sub == 0) zf[row] = rowe ? 1 : 0;
 #pragma unroll
   for (int e = 0; e < EPL; ++e) {
     const int64_t j = sub + (int64_t)e * LPR;
@@ -236,6 +279,7 @@ __global__ __launch_bounds__(256) void k_fista_trial(
       xc[base + j] = xcv[e];
       vnext[base + j] = vnv[e];
       ynext[base + j] = ynv[e];
+      if (ec != nullptr) ec[base + j] = ecv[e];
     }
   }
   GLX_ROW_LOOP_END
@@ -515,6 +559,24 @@ void launch_finalize_residual(const T* P, int S, const T* B, int nsrc, T* const*
   else by_g(std::integral_constant<int, 3>{});
 }
 template <typename T>
+void launch_finalize_fista(const T* P, int S, const T* Pe, int S0, const T* B, T* Ry, const T* sxo,
+                           T* sxo_out, int64_t ml, double a1, double b1, double theta, const T* cx,
+                           int64_t cn, const double* cmax, const unsigned* counts, int nl, Red red,
+                           hipStream_t st) {
+  const int G = finalize_groups(S > S0 ? S : S0);
+  if (G > 8) throw Error{GLX_E_INVALID, "finalize: more than 64 K-split slabs"};
+  const int64_t work = ml * G > cn ? ml * G : cn;
+  const dim3 grid(grid_for(work, 256 * 2));
+  auto go = [&](auto g) {
+    hipLaunchKernelGGL((k_finalize_fista<T, decltype(g)::value>), grid, dim3(256), 0, st, P, S, Pe,
+                       S0, B, Ry, sxo, sxo_out, ml, a1, b1, theta, cx, cn, cmax, counts, nl, red);
+  };
+  if (G == 1) go(std::integral_constant<int, 1>{});
+  else if (G == 2) go(std::integral_constant<int, 2>{});
+  else if (G == 4) go(std::integral_constant<int, 4>{});
+  else go(std::integral_constant<int, 8>{});
+}
+template <typename T>
 void launch_sum_partials(const T* Gp, int S, T* G, int64_t nl, hipStream_t st) {
   hipLaunchKernelGGL(k_sum_partials<T>, dim3(grid_for(nl, 256 * 4)), dim3(256), 0, st, Gp, S, G, nl);
 }
@@ -532,18 +594,18 @@ template <typename T>
 void launch_fista_trial(bool prox, const T* y, const T* g, int S, T* gout, const T* xk, T* xc,
                         T* vnext, T* ynext, int64_t n, int64_t l, double t, double mu, double thres,
                         double theta, double theta_next, double delta, Red red, hipStream_t st,
-                        Pub pub) {
+                        Pub pub, T* ec, uint8_t* zf) {
   dispatch_row(l, [&](auto lpr, auto epl) {
     if (prox)
       hipLaunchKernelGGL((k_fista_trial<T, decltype(lpr)::value, decltype(epl)::value, true>),
                          dim3(row_grid_pub(n, lpr, pub)), dim3(256), 0, st, y, g, S, gout, xk, xc,
                          vnext, ynext, n, l, t, t * mu, thres, theta, 1.0 - theta_next, theta_next,
-                         delta * delta, delta, red, pub);
+                         delta * delta, delta, red, pub, ec, zf);
     else
       hipLaunchKernelGGL((k_fista_trial<T, decltype(lpr)::value, decltype(epl)::value, false>),
                          dim3(row_grid_pub(n, lpr, pub)), dim3(256), 0, st, y, g, S, gout, xk, xc,
                          vnext, ynext, n, l, t, t * mu, thres, theta, 1.0 - theta_next, theta_next,
-                         delta * delta, delta, red, pub);
+                         delta * delta, delta, red, pub, ec, zf);
   });
 }
 template <typename T>
@@ -619,11 +681,14 @@ void launch_publish(const double* s, int ns, double* host, unsigned* host_seq, u
                                             double*, double, const double*, Red, hipStream_t,       \
                                             const double*, double*, int, int, int);                 \
   template void launch_sum_partials<T>(const T*, int, T*, int64_t, hipStream_t);                    \
+  template void launch_finalize_fista<T>(const T*, int, const T*, int, const T*, T*, const T*, T*,  \
+                                         int64_t, double, double, double, const T*, int64_t,        \
+                                         const double*, const unsigned*, int, Red, hipStream_t);    \
   template void launch_prox_pgd<T>(const T*, const T*, int, T*, T*, T*, T*, int64_t, int64_t,       \
                                    double, double, double, Red, hipStream_t, Pub, uint8_t*);        \
   template void launch_fista_trial<T>(bool, const T*, const T*, int, T*, const T*, T*, T*, T*,      \
                                       int64_t, int64_t, double, double, double, double, double,     \
-                                      double, Red, hipStream_t, Pub);                               \
+                                      double, Red, hipStream_t, Pub, T*, uint8_t*);                 \
   template void launch_prox_plain<T>(const T*, T*, int64_t, int64_t, double, double, double, Red,   \
                                      hipStream_t);                                                  \
   template void launch_rownorm_max<T>(const T*, int64_t, int64_t, Red, hipStream_t);                \

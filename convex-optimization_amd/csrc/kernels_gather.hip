@@ -195,6 +195,9 @@ size_t gather_lists_bytes(int64_t n);
 static unsigned* list_counts(void* lists_ws, int64_t n) {
   return reinterpret_cast<unsigned*>(static_cast<char*>(lists_ws) + gather_lists_bytes(n) - 256);
 }
+const unsigned* gather_counts(const void* lists_ws, int64_t n) {
+  return list_counts(const_cast<void*>(lists_ws), n);
+}
 
 template <typename T>
 void launch_e_lists(const T* E, const uint8_t* zf, int64_t n, int64_t l, void* lists_ws, hipStream_t st) {

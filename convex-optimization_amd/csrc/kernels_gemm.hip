@@ -1135,7 +1135,8 @@ __global__ __launch_bounds__(256, sizeof(T) == 8 ? 2 : 1) void k_atr_fista(const
                                                    T* __restrict__ ynext, double t_, double tmu_,
                                                    double thres_, double theta_, double a1_,
                                                    double b1_, Red red, Pub pub, int S,
-                                                   T* __restrict__ Gp, unsigned* __restrict__ pcnt) {
+                                                   T* __restrict__ Gp, unsigned* __restrict__ pcnt,
+                                                   T* __restrict__ ec, uint8_t* __restrict__ zf) {
   if (publisher_first<4, 0x8u>(pub, red)) return;
   typedef MF<T> M;
   constexpr int L = 16 * NT;
@@ -1170,7 +1171,7 @@ __global__ __launch_bounds__(256, sizeof(T) == 8 ? 2 : 1) void k_atr_fista(const
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       const int64_t row = col0 + 4 * M::row(lane, r) + e;
-      T gv[NT], xcv[NT], vnv[NT], ynv[NT];
+      T gv[NT], xcv[NT], vnv[NT], ynv[NT], ecv[NT];
       bool ok[NT];
 #pragma unroll
       for (int nt = 0; nt < NT; ++nt) {
@@ -1178,13 +1179,16 @@ __global__ __launch_bounds__(256, sizeof(T) == 8 ? 2 : 1) void k_atr_fista(const
         ok[nt] = true;
         G[row * L + nt * 16 + i] = gv[nt];
       }
-      fista_row<T, 16, NT, true>(ya[r], gv, xa[r], ok, true, i, t, tmu, thres, theta, a1, b1, T(0),
-                                 T(0), xcv, vnv, ynv, accr);
+      const bool rowe = fista_row<T, 16, NT, true>(ya[r], gv, xa[r], ok, true, i, t, tmu, thres, theta,
+                                                   a1, b1, T(0), T(0), xcv, vnv, ynv, accr,
+                                                   ec != nullptr ? ecv : nullptr);
+      if (zf != nullptr && i == 0) zf[row] = rowe ? 1 : 0;
 #pragma unroll
       for (int nt = 0; nt < NT; ++nt) {
         xc[row * L + nt * 16 + i] = xcv[nt];
         vnext[row * L + nt * 16 + i] = vnv[nt];
         ynext[row * L + nt * 16 + i] = ynv[nt];
+        if (ec != nullptr) ec[row * L + nt * 16 + i] = ecv[nt];
       }
     }
   }
@@ -1900,49 +1904,52 @@ void launch_atr_prox(const GemmPlan& p, const T* A, const T* R, T* G, const T* x
 template <typename T, int NT, int PF, bool NTL>
 static void atr_fista_go(const GemmPlan& p, const T* A, const T* R, T* G, const T* y, const T* xk,
                          T* xc, T* vn, T* yn, double t, double mu, double thres, double theta,
-                         double theta_next, Red red, hipStream_t st, Pub pub, T* Gp, unsigned* pcnt) {
+                         double theta_next, Red red, hipStream_t st, Pub pub, T* Gp, unsigned* pcnt,
+                         T* ec, uint8_t* zf) {
   const dim3 grid((unsigned)(p.n / 64 * p.atr_S + (pub.host ? 1 : 0)));
   if (p.atr_S > 1) {
     hipLaunchKernelGGL((k_atr_fista<T, NT, PF, NTL, true>), grid, dim3(256), 0, st, A, R, G, p.m,
                        p.n, y, xk, xc, vn, yn, t, t * mu, thres, theta, 1.0 - theta_next,
-                       theta_next, red, pub, p.atr_S, Gp, pcnt);
+                       theta_next, red, pub, p.atr_S, Gp, pcnt, ec, zf);
     return;
   }
   static const size_t pad = lds_pad(k_atr_fista<T, NT, PF, NTL, false>, "GLX_ATR_LDS_PAD");
   hipLaunchKernelGGL((k_atr_fista<T, NT, PF, NTL, false>), grid, dim3(256), pad, st, A, R, G, p.m,
                      p.n, y, xk, xc, vn, yn, t, t * mu, thres, theta, 1.0 - theta_next, theta_next,
-                     red, pub, 1, Gp, pcnt);
+                     red, pub, 1, Gp, pcnt, ec, zf);
 }
 template <typename T, int NT>
 static void atr_fista_nt(const GemmPlan& p, const T* A, const T* R, T* G, const T* y, const T* xk,
                          T* xc, T* vn, T* yn, double t, double mu, double thres, double theta,
-                         double theta_next, Red red, hipStream_t st, Pub pub, T* Gp, unsigned* pcnt) {
+                         double theta_next, Red red, hipStream_t st, Pub pub, T* Gp, unsigned* pcnt,
+                         T* ec, uint8_t* zf) {
   switch (p.atr_ntl * 100 + p.atr_pf) {
-    case 4: atr_fista_go<T, NT, 4, false>(p, A, R, G, y, xk, xc, vn, yn, t, mu, thres, theta, theta_next, red, st, pub, Gp, pcnt); break;
-    case 104: atr_fista_go<T, NT, 4, true>(p, A, R, G, y, xk, xc, vn, yn, t, mu, thres, theta, theta_next, red, st, pub, Gp, pcnt); break;
-    case 108: atr_fista_go<T, NT, 8, true>(p, A, R, G, y, xk, xc, vn, yn, t, mu, thres, theta, theta_next, red, st, pub, Gp, pcnt); break;
-    default: atr_fista_go<T, NT, 8, false>(p, A, R, G, y, xk, xc, vn, yn, t, mu, thres, theta, theta_next, red, st, pub, Gp, pcnt); break;
+    case 4: atr_fista_go<T, NT, 4, false>(p, A, R, G, y, xk, xc, vn, yn, t, mu, thres, theta, theta_next, red, st, pub, Gp, pcnt, ec, zf); break;
+    case 104: atr_fista_go<T, NT, 4, true>(p, A, R, G, y, xk, xc, vn, yn, t, mu, thres, theta, theta_next, red, st, pub, Gp, pcnt, ec, zf); break;
+    case 108: atr_fista_go<T, NT, 8, true>(p, A, R, G, y, xk, xc, vn, yn, t, mu, thres, theta, theta_next, red, st, pub, Gp, pcnt, ec, zf); break;
+    default: atr_fista_go<T, NT, 8, false>(p, A, R, G, y, xk, xc, vn, yn, t, mu, thres, theta, theta_next, red, st, pub, Gp, pcnt, ec, zf); break;
   }
 }
 template <typename T>
 void launch_atr_fista(const GemmPlan& p, const T* A, const T* R, T* G, const T* y, const T* xk,
                       T* xc, T* vn, T* yn, double t, double mu, double thres, double theta,
-                      double theta_next, Red red, hipStream_t st, Pub pub, T* Gp, unsigned* pcnt) {
+                      double theta_next, Red red, hipStream_t st, Pub pub, T* Gp, unsigned* pcnt,
+                         T* ec, uint8_t* zf) {
   if (p.atr_S > 1 && (Gp == nullptr || pcnt == nullptr))
     throw Error{GLX_E_INVALID, "fused A^T R with K splits needs slab and counter buffers"};
-  if (p.l == 16) atr_fista_nt<T, 1>(p, A, R, G, y, xk, xc, vn, yn, t, mu, thres, theta, theta_next, red, st, pub, Gp, pcnt);
-  else atr_fista_nt<T, 2>(p, A, R, G, y, xk, xc, vn, yn, t, mu, thres, theta, theta_next, red, st, pub, Gp, pcnt);
+  if (p.l == 16) atr_fista_nt<T, 1>(p, A, R, G, y, xk, xc, vn, yn, t, mu, thres, theta, theta_next, red, st, pub, Gp, pcnt, ec, zf);
+  else atr_fista_nt<T, 2>(p, A, R, G, y, xk, xc, vn, yn, t, mu, thres, theta, theta_next, red, st, pub, Gp, pcnt, ec, zf);
 }
 
 template void launch_atr<double>(const GemmPlan&, const double*, const double*, double*, hipStream_t);
 template void launch_atr_fista<double>(const GemmPlan&, const double*, const double*, double*,
                                        const double*, const double*, double*, double*, double*,
                                        double, double, double, double, double, Red, hipStream_t, Pub,
-                                       double*, unsigned*);
+                                       double*, unsigned*, double*, uint8_t*);
 template void launch_atr_fista<float>(const GemmPlan&, const float*, const float*, float*,
                                       const float*, const float*, float*, float*, float*, double,
                                       double, double, double, double, Red, hipStream_t, Pub,
-                                      float*, unsigned*);
+                                      float*, unsigned*, float*, uint8_t*);
 template void launch_atr_prox<double>(const GemmPlan&, const double*, const double*, double*,
                                       const double*, double*, double*, double*, double, double,
                                       double, Red, hipStream_t, Pub, double*, unsigned*, uint8_t*);

@@ -114,10 +114,19 @@ static void validate(const glx_problem* P, const glx_opts* O) {
 // fp64 only: in fp32 the regrouped sum (A p_thr - b) + A e moves f by ~1e-6 relative on short
 // unconverged runs (measured 1.5e-6 on mid_384x640x16 against the 1e-6 fp32 bar), and no fp32
 // ProxGD configuration is on the benchmark path.
+// FProxGD with line search takes the gather form too (iter_fista: A y_next by linearity from
+// A xc, A e_c and the kept A thr(x_k)); GLX_SPLIT_FISTA=0 keeps its dense [xc | y_next] batch.
 static int split_mode(const glx_problem& P, const glx_opts& O) {
-  if (P.method != GLX_PROXGD || O.exact_objective != 0 || P.dtype != GLX_F64) return 0;
+  if (O.exact_objective != 0 || P.dtype != GLX_F64) return 0;
+  if (P.method != GLX_PROXGD && P.method != GLX_FPROXGD) return 0;
   const char* sc = std::getenv("GLX_SPLIT_CAND");
   if (sc && std::strcmp(sc, "0") == 0) return 0;
+  if (P.method == GLX_FPROXGD) {
+    const char* sf = std::getenv("GLX_SPLIT_FISTA");
+    if (sf && std::strcmp(sf, "0") == 0) return 0;
+    const bool ls = O.step_type == GLX_STEP_LINE_SEARCH && O.ls_maxit > 0;
+    return (ls && gather_ok(P.n, P.l)) ? 1 : 0;
+  }
   if (sc && std::strcmp(sc, "sp") == 0) return 2;
   return gather_ok(P.n, P.l) ? 1 : 2;
 }
@@ -177,6 +186,12 @@ class Session : public SessionBase {
     T* pp = static_cast<T*>(c.take(sizeof(T) * ml * pslabs));
     T* at = smode == 1 ? static_cast<T*>(c.take(sizeof(T) * P.m * P.n)) : nullptr;   // A^T
     void* glists = smode == 1 ? c.take(gather_lists_bytes(P.n)) : nullptr;
+    // split-candidate FISTA: e_c and a ring of three A thr(x) (x_k's, the trial's, the
+    // speculated next trial's)
+    const bool fsp = smode == 1 && P.method == GLX_FPROXGD;
+    T* ec = fsp ? static_cast<T*>(c.take(sizeof(T) * nl)) : nullptr;
+    T* sxo[3] = {nullptr, nullptr, nullptr};
+    for (int k = 0; k < 3 && fsp; ++k) sxo[k] = static_cast<T*>(c.take(sizeof(T) * ml));
     double* scal = static_cast<double*>(c.take(sizeof(double) * NSCAL_DEV));
     double* part = static_cast<double*>(c.take(sizeof(double) * kMaxRedVals * kMaxBlocks));
     unsigned* ticket = static_cast<unsigned*>(c.take(kTicketBytes));
@@ -197,6 +212,8 @@ class Session : public SessionBase {
       s->scal_ = scal; s->part_ = part; s->ticket_ = ticket; s->flag_ = flag; s->fh_dev_ = fh;
       s->pcnt_ = pcnt;
       s->zf_ = zf;
+      s->E_ = ec;
+      for (int k = 0; k < 3; ++k) s->SXO_[k] = sxo[k];
       s->sp100_ = sp100;
       s->gemv_slabs_ = gs;
       s->gemv_blocks_ = gb;
@@ -260,7 +277,12 @@ class Session : public SessionBase {
     fused_ok_ = fuse_any && P.method == GLX_PROXGD;
     // ProxGD's fast objective mode evaluates the candidate as A p = A p_thr + A e, e = p - p_thr
     // nonzero only where the hard threshold zeroed p (see iter_proxgd, split_mode)
-    emode_ = smode_ != 0;
+    emode_ = smode_ != 0 && P.method == GLX_PROXGD;
+    fsplit_ = smode_ == 1 && P.method == GLX_FPROXGD;
+    {
+      const char* nb = std::getenv("GLX_SPLIT_NNZ");
+      nnz_budget_ = (nb ? std::atof(nb) : 0.35) * (double)n_;
+    }
     gsplit_ = gather_split(m_);
     if (smode_ == 1) {
       launch_transpose<T>(static_cast<const T*>(P.A), At_, m_, n_, st_);   // once
@@ -373,6 +395,7 @@ class Session : public SessionBase {
     spec_ready_ = false;
     spec_trial_ready_ = false;
     ax_queued_ = false;
+    kslot_ = -1;
   }
 
   void trace(double* sp_after, int64_t cap, int64_t* n, int64_t phase_info[6]) const override {
@@ -893,6 +916,7 @@ class Session : public SessionBase {
     const bool ls = O_.step_type == GLX_STEP_LINE_SEARCH && O_.ls_maxit > 0;
     const double t0 = ls ? tk_ : schedule(inner_);
     const bool fuse = fused_fista_ok_ && !smooth;
+    if (fsplit_ && ls && kslot_ < 0 && dense_left_ == 0) fista_split_prologue();
     // first trial: from the previous iteration's speculative fused kernel, fused into this
     // iteration's A^T r, or (FGD / unfusable plans) the gradient and k_fista_trial
     std::pair<const T*, int> g{nullptr, 0};
@@ -930,10 +954,11 @@ class Session : public SessionBase {
       launch_fista_trial<T>(!smooth, y, first ? g.first : G_, first ? g.second : 1,
                             (first && g.first != G_) ? G_ : nullptr, X_[ix_], X_[ic_], X_[ivn_],
                             X_[iyn_], n_, l_, tt, mu_, O_.thres, theta, theta_next, O_.delta,
-                            red(S_TR), st_);
+                            red(S_TR), st_, Pub{}, fec(), fzf());
       check_launch();
     };
     const int i_rn = smooth ? 3 : 2, i_max = smooth ? 4 : 3;
+    bool fs_batch = false;
     if (ls) {
       t = t0;
       for (int it = 0; it < O_.ls_maxit; ++it) {
@@ -944,8 +969,14 @@ class Session : public SessionBase {
         const bool spec = want_spec(it);
         const bool merge = spec && fuse && merge_tail();
         const bool late_pub = merge || (spec && fuse && attach_ok_ && comm_ == nullptr);
-        residuals(2, xs, rs, S_RT, X_[ic_], scal_ + S_TR + i_max, nullptr, 0.0,   // A @ [x | y_next]
-                  late_pub ? nullptr : &seq, merge ? tail(1 - gset_) : nullptr);
+        fs_batch = fsplit_ && kslot_ >= 0 && dense_left_ == 0;
+        if (fs_batch) {   // A xc dense, A e_c gathered, A y_next by linearity
+          fista_split_batch(R_[ryn], theta, theta_next, S_RT, X_[ic_], scal_ + S_TR + i_max,
+                            late_pub ? nullptr : &seq, merge ? tail(1 - gset_) : nullptr);
+        } else {
+          residuals(2, xs, rs, S_RT, X_[ic_], scal_ + S_TR + i_max, nullptr, 0.0,   // A @ [x | y_next]
+                    late_pub ? nullptr : &seq, merge ? tail(1 - gset_) : nullptr);
+        }
         std::pair<const T*, int> sg;
         if (spec && fuse) {
           // the next iteration's gradient at y_next and its first trial (t, theta' = theta_next)
@@ -994,6 +1025,17 @@ class Session : public SessionBase {
       std::swap(iy_, iyn_);
     }
     tk_ = t;
+    kslot_ = (accepted && fs_batch) ? (kslot_ + 1) % 3 : -1;
+    if (fsplit_ && ls) {
+      if (fs_batch) {
+        stats_[3] += 1;
+        stats_[5] += hs_[S_RT + 2];
+        if (accepted && hs_[S_RT + 2] > nnz_budget_) dense_left_ = kFistaDenseRun;
+      } else {
+        stats_[4] += 1;
+        if (dense_left_ > 0) --dense_left_;
+      }
+    }
     if (accepted) {
       iry_ = ryn;
       gy_sq_ = hs_[S_RT + 1];
@@ -1005,6 +1047,50 @@ class Session : public SessionBase {
       y_ready_ = false;
       f_known_ = false;
     }
+  }
+
+  // Split-candidate FProxGD. The batch of a trial needs A xc (the objective, exact) and
+  // A y_next (the next gradient residual and g(y)). y_next = a1 thr(xc) + b1 v_next with
+  // v_next = thr(x_k) + (xc - thr(x_k))/theta (fista_row) is linear in xc, e_c = xc - thr(xc)
+  // and thr(x_k), so one dense source suffices:
+  //   A y_next = a1 (A xc - A e_c) + b1 (A thr(x_k) + (A xc - A thr(x_k))/theta)
+  // with A e_c gathered from the transposed copy of A over the rows the threshold touched
+  // (cand_ax) and A thr(x_k) = the previous accepted trial's A xc - A e_c, kept in a ring of
+  // three (x_k's, this trial's, the speculated next trial's). The regrouping changes A y_next at
+  // the rounding level only (the GEMMs' own summation order does as much); A xc, hence the
+  // recorded objective, is computed directly. Without a kept A thr(x_k) (first iteration, after
+  // an untested step or finish) one dense pass restores it.
+  //
+  // The gather reads one m-vector of At per nonzero of e_c, so it beats the second dense source
+  // only while nnz(e_c) stays below a fraction of n (gather bytes / A bytes = nnz / n). FISTA's
+  // candidates can carry many small entries late in a phase: each gathered batch reports its
+  // nnz, and above the budget (GLX_SPLIT_NNZ, a fraction of n, default 0.35) the next
+  // kFistaDenseRun batches are the dense [xc | y_next] pair, then A thr(x_k) is restored and
+  // the gather form tried again.
+  static constexpr int kFistaDenseRun = 128;
+  void fista_split_prologue() {
+    T* scratch = X_[ff1_];   // free between iterations (the speculation's spare)
+    launch_threshold<T>(X_[ix_], scratch, nl_, O_.thres, flag_, ++epoch_, st_);
+    check_launch();
+    const T* xs[3] = {scratch, nullptr, nullptr};
+    spec_ax(1, xs);
+    launch_sum_partials<T>(Pp_, ax_split(plan_, 1), SXO_[0], ml_, st_);
+    check_launch();
+    kslot_ = 0;
+    stats_[6] += 1;
+  }
+  void fista_split_batch(T* ry, double theta, double theta_next, int slot, const T* cx,
+                         const double* cmax, unsigned* pub_seq, double* defer) {
+    const T* xs[3] = {E_, X_[ic_], nullptr};
+    cand_ax(xs);
+    launch_finalize_fista<T>(Pp_ + (size_t)gsplit_ * ml_, ax_split(plan_, 1), Pp_, gsplit_, B_, ry,
+                             SXO_[kslot_], SXO_[(kslot_ + 1) % 3], ml_, 1.0 - theta_next,
+                             theta_next, theta, cx, nl_, cmax, gather_counts(glists_, n_), (int)l_,
+                             defer ? Red{part_, ticket_, defer} : red(slot), st_);
+    check_launch();
+    if (defer) return;
+    if (comm_) comm_allreduce(comm_, scal_ + slot, 2, GLX_F64, st_);
+    if (pub_seq != nullptr) *pub_seq = post_readback();
   }
 
   // A^T r fused with a FISTA trial at y (gradient set `set`; x_k = xk; outputs X_[oc], X_[ov],
@@ -1019,7 +1105,8 @@ class Session : public SessionBase {
       if (pub_seq && attach_ok_) pb = make_pub(extra, pub_seq);
       else if (pub_seq) *pub_seq = post_readback(extra);
       launch_fista_trial<T>(true, yv, g.first, g.second, nullptr, xk, X_[oc], X_[ov], X_[oy], n_,
-                            l_, t, mu_, O_.thres, theta, theta_next, O_.delta, red(S_TR), st_, pb);
+                            l_, t, mu_, O_.thres, theta, theta_next, O_.delta, red(S_TR), st_, pb,
+                            fec(), fzf());
       check_launch();
       return;
     }
@@ -1027,7 +1114,7 @@ class Session : public SessionBase {
     if (pub_seq) pb = make_pub(extra, pub_seq);
     hipEvent_t e0 = prof_begin(1);
     launch_atr_fista<T>(plan_, A_, r, Gs_[set], yv, xk, X_[oc], X_[ov], X_[oy], t, mu_, O_.thres,
-                        theta, theta_next, red(S_TR), st_, pb, Gps_[set], pcnt_);
+                        theta, theta_next, red(S_TR), st_, pb, Gps_[set], pcnt_, fec(), fzf());
     check_launch();
     prof_end(1, e0);
     ++atr_calls_;
@@ -1128,6 +1215,16 @@ class Session : public SessionBase {
   int smode_ = 0, gsplit_ = 1;
   bool emode_ = false;         // split-candidate ProxGD: trials write e = p - p_thr, not z
   uint8_t* ezf() const { return emode_ ? zf_ : nullptr; }
+  // split-candidate FProxGD (iter_fista): trials also write e_c = xc - thr(xc) to E_ and its
+  // row flags to zf_; SXO_[kslot_] = A thr(x_k) (kslot_ < 0: not known)
+  bool fsplit_ = false;
+  T* E_ = nullptr;
+  T* SXO_[3] = {nullptr, nullptr, nullptr};
+  int kslot_ = -1;
+  double nnz_budget_ = 0;      // nnz(e_c) above which the dense batch is cheaper
+  int dense_left_ = 0;         // dense batches before the gather form is tried again
+  T* fec() const { return fsplit_ ? E_ : nullptr; }
+  uint8_t* fzf() const { return fsplit_ ? zf_ : nullptr; }
   int* flag_ = nullptr;
   int64_t fh_cap_ = 0;
   double* sp100_ = nullptr;   // SGD/GD: count(|x| > 1e-6 max|x|) after every 100th iteration

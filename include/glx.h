@@ -99,7 +99,9 @@ typedef struct glx_result {
   int64_t syncs;        /* host<->device synchronisations                             */
   int64_t ax_sources;   /* right-hand sides batched into those A@x passes (>= ax_calls) */
   double stats[8];      /* diagnostics: [0] threshold-changed entries and [1] rows summed over
-                           accepted ProxGD steps, [2] accepted steps                    */
+                           accepted ProxGD steps, [2] accepted steps; split-candidate
+                           FProxGD: [3] gathered batches, [4] dense batches, [5] nnz(e_c)
+                           summed over the gathered ones, [6] A thr(x_k) restores       */
 } glx_result;
 
 typedef struct glx_session glx_session;

@@ -43,7 +43,8 @@ def main():
     torch.cuda.synchronize()
     wall = time.perf_counter() - t0
     print(json.dumps({"method": a.method, "k": int(k), "tt": out["tt"], "wall": wall,
-                      "its": k / out["tt"], "fval": float(out["fval"]),
+                      "its": k / out["tt"], "fval": float(out["fval"]), "stats": out.get("stats"),
+                      "ax_calls": out.get("ax_calls"), "ax_sources": out.get("ax_sources"),
                       "env": {k2: v for k2, v in os.environ.items() if k2.startswith("GLX_")}}))
 
 

@@ -98,16 +98,21 @@ def test_make_opts_merging_and_errors():
 def test_workspace_planning_host_only():
     from glx import _lib
     from glx.solver import make_opts
-    for (m, n, l, dt) in [(8192, 16384, 32, 1), (4096, 8192, 16, 1), (65536, 8192, 1, 1),
-                          (256, 512, 2, 1), (301, 517, 3, 0), (8192, 16384, 32, 0)]:
-        p = _lib.GlxProblem(dtype=dt, method=0, m=m, n=n, l=l, A=256, b=256, x=256, mu0=0.01)
-        nb = ctypes.c_size_t(0)
-        _lib.check(_lib.lib().glx_workspace_bytes(ctypes.byref(p), ctypes.byref(make_opts(0, {})), ctypes.byref(nb)))
-        es = 8 if dt == 1 else 4
-        # fp64 ProxGD's split-candidate trial keeps a transposed copy of A (kernels_gather.hip)
-        at = es * m * n if (dt == 1 and l in (16, 32)) else 0
-        assert nb.value >= es * (2 * n * l + 2 * m * l) + at  # x-buffers + residuals at least
-        assert nb.value < at + es * (m * n) // 4 + (64 << 20)   # else never close to the size of A
+    for meth in (_lib.GLX_PROXGD, _lib.GLX_FPROXGD):
+        for (m, n, l, dt) in [(8192, 16384, 32, 1), (4096, 8192, 16, 1), (65536, 8192, 1, 1),
+                              (256, 512, 2, 1), (301, 517, 3, 0), (8192, 16384, 32, 0)]:
+            p = _lib.GlxProblem(dtype=dt, method=meth, m=m, n=n, l=l, A=256, b=256, x=256, mu0=0.01)
+            nb = ctypes.c_size_t(0)
+            _lib.check(_lib.lib().glx_workspace_bytes(ctypes.byref(p), ctypes.byref(make_opts(meth, {})),
+                                                      ctypes.byref(nb)))
+            es = 8 if dt == 1 else 4
+            # fp64 split-candidate trials keep a transposed copy of A (kernels_gather.hip);
+            # FProxGD's also e_c and three A thr(x) residual-sized slots
+            split = dt == 1 and l in (16, 32)
+            at = es * m * n if split else 0
+            extra = es * (n * l + 3 * m * l) if (split and meth == _lib.GLX_FPROXGD) else 0
+            assert nb.value >= es * (2 * n * l + 2 * m * l) + at + extra  # x-buffers + residuals at least
+            assert nb.value < at + es * (m * n) // 4 + (64 << 20)   # else never close to the size of A
 
 
 def test_invalid_problem_rejected_on_host():
