@@ -876,11 +876,23 @@ __global__ __launch_bounds__(64 * WAVES) void k_ax_lds2(const T* __restrict__ A,
 // blockIdx.y = row split. Needs n % 64 == 0 (n % 256 for WL = 1), m % 4 == 0.
 // Gp[split][n][16*NT].
 // ------------------------------------------------------------------------------------------
+// A lane (i, q) of a row step feeds the four MFMAs e = 0..3 with row q of A at panel columns
+// atr_col(i, e); MFMA e's output row i is then G row col0 + atr_col(i, e). f64: columns
+// {2i, 2i+1} and {32 + 2i, 33 + 2i}, so each of the two 16-B loads of a wave-instruction covers
+// 256 contiguous bytes of each of its four rows (the streaming probe, scripts/stream_probe.hip:
+// 6.1 TB/s for the 4i..4i+3 form, whose loads leave every other 16 B of a 512-B span to the
+// next instruction, against 6.3-7.1 TB/s for contiguous 256/512-B pieces). f32: one 16-B load
+// already covers columns 4i..4i+3.
+template <typename T>
+__device__ inline int atr_col(int i, int e) {
+  if constexpr (sizeof(T) == 8) return (e >> 1) * 32 + 2 * i + (e & 1);
+  else return 4 * i + e;
+}
 template <typename T, bool NTL> struct Load4;
 template <bool NTL> struct Load4<double, NTL> {
-  __device__ static inline void go(const double* p, double (&a)[4]) {
+  __device__ static inline void go(const double* p, double (&a)[4]) {   // p = row + col0 + 2i
     const d2_t v0 = load_vec<double, NTL>(p);
-    const d2_t v1 = load_vec<double, NTL>(p + 2);
+    const d2_t v1 = load_vec<double, NTL>(p + 32);
     a[0] = v0[0]; a[1] = v0[1]; a[2] = v1[0]; a[3] = v1[1];
   }
 };
@@ -892,7 +904,7 @@ template <bool NTL> struct Load4<float, NTL> {
 };
 
 // One 64-column panel of A^T R over this wave's (WL 1: this block's) row range; returns the
-// panel's first column. acc[e][nt] holds rows col0 + 4 * M::row(lane, r) + e. For WL 0 the
+// panel's first column. acc[e][nt] holds rows col0 + atr_col(M::row(lane, r), e). For WL 0 the
 // block's four waves split the rows (K) and are summed through LDS in the fixed order
 // ((w0 + w1) + w2) + w3; afterwards wave w holds the complete sum for e == w in acc[w][*]
 // (the other e of a wave are partial and unused), so the four waves share the epilogue.
@@ -915,7 +927,7 @@ __device__ inline int64_t atr_panel(const T* __restrict__ A, const T* __restrict
   const int64_t w = WL == 0 ? pby * 4 + wave : pby;
   const int64_t sb = steps * w / W, se = steps * (w + 1) / W;
 
-  const T* ap = A + (sb * 4 + q) * n + col0 + 4 * i;
+  const T* ap = A + (sb * 4 + q) * n + col0 + atr_col<T>(i, 0);
   const T* rp = R + (sb * 4 + q) * L + i;
 
 #pragma unroll
@@ -1000,7 +1012,7 @@ __device__ inline bool atr_split_combine(typename MF<T>::acc_t (&acc)[4][NT], T*
     if (e != wave) continue;
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
-      const int64_t row = col0 + 4 * M::row(lane, r) + e;
+      const int64_t row = col0 + atr_col<T>(M::row(lane, r), e);
 #pragma unroll
       for (int nt = 0; nt < NT; ++nt)
         __hip_atomic_store(Gp + split * nl + row * L + nt * 16 + i, acc[e][nt][r], __ATOMIC_RELAXED,
@@ -1019,7 +1031,7 @@ __device__ inline bool atr_split_combine(typename MF<T>::acc_t (&acc)[4][NT], T*
     if (e != wave) continue;
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
-      const int64_t row = col0 + 4 * M::row(lane, r) + e;
+      const int64_t row = col0 + atr_col<T>(M::row(lane, r), e);
 #pragma unroll
       for (int nt = 0; nt < NT; ++nt) {
         const T* g = Gp + row * L + nt * 16 + i;
@@ -1050,7 +1062,7 @@ __global__ __launch_bounds__(256) void k_atr_mfma(const T* __restrict__ A, const
     if (WL == 0 && e != wave) continue;   // WL 0: wave w owns the rows e == w
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
-      const int64_t grow = col0 + 4 * M::row(lane, r) + e;
+      const int64_t grow = col0 + atr_col<T>(M::row(lane, r), e);
 #pragma unroll
       for (int nt = 0; nt < NT; ++nt) gout[grow * L + nt * 16 + i] = acc[e][nt][r];
     }
@@ -1095,13 +1107,13 @@ __global__ __launch_bounds__(256, sizeof(T) == 8 ? 2 : 1) void k_atr_prox(const 
     T xa[4][NT];
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
-      const int64_t row = col0 + 4 * M::row(lane, r) + e;
+      const int64_t row = col0 + atr_col<T>(M::row(lane, r), e);
 #pragma unroll
       for (int nt = 0; nt < NT; ++nt) xa[r][nt] = x[row * L + nt * 16 + i];
     }
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
-      const int64_t row = col0 + 4 * M::row(lane, r) + e;
+      const int64_t row = col0 + atr_col<T>(M::row(lane, r), e);
       T gv[NT], pv[NT], pth[NT], zv[NT];
       bool ok[NT];
 #pragma unroll
@@ -1161,7 +1173,7 @@ __global__ __launch_bounds__(256, sizeof(T) == 8 ? 2 : 1) void k_atr_fista(const
     T ya[4][NT], xa[4][NT];
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
-      const int64_t row = col0 + 4 * M::row(lane, r) + e;
+      const int64_t row = col0 + atr_col<T>(M::row(lane, r), e);
 #pragma unroll
       for (int nt = 0; nt < NT; ++nt) {
         ya[r][nt] = y[row * L + nt * 16 + i];
@@ -1170,7 +1182,7 @@ __global__ __launch_bounds__(256, sizeof(T) == 8 ? 2 : 1) void k_atr_fista(const
     }
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
-      const int64_t row = col0 + 4 * M::row(lane, r) + e;
+      const int64_t row = col0 + atr_col<T>(M::row(lane, r), e);
       T gv[NT], xcv[NT], vnv[NT], ynv[NT], ecv[NT];
       bool ok[NT];
 #pragma unroll
@@ -1382,7 +1394,12 @@ static constexpr int kAxDefault = 52228;       // f64 single RHS: LDS, MT 2, PF 
 static constexpr int kAxFallback = 21820;      // f64: VPL 2, direct loads, MT 8, PF 2
 static constexpr int kAxDefault32 = 21410;     // f32: VPL 2, direct loads, MT 4, PF 1
 // A^T R code: NTL*1000 + WL*10 + PF (WL 1 = four panels of a block share rows, PF = ring depth)
-static constexpr int kAtrDefault = 108;        // f64: WL 0, PF 8
+static constexpr int kAtrDefault = 108;        // f64: WL 0, PF 8 (A that stays in the MALL)
+static constexpr int kAtrDefaultBig = 1008;    // f64: non-temporal A, WL 0, PF 8
+// Non-temporal A loads pay only when A cannot stay in the 256 MiB Infinity Cache between the
+// passes: NS (1 GiB) 2278 -> 2326 it/s, FProxGD 2397 -> 2451, but C2 (256 MiB) 7477 -> 6250 and
+// the 1024-row shard (128 MiB) 9477 -> 8323 (profiles/r2_axat/)
+static constexpr double kAtrNtBytes = 384.0 * 1024 * 1024;
 static constexpr int kAtrDefault32 = 1114;     // f32: non-temporal A, WL 1, PF 4
 // batched right-hand sides (MFMA-bound at l = 32, both dtypes): the LDS tile, 2 waves per SIMD
 // (end-to-end sweep, profiles/r1_tuning: f64 8-wave blocks, f32 4-wave blocks with PF 3)
@@ -1525,7 +1542,9 @@ GemmPlan make_plan(int esize, int64_t m, int64_t n, int64_t l, int ax_variant) {
   }
   // ---- A^T R ----
   int atr_code = env_int("GLX_ATR_VARIANT", 0);
-  if (atr_code == 0) atr_code = esize == 8 ? kAtrDefault : kAtrDefault32;
+  if (atr_code == 0)
+    atr_code = esize == 8 ? ((double)m * n * esize > kAtrNtBytes ? kAtrDefaultBig : kAtrDefault)
+                          : kAtrDefault32;
   const int ntl = atr_code >= 1000 ? 1 : 0;
   int wl = (atr_code / 10) % 10;
   const int pf = atr_code % 10;

@@ -116,11 +116,19 @@ static void validate(const glx_problem* P, const glx_opts* O) {
 // ProxGD configuration is on the benchmark path.
 // FProxGD with line search takes the gather form too (iter_fista: A y_next by linearity from
 // A xc, A e_c and the kept A thr(x_k)); GLX_SPLIT_FISTA=0 keeps its dense [xc | y_next] batch.
+// Only for A of at least kSplitMinBytes (this rank's rows): the column lists and the gather
+// carry a fixed ~70 + 50 us that a short dense pass cannot hide. Measured against the dense
+// batch (profiles/r2_splitgate/): NS (1 GiB) 2295 vs 2080 it/s, (4096,16384,32) 3894 vs 3832,
+// but C2 (4096,8192,16) 7329 vs 8948 and the comm-path shards of 4096 / 2048 / 1024 rows
+// 3543 / 6756 / 9748 vs 3623 / 6884 / 11162. GLX_SPLIT_CAND=1 forces it at any size (tests).
+static constexpr double kSplitMinBytes = 768.0 * 1024 * 1024;
 static int split_mode(const glx_problem& P, const glx_opts& O) {
   if (O.exact_objective != 0 || P.dtype != GLX_F64) return 0;
   if (P.method != GLX_PROXGD && P.method != GLX_FPROXGD) return 0;
   const char* sc = std::getenv("GLX_SPLIT_CAND");
   if (sc && std::strcmp(sc, "0") == 0) return 0;
+  const bool force = sc && (std::strcmp(sc, "1") == 0 || std::strcmp(sc, "sp") == 0);
+  if (!force && (double)P.m * (double)P.n * 8.0 < kSplitMinBytes) return 0;
   if (P.method == GLX_FPROXGD) {
     const char* sf = std::getenv("GLX_SPLIT_FISTA");
     if (sf && std::strcmp(sf, "0") == 0) return 0;

@@ -65,6 +65,19 @@ def test_sharded_matches_oracle(tmp_path, world, solver, shape):
     assert v["x_maxdiff"] <= 1e-6 * v["x_scale"]
 
 
+@pytest.mark.parametrize("solver", ["gl_ProxGD_primal", "gl_FProxGD_primal"])
+def test_sharded_split_candidate_forced(tmp_path, monkeypatch, solver):
+    # the split-candidate trial (default only for A >= 768 MiB per rank) forced at a small shard
+    monkeypatch.setenv("GLX_SPLIT_CAND", "1")
+    v = run_sharded(tmp_path, 2, solver, 512, 1024, 32, maxit=25)
+    ranks = v["ranks"]
+    assert ranks[0]["x_sha"] == ranks[1]["x_sha"] and ranks[0]["k"] == ranks[1]["k"]
+    assert ranks[0]["k"] == v["oracle_k"]
+    fh, fo = np.asarray(ranks[0]["f_hist"]), np.asarray(v["oracle_f_hist"])
+    assert np.max(np.abs(fh - fo) / np.abs(fo)) < 1e-8
+    assert v["x_maxdiff"] <= 1e-6 * v["x_scale"]
+
+
 def test_sharded_proxgd_line_search_rejections(tmp_path):
     # alpha0 above 1/L: first trials are rejected and retried (k_prox_pgd), others accepted
     # (the trial staged into A @ [z | p_thr]); speculation is dropped and resumed around them

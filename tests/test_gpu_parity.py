@@ -83,6 +83,32 @@ def test_solver_matches_reference_golden(name):
             assert _rel(f_hist, gold["f_hist"]) < FP32_FHIST_BAR
 
 
+def _split_capable(meta):
+    return (meta["dtype"] == "f64" and meta["solver"] in ("gl_ProxGD_primal", "gl_FProxGD_primal")
+            and meta["l"] in (16, 32) and meta.get("opts", {}).get("step_type", "line_search")
+            == "line_search")
+
+
+SPLIT_CASES = sorted(c for c, meta in golden_index().items() if _split_capable(meta))
+
+
+@pytest.mark.parametrize("name", SPLIT_CASES)
+def test_split_candidate_forced_golden(name, monkeypatch):
+    """The split-candidate trial (ProxGD: A p = A p_thr + A e, A e gathered from A^T; FProxGD:
+    A y_next by linearity from A xc, A e_c and the kept A thr(x_k)) is the default only for A of
+    768 MiB or more (solver.cpp split_mode); GLX_SPLIT_CAND=1 forces it on every golden case it
+    supports, against the same fp64 bars as test_solver_matches_reference_golden."""
+    monkeypatch.setenv("GLX_SPLIT_CAND", "1")
+    meta, gold = golden_case(name)
+    A, b, u, x0, mu = golden_inputs(meta)
+    x, k, out = _solve(meta, A, b, x0, mu)
+    assert k == int(gold["k"]), (k, int(gold["k"]))
+    assert _rel(out["fval"], gold["fval"]) < 1e-8
+    assert _rel(np.asarray([float(v) for v in out["f_hist"]]), gold["f_hist"]) < 1e-8
+    xg = gold["x"]
+    assert np.max(np.abs(x - xg)) <= 1e-6 * max(1.0, np.max(np.abs(xg)))
+
+
 @pytest.mark.parametrize("name", ["default_gl_ProxGD_primal", "seed114514_gl_ProxGD_primal",
                                   "mid_512x1024x16_f64_gl_ProxGD_primal"])
 def test_proxgd_exact_objective_mode(name):
