@@ -44,7 +44,9 @@ def main():
     write = load(args.write, "WRITE_SIZE")
     summary = {}
     for name in fetch:
-        short = "ax" if ("k_ax_" in name or "k_gemv_" in name) else ("atr" if "k_atr_" in name else None)
+        short = ("ax" if ("k_ax_" in name or "k_gemv_" in name) else
+                 ("atr" if "k_atr_" in name else
+                  ("gather" if ("k_at_gather" in name or "k_e_lists" in name) else None)))
         if short is None:
             continue
         f = sum(fetch[name]) / len(fetch[name])
@@ -55,14 +57,21 @@ def main():
     # dominant kernel = the A@x launch with the most dispatches
     entry = {}
     for k, v in summary.items():
+        if k == "gather":   # split-candidate A e: the column lists and the gather, both per trial
+            entry[k] = {"kernels": v, "bytes_per_launch": sum(e["bytes_per_launch"] for e in v)}
+            continue
         best = max(v, key=lambda e: e["launches"])
         entry[k] = best
     out = {}
     if os.path.exists(args.out):
         out = json.load(open(args.out))
     if "ax" in entry:
-        out[args.key] = {"bytes_per_launch": entry["ax"]["bytes_per_launch"], "detail": entry,
-                         "correction": "traffic = (2*FETCH_SIZE + WRITE_SIZE) KB * 1024 (gfx950)"}
+        # split-candidate mode: bench.py times the dense pass and the A e gather as one A@X
+        # launch, so its traffic is the sum of the two
+        tot = entry["ax"]["bytes_per_launch"] + entry.get("gather", {}).get("bytes_per_launch", 0.0)
+        out[args.key] = {"bytes_per_launch": tot, "detail": entry,
+                         "correction": "traffic = (2*FETCH_SIZE + WRITE_SIZE) KB * 1024 (gfx950)",
+                         "source": "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes, round 2"}
     os.makedirs(os.path.dirname(args.out) or ".", exist_ok=True)
     json.dump(out, open(args.out, "w"), indent=1, sort_keys=True)
     print(json.dumps(out.get(args.key), indent=1))
