@@ -20,6 +20,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cstdlib>
 
 #include "glx_device.h"
 
@@ -38,8 +39,12 @@ constexpr int kGemvMaxBlocks = 256;    // one 8-wave workgroup per CU
 }  // namespace
 
 // RB rows per batch (two batches in flight): 2 for VPT <= 4, 1 for VPT = 8 (register budget of
-// two waves per SIMD: 2 x RB x VPT row vectors + x, thr(x) and G)
-template <typename T, int VPT, int RB>
+// two waves per SIMD: 2 x RB x VPT row vectors + x, thr(x) and G).
+// NT: A read with the non-temporal policy. A workgroup streams one contiguous range of rows in
+// whole 1-KiB wave-instructions, the shape the streaming probe reads at 7.1-7.2 TB/s
+// non-temporal against 6.1-6.2 TB/s default (scripts/stream_probe.hip, "chunk"); used when A
+// cannot stay in the Infinity Cache anyway (kGemvNtBytes).
+template <typename T, int VPT, int RB, bool NT>
 __global__ __launch_bounds__(kGemvThreads) void k_gemv_pair_fused(
     const T* __restrict__ A, const T* __restrict__ x, const T* __restrict__ xt,
     const T* __restrict__ b, T* __restrict__ Gp, int64_t m, int64_t n, double* fh, double fh_mu,
@@ -75,7 +80,9 @@ __global__ __launch_bounds__(kGemvThreads) void k_gemv_pair_fused(
       i = i < nrows ? i : nrows - 1;
       const T* rowp = A + (r0 + i) * n;
 #pragma unroll
-      for (int k = 0; k < VPT; ++k) dst[r][k] = *reinterpret_cast<const V*>(rowp + col[k]);
+      for (int k = 0; k < VPT; ++k)
+        dst[r][k] = NT ? __builtin_nontemporal_load(reinterpret_cast<const V*>(rowp + col[k]))
+                       : *reinterpret_cast<const V*>(rowp + col[k]);
     }
   };
 
@@ -188,11 +195,21 @@ int gemv_fused_blocks(int esize, int64_t m, int64_t n, int64_t l) {
   return (int)std::max<int64_t>(1, blocks);
 }
 
+constexpr double kGemvNtBytes = 384.0 * 1024 * 1024;
 template <typename T, int VPT, int RB>
 static void gemv_go(int blocks, const T* A, const T* x, const T* xt, const T* b, T* Gp, int64_t m,
                     int64_t n, double* fh, double fh_mu, const double* rn, Red red, hipStream_t st) {
-  hipLaunchKernelGGL((k_gemv_pair_fused<T, VPT, RB>), dim3((unsigned)blocks), dim3(kGemvThreads), 0, st,
-                     A, x, xt, b, Gp, m, n, fh, fh_mu, rn, red);
+  static const int nt_env = [] {
+    const char* e = std::getenv("GLX_GEMV_NT");
+    return e ? std::atoi(e) : -1;
+  }();
+  const bool nt = nt_env >= 0 ? nt_env != 0 : (double)m * n * sizeof(T) > kGemvNtBytes;
+  if (nt)
+    hipLaunchKernelGGL((k_gemv_pair_fused<T, VPT, RB, true>), dim3((unsigned)blocks),
+                       dim3(kGemvThreads), 0, st, A, x, xt, b, Gp, m, n, fh, fh_mu, rn, red);
+  else
+    hipLaunchKernelGGL((k_gemv_pair_fused<T, VPT, RB, false>), dim3((unsigned)blocks),
+                       dim3(kGemvThreads), 0, st, A, x, xt, b, Gp, m, n, fh, fh_mu, rn, red);
 }
 
 template <typename T>
