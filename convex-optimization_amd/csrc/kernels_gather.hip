@@ -19,6 +19,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdlib>
+#include <cstring>
 
 #include "glx.h"
 #include "glx_device.h"
@@ -143,7 +144,9 @@ __global__ __launch_bounds__(kGThreads) void k_e_lists(const T* __restrict__ E,
 // over column c's list (k_e_lists) in its ascending order (deterministic); thread t (row
 // r = 256 rb + t) keeps 8 loads in flight and the 64 lanes of a wave read 512 contiguous bytes
 // of one At row. out[r][c] = the sum (one slab: no K split).
-template <typename T, int L>
+// NT: At read with the non-temporal policy (each of its rows is read at most once per trial;
+// GLX_GATHER_NT)
+template <typename T, int L, bool NT>
 __global__ __launch_bounds__(kGThreads) void k_at_gather(const T* __restrict__ At,
                                                          const T* __restrict__ E,
                                                          const unsigned short* __restrict__ lists,
@@ -163,7 +166,7 @@ __global__ __launch_bounds__(kGThreads) void k_at_gather(const T* __restrict__ A
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       const int64_t k = lst[idx + u];
-      a[u] = At[k * m + rr];
+      a[u] = NT ? __builtin_nontemporal_load(At + k * m + rr) : At[k * m + rr];
       ev[u] = E[k * L + c];
     }
 #pragma unroll
@@ -171,7 +174,7 @@ __global__ __launch_bounds__(kGThreads) void k_at_gather(const T* __restrict__ A
   }
   for (; idx < total; ++idx) {
     const int64_t k = lst[idx];
-    acc = acc + At[k * m + rr] * E[k * L + c];
+    acc = acc + (NT ? __builtin_nontemporal_load(At + k * m + rr) : At[k * m + rr]) * E[k * L + c];
   }
   if (r < m) P[r * L + c] = acc;
 }
@@ -223,12 +226,16 @@ void launch_at_gather(const T* At, const T* E, int64_t m, int64_t n, int64_t l, 
   if (!gather_ok(n, l)) throw Error{GLX_E_INVALID, "A e gather: needs l in {16, 32}, n < 65536"};
   const int gx = (int)((m + kGThreads - 1) / kGThreads);
   const unsigned short* lists = static_cast<const unsigned short*>(lists_ws);
-  if (l == 32)
-    hipLaunchKernelGGL((k_at_gather<T, 32>), dim3((unsigned)(gx * l)), dim3(kGThreads), 0, st, At, E,
-                       lists, list_counts(lists_ws, n), m, n, P, gx);
-  else
-    hipLaunchKernelGGL((k_at_gather<T, 16>), dim3((unsigned)(gx * l)), dim3(kGThreads), 0, st, At, E,
-                       lists, list_counts(lists_ws, n), m, n, P, gx);
+  static const bool nt = [] {
+    const char* e = std::getenv("GLX_GATHER_NT");
+    return !(e && std::strcmp(e, "0") == 0);
+  }();
+  auto go = [&](auto kern) {
+    hipLaunchKernelGGL(kern, dim3((unsigned)(gx * l)), dim3(kGThreads), 0, st, At, E, lists,
+                       list_counts(lists_ws, n), m, n, P, gx);
+  };
+  if (l == 32) nt ? go(k_at_gather<T, 32, true>) : go(k_at_gather<T, 32, false>);
+  else nt ? go(k_at_gather<T, 16, true>) : go(k_at_gather<T, 16, false>);
 }
 
 // workspace of the column lists: l * n indices + 256 B of counts
