@@ -303,17 +303,32 @@ def main():
         # Gather form (default): A e reads the flagged rows of a transposed copy of A (m values
         # each) on top of the dense pass; the "sp" form skips unflagged K chunks in the tile.
         nsrc = work["ax_sources"] / max(1, work["ax_calls"])
-        split_env = os.environ.get("GLX_SPLIT_CAND", "1")
-        split_cand = (args.method == "gl_ProxGD_primal" and not args.exact and split_env != "0")
-        sparse_rows = res["stats"][1] / max(1.0, res["stats"][2]) if split_cand else 0.0
-        gather_rows = sparse_rows if (split_cand and split_env != "sp") else 0.0
+        # the solver's split-candidate rule (solver.cpp split_mode): fp64, not exact, A of this
+        # rank >= 768 MiB unless GLX_SPLIT_CAND=1/sp forces it; FProxGD only in the gather form
+        split_env = os.environ.get("GLX_SPLIT_CAND", "")
+        split_on = (args.dtype == "f64" and not args.exact and split_env != "0" and
+                    (ml * n * 8 >= 768 * 2 ** 20 or split_env in ("1", "sp")))
+        gather_fits = l in (16, 32) and n <= 65535
+        st = res["stats"]
+        if args.method == "gl_ProxGD_primal":
+            split_cand = split_on
+            sparse_rows = st[1] / max(1.0, st[2]) if split_cand else 0.0
+            gather_rows = sparse_rows if (split_cand and split_env != "sp" and gather_fits) else 0.0
+        elif args.method == "gl_FProxGD_primal":
+            split_cand = (split_on and gather_fits and
+                          os.environ.get("GLX_SPLIT_FISTA", "") != "0")
+            # nnz(e_c) per gathered batch; bytes averaged over all trial batches (some are dense)
+            sparse_rows = st[5] / max(1.0, st[3]) if split_cand else 0.0
+            gather_rows = st[5] / max(1.0, st[3] + st[4]) if split_cand else 0.0
+        else:
+            split_cand, sparse_rows, gather_rows = False, 0.0, 0.0
         ax_bytes = es * (ml * n + (ml + n) * l * nsrc + (n * l if split_cand else 0) + ml * gather_rows)
         atr_bytes = es * (ml * n + (ml + n) * l)
         ax_flops = 2.0 * ml * n * l * nsrc + 2.0 * ml * l * sparse_rows
         atr_flops = 2.0 * ml * n * l
         ach = ax_bytes / ax_avg_s / 1e9 if ax_n else None
         cfg_key = "%s_%s_%dx%dx%d_g%d%s" % (args.method, args.dtype, m, n, l, world,
-                                            "_sc" if split_cand else "")
+                                            "_sc" if split_cand and gather_rows else "")
         peak_tf = MFMA_PEAK_TFS[args.dtype]
         mfma_bound = ax_flops / (peak_tf * 1e12) >= ax_bytes / (HBM_PEAK_GBS * 1e9)
         ax_tf = ax_flops / ax_avg_s / 1e12 if ax_n else None
@@ -336,8 +351,8 @@ def main():
                 "bytes_per_launch": ax_bytes, "avg_launch_us": ax_avg_s * 1e6, "launches_timed": ax_n,
                 "timed_every": args.profile,
                 "rhs_per_launch": nsrc,
-                "split_candidate": ("gather" if gather_rows or (split_cand and split_env != "sp") else
-                                    ("sp" if split_cand else False)),
+                "split_candidate": (False if not split_cand else
+                                    ("sp" if (split_env == "sp" or not gather_fits) else "gather")),
                 "sparse_rows_per_launch": sparse_rows, "hbm_GBs": ax_gbs, "hbm_frac": ax_gbs / HBM_PEAK_GBS if ax_n else None,
                 "mfma_tflops": ax_tf, "mfma_frac": ax_tf / peak_tf if ax_n else None,
                 "atr_avg_launch_us": atr_avg_s * 1e6,
