@@ -391,7 +391,10 @@ def main():
                      "syncs_per_iter": work["syncs"] / steps,
                      "thr_changed_entries_per_step": res["stats"][0] / max(1.0, res["stats"][2]),
                      "thr_changed_rows_per_step": res["stats"][1] / max(1.0, res["stats"][2]),
-                     "syncs_total": res["syncs"], "iters_total": res["k"]},
+                     "syncs_total": res["syncs"], "iters_total": res["k"],
+                     # ProxGD line-search decisions taken on the device (solver.cpp dc_run)
+                     "device_decided_frac": (res["stats"][7] / max(1, res["k"])
+                                             if args.method == "gl_ProxGD_primal" else 0.0)},
         }
         if world == 1 and not args.no_cpu_baseline:
             try:

@@ -27,6 +27,14 @@ __device__ inline double waves_combine(int op, const double* w) {
   return a;
 }
 
+// A launch of a device-controlled batch that an earlier decision has cancelled (Red::skip);
+// the flag was written by an earlier kernel in the stream, so every workgroup reads the same value
+__device__ inline bool red_skipped(const Red& red) {
+  if (red.skip == nullptr) return false;
+  const int v = *red.skip;
+  return v != 0 && v != red.skip_pass;
+}
+
 // Reduce NV per-thread values over the grid; block size must be 64 * NW (NW = 4 or 8).
 // MAXMASK bit v = max op. slot = this block's partials slot (default blockIdx.x): a launch
 // whose first workgroup is a publisher (publisher_first) puts that one last and the others at

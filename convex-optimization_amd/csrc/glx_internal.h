@@ -33,7 +33,37 @@ struct Red {
   double* part;
   unsigned* ticket;
   double* out;     // kMaxRedVals consecutive doubles (caller picks the slots)
+  // device-controlled batches (solver.cpp dc_run): the whole launch is skipped, uniformly over
+  // the grid (nobody touches a ticket or counter), when skip != NULL and *skip is neither 0 nor
+  // skip_pass
+  const int* skip = nullptr;
+  int skip_pass = 0;
 };
+
+// Device-side line-search decision of a device-controlled ProxGD batch (solver.cpp dc_batch),
+// run by the last block of the trial's residual finalize once the residual sums are final
+// (gl_ProxGD_primal.py:86-99 Armijo test, :118-125 stop rule). ring == NULL: off.
+//   state[0..3] = gx (1/2 ||A thr(x) - b||^2), f and sparsity of the last record, stable count
+//   tr = the trial's six sums (k_prox_pgd / k_atr_prox), t = the trial's step
+// On acceptance the next record (f, s) and the stop rule are evaluated and the state advances.
+// *abort = 0 (accepted), pass (accepted, the next record stops the phase), -1 (rejected):
+// the speculative gradient queued right behind this decision runs on 0 and on this tag
+// (Red::skip_pass), the rest of the batch only on 0. ring[10] = 0, 1 (stop), 2 (rejected).
+// rec[0..10] (device) = the four residual sums, the six trial sums and the code as a double.
+// The speculative kernel queued behind the decision hands rec to the host from its publisher
+// workgroup (Pub), also when the decision cancels it, so the PCIe write latency stays off the
+// finalize's critical path.
+struct Ctl {
+  double* rec = nullptr;
+  double* state = nullptr;
+  int* abort = nullptr;
+  const double* tr = nullptr;
+  double tag = 0.0, t = 0.0, mu0 = 0.0, ftol = 0.0, nl = 1.0;
+  int stable_thr = 0, use_sp = 1, emode = 0;
+  int pass = 0;    // nonzero; the abort word's value for "stop" (Red::skip_pass of the kernel behind)
+};
+constexpr int kCtlRec = 16;        // doubles per ring record
+constexpr int kCtlMaxBatch = 64;   // ring records
 
 // A scalar packet for the host (what k_publish writes) carried by a kernel launch as one extra
 // workgroup (publisher_first, glx_device.h); host == NULL: none.
@@ -135,10 +165,11 @@ size_t gather_lists_bytes(int64_t n);
 // the l per-column list lengths inside lists_ws (device)
 const unsigned* gather_counts(const void* lists_ws, int64_t n);
 template <typename T>
-void launch_e_lists(const T* E, const uint8_t* zf, int64_t n, int64_t l, void* lists_ws, hipStream_t st);
+void launch_e_lists(const T* E, const uint8_t* zf, int64_t n, int64_t l, void* lists_ws, hipStream_t st,
+                    const int* skip = nullptr);
 template <typename T>
 void launch_at_gather(const T* At, const T* E, int64_t m, int64_t n, int64_t l, T* P, void* lists_ws,
-                      hipStream_t st);
+                      hipStream_t st, const int* skip = nullptr);
 
 // ---- fused residual + gradient in one pass over A (kernels_fused.hip) ----
 // Sraw = A X (m x 32) and Gs[RG][n][32] with G = A^T (A X - B) = sum of the RG slabs in order.
@@ -169,7 +200,11 @@ void launch_finalize_residual(const T* P, int S, const T* B, int nsrc, T* const*
                               const int* gate, int epoch, int gate_mode, const T* cx, int64_t cn,
                               const double* cmax, double* fh, double fh_mu, const double* fh_rn,
                               Red red, hipStream_t st, const double* snap_src = nullptr,
-                              double* snap_dst = nullptr, int nsnap = 0, int chain = 0, int S0 = 0);
+                              double* snap_dst = nullptr, int nsnap = 0, int chain = 0, int S0 = 0,
+                              Ctl ctl = Ctl{});
+// state[0..3] = s0..s3, *abort = 0 (one thread; the seed of a device-controlled batch)
+void launch_ctl_seed(double* state, int* abort, double s0, double s1, double s2, double s3,
+                     hipStream_t st);
 template <typename T>
 void launch_sum_partials(const T* Gp, int S, T* G, int64_t nl, hipStream_t st);
 // ProxGD trial: p = prox(x - t g, t), G_t = (x - p)/t, z = x - t G_t, pthr = p thresholded.

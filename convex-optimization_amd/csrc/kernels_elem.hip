@@ -71,13 +71,66 @@ __device__ inline T group_slab_sum(const T* __restrict__ P, int S, int64_t ml, i
   return v;
 }
 
+// Device-side control of a ProxGD line-search iteration (struct Ctl, solver.cpp dc_batch): the
+// Armijo test of gl_ProxGD_primal.py:89-92 with t = the trial's step, then — on acceptance — the
+// next record's objective and sparsity (:132-133 via the split-candidate/dense residual sums) and
+// the stop rule of :118-125. The expressions are the host's (solver.cpp iter_proxgd, stop_rule)
+// term for term, so with -ffp-contract=off the decision is the host's bit for bit; the host
+// re-derives it from the record and checks it. out = the four residual sums of this finalize.
+// pre = tr[0..5], state[0..3], loaded when the kernel starts (they were final before it began),
+// so the last block's decision costs no dependent global loads at the end of the kernel
+__device__ inline void ctl_decide(const Ctl& c, const double* out, const double (&pre)[10]) {
+  double* st = c.state;
+  const double* tr = pre;
+  double rec[kCtlRec];
+  for (int k = 0; k < 4; ++k) rec[k] = out[k];
+  for (int k = 0; k < 6; ++k) rec[4 + k] = tr[k];
+  const double gz = 0.5 * out[0];
+  const double gx = pre[6];
+  const bool acc = gz <= gx - c.t * tr[0] + 0.5 * c.t * tr[1];
+  int code = 2;
+  if (acc) {
+    const double sqx = (c.emode || tr[4] != 0) ? out[0] : out[1];
+    const double f = 0.5 * sqx + c.mu0 * tr[2];
+    const double s = out[3] / c.nl;
+    const double fl = pre[7], sl = pre[8];
+    bool ok = fabs(f - fl) / fabs(fl) < c.ftol;
+    if (ok && c.use_sp) ok = fabs(s - sl) / fabs(sl) < c.ftol;
+    const double stable = ok ? pre[9] + 1.0 : 0.0;
+    st[0] = 0.5 * out[1];
+    st[1] = f;
+    st[2] = s;
+    st[3] = stable;
+    code = stable > (double)c.stable_thr ? 1 : 0;
+  }
+  *c.abort = code == 0 ? 0 : (code == 1 ? c.pass : -1);
+  rec[10] = (double)code;
+  for (int k = 0; k <= 10; ++k) c.rec[k] = rec[k];
+}
+
+__global__ void k_ctl_seed(double* state, int* abort, double s0, double s1, double s2, double s3) {
+  if (threadIdx.x == 0) {
+    state[0] = s0;
+    state[1] = s1;
+    state[2] = s2;
+    state[3] = s3;
+    *abort = 0;
+  }
+}
+
 template <typename T, int NSRC, int G>
 __global__ __launch_bounds__(256) void k_finalize_residual(
     const T* __restrict__ P, int S, const T* __restrict__ B, T* __restrict__ R0, T* __restrict__ R1,
     T* __restrict__ R2, int64_t ml, const int* __restrict__ gate, int epoch, int gate_mode,
     const T* __restrict__ cx, int64_t cn, const double* __restrict__ cmax, double* __restrict__ fh,
     double fh_mu, const double* __restrict__ fh_rn, Red red, const double* __restrict__ snap_src,
-    double* __restrict__ snap_dst, int nsnap, int chain, const T* __restrict__ P0, int S0) {
+    double* __restrict__ snap_dst, int nsnap, int chain, const T* __restrict__ P0, int S0, Ctl ctl) {
+  if (red_skipped(red)) return;
+  double pre[10];
+  if (ctl.rec != nullptr && threadIdx.x == 0) {
+    for (int k = 0; k < 6; ++k) pre[k] = ctl.tr[k];
+    for (int k = 0; k < 4; ++k) pre[6 + k] = ctl.state[k];
+  }
   const bool live = (gate == nullptr) || (*gate == epoch);
   if (!live && gate_mode == 0) return;  // uniform over the grid: nobody touches the ticket
   double v[4] = {0.0, 0.0, 0.0, 0.0};
@@ -120,6 +173,7 @@ __global__ __launch_bounds__(256) void k_finalize_residual(
   // snapshot of the preceding trial's sums for a packet published after the next trial has
   // overwritten them (the A@X-carried packet of the multi-GPU path)
   if (last && (int)threadIdx.x < nsnap) snap_dst[threadIdx.x] = snap_src[threadIdx.x];
+  if (last && ctl.rec != nullptr && threadIdx.x == 0) ctl_decide(ctl, red.out, pre);
 }
 
 // Split-candidate FISTA batch (solver.cpp iter_fista): the dense source is A xc (S slabs at P),
@@ -534,7 +588,7 @@ void launch_finalize_residual(const T* P, int S, const T* B, int nsrc, T* const*
                               const int* gate, int epoch, int gate_mode, const T* cx, int64_t cn,
                               const double* cmax, double* fh, double fh_mu, const double* fh_rn,
                               Red red, hipStream_t st, const double* snap_src, double* snap_dst,
-                              int nsnap, int chain, int S0) {
+                              int nsnap, int chain, int S0, Ctl ctl) {
   if (chain && (nsrc != 2 || gate != nullptr)) throw Error{GLX_E_INVALID, "finalize: chain needs 2 ungated sources"};
   if (S0 <= 0) S0 = S;
   const int G = finalize_groups(S > S0 ? S : S0);
@@ -546,7 +600,7 @@ void launch_finalize_residual(const T* P, int S, const T* B, int nsrc, T* const*
   auto go = [&](auto ns, auto g) {
     hipLaunchKernelGGL((k_finalize_residual<T, decltype(ns)::value, decltype(g)::value>), grid,
                        dim3(256), 0, st, P, S, B, R[0], r1, r2, ml, gate, epoch, gate_mode, cx, cn,
-                       cmax, fh, fh_mu, fh_rn, red, snap_src, snap_dst, nsnap, chain, P, S0);
+                       cmax, fh, fh_mu, fh_rn, red, snap_src, snap_dst, nsnap, chain, P, S0, ctl);
   };
   auto by_g = [&](auto ns) {
     if (G == 1) go(ns, std::integral_constant<int, 1>{});
@@ -669,6 +723,11 @@ void launch_record_f(const double* s, int i_sumsq, int i_reg, double mu, double*
                      hipStream_t st) {
   hipLaunchKernelGGL(k_record_f, dim3(1), dim3(64), 0, st, s, i_sumsq, i_reg, mu, fh, idx);
 }
+void launch_ctl_seed(double* state, int* abort, double s0, double s1, double s2, double s3,
+                     hipStream_t st) {
+  hipLaunchKernelGGL(k_ctl_seed, dim3(1), dim3(64), 0, st, state, abort, s0, s1, s2, s3);
+}
+
 void launch_publish(const double* s, int ns, double* host, unsigned* host_seq, unsigned seq,
                     hipStream_t st, const double* s2, int off2, int n2) {
   hipLaunchKernelGGL(k_publish, dim3(1), dim3(64), 0, st, s, ns, host, host_seq, seq, s2, off2,
@@ -679,7 +738,7 @@ void launch_publish(const double* s, int ns, double* host, unsigned* host_seq, u
   template void launch_finalize_residual<T>(const T*, int, const T*, int, T* const*, int64_t,       \
                                             const int*, int, int, const T*, int64_t, const double*, \
                                             double*, double, const double*, Red, hipStream_t,       \
-                                            const double*, double*, int, int, int);                 \
+                                            const double*, double*, int, int, int, Ctl);            \
   template void launch_sum_partials<T>(const T*, int, T*, int64_t, hipStream_t);                    \
   template void launch_finalize_fista<T>(const T*, int, const T*, int, const T*, T*, const T*, T*,  \
                                          int64_t, double, double, double, const T*, int64_t,        \

@@ -60,7 +60,9 @@ template <typename T, int L>
 __global__ __launch_bounds__(kGThreads) void k_e_lists(const T* __restrict__ E,
                                                        const uint8_t* __restrict__ zf, int64_t n,
                                                        unsigned short* __restrict__ lists,
-                                                       unsigned* __restrict__ counts) {
+                                                       unsigned* __restrict__ counts,
+                                                       const int* __restrict__ skip) {
+  if (skip != nullptr && *skip != 0) return;
   extern __shared__ unsigned short fl[];             // the flagged rows (n entries worst case)
   __shared__ unsigned wsum[kGW];
   const int tid = threadIdx.x;
@@ -152,7 +154,8 @@ __global__ __launch_bounds__(kGThreads) void k_at_gather(const T* __restrict__ A
                                                          const unsigned short* __restrict__ lists,
                                                          const unsigned* __restrict__ counts,
                                                          int64_t m, int64_t n, T* __restrict__ P,
-                                                         int gx) {
+                                                         int gx, const int* __restrict__ skip) {
+  if (skip != nullptr && *skip != 0) return;
   const int rb = (int)blockIdx.x % gx, c = (int)blockIdx.x / gx;
   const int total = (int)counts[c];
   const unsigned short* lst = lists + (int64_t)c * n;
@@ -203,7 +206,8 @@ const unsigned* gather_counts(const void* lists_ws, int64_t n) {
 }
 
 template <typename T>
-void launch_e_lists(const T* E, const uint8_t* zf, int64_t n, int64_t l, void* lists_ws, hipStream_t st) {
+void launch_e_lists(const T* E, const uint8_t* zf, int64_t n, int64_t l, void* lists_ws, hipStream_t st,
+                    const int* skip) {
   if (!gather_ok(n, l)) throw Error{GLX_E_INVALID, "A e gather: needs l in {16, 32}, n < 65536"};
   const size_t lds = sizeof(unsigned short) * (size_t)n;
   auto go = [&](auto kern) {
@@ -214,7 +218,7 @@ void launch_e_lists(const T* E, const uint8_t* zf, int64_t n, int64_t l, void* l
       attr = true;
     }
     hipLaunchKernelGGL(kern, dim3((unsigned)l), dim3(kGThreads), lds, st, E, zf, n,
-                       static_cast<unsigned short*>(lists_ws), list_counts(lists_ws, n));
+                       static_cast<unsigned short*>(lists_ws), list_counts(lists_ws, n), skip);
   };
   if (l == 32) go(k_e_lists<T, 32>);
   else go(k_e_lists<T, 16>);
@@ -222,7 +226,7 @@ void launch_e_lists(const T* E, const uint8_t* zf, int64_t n, int64_t l, void* l
 
 template <typename T>
 void launch_at_gather(const T* At, const T* E, int64_t m, int64_t n, int64_t l, T* P, void* lists_ws,
-                      hipStream_t st) {
+                      hipStream_t st, const int* skip) {
   if (!gather_ok(n, l)) throw Error{GLX_E_INVALID, "A e gather: needs l in {16, 32}, n < 65536"};
   const int gx = (int)((m + kGThreads - 1) / kGThreads);
   const unsigned short* lists = static_cast<const unsigned short*>(lists_ws);
@@ -232,7 +236,7 @@ void launch_at_gather(const T* At, const T* E, int64_t m, int64_t n, int64_t l, 
   }();
   auto go = [&](auto kern) {
     hipLaunchKernelGGL(kern, dim3((unsigned)(gx * l)), dim3(kGThreads), 0, st, At, E, lists,
-                       list_counts(lists_ws, n), m, n, P, gx);
+                       list_counts(lists_ws, n), m, n, P, gx, skip);
   };
   if (l == 32) nt ? go(k_at_gather<T, 32, true>) : go(k_at_gather<T, 32, false>);
   else nt ? go(k_at_gather<T, 16, true>) : go(k_at_gather<T, 16, false>);
@@ -243,11 +247,13 @@ size_t gather_lists_bytes(int64_t n) { return (((size_t)32 * n * 2 + 255) & ~siz
 
 template void launch_transpose<double>(const double*, double*, int64_t, int64_t, hipStream_t);
 template void launch_transpose<float>(const float*, float*, int64_t, int64_t, hipStream_t);
-template void launch_e_lists<double>(const double*, const uint8_t*, int64_t, int64_t, void*, hipStream_t);
-template void launch_e_lists<float>(const float*, const uint8_t*, int64_t, int64_t, void*, hipStream_t);
+template void launch_e_lists<double>(const double*, const uint8_t*, int64_t, int64_t, void*, hipStream_t,
+                                     const int*);
+template void launch_e_lists<float>(const float*, const uint8_t*, int64_t, int64_t, void*, hipStream_t,
+                                    const int*);
 template void launch_at_gather<double>(const double*, const double*, int64_t, int64_t, int64_t, double*,
-                                       void*, hipStream_t);
+                                       void*, hipStream_t, const int*);
 template void launch_at_gather<float>(const float*, const float*, int64_t, int64_t, int64_t, float*,
-                                      void*, hipStream_t);
+                                      void*, hipStream_t, const int*);
 
 }  // namespace glx

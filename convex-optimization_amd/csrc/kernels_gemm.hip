@@ -995,13 +995,19 @@ __device__ inline int64_t atr_panel(const T* __restrict__ A, const T* __restrict
 // Hand-off: sc1 (agent-scope) stores, vmcnt(0), a workgroup barrier, one agent-scope add per
 // block; the last arriver loads with sc1 after a barrier (MI355X_MICROARCH.md "Valid forms",
 // row 1). Returns false in the blocks that are not last (they only join the grid reduction).
+// *slot = this block's grid-reduction slot, fixed whatever the arrival order: the panel's
+// trial sums (last arriver) at `panel`, the identity partials of the other S - 1 blocks at
+// n/64 + panel (S - 1) + their arrival index. So the trial's scalar sums come out in panel
+// order, bit-identical from run to run (a last arriver at its own block slot made their
+// summation order depend on timing).
 template <typename T, int NT>
 __device__ inline bool atr_split_combine(typename MF<T>::acc_t (&acc)[4][NT], T* __restrict__ Gp,
                                          int64_t n, int S, int64_t panel, int64_t split,
-                                         unsigned* __restrict__ pcnt) {
+                                         unsigned* __restrict__ pcnt, int* slot) {
   typedef MF<T> M;
   constexpr int L = 16 * NT;
   __shared__ int last;
+  __shared__ unsigned arrival;
   const int lane = threadIdx.x & 63;
   const int wave = threadIdx.x >> 6;
   const int i = lane & 15;
@@ -1021,10 +1027,12 @@ __device__ inline bool atr_split_combine(typename MF<T>::acc_t (&acc)[4][NT], T*
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
-  if (threadIdx.x == 0)
-    last = __hip_atomic_fetch_add(pcnt + panel, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
-           (unsigned)S - 1;
+  if (threadIdx.x == 0) {
+    arrival = __hip_atomic_fetch_add(pcnt + panel, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    last = arrival == (unsigned)S - 1;
+  }
   __syncthreads();
+  *slot = last ? (int)panel : (int)(n / 64 + panel * (S - 1) + arrival);
   if (!last) return false;
 #pragma unroll
   for (int e = 0; e < 4; ++e) {
@@ -1083,6 +1091,12 @@ __global__ __launch_bounds__(256, sizeof(T) == 8 ? 2 : 1) void k_atr_prox(const 
                                                   Pub pub, int S, T* __restrict__ Gp,
                                                   unsigned* __restrict__ pcnt,
                                                   uint8_t* __restrict__ zf) {
+  if (red_skipped(red)) {   // cancelled by a device-side decision (solver.cpp dc_run)
+    // the decision record still goes to the host (the cancelling decision's own record)
+    if (pub.host != nullptr && blockIdx.x == 0 && threadIdx.x == 0)
+      publish_packet(pub.s, pub.ns, pub.host, pub.host_seq, pub.seq);
+    return;
+  }
   if (publisher_first<6, 0x8u>(pub, red)) return;   // the extra workgroup (n / 64 * S + 1 in all)
   typedef MF<T> M;
   constexpr int L = 16 * NT;
@@ -1094,9 +1108,10 @@ __global__ __launch_bounds__(256, sizeof(T) == 8 ? 2 : 1) void k_atr_prox(const 
   const int64_t panel = SPLIT ? bid / S : bid, split = SPLIT ? bid % S : 0;
   const int64_t col0 = atr_panel<T, NT, PF, 0, NTL>(A, R, m, n, SPLIT ? S : 1, acc, panel, split);
   double accr[6] = {0.0, 0.0, 0.0, -__builtin_inf(), 0.0, 0.0};
+  int slot = work_slot(pub);
   if constexpr (SPLIT) {   // a separate instantiation: the S = 1 kernel keeps 2 blocks per CU
-    if (!atr_split_combine<T, NT>(acc, Gp, n, S, panel, split, pcnt)) {
-      grid_reduce<6, 0x8u>(accr, red, work_slot(pub));
+    if (!atr_split_combine<T, NT>(acc, Gp, n, S, panel, split, pcnt, &slot)) {
+      grid_reduce<6, 0x8u>(accr, red, slot);
       return;
     }
   }
@@ -1133,7 +1148,7 @@ __global__ __launch_bounds__(256, sizeof(T) == 8 ? 2 : 1) void k_atr_prox(const 
       }
     }
   }
-  grid_reduce<6, 0x8u>(accr, red, work_slot(pub));
+  grid_reduce<6, 0x8u>(accr, red, slot);
 }
 
 // FISTA's backtracking trial fused into A^T R the same way (WL 0, one K split): each wave runs
@@ -1160,9 +1175,10 @@ __global__ __launch_bounds__(256, sizeof(T) == 8 ? 2 : 1) void k_atr_fista(const
   const int64_t panel = SPLIT ? bid / S : bid, split = SPLIT ? bid % S : 0;
   const int64_t col0 = atr_panel<T, NT, PF, 0, NTL>(A, R, m, n, SPLIT ? S : 1, acc, panel, split);
   double accr[4] = {0.0, 0.0, 0.0, -__builtin_inf()};
-  if constexpr (SPLIT) {
-    if (!atr_split_combine<T, NT>(acc, Gp, n, S, panel, split, pcnt)) {
-      grid_reduce<4, 0x8u>(accr, red, work_slot(pub));
+  int slot = work_slot(pub);
+  if constexpr (SPLIT) {   // fixed reduction slots, see atr_split_combine
+    if (!atr_split_combine<T, NT>(acc, Gp, n, S, panel, split, pcnt, &slot)) {
+      grid_reduce<4, 0x8u>(accr, red, slot);
       return;
     }
   }
@@ -1204,7 +1220,7 @@ __global__ __launch_bounds__(256, sizeof(T) == 8 ? 2 : 1) void k_atr_fista(const
       }
     }
   }
-  grid_reduce<4, 0x8u>(accr, red, work_slot(pub));
+  grid_reduce<4, 0x8u>(accr, red, slot);
 }
 
 // ------------------------------------------------------------------------------------------

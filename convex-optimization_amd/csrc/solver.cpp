@@ -82,6 +82,7 @@ static int method_bufs(int method) {
 constexpr int kBufs = 9;
 constexpr int kTailBytes = 64;   // behind each gradient set: scalars that ride its all-reduce
 constexpr int kRes = 4;
+constexpr int kDcWindow = 8;     // device-controlled ProxGD: iterations in flight (GLX_DC_BATCH)
 
 static void validate(const glx_problem* P, const glx_opts* O) {
   if (!P || !O) throw Error{GLX_E_INVALID, "null problem/opts"};
@@ -206,6 +207,9 @@ class Session : public SessionBase {
     // per-panel arrival counters of the fused A^T R with K splits (atr_split_combine)
     unsigned* pcnt = static_cast<unsigned*>(c.take(sizeof(unsigned) * (P.n / 64 + 64)));
     int* flag = static_cast<int*>(c.take(256));
+    // device-controlled batches: Ctl::state (4 doubles) and the abort word; decision records
+    double* dcs = static_cast<double*>(c.take(256));
+    double* dcr = static_cast<double*>(c.take(sizeof(double) * kCtlRec * kCtlMaxBatch));
     // split-candidate mode: row flags of e = p - p_thr (z's buffer), read in chunks of up to 32
     uint8_t* zf = static_cast<uint8_t*>(c.take((size_t)((P.n + 255) / 256) * 256));
     double* fh = static_cast<double*>(c.take(sizeof(double) * (fh_cap + 1)));
@@ -219,6 +223,9 @@ class Session : public SessionBase {
       s->G_ = g[0]; s->Gp_ = gp[0]; s->Pp_ = pp; s->At_ = at; s->glists_ = glists;
       s->scal_ = scal; s->part_ = part; s->ticket_ = ticket; s->flag_ = flag; s->fh_dev_ = fh;
       s->pcnt_ = pcnt;
+      s->dc_state_ = dcs;
+      s->dc_abort_ = reinterpret_cast<int*>(dcs + 8);
+      s->dc_rec_ = dcr;
       s->zf_ = zf;
       s->E_ = ec;
       for (int k = 0; k < 3; ++k) s->SXO_[k] = sxo[k];
@@ -299,6 +306,22 @@ class Session : public SessionBase {
       GLX_HIP(hipEventCreateWithFlags(&ev_lists_, hipEventDisableTiming));
     }
     fused_fista_ok_ = fuse_any && P.method == GLX_FPROXGD;
+    // device-controlled batches (dc_run): ProxGD with line search on the fused speculative path
+    // of one GPU; GLX_DC_BATCH = iterations in flight (0: the host decides every iteration)
+    {
+      const char* dc = std::getenv("GLX_DC_BATCH");
+      const int w = dc ? std::atoi(dc) : kDcWindow;
+      dc_window_ = std::max(0, std::min(w, kCtlMaxBatch / 2));
+    }
+    if (!(fused_ok_ && comm_ == nullptr && spin_readback_ && O.exact_objective == 0 &&
+          O.step_type == GLX_STEP_LINE_SEARCH && O.ls_maxit > 0))
+      dc_window_ = 0;
+    if (dc_window_ > 0) {
+      GLX_HIP(hipHostMalloc(reinterpret_cast<void**>(&dc_ring_), sizeof(double) * kCtlRec * kCtlMaxBatch,
+                            hipHostMallocMapped | hipHostMallocCoherent));
+      std::memset(dc_ring_, 0, sizeof(double) * kCtlRec * kCtlMaxBatch);   // tags start at 1
+      GLX_HIP(hipHostGetDevicePointer(reinterpret_cast<void**>(&dc_ring_dev_), dc_ring_, 0));
+    }
     GLX_HIP(hipMemsetAsync(ticket_, 0, kTicketBytes, st_));
     GLX_HIP(hipMemsetAsync(pcnt_, 0, sizeof(unsigned) * (P.n / 64 + 64), st_));
     GLX_HIP(hipMemsetAsync(flag_, 0, 256, st_));
@@ -324,6 +347,7 @@ class Session : public SessionBase {
     if (ev_trial_) (void)hipEventDestroy(ev_trial_);
     if (ev_lists_) (void)hipEventDestroy(ev_lists_);
     if (hs_) (void)hipHostFree(hs_);
+    if (dc_ring_) (void)hipHostFree(dc_ring_);
     if (rb_event_) (void)hipEventDestroy(rb_event_);
     for (auto& v : ev_)
       for (auto& p : v) { (void)hipEventDestroy(p.first); (void)hipEventDestroy(p.second); }
@@ -336,13 +360,16 @@ class Session : public SessionBase {
     int64_t steps = 0;
     while (!finished_ && (max_steps <= 0 || steps < max_steps)) {
       if (inner_ >= O_.maxit) { end_phase(); continue; }
+      // iterations a device-controlled batch may run from here (each records once)
+      step_room_ = max_steps > 0 ? max_steps - steps : INT64_MAX;
+      const int64_t k0 = k_;
       switch (method_) {
         case GLX_PROXGD: iter_proxgd(); break;
         case GLX_FPROXGD: iter_fista(false); break;
         case GLX_FGD: iter_fista(true); break;
         default: iter_descent(); break;
       }
-      ++steps;
+      steps += k_ - k0;
       if (O_.max_total_iters > 0 && k_ >= O_.max_total_iters) finished_ = true;
     }
     GLX_HIP(hipStreamSynchronize(st_));
@@ -440,7 +467,14 @@ class Session : public SessionBase {
 
  private:
   // ------------------------------------------------------------------ helpers
-  Red red(int slot) { return Red{part_, ticket_, scal_ + slot}; }
+  // while a device-controlled batch is queued every reduction carries its abort word: the launch
+  // is skipped once a decision has cancelled the rest of the batch (*skip not 0 and not pass)
+  Red red(int slot, int pass = 0) {
+    Red r{part_, ticket_, scal_ + slot};
+    r.skip = dc_gate_;
+    r.skip_pass = pass;
+    return r;
+  }
 
   // HIP-event timing of A@X (kind 0) / A^T R (kind 1) launches. opts.profile = k > 0 times every
   // k-th launch of each kind: a timed event pair opens a gap of a few us in the queue, so
@@ -508,7 +542,7 @@ class Session : public SessionBase {
                                 defer ? Red{part_, ticket_, defer} : red(slot), st_,
                                 snap_trial ? scal_ + S_TR : nullptr,
                                 snap_trial ? scal_ + S_SNAP : nullptr, snap_trial ? 6 : 0,
-                                chain ? 1 : 0, gat ? gsplit_ : 0);
+                                chain ? 1 : 0, gat ? gsplit_ : 0, dc_ctl_);
     check_launch();
     if (defer) return;
     if (comm_) {
@@ -748,6 +782,7 @@ class Session : public SessionBase {
     if (!state_valid_) proxgd_prologue(thr_from_trial_);
     record(f_cur_, s_cur_);
     if (stop_rule()) { end_phase(true); return; }
+    if (dc_ready()) { dc_run(); return; }
     const bool ls = O_.step_type == GLX_STEP_LINE_SEARCH && O_.ls_maxit > 0;
     const double t0 = ls ? O_.alpha0 : schedule(inner_);
     std::pair<const T*, int> g{nullptr, 0};
@@ -765,6 +800,13 @@ class Session : public SessionBase {
     } else {
       g = take_gradient(R_[irg_]);
     }
+    proxgd_trials(g, first_done, t0, 0);
+  }
+
+  // The line search from trial it0 (it0 = 1: the first trial was rejected by a device-side
+  // decision, dc_run; t0 is then already alpha0 * ls_coeff), or the fixed step, and the update.
+  void proxgd_trials(std::pair<const T*, int> g, bool first_done, double t0, int it0) {
+    const bool ls = O_.step_type == GLX_STEP_LINE_SEARCH && O_.ls_maxit > 0;
     const T* xt = X_[ixt_];
     const bool exact = O_.exact_objective != 0;
     // trial residual buffers: never the gradient residual
@@ -779,7 +821,7 @@ class Session : public SessionBase {
     };
     if (ls) {
       t = t0;
-      for (int it = 0; it < O_.ls_maxit; ++it) {
+      for (int it = it0; it < O_.ls_maxit; ++it) {
         if (!(it == 0 && first_done)) trial(t, it == 0);
         // one pass: the candidate's g for the test (:91) + the next iteration's residual
         // A p_thr (exact mode: g(z) and A p as a third source). Split-candidate mode (emode_,
@@ -845,35 +887,181 @@ class Session : public SessionBase {
       if (!first_done) trial(t, true);
     }
     if (accepted) {   // the packet holds the accepted trial's sums (read before any speculation)
-      stats_[0] += hs_[S_TR + 4];
-      stats_[1] += hs_[S_TR + 5];
-      stats_[2] += 1;
-      irg_ = rpt;
-      gx_ = 0.5 * hs_[S_RT + 1];
-      // exact: A p from the batch; split-candidate: A p - b = (A p_thr - b) + A e; dense z
-      // batch (GLX_SPLIT_CAND=0): A z - b (z = x - t G_t is ulp-close to p) unless the
-      // threshold changed nothing, in which case A p_thr - b == A p - b exactly
-      const double sq_x = exact ? hs_[S_RT + 2]
-                                : ((emode_ || hs_[S_TR + 4] != 0) ? hs_[S_RT] : hs_[S_RT + 1]);
-      f_cur_ = 0.5 * sq_x + P_.mu0 * hs_[S_TR + 2];
-      s_cur_ = hs_[S_RT + 3] / (double)nl_;
-      state_valid_ = true;
+      proxgd_accept(rpt, exact);
     } else {
       state_valid_ = false;
       thr_from_trial_ = true;                     // x_thr came out of the trial kernel
     }
     // x = prox(x - t grad, t)  (:132)
     if (spec_trial) {   // x <- p, x_thr <- p_thr, the speculative outputs become the trial's
-      const int ox = ix_, oxt = ixt_;
-      ix_ = ip_; ixt_ = ipt_; ip_ = if1_; ipt_ = if2_;   // z's buffer already holds the new z
-      if1_ = ox; if2_ = oxt;
-      spec_trial_ready_ = true;
-      spec_set_ = 1 - gset_;
-      spec_trial_mu_ = mu_;
-      spec_trial_t_ = O_.alpha0;
+      proxgd_spec_rotate();
     } else {
       std::swap(ix_, ip_);
       std::swap(ixt_, ipt_);
+    }
+  }
+
+  // accepted trial: the packet (hs_) holds its sums
+  void proxgd_accept(int rpt, bool exact) {
+    stats_[0] += hs_[S_TR + 4];
+    stats_[1] += hs_[S_TR + 5];
+    stats_[2] += 1;
+    irg_ = rpt;
+    gx_ = 0.5 * hs_[S_RT + 1];
+    // exact: A p from the batch; split-candidate: A p - b = (A p_thr - b) + A e; dense z
+    // batch (GLX_SPLIT_CAND=0): A z - b (z = x - t G_t is ulp-close to p) unless the
+    // threshold changed nothing, in which case A p_thr - b == A p - b exactly
+    const double sq_x = exact ? hs_[S_RT + 2]
+                              : ((emode_ || hs_[S_TR + 4] != 0) ? hs_[S_RT] : hs_[S_RT + 1]);
+    f_cur_ = 0.5 * sq_x + P_.mu0 * hs_[S_TR + 2];
+    s_cur_ = hs_[S_RT + 3] / (double)nl_;
+    state_valid_ = true;
+  }
+  // x <- p, x_thr <- p_thr; the speculative outputs become the next iteration's first trial
+  // (z's buffer already holds its z)
+  void proxgd_spec_rotate() {
+    const int ox = ix_, oxt = ixt_;
+    ix_ = ip_; ixt_ = ipt_; ip_ = if1_; ipt_ = if2_;
+    if1_ = ox; if2_ = oxt;
+    spec_trial_ready_ = true;
+    spec_set_ = 1 - gset_;
+    spec_trial_mu_ = mu_;
+    spec_trial_t_ = O_.alpha0;
+  }
+
+  // ------------------------------------------------------------------ device-controlled ProxGD
+  // SURVEY 8f row 2. In the speculative steady state (the previous first trial was accepted and
+  // its fused kernel left G and this iteration's first trial ready) every iteration launches the
+  // same kernels on buffer roles that rotate the same way: A@[e | p_thr] (+ the A e gather),
+  // its finalize, and the fused A^T r + next trial. So up to dc_window_ iterations are queued
+  // ahead of the host. The Armijo test (gl_ProxGD_primal.py:89-92), the next record and the stop
+  // rule (:118-125) run in the finalize's last block (ctl_decide, kernels_elem.hip), which writes
+  // a decision record to host-mapped memory and an abort word every later launch of the batch
+  // tests first: a rejection cancels everything behind it, a stop lets only the speculative
+  // gradient finish (the next phase starts from it, as on the host path). The host reads the
+  // records in order — re-deriving every decision from the record's sums and checking it —
+  // and tops the window up; it never blocks the GPU. A rejection continues on the host path at
+  // the second trial; a stop ends the phase there. Results are bit-identical to host control.
+  struct Roles { int ix, ixt, ip, ipt, if1, if2, iz, irg, gset; };
+  bool dc_ready() const {
+    return dc_window_ > 0 && spec_trial_ready_ && spec_trial_mu_ == mu_ &&
+           spec_trial_t_ == O_.alpha0 && want_spec(0) && !ax_queued_;
+  }
+  // Gated (cancellable) launches: the finalize (it would overwrite the decision state and the
+  // gradient residual of the iteration the host resumes) and the speculative fused kernel (the
+  // next gradient set and iterate buffers). A@X and the gather only write the scratch slabs, so
+  // a cancelled one runs to no effect instead of paying a flag load at its start (measured).
+  void dc_queue(Roles& q, int64_t tag) {
+    const int rz = (q.irg + 1) % kRes, rpt = (q.irg + 2) % kRes, rp = (q.irg + 3) % kRes;
+    const T* xs[3] = {X_[q.iz], X_[q.ipt], X_[q.ip]};
+    T* rs[3] = {R_[rz], R_[rpt], R_[rp]};
+    dc_gate_ = dc_abort_;
+    dc_ctl_ = Ctl{};
+    const int64_t slot = (tag % kCtlMaxBatch) * kCtlRec;
+    dc_ctl_.rec = dc_rec_ + slot;
+    dc_ctl_.state = dc_state_;
+    dc_ctl_.abort = dc_abort_;
+    dc_ctl_.tr = scal_ + S_TR;
+    dc_ctl_.tag = (double)tag;
+    dc_ctl_.t = O_.alpha0;
+    dc_ctl_.mu0 = P_.mu0;
+    dc_ctl_.ftol = O_.ftol;
+    dc_ctl_.nl = (double)nl_;
+    dc_ctl_.stable_thr = O_.stable_len_threshold;
+    dc_ctl_.use_sp = use_sparsity_ ? 1 : 0;
+    dc_ctl_.emode = emode_ ? 1 : 0;
+    dc_ctl_.pass = 1 + (int)(tag % 0x3FFFFFFF);
+    residuals(2, xs, rs, S_RT, X_[q.ip], scal_ + S_TR + 3, nullptr, 0.0, nullptr, nullptr, false,
+              false, emode_);
+    dc_ctl_ = Ctl{};
+    dc_pass_ = 1 + (int)(tag % 0x3FFFFFFF);
+    dc_pub_ = Pub{};
+    dc_pub_.s = dc_rec_ + slot;
+    dc_pub_.ns = 11;
+    dc_pub_.host = dc_ring_dev_ + slot;
+    dc_pub_.host_seq = reinterpret_cast<unsigned*>(dc_ring_dev_ + slot + kCtlRec - 1);
+    dc_pub_.seq = (unsigned)tag;
+    atr_prox(R_[rpt], 1 - q.gset, X_[q.ipt], q.if1, q.if2, q.iz, O_.alpha0);
+    dc_pub_ = Pub{};
+    dc_pass_ = 0;
+    dc_gate_ = nullptr;
+    // the roles after an accepted first trial (proxgd_accept + proxgd_spec_rotate + use_gset)
+    q.irg = rpt;
+    const int ox = q.ix, oxt = q.ixt;
+    q.ix = q.ip; q.ixt = q.ipt; q.ip = q.if1; q.ipt = q.if2;
+    q.if1 = ox; q.if2 = oxt;
+    q.gset = 1 - q.gset;
+  }
+  const double* dc_wait(int64_t tag) {
+    const double* rec = dc_ring_ + (tag % kCtlMaxBatch) * kCtlRec;
+    volatile const unsigned* tp = reinterpret_cast<const unsigned*>(rec + kCtlRec - 1);
+    const unsigned want = (unsigned)tag;
+    uint64_t spins = 0;
+    auto t0 = std::chrono::steady_clock::time_point{};
+    while (*tp != want) {
+      __builtin_ia32_pause();
+      if ((++spins & 0xFFFFF) == 0) {
+        if (spins == 0x100000) t0 = std::chrono::steady_clock::now();
+        else if (std::chrono::steady_clock::now() - t0 > std::chrono::seconds(5)) {
+          GLX_HIP(hipStreamSynchronize(st_));   // surfaces a device error, if any
+          if (*tp != want) throw Error{GLX_E_STATE, "device-controlled batch: decision record missing"};
+        }
+      }
+    }
+    __atomic_thread_fence(__ATOMIC_ACQUIRE);
+    return rec;
+  }
+  void dc_run() {
+    // iterations from here (this one is recorded): to the phase's maxit, max_total_iters and
+    // the steps run() may still take
+    int64_t budget = O_.maxit - inner_ + 1;
+    if (O_.max_total_iters > 0) budget = std::min<int64_t>(budget, O_.max_total_iters - k_ + 1);
+    budget = std::max<int64_t>(1, std::min<int64_t>(budget, step_room_));
+    ++syncs_;   // the host's one blocking read per batch is this batch's records
+    launch_ctl_seed(dc_state_, dc_abort_, gx_, f_cur_, s_cur_, (double)stable_, st_);
+    check_launch();
+    Roles q{ix_, ixt_, ip_, ipt_, if1_, if2_, iz_, irg_, spec_set_};
+    const int64_t tag0 = dc_tag_;
+    int64_t queued = 0;
+    const int64_t w = std::min<int64_t>(dc_window_, budget);
+    auto push = [&]() {   // tags are never reused: dc_tag_ = the last one queued
+      dc_tag_ = tag0 + 1 + queued++;
+      dc_queue(q, dc_tag_);
+    };
+    while (queued < w) push();
+    int prev = 0;
+    for (int64_t d = 0; d < budget; ++d) {
+      if (d > 0) {
+        record(f_cur_, s_cur_);
+        const bool stop = stop_rule();
+        if (stop != (prev == 1))
+          throw Error{GLX_E_STATE, "device-controlled batch: stop rule differs from the host's"};
+        if (stop) { end_phase(true); return; }
+      }
+      const double* rec = dc_wait(tag0 + 1 + d);
+      if (queued < budget) push();
+      for (int i = 0; i < 4; ++i) hs_[S_RT + i] = rec[i];
+      for (int i = 0; i < 6; ++i) hs_[S_TR + i] = rec[4 + i];
+      const int code = (int)rec[10];
+      spec_trial_ready_ = false;   // iteration start: the speculated gradient set
+      use_gset(spec_set_);
+      const int rpt = (irg_ + 2) % kRes;
+      const double t = O_.alpha0;
+      const double gz = 0.5 * hs_[S_RT];
+      const bool acc = gz <= gx_ - t * hs_[S_TR + 0] + 0.5 * t * hs_[S_TR + 1];
+      if (acc != (code != 2))
+        throw Error{GLX_E_STATE, "device-controlled batch: Armijo decision differs from the host's"};
+      stats_[7] += 1;
+      if (!acc) {   // everything queued behind this decision was cancelled on the device
+        spec_on_ = false;
+        ax_queued_ = false;
+        proxgd_trials({G_, 1}, true, t * O_.ls_coeff, 1);
+        return;
+      }
+      spec_on_ = true;
+      proxgd_accept(rpt, false);
+      proxgd_spec_rotate();
+      prev = code;
     }
   }
 
@@ -897,11 +1085,14 @@ class Session : public SessionBase {
       check_launch();
       return;
     }
-    Pub pb;   // without a communicator pub_seq is only passed when attaching
+    Pub pb = dc_pub_;   // without a communicator pub_seq is only passed when attaching
     if (pub_seq) pb = make_pub(extra, pub_seq);
     hipEvent_t e0 = prof_begin(1);
+    // in a device-controlled batch this speculative kernel also runs when the decision before it
+    // stops the phase (abort = that decision's tag): the next phase starts from its gradient, as
+    // on the host path; the speculative kernels queued after it do not run
     launch_atr_prox<T>(plan_, A_, r, Gs_[set], x, X_[op], X_[opt], X_[oz], t, mu_, O_.thres,
-                       red(S_TR), st_, pb, Gps_[set], pcnt_, ezf());
+                       red(S_TR, dc_pass_), st_, pb, Gps_[set], pcnt_, ezf());
     check_launch();
     prof_end(1, e0);
     ++atr_calls_;
@@ -1234,6 +1425,19 @@ class Session : public SessionBase {
   T* fec() const { return fsplit_ ? E_ : nullptr; }
   uint8_t* fzf() const { return fsplit_ ? zf_ : nullptr; }
   int* flag_ = nullptr;
+  // device-controlled ProxGD batches (dc_run)
+  double* dc_state_ = nullptr;    // Ctl::state
+  int* dc_abort_ = nullptr;       // 0 live, a decision's tag: stop at the next record, -1 rejected
+  int dc_pass_ = 0;               // while queuing: the tag the speculative kernel also runs on
+  double* dc_rec_ = nullptr;      // device decision records (Ctl::rec), kCtlMaxBatch slots
+  Pub dc_pub_{};                  // while queuing: the record's hand-off, carried by atr_prox
+  double* dc_ring_ = nullptr;     // host-mapped decision records
+  double* dc_ring_dev_ = nullptr;
+  int dc_window_ = 0;             // iterations in flight (0: off)
+  int64_t dc_tag_ = 0;            // decision records issued
+  int64_t step_room_ = INT64_MAX;
+  const int* dc_gate_ = nullptr;  // while queuing a batch: the abort word the launches test
+  Ctl dc_ctl_{};                  // while queuing a batch: the finalize's decision epilogue
   int64_t fh_cap_ = 0;
   double* sp100_ = nullptr;   // SGD/GD: count(|x| > 1e-6 max|x|) after every 100th iteration
   T* gemv_slabs_ = nullptr;
