@@ -125,7 +125,9 @@ __global__ __launch_bounds__(256) void k_finalize_residual(
     const T* __restrict__ cx, int64_t cn, const double* __restrict__ cmax, double* __restrict__ fh,
     double fh_mu, const double* __restrict__ fh_rn, Red red, const double* __restrict__ snap_src,
     double* __restrict__ snap_dst, int nsnap, int chain, const T* __restrict__ P0, int S0, Ctl ctl) {
-  if (red_skipped(red)) return;
+  // a cancelled launch (device-controlled batch) stores nothing and returns before the
+  // reduction; the flag is tested at the first store, so its load overlaps the slab loads
+  const bool skipped = red_skipped(red);
   double pre[10];
   if (ctl.rec != nullptr && threadIdx.x == 0) {
     for (int k = 0; k < 6; ++k) pre[k] = ctl.tr[k];
@@ -146,6 +148,7 @@ __global__ __launch_bounds__(256) void k_finalize_residual(
     if (NSRC == 2 && chain) {   // split-candidate: R0 = (A p_thr - b) + A e (always live)
       const T r1 = group_slab_sum<T, G>(P + (int64_t)S0 * ml, S, ml, idx, sub) - bv;
       const T r0 = r1 + group_slab_sum<T, G>(P0, S0, ml, idx, sub);
+      if (skipped) return;
       if (sub == 1 % G) rs[1][idx] = r1;
       if (R0 != nullptr && sub == 0) rs[0][idx] = r0;
       if (sub == 0) {
@@ -159,6 +162,7 @@ __global__ __launch_bounds__(256) void k_finalize_residual(
       T r;
       if (live) {
         r = group_slab_sum<T, G>(P + (int64_t)sr * S * ml, S, ml, idx, sub) - bv;
+        if (skipped) return;
         if (sub == sr % G) rs[sr][idx] = r;
       } else {
         r = rs[sr][idx];
@@ -166,6 +170,7 @@ __global__ __launch_bounds__(256) void k_finalize_residual(
       if (sub == 0) v[sr] += (double)(r * r);
     }
   }
+  if (skipped) return;   // (threads without a residual element)
   if (cx != nullptr)
     for (int64_t idx = tid; idx < cn; idx += stride) v[3] += (tabs(cx[idx]) > thr) ? 1.0 : 0.0;
   const bool last = grid_reduce<4, 0u>(v, red);

@@ -1091,8 +1091,11 @@ __global__ __launch_bounds__(256, sizeof(T) == 8 ? 2 : 1) void k_atr_prox(const 
                                                   Pub pub, int S, T* __restrict__ Gp,
                                                   unsigned* __restrict__ pcnt,
                                                   uint8_t* __restrict__ zf) {
-  if (red_skipped(red)) {   // cancelled by a device-side decision (solver.cpp dc_run)
-    // the decision record still goes to the host (the cancelling decision's own record)
+  // Cancelled by a device-side decision (solver.cpp dc_run): nothing is computed or stored, no
+  // counter or ticket is touched. (Testing the flag after the main loop instead measured no
+  // faster and would spend a whole pass per cancelled launch.) The decision record still goes
+  // to the host: the cancelling decision's own.
+  if (red_skipped(red)) {
     if (pub.host != nullptr && blockIdx.x == 0 && threadIdx.x == 0)
       publish_packet(pub.s, pub.ns, pub.host, pub.host_seq, pub.seq);
     return;

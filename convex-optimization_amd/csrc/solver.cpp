@@ -950,7 +950,7 @@ class Session : public SessionBase {
   // Gated (cancellable) launches: the finalize (it would overwrite the decision state and the
   // gradient residual of the iteration the host resumes) and the speculative fused kernel (the
   // next gradient set and iterate buffers). A@X and the gather only write the scratch slabs, so
-  // a cancelled one runs to no effect instead of paying a flag load at its start (measured).
+  // a cancelled one runs to no effect instead of testing the flag.
   void dc_queue(Roles& q, int64_t tag) {
     const int rz = (q.irg + 1) % kRes, rpt = (q.irg + 2) % kRes, rp = (q.irg + 3) % kRes;
     const T* xs[3] = {X_[q.iz], X_[q.ipt], X_[q.ip]};
