@@ -19,6 +19,8 @@
 // Reductions are deterministic: block partials in a fixed tree order, then the last block to
 // arrive (sc1 partials + a two-level agent-scope arrival ticket, see grid_reduce) sums the
 // block partials in block order. max() propagates NaN like np.max.
+#include <cstdlib>
+
 #include "glx.h"
 #include "glx_device.h"
 
@@ -599,7 +601,13 @@ void launch_finalize_residual(const T* P, int S, const T* B, int nsrc, T* const*
   const int G = finalize_groups(S > S0 ? S : S0);
   if (G > 8) throw Error{GLX_E_INVALID, "finalize: more than 64 K-split slabs"};
   const int64_t work = ml * G > cn ? ml * G : cn;
-  const dim3 grid(grid_for(work, 256 * 2));
+  // work items per workgroup (GLX_FIN_PER_BLOCK, A/B experiments)
+  static const int per_block = [] {
+    const char* e = std::getenv("GLX_FIN_PER_BLOCK");
+    const int v = e ? std::atoi(e) : 0;
+    return v >= 256 ? v : 512;
+  }();
+  const dim3 grid(grid_for(work, per_block));
   T* r1 = nsrc > 1 ? R[1] : nullptr;
   T* r2 = nsrc > 2 ? R[2] : nullptr;
   auto go = [&](auto ns, auto g) {
