@@ -601,11 +601,13 @@ void launch_finalize_residual(const T* P, int S, const T* B, int nsrc, T* const*
   const int G = finalize_groups(S > S0 ? S : S0);
   if (G > 8) throw Error{GLX_E_INVALID, "finalize: more than 64 K-split slabs"};
   const int64_t work = ml * G > cn ? ml * G : cn;
-  // work items per workgroup (GLX_FIN_PER_BLOCK, A/B experiments)
+  // work items per workgroup (GLX_FIN_PER_BLOCK): one per thread, within the 1024-block cap.
+  // Measured (profiles/r2_fin*): 512 -> 256 takes C2 from 256 to 512 workgroups, +2.3 %;
+  // NS and the 1024-row shape sit at the cap either way; 1024-4096 lost 0-24 %.
   static const int per_block = [] {
     const char* e = std::getenv("GLX_FIN_PER_BLOCK");
     const int v = e ? std::atoi(e) : 0;
-    return v >= 256 ? v : 512;
+    return v >= 256 ? v : 256;
   }();
   const dim3 grid(grid_for(work, per_block));
   T* r1 = nsrc > 1 ? R[1] : nullptr;
