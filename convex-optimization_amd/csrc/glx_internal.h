@@ -128,6 +128,12 @@ bool ax_pub_ok(const GemmPlan& p, int nsrc);
 template <typename T>
 void launch_ax(const GemmPlan& p, int nsrc, const T* A, const T* const* X, T* P, const int* gate,
                int epoch, hipStream_t st, Pub pub = Pub{}, const uint8_t* sf = nullptr);
+// the kind-8 (LDS-DMA, f64) A @ X tile of `code` (kernels_axdma.hip); false: unknown code.
+// dma_lds_need: its LDS bytes for l columns and nsrc right-hand sides (<= 160 KiB to launch).
+template <typename T>
+bool launch_ax_dma(const GemmPlan& p, int code, int nsrc, int S, const T* A, const T* const* X, T* P,
+                   const int* gate, int epoch, hipStream_t st, Pub pub);
+int dma_lds_need(int code, int64_t l, int nsrc);
 template <typename T>
 void launch_atr(const GemmPlan& p, const T* A, const T* R, T* Gp, hipStream_t st);
 // ProxGD trial fused into A^T R (needs atr_prox_ok: MFMA panels, WL 0, at most 8 K splits):
@@ -181,7 +187,9 @@ bool resgrad_device_ok();
 int resgrad_groups(int64_t n);
 size_t resgrad_ws_bytes(int64_t m, int64_t n);
 void resgrad_reset(void* ws, int64_t m, int64_t n, hipStream_t st);
-void launch_resgrad(const double* A, const double* X, const double* B, double* Sraw, double* Gs,
+// returns false (nothing launched) when the runtime refuses the cooperative launch; *err != 0
+// after the launch: a hand-off wait timed out or the XCD grouping failed, R / G are invalid
+bool launch_resgrad(const double* A, const double* X, const double* B, double* Sraw, double* Gs,
                     void* ws, unsigned launch_count, int64_t m, int64_t n, int* err, hipStream_t st);
 
 // ---- row / elementwise kernels (kernels_elem.hip) ----

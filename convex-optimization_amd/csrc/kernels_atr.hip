@@ -1,0 +1,582 @@
+// kernels_atr.hip — the gradient contraction A^T R (reference: gl_ProxGD_primal.py:129
+// `A.T @ (A @ x - b)`; gl_FProxGD_primal.py:65-66) on MFMA, with the ProxGD / FISTA line-search
+// trial fused into its epilogue (k_atr_prox, k_atr_fista), and the VALU fallback for small l.
+//
+// The K index (rows of A) is on l>>4 and the 16-wide M index (columns of A) on l&15, so lanes
+// 0..15 read consecutive columns: a lane loads 4 columns of one row (atr_col) and feeds 4 MFMAs
+// whose output rows are those columns. Split-K partials (waves through LDS, workgroups as
+// slabs) are summed in a fixed order, so every result is deterministic run to run.
+#include <cstdio>
+
+#include "glx_mfma.h"
+
+namespace glx {
+
+// ------------------------------------------------------------------------------------------
+// A^T R on MFMA: a wave owns 64 columns of A (= 64 rows of G) x NT 16-col tiles of G.
+//   WL = 0: a block = one 64-column panel, its 4 waves split the block's rows (LDS-reduced);
+//   WL = 1: a block = four adjacent panels (256 columns) sharing one row range, so the four
+//           waves read the same R fragments (L1 hits) and write their slabs directly.
+// blockIdx.y = row split. Needs n % 64 == 0 (n % 256 for WL = 1), m % 4 == 0.
+// Gp[split][n][16*NT].
+// ------------------------------------------------------------------------------------------
+// A lane (i, q) of a row step feeds the four MFMAs e = 0..3 with row q of A at panel columns
+// atr_col(i, e); MFMA e's output row i is then G row col0 + atr_col(i, e). f64: columns
+// {2i, 2i+1} and {32 + 2i, 33 + 2i}, so each of the two 16-B loads of a wave-instruction covers
+// 256 contiguous bytes of each of its four rows (the streaming probe, scripts/stream_probe.hip:
+// 6.1 TB/s for the 4i..4i+3 form, whose loads leave every other 16 B of a 512-B span to the
+// next instruction, against 6.3-7.1 TB/s for contiguous 256/512-B pieces). f32: one 16-B load
+// already covers columns 4i..4i+3.
+template <typename T>
+__device__ inline int atr_col(int i, int e) {
+  if constexpr (sizeof(T) == 8) return (e >> 1) * 32 + 2 * i + (e & 1);
+  else return 4 * i + e;
+}
+template <typename T, bool NTL> struct Load4;
+template <bool NTL> struct Load4<double, NTL> {
+  __device__ static inline void go(const double* p, double (&a)[4]) {   // p = row + col0 + 2i
+    const d2_t v0 = load_vec<double, NTL>(p);
+    const d2_t v1 = load_vec<double, NTL>(p + 32);
+    a[0] = v0[0]; a[1] = v0[1]; a[2] = v1[0]; a[3] = v1[1];
+  }
+};
+template <bool NTL> struct Load4<float, NTL> {
+  __device__ static inline void go(const float* p, float (&a)[4]) {
+    const f4_t v = load_vec<float, NTL>(p);
+    a[0] = v[0]; a[1] = v[1]; a[2] = v[2]; a[3] = v[3];
+  }
+};
+
+// One 64-column panel of A^T R over this wave's (WL 1: this block's) row range; returns the
+// panel's first column. acc[e][nt] holds rows col0 + atr_col(M::row(lane, r), e). For WL 0 the
+// block's four waves split the rows (K) and are summed through LDS in the fixed order
+// ((w0 + w1) + w2) + w3; afterwards wave w holds the complete sum for e == w in acc[w][*]
+// (the other e of a wave are partial and unused), so the four waves share the epilogue.
+// (pbx, pby) = (panel, K split) of this block: (blockIdx.x, blockIdx.y) for k_atr_mfma.
+template <typename T, int NT, int PF, int WL, bool NTL>
+__device__ inline int64_t atr_panel(const T* __restrict__ A, const T* __restrict__ R, int64_t m,
+                                    int64_t n, int S, typename MF<T>::acc_t (&acc)[4][NT],
+                                    int64_t pbx, int64_t pby) {
+  typedef MF<T> M;
+  typedef typename M::acc_t C;
+  constexpr int L = 16 * NT;
+  __shared__ C red[WL == 0 ? 4 : 1][WL == 0 ? 4 * NT : 1][64];   // [wave][e * NT + nt][lane]
+
+  const int lane = threadIdx.x & 63;
+  const int wave = threadIdx.x >> 6;
+  const int i = lane & 15, q = lane >> 4;
+  const int64_t col0 = WL == 0 ? pbx * 64 : pbx * 256 + wave * 64;
+  const int64_t steps = m / 4;
+  const int64_t W = WL == 0 ? (int64_t)S * 4 : (int64_t)S;
+  const int64_t w = WL == 0 ? pby * 4 + wave : pby;
+  const int64_t sb = steps * w / W, se = steps * (w + 1) / W;
+
+  const T* ap = A + (sb * 4 + q) * n + col0 + atr_col<T>(i, 0);
+  const T* rp = R + (sb * 4 + q) * L + i;
+
+#pragma unroll
+  for (int e = 0; e < 4; ++e)
+#pragma unroll
+    for (int nt = 0; nt < NT; ++nt) acc[e][nt] = C{};
+
+  // Ring of PF row steps, consumed in place: a step's fragments feed its MFMAs and are then
+  // refilled with step s + PF in the same registers, at a clamped offset so that the main
+  // loop carries no load predicates (a predicate or a register copy at the loop's back edge
+  // makes the compiler drain vmcnt to 0 there). Lookahead = PF - 1 steps.
+  const int64_t nst = se - sb;
+  T a[PF][4], rb[PF][NT];
+  auto ld = [&](int p, int64_t off) {
+    off = off < nst ? off : nst - 1;
+    Load4<T, NTL>::go(ap + off * 4 * n, a[p]);
+#pragma unroll
+    for (int nt = 0; nt < NT; ++nt) rb[p][nt] = rp[off * 4 * L + nt * 16];
+  };
+  auto mma_step = [&](int p) {
+#pragma unroll
+    for (int e = 0; e < 4; ++e)
+#pragma unroll
+      for (int nt = 0; nt < NT; ++nt) acc[e][nt] = M::mma(a[p][e], rb[p][nt], acc[e][nt]);
+  };
+  if (nst > 0) {
+#pragma unroll
+    for (int p = 0; p < PF; ++p) ld(p, p);
+    int64_t s0 = 0;
+    for (; s0 + PF <= nst; s0 += PF) {
+#pragma unroll
+      for (int p = 0; p < PF; ++p) {
+        mma_step(p);
+        ld(p, s0 + p + PF);
+      }
+    }
+#pragma unroll
+    for (int p = 0; p < PF - 1; ++p)
+      if (s0 + p < nst) mma_step(p);
+  }
+
+  if (WL == 0) {
+#pragma unroll
+    for (int e = 0; e < 4; ++e)
+#pragma unroll
+      for (int nt = 0; nt < NT; ++nt) red[wave][e * NT + nt][lane] = acc[e][nt];
+    __syncthreads();
+#pragma unroll
+    for (int nt = 0; nt < NT; ++nt) {
+      C v = red[0][wave * NT + nt][lane];
+#pragma unroll
+      for (int s = 1; s < 4; ++s) v += red[s][wave * NT + nt][lane];
+#pragma unroll
+      for (int e = 0; e < 4; ++e)
+        if (e == wave) acc[e][nt] = v;   // static register index; e == wave selects one
+    }
+  }
+  return col0;
+}
+
+// K splits of a fused A^T R (WL 0, S > 1): a 1-D grid of n/64 panels x S splits (+ the
+// publisher). Every block stores its panel rows (wave w: rows e == w) into slab `split` of Gp;
+// the block that arrives last on its panel's counter sums the S slabs in slab order (the
+// order of slab_sum, so G is bit-identical to the unfused path) and runs the trial epilogue.
+// Hand-off: sc1 (agent-scope) stores, vmcnt(0), a workgroup barrier, one agent-scope add per
+// block; the last arriver loads with sc1 after a barrier (MI355X_MICROARCH.md "Valid forms",
+// row 1). Returns false in the blocks that are not last (they only join the grid reduction).
+// *slot = this block's grid-reduction slot, fixed whatever the arrival order: the panel's
+// trial sums (last arriver) at `panel`, the identity partials of the other S - 1 blocks at
+// n/64 + panel (S - 1) + their arrival index. So the trial's scalar sums come out in panel
+// order, bit-identical from run to run (a last arriver at its own block slot made their
+// summation order depend on timing).
+template <typename T, int NT>
+__device__ inline bool atr_split_combine(typename MF<T>::acc_t (&acc)[4][NT], T* __restrict__ Gp,
+                                         int64_t n, int S, int64_t panel, int64_t split,
+                                         unsigned* __restrict__ pcnt, int* slot) {
+  typedef MF<T> M;
+  constexpr int L = 16 * NT;
+  __shared__ int last;
+  __shared__ unsigned arrival;
+  const int lane = threadIdx.x & 63;
+  const int wave = threadIdx.x >> 6;
+  const int i = lane & 15;
+  const int64_t col0 = panel * 64;
+  const int64_t nl = n * L;
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    if (e != wave) continue;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int64_t row = col0 + atr_col<T>(M::row(lane, r), e);
+#pragma unroll
+      for (int nt = 0; nt < NT; ++nt)
+        __hip_atomic_store(Gp + split * nl + row * L + nt * 16 + i, acc[e][nt][r], __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    arrival = __hip_atomic_fetch_add(pcnt + panel, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    last = arrival == (unsigned)S - 1;
+  }
+  __syncthreads();
+  *slot = last ? (int)panel : (int)(n / 64 + panel * (S - 1) + arrival);
+  if (!last) return false;
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    if (e != wave) continue;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int64_t row = col0 + atr_col<T>(M::row(lane, r), e);
+#pragma unroll
+      for (int nt = 0; nt < NT; ++nt) {
+        const T* g = Gp + row * L + nt * 16 + i;
+        T v = __hip_atomic_load(g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        for (int k = 1; k < S; ++k)
+          v = v + __hip_atomic_load(g + (int64_t)k * nl, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        acc[e][nt][r] = v;
+      }
+    }
+  }
+  if (threadIdx.x == 0) __hip_atomic_store(pcnt + panel, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  return true;
+}
+
+template <typename T, int NT, int PF, int WL, bool NTL>
+__global__ __launch_bounds__(256) void k_atr_mfma(const T* __restrict__ A, const T* __restrict__ R,
+                                                  T* __restrict__ Gp, int64_t m, int64_t n, int S) {
+  typedef MF<T> M;
+  constexpr int L = 16 * NT;
+  const int lane = threadIdx.x & 63;
+  const int wave = threadIdx.x >> 6;
+  const int i = lane & 15;
+  typename M::acc_t acc[4][NT];
+  const int64_t col0 = atr_panel<T, NT, PF, WL, NTL>(A, R, m, n, S, acc, blockIdx.x, blockIdx.y);
+  T* gout = Gp + (int64_t)blockIdx.y * n * L;
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    if (WL == 0 && e != wave) continue;   // WL 0: wave w owns the rows e == w
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int64_t grow = col0 + atr_col<T>(M::row(lane, r), e);
+#pragma unroll
+      for (int nt = 0; nt < NT; ++nt) gout[grow * L + nt * 16 + i] = acc[e][nt][r];
+    }
+  }
+}
+
+// ProxGD's line-search trial fused into A^T R (WL 0, one K split): once the block's LDS
+// reduction leaves each wave w the 16 gradient rows e == w of its panel — lane (i, q) holding
+// columns i and 16 + i of 4 rows, exactly the 16-lanes-per-row layout of k_prox_pgd — every
+// wave writes its rows of G and runs the trial on them (prox_pgd_row, the same arithmetic as
+// k_prox_pgd) with x = the thresholded iterate; the six trial sums are reduced over the grid.
+template <typename T, int NT, int PF, bool NTL, bool SPLIT>
+__global__ __launch_bounds__(256, sizeof(T) == 8 ? 2 : 1) void k_atr_prox(const T* __restrict__ A, const T* __restrict__ R,
+                                                  T* __restrict__ G, int64_t m, int64_t n,
+                                                  const T* __restrict__ x, T* __restrict__ p,
+                                                  T* __restrict__ pthr, T* __restrict__ z,
+                                                  double t_, double tmu_, double thres_, Red red,
+                                                  Pub pub, int S, T* __restrict__ Gp,
+                                                  unsigned* __restrict__ pcnt,
+                                                  uint8_t* __restrict__ zf) {
+  // Cancelled by a device-side decision (solver.cpp dc_run): nothing is computed or stored, no
+  // counter or ticket is touched. (Testing the flag after the main loop instead measured no
+  // faster and would spend a whole pass per cancelled launch.) The decision record still goes
+  // to the host: the cancelling decision's own.
+  if (red_skipped(red)) {
+    if (pub.host != nullptr && blockIdx.x == 0 && threadIdx.x == 0)
+      publish_packet(pub.s, pub.ns, pub.host, pub.host_seq, pub.seq);
+    return;
+  }
+  if (publisher_first<6, 0x8u>(pub, red)) return;   // the extra workgroup (n / 64 * S + 1 in all)
+  typedef MF<T> M;
+  constexpr int L = 16 * NT;
+  const int lane = threadIdx.x & 63;
+  const int wave = threadIdx.x >> 6;
+  const int i = lane & 15;
+  typename M::acc_t acc[4][NT];
+  const int64_t bid = (int64_t)blockIdx.x - (pub.host ? 1 : 0);
+  const int64_t panel = SPLIT ? bid / S : bid, split = SPLIT ? bid % S : 0;
+  const int64_t col0 = atr_panel<T, NT, PF, 0, NTL>(A, R, m, n, SPLIT ? S : 1, acc, panel, split);
+  double accr[6] = {0.0, 0.0, 0.0, -__builtin_inf(), 0.0, 0.0};
+  int slot = work_slot(pub);
+  if constexpr (SPLIT) {   // a separate instantiation: the S = 1 kernel keeps 2 blocks per CU
+    if (!atr_split_combine<T, NT>(acc, Gp, n, S, panel, split, pcnt, &slot)) {
+      grid_reduce<6, 0x8u>(accr, red, slot);
+      return;
+    }
+  }
+  const T t = (T)t_, tmu = (T)tmu_, thres = (T)thres_;
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    if (e != wave) continue;   // wave w owns the rows e == w (4 per lane group)
+    T xa[4][NT];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int64_t row = col0 + atr_col<T>(M::row(lane, r), e);
+#pragma unroll
+      for (int nt = 0; nt < NT; ++nt) xa[r][nt] = x[row * L + nt * 16 + i];
+    }
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int64_t row = col0 + atr_col<T>(M::row(lane, r), e);
+      T gv[NT], pv[NT], pth[NT], zv[NT];
+      bool ok[NT];
+#pragma unroll
+      for (int nt = 0; nt < NT; ++nt) {
+        gv[nt] = acc[e][nt][r];
+        ok[nt] = true;
+        G[row * L + nt * 16 + i] = gv[nt];
+      }
+      const bool rowe =
+          prox_pgd_row<T, 16, NT>(xa[r], gv, ok, true, i, t, tmu, thres, pv, pth, zv, accr, zf != nullptr);
+      if (zf != nullptr && i == 0) zf[row] = rowe ? 1 : 0;
+#pragma unroll
+      for (int nt = 0; nt < NT; ++nt) {
+        p[row * L + nt * 16 + i] = pv[nt];
+        pthr[row * L + nt * 16 + i] = pth[nt];
+        z[row * L + nt * 16 + i] = zv[nt];
+      }
+    }
+  }
+  grid_reduce<6, 0x8u>(accr, red, slot);
+}
+
+// FISTA's backtracking trial fused into A^T R the same way (WL 0, one K split): each wave runs
+// fista_row (the arithmetic of k_fista_trial) on its 16 gradient rows, with y the extrapolated
+// point and xk the current iterate; writes G, xc, v_next, y_next and reduces the four sums.
+template <typename T, int NT, int PF, bool NTL, bool SPLIT>
+__global__ __launch_bounds__(256, sizeof(T) == 8 ? 2 : 1) void k_atr_fista(const T* __restrict__ A, const T* __restrict__ R,
+                                                   T* __restrict__ G, int64_t m, int64_t n,
+                                                   const T* __restrict__ y, const T* __restrict__ xk,
+                                                   T* __restrict__ xc, T* __restrict__ vnext,
+                                                   T* __restrict__ ynext, double t_, double tmu_,
+                                                   double thres_, double theta_, double a1_,
+                                                   double b1_, Red red, Pub pub, int S,
+                                                   T* __restrict__ Gp, unsigned* __restrict__ pcnt,
+                                                   T* __restrict__ ec, uint8_t* __restrict__ zf) {
+  if (publisher_first<4, 0x8u>(pub, red)) return;
+  typedef MF<T> M;
+  constexpr int L = 16 * NT;
+  const int lane = threadIdx.x & 63;
+  const int wave = threadIdx.x >> 6;
+  const int i = lane & 15;
+  typename M::acc_t acc[4][NT];
+  const int64_t bid = (int64_t)blockIdx.x - (pub.host ? 1 : 0);
+  const int64_t panel = SPLIT ? bid / S : bid, split = SPLIT ? bid % S : 0;
+  const int64_t col0 = atr_panel<T, NT, PF, 0, NTL>(A, R, m, n, SPLIT ? S : 1, acc, panel, split);
+  double accr[4] = {0.0, 0.0, 0.0, -__builtin_inf()};
+  int slot = work_slot(pub);
+  if constexpr (SPLIT) {   // fixed reduction slots, see atr_split_combine
+    if (!atr_split_combine<T, NT>(acc, Gp, n, S, panel, split, pcnt, &slot)) {
+      grid_reduce<4, 0x8u>(accr, red, slot);
+      return;
+    }
+  }
+  const T t = (T)t_, tmu = (T)tmu_, thres = (T)thres_, theta = (T)theta_, a1 = (T)a1_, b1 = (T)b1_;
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    if (e != wave) continue;   // wave w owns the rows e == w
+    T ya[4][NT], xa[4][NT];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int64_t row = col0 + atr_col<T>(M::row(lane, r), e);
+#pragma unroll
+      for (int nt = 0; nt < NT; ++nt) {
+        ya[r][nt] = y[row * L + nt * 16 + i];
+        xa[r][nt] = xk[row * L + nt * 16 + i];
+      }
+    }
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int64_t row = col0 + atr_col<T>(M::row(lane, r), e);
+      T gv[NT], xcv[NT], vnv[NT], ynv[NT], ecv[NT];
+      bool ok[NT];
+#pragma unroll
+      for (int nt = 0; nt < NT; ++nt) {
+        gv[nt] = acc[e][nt][r];
+        ok[nt] = true;
+        G[row * L + nt * 16 + i] = gv[nt];
+      }
+      const bool rowe = fista_row<T, 16, NT, true>(ya[r], gv, xa[r], ok, true, i, t, tmu, thres, theta,
+                                                   a1, b1, T(0), T(0), xcv, vnv, ynv, accr,
+                                                   ec != nullptr ? ecv : nullptr);
+      if (zf != nullptr && i == 0) zf[row] = rowe ? 1 : 0;
+#pragma unroll
+      for (int nt = 0; nt < NT; ++nt) {
+        xc[row * L + nt * 16 + i] = xcv[nt];
+        vnext[row * L + nt * 16 + i] = vnv[nt];
+        ynext[row * L + nt * 16 + i] = ynv[nt];
+        if (ec != nullptr) ec[row * L + nt * 16 + i] = ecv[nt];
+      }
+    }
+  }
+  grid_reduce<4, 0x8u>(accr, red, slot);
+}
+
+// A^T R on VALU: a thread owns E consecutive columns of A over a row range; R[row][c0..c0+LB)
+// is wave-uniform (scalar loads). Gp[blockIdx.y][n][l].
+template <typename T, int LB, bool VEC>
+__global__ __launch_bounds__(256) void k_atr_valu(const T* __restrict__ A, const T* __restrict__ R,
+                                                  T* __restrict__ Gp, int64_t m, int64_t n,
+                                                  int64_t l, int c0, int S) {
+  constexpr int E = VEC ? (16 / (int)sizeof(T)) : 1;
+  const int64_t col = ((int64_t)blockIdx.x * 256 + threadIdx.x) * E;
+  const int s = blockIdx.y;
+  const int64_t rb = m * s / S, re = m * (s + 1) / S;
+  const int nc = (int)((l - c0) < LB ? (l - c0) : LB);
+  const bool active = col < n;
+  const int64_t ccol = active ? col : 0;
+
+  T acc[E][LB];
+#pragma unroll
+  for (int e = 0; e < E; ++e)
+#pragma unroll
+    for (int c = 0; c < LB; ++c) acc[e][c] = T(0);
+
+  const T* ap = A + rb * n + ccol;
+  const T* rp = R + rb * l + c0;
+#pragma unroll 4
+  for (int64_t row = rb; row < re; ++row) {
+    T a[E];
+    if constexpr (VEC) {
+      typedef typename MF<T>::vec_t V;
+      const V v = *reinterpret_cast<const V*>(ap);
+#pragma unroll
+      for (int e = 0; e < E; ++e) a[e] = v[e];
+    } else {
+      a[0] = *ap;
+    }
+    T rv[LB];
+#pragma unroll
+    for (int c = 0; c < LB; ++c) rv[c] = (c < nc) ? rp[c] : T(0);
+#pragma unroll
+    for (int e = 0; e < E; ++e)
+#pragma unroll
+      for (int c = 0; c < LB; ++c) acc[e][c] = __builtin_fma(a[e], rv[c], acc[e][c]);
+    ap += n;
+    rp += l;
+  }
+  if (!active) return;
+  T* gout = Gp + (int64_t)s * n * l;
+#pragma unroll
+  for (int e = 0; e < E; ++e)
+#pragma unroll
+    for (int c = 0; c < LB; ++c)
+      if (c < nc) gout[(col + e) * l + c0 + c] = acc[e][c];
+}
+
+
+template <typename T, int LB>
+static void atr_valu_lb(const GemmPlan& p, const T* A, const T* R, T* Gp, hipStream_t st) {
+  constexpr int E = 16 / sizeof(T);
+  const int64_t cols_per_block = 256 * (p.atr_vec ? E : 1);
+  const dim3 grid((unsigned)cdiv(p.n, cols_per_block), (unsigned)p.atr_S);
+  for (int64_t c0 = 0; c0 < p.l; c0 += LB) {
+    if (p.atr_vec)
+      hipLaunchKernelGGL((k_atr_valu<T, LB, true>), grid, dim3(256), 0, st, A, R, Gp, p.m, p.n,
+                         p.l, (int)c0, p.atr_S);
+    else
+      hipLaunchKernelGGL((k_atr_valu<T, LB, false>), grid, dim3(256), 0, st, A, R, Gp, p.m, p.n,
+                         p.l, (int)c0, p.atr_S);
+  }
+}
+
+template <typename T, int NT, int PF, int WL, bool NTL>
+static void atr_mfma_go(const GemmPlan& p, const T* A, const T* R, T* Gp, hipStream_t st) {
+  const dim3 grid((unsigned)(p.n / (WL ? 256 : 64)), (unsigned)p.atr_S);
+  static const size_t pad = lds_pad(k_atr_mfma<T, NT, PF, WL, NTL>, "GLX_ATR_LDS_PAD");
+  hipLaunchKernelGGL((k_atr_mfma<T, NT, PF, WL, NTL>), grid, dim3(256), pad, st, A, R, Gp, p.m, p.n, p.atr_S);
+}
+
+template <typename T, int NT>
+static void atr_mfma_nt(const GemmPlan& p, const T* A, const T* R, T* Gp, hipStream_t st) {
+  switch (p.atr_ntl * 100 + p.atr_wl * 10 + p.atr_pf) {
+    case 3: atr_mfma_go<T, NT, 3, 0, false>(p, A, R, Gp, st); break;
+    case 4: atr_mfma_go<T, NT, 4, 0, false>(p, A, R, Gp, st); break;
+    case 6: atr_mfma_go<T, NT, 6, 0, false>(p, A, R, Gp, st); break;
+    case 8: atr_mfma_go<T, NT, 8, 0, false>(p, A, R, Gp, st); break;
+    case 14: atr_mfma_go<T, NT, 4, 1, false>(p, A, R, Gp, st); break;
+    case 102: atr_mfma_go<T, NT, 2, 0, true>(p, A, R, Gp, st); break;
+    case 104: atr_mfma_go<T, NT, 4, 0, true>(p, A, R, Gp, st); break;
+    case 106: atr_mfma_go<T, NT, 6, 0, true>(p, A, R, Gp, st); break;
+    case 108: atr_mfma_go<T, NT, 8, 0, true>(p, A, R, Gp, st); break;
+    case 114: atr_mfma_go<T, NT, 4, 1, true>(p, A, R, Gp, st); break;
+    default: atr_mfma_go<T, NT, 2, 0, false>(p, A, R, Gp, st); break;
+  }
+}
+
+template <typename T>
+void launch_atr(const GemmPlan& p, const T* A, const T* R, T* Gp, hipStream_t st) {
+  if (p.atr_kind == 3) {
+    switch (p.atr_lb) {
+      case 1: atr_valu_lb<T, 1>(p, A, R, Gp, st); break;
+      case 2: atr_valu_lb<T, 2>(p, A, R, Gp, st); break;
+      case 4: atr_valu_lb<T, 4>(p, A, R, Gp, st); break;
+      default: atr_valu_lb<T, 8>(p, A, R, Gp, st); break;
+    }
+    return;
+  }
+  if (p.l == 16) atr_mfma_nt<T, 1>(p, A, R, Gp, st);
+  else atr_mfma_nt<T, 2>(p, A, R, Gp, st);
+}
+
+
+bool atr_prox_ok(const GemmPlan& p) {
+  return p.atr_kind == 1 && p.atr_wl == 0 && p.atr_S >= 1 && p.atr_S <= 8 &&
+         (p.l == 16 || p.l == 32) && p.n % 64 == 0 &&
+         (p.n / 64) * p.atr_S < kMaxBlocks &&   // + a publisher workgroup
+         (p.atr_S == 1 || env_int("GLX_ATR_FUSE_SPLIT", 1) != 0);
+}
+
+template <typename T, int NT, int PF, bool NTL>
+static void atr_prox_go(const GemmPlan& p, const T* A, const T* R, T* G, const T* x, T* pp,
+                        T* pthr, T* z, double t, double mu, double thres, Red red, hipStream_t st,
+                        Pub pub, T* Gp, unsigned* pcnt, uint8_t* zf) {
+  const dim3 grid((unsigned)(p.n / 64 * p.atr_S + (pub.host ? 1 : 0)));
+  if (p.atr_S > 1) {
+    hipLaunchKernelGGL((k_atr_prox<T, NT, PF, NTL, true>), grid, dim3(256), 0, st, A, R, G, p.m,
+                       p.n, x, pp, pthr, z, t, t * mu, thres, red, pub, p.atr_S, Gp, pcnt, zf);
+    return;
+  }
+  static const size_t pad = lds_pad(k_atr_prox<T, NT, PF, NTL, false>, "GLX_ATR_LDS_PAD");
+  hipLaunchKernelGGL((k_atr_prox<T, NT, PF, NTL, false>), grid, dim3(256), pad, st, A, R, G, p.m,
+                     p.n, x, pp, pthr, z, t, t * mu, thres, red, pub, 1, Gp, pcnt, zf);
+}
+template <typename T, int NT>
+static void atr_prox_nt(const GemmPlan& p, const T* A, const T* R, T* G, const T* x, T* pp,
+                        T* pthr, T* z, double t, double mu, double thres, Red red, hipStream_t st,
+                        Pub pub, T* Gp, unsigned* pcnt, uint8_t* zf) {
+  switch (p.atr_ntl * 100 + p.atr_pf) {
+    case 4: atr_prox_go<T, NT, 4, false>(p, A, R, G, x, pp, pthr, z, t, mu, thres, red, st, pub, Gp, pcnt, zf); break;
+    case 6: atr_prox_go<T, NT, 6, false>(p, A, R, G, x, pp, pthr, z, t, mu, thres, red, st, pub, Gp, pcnt, zf); break;
+    case 104: atr_prox_go<T, NT, 4, true>(p, A, R, G, x, pp, pthr, z, t, mu, thres, red, st, pub, Gp, pcnt, zf); break;
+    case 108: atr_prox_go<T, NT, 8, true>(p, A, R, G, x, pp, pthr, z, t, mu, thres, red, st, pub, Gp, pcnt, zf); break;
+    default: atr_prox_go<T, NT, 8, false>(p, A, R, G, x, pp, pthr, z, t, mu, thres, red, st, pub, Gp, pcnt, zf); break;
+  }
+}
+template <typename T>
+void launch_atr_prox(const GemmPlan& p, const T* A, const T* R, T* G, const T* x, T* pp, T* pthr,
+                     T* z, double t, double mu, double thres, Red red, hipStream_t st, Pub pub,
+                     T* Gp, unsigned* pcnt, uint8_t* zf) {
+  if (p.atr_S > 1 && (Gp == nullptr || pcnt == nullptr))
+    throw Error{GLX_E_INVALID, "fused A^T R with K splits needs slab and counter buffers"};
+  if (p.l == 16) atr_prox_nt<T, 1>(p, A, R, G, x, pp, pthr, z, t, mu, thres, red, st, pub, Gp, pcnt, zf);
+  else atr_prox_nt<T, 2>(p, A, R, G, x, pp, pthr, z, t, mu, thres, red, st, pub, Gp, pcnt, zf);
+}
+
+template <typename T, int NT, int PF, bool NTL>
+static void atr_fista_go(const GemmPlan& p, const T* A, const T* R, T* G, const T* y, const T* xk,
+                         T* xc, T* vn, T* yn, double t, double mu, double thres, double theta,
+                         double theta_next, Red red, hipStream_t st, Pub pub, T* Gp, unsigned* pcnt,
+                         T* ec, uint8_t* zf) {
+  const dim3 grid((unsigned)(p.n / 64 * p.atr_S + (pub.host ? 1 : 0)));
+  if (p.atr_S > 1) {
+    hipLaunchKernelGGL((k_atr_fista<T, NT, PF, NTL, true>), grid, dim3(256), 0, st, A, R, G, p.m,
+                       p.n, y, xk, xc, vn, yn, t, t * mu, thres, theta, 1.0 - theta_next,
+                       theta_next, red, pub, p.atr_S, Gp, pcnt, ec, zf);
+    return;
+  }
+  static const size_t pad = lds_pad(k_atr_fista<T, NT, PF, NTL, false>, "GLX_ATR_LDS_PAD");
+  hipLaunchKernelGGL((k_atr_fista<T, NT, PF, NTL, false>), grid, dim3(256), pad, st, A, R, G, p.m,
+                     p.n, y, xk, xc, vn, yn, t, t * mu, thres, theta, 1.0 - theta_next, theta_next,
+                     red, pub, 1, Gp, pcnt, ec, zf);
+}
+template <typename T, int NT>
+static void atr_fista_nt(const GemmPlan& p, const T* A, const T* R, T* G, const T* y, const T* xk,
+                         T* xc, T* vn, T* yn, double t, double mu, double thres, double theta,
+                         double theta_next, Red red, hipStream_t st, Pub pub, T* Gp, unsigned* pcnt,
+                         T* ec, uint8_t* zf) {
+  switch (p.atr_ntl * 100 + p.atr_pf) {
+    case 4: atr_fista_go<T, NT, 4, false>(p, A, R, G, y, xk, xc, vn, yn, t, mu, thres, theta, theta_next, red, st, pub, Gp, pcnt, ec, zf); break;
+    case 104: atr_fista_go<T, NT, 4, true>(p, A, R, G, y, xk, xc, vn, yn, t, mu, thres, theta, theta_next, red, st, pub, Gp, pcnt, ec, zf); break;
+    case 108: atr_fista_go<T, NT, 8, true>(p, A, R, G, y, xk, xc, vn, yn, t, mu, thres, theta, theta_next, red, st, pub, Gp, pcnt, ec, zf); break;
+    default: atr_fista_go<T, NT, 8, false>(p, A, R, G, y, xk, xc, vn, yn, t, mu, thres, theta, theta_next, red, st, pub, Gp, pcnt, ec, zf); break;
+  }
+}
+template <typename T>
+void launch_atr_fista(const GemmPlan& p, const T* A, const T* R, T* G, const T* y, const T* xk,
+                      T* xc, T* vn, T* yn, double t, double mu, double thres, double theta,
+                      double theta_next, Red red, hipStream_t st, Pub pub, T* Gp, unsigned* pcnt,
+                         T* ec, uint8_t* zf) {
+  if (p.atr_S > 1 && (Gp == nullptr || pcnt == nullptr))
+    throw Error{GLX_E_INVALID, "fused A^T R with K splits needs slab and counter buffers"};
+  if (p.l == 16) atr_fista_nt<T, 1>(p, A, R, G, y, xk, xc, vn, yn, t, mu, thres, theta, theta_next, red, st, pub, Gp, pcnt, ec, zf);
+  else atr_fista_nt<T, 2>(p, A, R, G, y, xk, xc, vn, yn, t, mu, thres, theta, theta_next, red, st, pub, Gp, pcnt, ec, zf);
+}
+
+template void launch_atr<double>(const GemmPlan&, const double*, const double*, double*, hipStream_t);
+template void launch_atr_fista<double>(const GemmPlan&, const double*, const double*, double*,
+                                       const double*, const double*, double*, double*, double*,
+                                       double, double, double, double, double, Red, hipStream_t, Pub,
+                                       double*, unsigned*, double*, uint8_t*);
+template void launch_atr_fista<float>(const GemmPlan&, const float*, const float*, float*,
+                                      const float*, const float*, float*, float*, float*, double,
+                                      double, double, double, double, Red, hipStream_t, Pub,
+                                      float*, unsigned*, float*, uint8_t*);
+template void launch_atr_prox<double>(const GemmPlan&, const double*, const double*, double*,
+                                      const double*, double*, double*, double*, double, double,
+                                      double, Red, hipStream_t, Pub, double*, unsigned*, uint8_t*);
+template void launch_atr_prox<float>(const GemmPlan&, const float*, const float*, float*,
+                                     const float*, float*, float*, float*, double, double, double,
+                                     Red, hipStream_t, Pub, float*, unsigned*, uint8_t*);
+template void launch_atr<float>(const GemmPlan&, const float*, const float*, float*, hipStream_t);
+
+
+}  // namespace glx

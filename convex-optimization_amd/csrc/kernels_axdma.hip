@@ -1,0 +1,264 @@
+// kernels_axdma.hip — A @ X (reference: gl_ProxGD_primal.py:25,61,129 `A @ x`) with A and X
+// staged in LDS by LDS-DMA, f64 (kind 8 of the A @ X planner, kernels_gemm.hip).
+#include "glx_mfma.h"
+
+namespace glx {
+
+// ------------------------------------------------------------------------------------------
+// A @ X, kind 8 (f64): A and X staged in LDS by LDS-DMA (global_load_lds_dwordx4). The kind-5
+// tile loads A straight into the MFMA operand registers, so one wave-instruction can only
+// cover 16 rows x 64 B (a lane's bytes must be its own row's); the streaming probe
+// (scripts/stream_probe.hip, profiles/r2_stream/) caps that shape at 5.9-6.2 TB/s against
+// 6.3-7.3 TB/s for whole 256-512-B pieces. Here the wave-instruction that fetches A is decoupled
+// from the lane that consumes it: each instruction lands 4 rows x 256 B (KC = 32) in LDS and
+// the lanes read their MFMA operands back with ds_read_b128.
+//
+// Block = WAVES waves; wave w owns 16 rows (row0 .. row0 + 15) and streams them itself; the
+// block's X chunk (KC rows of every source) is fetched by one 1-KiB instruction per wave and
+// shared. A ring of NS LDS slots, NS - 1 chunks in flight. Per chunk every wave waits for its
+// own DMAs of that chunk with a counted vmcnt, then ONE raw s_barrier (never __syncthreads(),
+// whose fence waits for vmcnt(0) and would drain the ring) makes every wave's DMAs visible,
+// then the next chunk is issued into the slot the previous chunk used (every wave has read it:
+// its ds_reads completed before the wave reached the barrier, lgkmcnt(0) in the same wait).
+//
+// LDS images (one __shared__ array; the DMA destination is lane-linear, so swizzles go on the
+// SOURCE address, cdna_hip_programming.md §5.4 rule 21):
+//   A: wave's [16][KC/2] 16-B slots, slot s of row i stored at s ^ sw(i). Lane (i, q) reads
+//      slots s = q + 4j (j < KC/8), i.e. k = 2s + e — conflict-free ds_read_b128 for every
+//      4 x 16-lane group (MI355X_MICROARCH.md §LDS), checked by scripts/lds_banks.py.
+//   X: per source KC rows of l values as 128-B units (k * NT + half); unit u stored at
+//      u ^ ((k >> 1) & 1), so the two 16-lane halves of a ds_read_b64 group (lane groups
+//      q = 0/1 and 2/3 read rows k = 2(q + 4j) + e) fall on different bank halves.
+// MFMA operand maps as in kind 5 (k permuted inside a chunk, X read with the same permutation).
+// Past the end of a block's K range the ring re-issues the last chunk (an L2 hit, discarded),
+// so every wave's DMA count per chunk is the same constant the counted vmcnt needs.
+// ------------------------------------------------------------------------------------------
+typedef __attribute__((address_space(1))) void g_void_t;
+typedef __attribute__((address_space(3))) void l_void_t;
+
+// one 16-B-per-lane LDS-DMA wave-instruction: lane j writes lds_base + 16 j (lds_base uniform)
+template <bool NTL>
+__device__ inline void glds16(const void* src, void* lds_base) {
+  __builtin_amdgcn_global_load_lds((g_void_t*)src, (l_void_t*)lds_base, 16, 0, NTL ? 2 : 0);
+}
+
+// LDS bytes of a kind-8 tile: NS slots of WAVES 16-row A chunks + the X chunk of every source
+// (+ 1 KiB dummy when the X pieces do not divide evenly among the waves)
+template <int NT, int NSRC, int NS, int KC, int WAVES>
+constexpr int dma_lds_bytes() {
+  return NS * (WAVES * 16 * KC * 8 + NSRC * KC * 16 * NT * 8) +
+         ((NSRC * KC * 16 * NT * 8 / 1024) % WAVES ? 1024 : 0);
+}
+
+template <int KC>
+__device__ inline int dma_sw(int i) { return KC >= 32 ? (i & 15) : ((i >> 1) & 7); }
+
+template <typename T, int NT, int NSRC, int NS, int KC, int WAVES, bool NTL>
+__global__ __launch_bounds__(64 * WAVES) void k_ax_dma(const T* __restrict__ A,
+                                                      const T* __restrict__ X0,
+                                                      const T* __restrict__ X1,
+                                                      const T* __restrict__ X2,
+                                                      T* __restrict__ P, int64_t m, int64_t n,
+                                                      int64_t chunks, int S, int gx, int xmap,
+                                                      const int* __restrict__ gate, int epoch,
+                                                      Pub pub) {
+  static_assert(sizeof(T) == 8, "f64 tile");
+  typedef MF<T> M;
+  typedef typename M::acc_t C;
+  constexpr int L = 16 * NT;
+  constexpr int NC = NT * NSRC;
+  constexpr int SLR = KC / 2;                       // 16-B slots per row of an A chunk
+  constexpr int AW = 16 * KC * (int)sizeof(T);      // one wave's A chunk (16 rows)
+  constexpr int NIA = AW / 1024;                    // its LDS-DMA instructions
+  constexpr int XS = KC * L * (int)sizeof(T);       // one source's X chunk
+  constexpr int XB = NSRC * XS;
+  constexpr int NXT = XB / 1024;                    // the block's X instructions per chunk
+  constexpr int NIX = (NXT + WAVES - 1) / WAVES;    // per wave (surplus ones load a dummy)
+  constexpr bool XDUP = NIX * WAVES != NXT;
+  constexpr int SLOT = WAVES * AW + XB;
+  constexpr int LDSB = NS * SLOT + (XDUP ? 1024 : 0);
+  constexpr int NI = NIA + NIX;                     // DMA instructions per wave and chunk
+  constexpr int D = NS - 1;                         // chunks in flight beyond the computed one
+  constexpr int JN = KC / 8;                        // ds_read_b128 of A per lane and chunk
+  constexpr int WAITN = (D - 1) * NI;
+  static_assert(KC == 16 || KC == 32 || KC == 64, "chunk of 16, 32 or 64 columns");
+  static_assert(XS % 1024 == 0 && AW % 1024 == 0, "whole 1-KiB pieces");
+  static_assert(D >= 1 && WAITN <= 63, "vmcnt range");
+  static_assert(LDSB <= 160 * 1024, "LDS");
+  __shared__ __attribute__((aligned(1024))) char lds[LDSB];
+
+  if (pub.host != nullptr && blockIdx.x == 0) {   // as k_ax_lds: workgroup 0 carries the packet
+    if (threadIdx.x == 0)
+      publish_packet(pub.s, pub.ns, pub.host, pub.host_seq, pub.seq, pub.s2, pub.off2, pub.n2,
+                     pub.s3, pub.off3, pub.n3);
+    return;
+  }
+  if (!gate_live(gate, epoch)) return;
+  int bx, by;
+  if (!ax_block(xmap, gx, S, bx, by, pub.host != nullptr ? 1 : 0)) return;
+
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int i = lane & 15, q = lane >> 4;
+  const int64_t row0 = (int64_t)bx * (16 * WAVES) + (int64_t)wave * 16;
+  const int64_t cb = chunks * by / S, ce = chunks * (by + 1) / S;
+  const int64_t nch = ce - cb;
+  if (nch <= 0) return;   // block-uniform
+
+  // A piece t of this wave: linear slot 64 t + lane of the [16][SLR] image
+  const T* asrc[NIA];
+#pragma unroll
+  for (int t = 0; t < NIA; ++t) {
+    const int ls = 64 * t + lane, ri = ls / SLR, p = ls % SLR;
+    int64_t r = row0 + ri;
+    r = r < m ? r : m - 1;
+    asrc[t] = A + r * n + cb * KC + 2 * (p ^ dma_sw<KC>(ri));
+  }
+  // X pieces: instruction tx = wave + WAVES r of the block covers 128-B units 8 tx .. 8 tx + 7
+  const T* xsrc[NIX];
+  int xdst[NIX];
+#pragma unroll
+  for (int r = 0; r < NIX; ++r) {
+    const int tx = wave + WAVES * r;
+    const int txc = tx % NXT;                        // surplus: a real piece into the dummy
+    const int pu = 8 * txc + (lane >> 3);
+    const int src = pu / (KC * NT), u = pu % (KC * NT);
+    const int k = u / NT;
+    const int us = u ^ ((k >> 1) & 1);
+    const T* xb = src == 0 ? X0 : (src == 1 ? X1 : X2);
+    xsrc[r] = xb + (cb * KC + us / NT) * L + (us % NT) * 16 + (lane & 7) * 2;
+    xdst[r] = tx < NXT ? WAVES * AW + tx * 1024 : -1;
+  }
+  const int64_t rot = ax_rot(xmap, bx, gx, nch);
+  auto issue = [&](int64_t c, int slot) {
+    c = (c < nch ? c : nch - 1) + rot;   // the walk starts at chunk rot (mod nch)
+    c = c >= nch ? c - nch : c;
+    char* sb = lds + slot * SLOT;
+#pragma unroll
+    for (int t = 0; t < NIA; ++t) glds16<NTL>(asrc[t] + c * KC, sb + wave * AW + t * 1024);
+#pragma unroll
+    for (int r = 0; r < NIX; ++r)
+      glds16<false>(xsrc[r] + c * KC * L, XDUP && xdst[r] < 0 ? lds + NS * SLOT : sb + xdst[r]);
+  };
+
+  C acc[NC];
+#pragma unroll
+  for (int c = 0; c < NC; ++c) acc[c] = C{};
+
+  // lane (i, q): A slots q + 4j of row i; X units of rows k = 2(q + 4j) + e, (k >> 1) & 1 = q & 1
+  const int aoff = wave * AW + i * (SLR * 16);
+  int asl[JN];
+#pragma unroll
+  for (int j = 0; j < JN; ++j) asl[j] = aoff + 16 * ((q + 4 * j) ^ dma_sw<KC>(i));
+  const int xoff = WAVES * AW + 8 * i;
+  auto compute = [&](int slot) {
+    const char* sb = lds + slot * SLOT;
+    d2_t av[JN];
+#pragma unroll
+    for (int j = 0; j < JN; ++j) av[j] = *reinterpret_cast<const d2_t*>(sb + asl[j]);
+#pragma unroll
+    for (int j = 0; j < JN; ++j)
+#pragma unroll
+      for (int e = 0; e < 2; ++e) {
+        const int k = 2 * (q + 4 * j) + e;
+#pragma unroll
+        for (int src = 0; src < NSRC; ++src)
+#pragma unroll
+          for (int nt = 0; nt < NT; ++nt) {
+            const int unit = (k * NT + nt) ^ (q & 1);
+            const T xv = *reinterpret_cast<const T*>(sb + xoff + src * XS + unit * 128);
+            acc[src * NT + nt] = M::mma(av[j][e], xv, acc[src * NT + nt]);
+          }
+      }
+  };
+
+#pragma unroll
+  for (int d = 0; d < D; ++d) issue(d, d);
+  int cs = 0;
+  for (int64_t c = 0; c < nch; ++c) {
+    // this wave's DMAs of chunk c have landed (the D - 1 younger chunks may be in flight) and
+    // its reads of chunk c - 1 are done; the barrier publishes both block-wide
+    asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(WAITN) : "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    const int is = cs == 0 ? NS - 1 : cs - 1;   // slot of chunk c - 1 = slot of chunk c + D
+    issue(c + D, is);
+    compute(cs);
+    cs = cs + 1 == NS ? 0 : cs + 1;
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the surplus re-issues, before exit
+
+#pragma unroll
+  for (int sr = 0; sr < NSRC; ++sr) {
+    T* pout = P + ((int64_t)sr * S + by) * m * L;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int64_t row = row0 + M::row(lane, r);
+      if (row < m) {
+#pragma unroll
+        for (int nt = 0; nt < NT; ++nt) pout[row * L + nt * 16 + i] = acc[sr * NT + nt][r];
+      }
+    }
+  }
+}
+
+template <typename T, int NT, int NSRC, int NS, int KC, int WAVES, bool NTL>
+static void ax_dma_go(const GemmPlan& p, int S, const T* A, const T* const* X, T* P,
+                      const int* gate, int epoch, hipStream_t st, Pub pub) {
+  if constexpr (sizeof(T) != 8 || dma_lds_bytes<NT, NSRC, NS, KC, WAVES>() > 160 * 1024) {
+    throw Error{GLX_E_INVALID, "A@X: this LDS-DMA tile does not fit (f64 only, 160 KiB of LDS)"};
+  } else {
+    const int gx = (int)cdiv(p.m, 16 * WAVES);
+    const int xmap = ax_xmap_flags(p, S);
+    const dim3 grid((unsigned)ax_grid(xmap, gx, S) + (pub.host ? 1u : 0u));
+    hipLaunchKernelGGL((k_ax_dma<T, NT, NSRC, NS, KC, WAVES, NTL>), grid, dim3(64 * WAVES), 0, st,
+                       A, X[0], X[1], X[2], P, p.m, p.n, p.n / KC, S, gx, xmap, gate, epoch, pub);
+  }
+}
+
+// kind 5 codes: 5 MT PF VPL WAVES; kind 8 (LDS-DMA): 8 NS KC/16 NTL WAVES
+// kind-8 code: 8 NS KC/16 NTL WAVES (LDS slots, chunk columns, non-temporal A, waves per block)
+template <typename T, int NT, int NSRC>
+static bool dma_code(const GemmPlan& p, int code, int S, const T* A, const T* const* X, T* P,
+                     const int* gate, int epoch, hipStream_t st, Pub pub) {
+  switch (code) {
+    case 84208: ax_dma_go<T, NT, NSRC, 4, 32, 8, false>(p, S, A, X, P, gate, epoch, st, pub); return true;
+    case 84218: ax_dma_go<T, NT, NSRC, 4, 32, 8, true>(p, S, A, X, P, gate, epoch, st, pub); return true;
+    case 83208: ax_dma_go<T, NT, NSRC, 3, 32, 8, false>(p, S, A, X, P, gate, epoch, st, pub); return true;
+    case 83218: ax_dma_go<T, NT, NSRC, 3, 32, 8, true>(p, S, A, X, P, gate, epoch, st, pub); return true;
+    case 82408: ax_dma_go<T, NT, NSRC, 2, 64, 8, false>(p, S, A, X, P, gate, epoch, st, pub); return true;
+    case 82418: ax_dma_go<T, NT, NSRC, 2, 64, 8, true>(p, S, A, X, P, gate, epoch, st, pub); return true;
+    case 88108: ax_dma_go<T, NT, NSRC, 8, 16, 8, false>(p, S, A, X, P, gate, epoch, st, pub); return true;
+    case 88118: ax_dma_go<T, NT, NSRC, 8, 16, 8, true>(p, S, A, X, P, gate, epoch, st, pub); return true;
+    case 85208: ax_dma_go<T, NT, NSRC, 5, 32, 4, false>(p, S, A, X, P, gate, epoch, st, pub); return true;
+    case 85218: ax_dma_go<T, NT, NSRC, 5, 32, 4, true>(p, S, A, X, P, gate, epoch, st, pub); return true;
+    case 84204: ax_dma_go<T, NT, NSRC, 4, 32, 4, false>(p, S, A, X, P, gate, epoch, st, pub); return true;
+    case 84214: ax_dma_go<T, NT, NSRC, 4, 32, 4, true>(p, S, A, X, P, gate, epoch, st, pub); return true;
+    default: return false;
+  }
+}
+
+int dma_lds_need(int code, int64_t l, int nsrc) {
+  const int ns = (code / 1000) % 10, kc = 16 * ((code / 100) % 10), waves = code % 10;
+  const int xb = nsrc * kc * (int)l * 8;
+  return ns * (waves * 16 * kc * 8 + xb) + ((xb / 1024) % waves ? 1024 : 0);
+}
+
+template <typename T>
+bool launch_ax_dma(const GemmPlan& p, int code, int nsrc, int S, const T* A, const T* const* X, T* P,
+                   const int* gate, int epoch, hipStream_t st, Pub pub) {
+  if (p.l == 16) {
+    if (nsrc == 1) return dma_code<T, 1, 1>(p, code, S, A, X, P, gate, epoch, st, pub);
+    if (nsrc == 2) return dma_code<T, 1, 2>(p, code, S, A, X, P, gate, epoch, st, pub);
+    return dma_code<T, 1, 3>(p, code, S, A, X, P, gate, epoch, st, pub);
+  }
+  if (nsrc == 1) return dma_code<T, 2, 1>(p, code, S, A, X, P, gate, epoch, st, pub);
+  if (nsrc == 2) return dma_code<T, 2, 2>(p, code, S, A, X, P, gate, epoch, st, pub);
+  return dma_code<T, 2, 3>(p, code, S, A, X, P, gate, epoch, st, pub);
+}
+template bool launch_ax_dma<double>(const GemmPlan&, int, int, int, const double*, const double* const*,
+                                    double*, const int*, int, hipStream_t, Pub);
+template bool launch_ax_dma<float>(const GemmPlan&, int, int, int, const float*, const float* const*,
+                                   float*, const int*, int, hipStream_t, Pub);
+
+}  // namespace glx

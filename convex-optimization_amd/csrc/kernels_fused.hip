@@ -31,13 +31,22 @@
 //     workgroup has published it), so slot (b+1) % 4 is never still being read.
 //   * counters: cnt[rg][b] gains P per launch; the host passes target = P * launch_count, so no
 //     counter is reset inside the launch. Every spin is bounded: on timeout the workgroup sets
-//     *err and carries on (its results are then wrong and the host raises).
+//     *err and carries on (its results are then wrong); glx_residual_gradient reads *err back
+//     and recomputes R and G with two passes when it is set.
 //
 // Outputs: Sraw = S (the finalize kernel forms r = S - b with the same subtraction, bit-identical
 // to the r used for G here) and Gs[rg] = the row group's part of G; the consumer sums the RG
 // slabs in slab order (slab_sum), so G is deterministic. All 256 workgroups must be resident at
-// once (they wait for each other): the host launches this only when the device has >= 256 CUs and
-// nothing else runs on the stream (launch_resgrad_ok).
+// once (they wait for each other): the host launches this only when the device has >= 256 CUs
+// (resgrad_device_ok), as a cooperative launch, which the runtime refuses when the grid cannot
+// be co-resident.
+//
+// XL mode relies on gfx950's write-through vector L1 and on the readers sharing the writer's XCD
+// L2: the granules are stored with workgroup-scope (plain) atomic stores, which the HIP memory
+// model does not make visible to other workgroups; on gfx950 they reach the XCD's L2, where the
+// readers' sc1 loads find them (measured correct at every tested shape, and a wrong placement
+// is caught: a granule never observed times the wait out, *err is set and the host recomputes).
+// GLX_RG_XCD=0 selects the placement-independent agent-scope form.
 #include <hip/hip_runtime.h>
 
 #include <cstdlib>
@@ -118,7 +127,7 @@ __global__ __launch_bounds__(kFThreads, kFPerCU) void k_resgrad(
     const double* __restrict__ A, const double* __restrict__ X, const double* __restrict__ B,
     double* __restrict__ Sraw, double* __restrict__ Gs, u64* Pg, u64* Rg, unsigned* xslot,
     unsigned epoch0,
-    int64_t m, int64_t n, int RG, int NB, int* err) {
+    int64_t m, int64_t n, int RG, int NB, int* err, unsigned spin_max) {
   __shared__ __attribute__((aligned(16))) double xs[kFW][kFCols * kFL];     // X slices
   __shared__ __attribute__((aligned(16))) double red[kFW / 2][kFBlk];        // wave partials
   __shared__ __attribute__((aligned(16))) double rb[kFBlk];                  // r of the block
@@ -185,7 +194,7 @@ __global__ __launch_bounds__(kFThreads, kFPerCU) void k_resgrad(
     while (!__all(gran_ok(x, tag))) {
       __builtin_amdgcn_s_sleep(1);
       x = get_gran(g);
-      if (++spins > (1u << 22)) {   // bounded: flag and continue with whatever is there
+      if (++spins > spin_max) {   // bounded: flag and continue with whatever is there
         if (lane == 0) {
           __hip_atomic_store(err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
           bad = 1;
@@ -434,23 +443,39 @@ static bool rg_xcd_mode(int64_t n) {
   return env != 0 && kFGrid / (n / kFPanel) == 8;
 }
 
-void launch_resgrad(const double* A, const double* X, const double* B, double* Sraw, double* Gs,
+bool launch_resgrad(const double* A, const double* X, const double* B, double* Sraw, double* Gs,
                     void* ws, unsigned launch_count, int64_t m, int64_t n, int* err, hipStream_t st) {
   const int64_t P = n / kFPanel, RG = kFGrid / P, NB = m / RG / kFRows;
   const RgLayout L = rg_layout(m, n);
   char* w = static_cast<char*>(ws);
   unsigned* xslot = reinterpret_cast<unsigned*>(w + L.xs);
-  const unsigned ep = (unsigned)((launch_count - 1) * NB);
-  if (rg_xcd_mode(n)) {
-    (void)hipMemsetAsync(xslot, 0, sizeof(unsigned) * 8 * 32, st);
-    hipLaunchKernelGGL(k_resgrad<true>, dim3((unsigned)(RG * P)), dim3(kFThreads), 0, st, A, X, B, Sraw,
-                       Gs, reinterpret_cast<u64*>(w + L.pg), reinterpret_cast<u64*>(w + L.rg), xslot,
-                       ep, m, n, (int)RG, (int)NB, err);
-  } else {
-    hipLaunchKernelGGL(k_resgrad<false>, dim3((unsigned)(RG * P)), dim3(kFThreads), 0, st, A, X, B, Sraw,
-                       Gs, reinterpret_cast<u64*>(w + L.pg), reinterpret_cast<u64*>(w + L.rg), xslot,
-                       ep, m, n, (int)RG, (int)NB, err);
+  unsigned ep = (unsigned)((launch_count - 1) * NB);
+  // spin bound of every hand-off wait (GLX_RG_SPIN = log2 of it, default 22; the tests force
+  // the error path with a tiny bound)
+  static const unsigned spin_max = [] {
+    const char* v = std::getenv("GLX_RG_SPIN");
+    const int lg = v && *v ? std::atoi(v) : 22;
+    return lg <= 0 ? 0u : (1u << (lg > 30 ? 30 : lg));
+  }();
+  unsigned smax = spin_max;
+  u64* pg = reinterpret_cast<u64*>(w + L.pg);
+  u64* rgp = reinterpret_cast<u64*>(w + L.rg);
+  int rgi = (int)RG, nbi = (int)NB;
+  void* args[] = {(void*)&A, (void*)&X, (void*)&B, (void*)&Sraw, (void*)&Gs, (void*)&pg, (void*)&rgp,
+                  (void*)&xslot, (void*)&ep, (void*)&m, (void*)&n, (void*)&rgi, (void*)&nbi,
+                  (void*)&err, (void*)&smax};
+  // cooperative launch: the workgroups wait for each other, so a grid that cannot be resident at
+  // once is refused at launch (the caller then runs two passes) instead of spinning
+  const bool xl = rg_xcd_mode(n);
+  if (xl) (void)hipMemsetAsync(xslot, 0, sizeof(unsigned) * 8 * 32, st);
+  const void* kern = xl ? reinterpret_cast<const void*>(k_resgrad<true>)
+                        : reinterpret_cast<const void*>(k_resgrad<false>);
+  const hipError_t e = hipLaunchCooperativeKernel(kern, dim3((unsigned)(RG * P)), dim3(kFThreads), args, 0, st);
+  if (e != hipSuccess) {
+    (void)hipGetLastError();
+    return false;
   }
+  return true;
 }
 
 // the granules must be zero before the first launch (launch_count 1)

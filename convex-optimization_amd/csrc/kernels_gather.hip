@@ -211,12 +211,11 @@ void launch_e_lists(const T* E, const uint8_t* zf, int64_t n, int64_t l, void* l
   if (!gather_ok(n, l)) throw Error{GLX_E_INVALID, "A e gather: needs l in {16, 32}, n < 65536"};
   const size_t lds = sizeof(unsigned short) * (size_t)n;
   auto go = [&](auto kern) {
-    static bool attr = false;
-    if (!attr) {   // the flagged-row list exceeds the default 64 KiB dynamic LDS only past n = 32768
+    // the flagged-row list exceeds the default 64 KiB of dynamic LDS only past n = 32768; the
+    // attribute is set on every such launch (cheap), since it is per kernel AND per device
+    if (lds > 64 * 1024)
       (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kern),
                                 hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024 - 64);
-      attr = true;
-    }
     hipLaunchKernelGGL(kern, dim3((unsigned)l), dim3(kGThreads), lds, st, E, zf, n,
                        static_cast<unsigned short*>(lists_ws), list_counts(lists_ws, n), skip);
   };

@@ -1,11 +1,13 @@
-// kernels_gemm.hip — the two dense contractions of the prox-grad iteration on CDNA4 (gfx950).
+// kernels_gemm.hip — the residual contraction of the prox-grad iteration on CDNA4 (gfx950) and
+// the launch planner of both dense products.
 //
 //   A @ X   (reference: gl_ProxGD_primal.py:25,61,129 — `A @ x`):   M = m, K = n, N = l
 //   A^T R   (reference: gl_ProxGD_primal.py:129 — `A.T @ (...)`):  M = n, K = m, N = l
+//           (kernels in kernels_atr.hip; the LDS-DMA A @ X tile in kernels_axdma.hip)
 //
-// Both stream A (m x n, row-major, 1 GiB at the north-star size) once per launch. A^T R (one
-// right-hand side, l/4 flop/B in fp64) is HBM-bound; A @ X batches 2-3 right-hand sides per
-// pass (the solver's line-search trial and the next gradient residual), which makes it
+// Both stream A (m x n, row-major, 1 GiB at the north-star size) once per launch. A^T R and
+// A @ X with one right-hand side (l/4 flop/B in fp64) are HBM-bound; A @ X batching 2-3
+// right-hand sides per pass (the line-search trial and the next gradient residual) is
 // MFMA-bound at l = 32 (v_mfma_f64_16x16x4f64 / v_mfma_f32_16x16x4f32).
 //
 // MFMA 16x16x4 operand maps (cdna_hip_programming.md §3): lane l supplies A_op[l&15][l>>4] and
@@ -17,13 +19,9 @@
 //   kind 1/2 — X gathered by every wave into registers (2: quad loads + ds_bpermute);
 //   kind 5   — X staged once per block in LDS, natural [k][col] order, conflict-free padding;
 //              the default (f64: 8-wave blocks, f32: 4-wave blocks with a 3-deep ring);
-//   kind 6/7 — kind 5 with X software-pipelined / a barrier every 2-4 chunks (measured slower
-//              or equal, kept selectable for sweeps: DESIGN.md, tuning record).
-// A^T R: the K index (rows of A) is on l>>4 and the 16-wide M index (columns of A) on l&15,
-// so lanes 0..15 read consecutive columns: a lane loads 4 consecutive columns (32 B f64 /
-// 16 B f32) of one row and feeds 4 MFMAs whose output rows are columns c0+4i+e. With one K
-// split the ProxGD / FISTA line-search trial runs in its epilogue (k_atr_prox, k_atr_fista).
-//
+//   kind 8   — (f64) A AND X staged in LDS by LDS-DMA, whole 256-B row pieces per wave
+//              instruction (k_ax_dma). Kinds 6/7 (pipelined X, sparse barriers) measured slower
+//              in round 1 and were removed (tuning record).
 // All main loops keep their register rings predicate-free and consume each ring slot in place
 // (no vmcnt(0) drain at the back edge). Split-K partials (waves through LDS, workgroups as
 // slabs) are summed in a fixed order, so every result is deterministic run to run.
@@ -32,95 +30,10 @@
 #include <cstdlib>
 #include <string>
 
-#include "glx.h"
-#include "glx_device.h"
+#include "glx_mfma.h"
 
 namespace glx {
 
-typedef double d2_t __attribute__((ext_vector_type(2)));
-typedef double d4_t __attribute__((ext_vector_type(4)));
-typedef float f4_t __attribute__((ext_vector_type(4)));
-
-template <typename T> struct MF;
-template <> struct MF<double> {
-  typedef d4_t acc_t;
-  typedef d2_t vec_t;
-  static constexpr int E = 2;
-  __device__ static inline acc_t mma(double a, double b, acc_t c) {
-    return __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, c, 0, 0, 0);
-  }
-  __device__ static inline int row(int lane, int r) { return (lane >> 4) + 4 * r; }
-};
-template <> struct MF<float> {
-  typedef f4_t acc_t;
-  typedef f4_t vec_t;
-  static constexpr int E = 4;
-  __device__ static inline acc_t mma(float a, float b, acc_t c) {
-    return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
-  }
-  __device__ static inline int row(int lane, int r) { return ((lane >> 4) << 2) + r; }
-};
-
-template <typename V>
-__device__ inline V bpermute_vec(V v, int src_lane) {
-  constexpr int ND = sizeof(V) / 4;
-  union U { V v; int d[ND]; };
-  U in, out;
-  in.v = v;
-#pragma unroll
-  for (int j = 0; j < ND; ++j) out.d[j] = __builtin_amdgcn_ds_bpermute(src_lane << 2, in.d[j]);
-  return out.v;
-}
-
-// ------------------------------------------------------------------------------------------
-// A @ X on MFMA: block = 4 waves; a wave owns MT 16-row tiles x NT 16-col tiles over its share
-// of the K chunks (CK = 4E values of k per chunk); the block's 4 waves split the block's chunks;
-// blockIdx.y = K split. PF chunks are kept in flight per wave (a register ring, statically
-// indexed). P[blockIdx.y][m][16*NT] receives the block's partial.
-// ------------------------------------------------------------------------------------------
-__device__ inline bool gate_live(const int* gate, int epoch) { return gate == nullptr || *gate == epoch; }
-
-template <typename T, bool NTL>
-__device__ inline typename MF<T>::vec_t load_vec(const T* p) {
-  typedef typename MF<T>::vec_t V;
-  if constexpr (NTL) return __builtin_nontemporal_load(reinterpret_cast<const V*>(p));
-  else return *reinterpret_cast<const V*>(p);
-}
-
-// NSRC right-hand sides X0..X2 (each n x 16NT) share every loaded A fragment: the batched
-// products of the next iteration (e.g. A @ [z | p_thr]) cost one pass over A.
-// P[src][S][m][16NT]. NTL: A streamed with non-temporal loads (keeps X resident in L2).
-// Logical (row block, K split) of a 1-D launch. xmap = 1 groups K splits by XCD: blocks are
-// observed to be dealt round-robin over the 8 XCDs (lin % 8 shares an L2), so split s is
-// given to XCD group s (S | 8: 8/S XCDs per split; 8 | S: S/8 splits per XCD). Each XCD's L2
-// then holds only its own slice of X instead of all of it. Placement is a speed matter only:
-// any other placement computes the same result.
-__device__ inline bool ax_block(int xmap, int gx, int S, int& bx, int& by, int shift = 0) {
-  const int lin = (int)blockIdx.x - shift;   // shift 1: workgroup 0 carries the scalar packet
-  if (xmap) {
-    const int xcd = lin & 7, slot = lin >> 3;
-    if (S <= 8) {
-      const int G = 8 / S;
-      by = xcd / G;
-      bx = slot * G + (xcd % G);
-    } else {
-      by = xcd + 8 * (slot / gx);
-      bx = slot % gx;
-    }
-    return bx < gx && by < S;
-  }
-  bx = lin % gx;
-  by = lin / gx;
-  return true;
-}
-static inline int ax_grid(int xmap, int gx, int S) {
-  if (xmap && S <= 8) {
-    const int G = 8 / S;
-    return ((gx + G - 1) / G) * G * S;
-  }
-  return gx * S;
-}
-static inline int ax_xmap_ok(int S) { return (S <= 8) ? (8 % S == 0) : (S % 8 == 0); }
 
 template <typename T, int MT, int NT, int NSRC, int PF, bool QUAD, bool NTL, int VPL>
 __global__ __launch_bounds__(256) void k_ax_mfma(const T* __restrict__ A, const T* __restrict__ X0,
@@ -343,6 +256,13 @@ __global__ __launch_bounds__(64 * WAVES) void k_ax_lds(const T* __restrict__ A,
   const int64_t cb = chunks * by / S, ce = chunks * (by + 1) / S;
   const int64_t nch = ce - cb;
   if (nch <= 0) return;   // block-uniform
+  const int64_t rot = ax_rot(xmap, bx, gx, nch);
+  // chunk `off` of the walk (clamped past the end: a re-read of the last one, see below) is
+  // chunk (off + rot) mod nch of the block's K range
+  auto kch = [&](int64_t off) -> int64_t {
+    off = (off < nch ? off : nch - 1) + rot;
+    return off >= nch ? off - nch : off;
+  };
 
   const T* ap[MT];
 #pragma unroll
@@ -379,13 +299,13 @@ __global__ __launch_bounds__(64 * WAVES) void k_ax_lds(const T* __restrict__ A,
   V a[PF][MT][VPL];
   V xr[PF][XPT];
   auto load_x = [&](V (&dst)[XPT], int64_t off) {
-    off = off < nch ? off : nch - 1;
+    off = kch(off);
 #pragma unroll
     for (int j = 0; j < XPT; ++j)
       if (XFULL || xon[j]) dst[j] = *reinterpret_cast<const V*>(xg[j] + off * CK * L);
   };
   auto load_a = [&](V (&dst)[MT][VPL], int64_t off) {
-    off = off < nch ? off : nch - 1;
+    off = kch(off);
 #pragma unroll
     for (int mt = 0; mt < MT; ++mt)
 #pragma unroll
@@ -422,7 +342,7 @@ __global__ __launch_bounds__(64 * WAVES) void k_ax_lds(const T* __restrict__ A,
   };
   // SP: does chunk `off` hold a flagged row of X0 (CK flag bytes, OR-ed as words)?
   auto flag_of = [&](int64_t off) -> unsigned {
-    off = off < nch ? off : nch - 1;
+    off = kch(off);
     const unsigned* fp = reinterpret_cast<const unsigned*>(sf + (cb + off) * CK);
     unsigned f = 0;
 #pragma unroll
@@ -453,8 +373,7 @@ __global__ __launch_bounds__(64 * WAVES) void k_ax_lds(const T* __restrict__ A,
       load_x(xr[p], c + PF);       // xr[p] (X(c)) has been in LDS since chunk c-1
       T xv[NC][EL];
       read_x(slot, xv);
-      int64_t off = c + PF;
-      off = off < nch ? off : nch - 1;
+      const int64_t off = kch(c + PF);
       if constexpr (SP) {
         // two straight-line bodies, so an active chunk runs exactly the dense schedule
         if (fl[p] != 0) {
@@ -521,726 +440,6 @@ __global__ __launch_bounds__(64 * WAVES) void k_ax_lds(const T* __restrict__ A,
   }
 }
 
-// ------------------------------------------------------------------------------------------
-// A @ X, kind 7: kind 5 with a barrier every BAR chunks instead of every chunk. X(c+BAR) is
-// written at chunk c into slot (c+BAR) % (2 BAR) and read at chunk c+BAR: a barrier ends every
-// BAR chunks, so one lies between each write and its read (RAW), and between the last read of
-// a slot (chunk c+BAR-2BAR) and its next write (chunk c) (WAR). Waves then drift up to BAR
-// chunks apart, which absorbs their different A-load latencies. PF (A and X register rings) is a
-// multiple of BAR and > BAR.
-// ------------------------------------------------------------------------------------------
-template <typename T, int MT, int NT, int NSRC, int PF, int VPL, int WAVES, int BAR>
-__global__ __launch_bounds__(64 * WAVES) void k_ax_lds3(const T* __restrict__ A,
-                                                       const T* __restrict__ X0,
-                                                       const T* __restrict__ X1,
-                                                       const T* __restrict__ X2,
-                                                       T* __restrict__ P, int64_t m, int64_t n,
-                                                       int64_t chunks, int S, int gx, int xmap,
-                                                       const int* __restrict__ gate, int epoch) {
-  typedef MF<T> M;
-  typedef typename M::vec_t V;
-  typedef typename M::acc_t C;
-  constexpr int E = M::E;
-  constexpr int EL = VPL * E;
-  constexpr int CK = 4 * EL;
-  constexpr int L = 16 * NT;
-  constexpr int NC = NT * NSRC;
-  constexpr int LP = L + (sizeof(T) == 8 ? 4 : 2);
-  constexpr bool W16 = (LP * sizeof(T)) % 16 == 0;
-  constexpr int XCH = NSRC * CK * LP;
-  constexpr int NTHR = 64 * WAVES;
-  constexpr int XV = NSRC * CK * L / E;
-  constexpr int XPT = (XV + NTHR - 1) / NTHR;
-  constexpr bool XFULL = (XV % NTHR) == 0;
-  constexpr int VPR = L / E;
-  constexpr int NSLOT = 2 * BAR;
-  static_assert(PF % BAR == 0 && PF > BAR, "ring depth: a multiple of BAR, more than BAR");
-  __shared__ __attribute__((aligned(16))) T xs[NSLOT][XCH];
-  if (!gate_live(gate, epoch)) return;
-  int bx, by;
-  if (!ax_block(xmap, gx, S, bx, by)) return;
-
-  const int lane = threadIdx.x & 63;
-  const int wave = threadIdx.x >> 6;
-  const int i = lane & 15, q = lane >> 4;
-  const int64_t row0 = (int64_t)bx * (16 * MT * WAVES) + (int64_t)wave * (16 * MT);
-  const int64_t cb = chunks * by / S, ce = chunks * (by + 1) / S;
-  const int64_t nch = ce - cb;
-  if (nch <= 0) return;   // block-uniform
-
-  const T* ap[MT];
-#pragma unroll
-  for (int mt = 0; mt < MT; ++mt) {
-    int64_t r = row0 + mt * 16 + i;
-    r = r < m ? r : m - 1;
-    ap[mt] = A + r * n + cb * CK + (int64_t)q * EL;
-  }
-  const T* xg[XPT];
-  int xo[XPT];
-  bool xon[XPT];
-#pragma unroll
-  for (int j = 0; j < XPT; ++j) {
-    const int v = threadIdx.x + NTHR * j;
-    xon[j] = XFULL || v < XV;
-    const int vv = xon[j] ? v : 0;
-    const int src = vv / (CK * VPR), rem = vv % (CK * VPR);
-    const int k = rem / VPR, c = (rem % VPR) * E;
-    const T* xb = src == 0 ? X0 : (src == 1 ? X1 : X2);
-    xg[j] = xb + (cb * CK + k) * L + c;
-    xo[j] = src * CK * LP + k * LP + c;
-  }
-
-  C acc[MT][NC];
-#pragma unroll
-  for (int mt = 0; mt < MT; ++mt)
-#pragma unroll
-    for (int c = 0; c < NC; ++c) acc[mt][c] = C{};
-
-  V a[PF][MT][VPL];
-  V xr[PF][XPT];
-  auto load_x = [&](V (&dst)[XPT], int64_t off) {
-    off = off < nch ? off : nch - 1;
-#pragma unroll
-    for (int j = 0; j < XPT; ++j)
-      if (XFULL || xon[j]) dst[j] = *reinterpret_cast<const V*>(xg[j] + off * CK * L);
-  };
-  auto load_a_tile = [&](V (&dst)[VPL], int mt, int64_t off) {
-    off = off < nch ? off : nch - 1;
-#pragma unroll
-    for (int v = 0; v < VPL; ++v) dst[v] = load_vec<T, false>(ap[mt] + off * CK + v * E);
-  };
-  auto put_x = [&](int slot, const V (&src)[XPT]) {
-#pragma unroll
-    for (int j = 0; j < XPT; ++j)
-      if (XFULL || xon[j]) lds_put<T, W16>(&xs[slot][xo[j]], src[j]);
-  };
-  auto read_x = [&](int slot, T (&dst)[NC][EL]) {
-#pragma unroll
-    for (int cc = 0; cc < NC; ++cc) {
-      const int src = cc / NT, nt = cc % NT;
-      const T* xp = &xs[slot][src * CK * LP + q * EL * LP + nt * 16 + i];
-#pragma unroll
-      for (int e = 0; e < EL; ++e) dst[cc][e] = xp[e * LP];
-    }
-  };
-  auto mma_tile = [&](int mt, const V (&av)[VPL], const T (&x)[NC][EL]) {
-#pragma unroll
-    for (int v = 0; v < VPL; ++v)
-#pragma unroll
-      for (int e = 0; e < E; ++e)
-#pragma unroll
-        for (int cc = 0; cc < NC; ++cc)
-          acc[mt][cc] = M::mma(av[v][e], x[cc][v * E + e], acc[mt][cc]);
-  };
-
-  // prologue: rings hold chunks 0..PF-1; X(0..BAR-1) staged into slots 0..BAR-1, their X
-  // registers refilled with X(PF..PF+BAR-1)
-#pragma unroll
-  for (int p = 0; p < PF; ++p) {
-    load_x(xr[p], p);
-#pragma unroll
-    for (int mt = 0; mt < MT; ++mt) load_a_tile(a[p][mt], mt, p);
-  }
-#pragma unroll
-  for (int p = 0; p < BAR; ++p) {
-    put_x(p, xr[p]);
-    load_x(xr[p], PF + p);
-  }
-  __syncthreads();
-
-  int64_t c0 = 0;
-  for (; c0 + PF <= nch; c0 += PF) {
-#pragma unroll
-    for (int p = 0; p < PF; ++p) {
-      const int64_t c = c0 + p;
-      put_x((int)((c + BAR) % NSLOT), xr[(p + BAR) % PF]);   // X(c+BAR); past the end harmless
-      load_x(xr[(p + BAR) % PF], c + BAR + PF);
-      T xv[NC][EL];
-      read_x((int)(c % NSLOT), xv);
-#pragma unroll
-      for (int mt = 0; mt < MT; ++mt) {
-        mma_tile(mt, a[p][mt], xv);
-        load_a_tile(a[p][mt], mt, c + PF);
-      }
-      if (p % BAR == BAR - 1) __syncthreads();
-    }
-  }
-  // tail (fewer than PF chunks): end every chunk with a barrier, which keeps both rules
-#pragma unroll
-  for (int p = 0; p < PF - 1; ++p) {
-    const int64_t c = c0 + p;
-    if (c < nch) {
-      if (c + BAR < nch) put_x((int)((c + BAR) % NSLOT), xr[(p + BAR) % PF]);
-      T xv[NC][EL];
-      read_x((int)(c % NSLOT), xv);
-#pragma unroll
-      for (int mt = 0; mt < MT; ++mt) mma_tile(mt, a[p][mt], xv);
-      __syncthreads();
-    }
-  }
-
-#pragma unroll
-  for (int sr = 0; sr < NSRC; ++sr) {
-    T* pout = P + ((int64_t)sr * S + by) * m * L;
-#pragma unroll
-    for (int mt = 0; mt < MT; ++mt)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int64_t row = row0 + mt * 16 + M::row(lane, r);
-        if (row < m) {
-#pragma unroll
-          for (int nt = 0; nt < NT; ++nt) pout[row * L + nt * 16 + i] = acc[mt][sr * NT + nt][r];
-        }
-      }
-  }
-}
-
-// ------------------------------------------------------------------------------------------
-// A @ X, kind 6: kind 5 with the X operand software-pipelined through a 3-slot LDS ring. At
-// chunk c a wave writes X(c+2) (loaded PF-2 chunks earlier) into slot (c+2) % 3, reads X(c+1)
-// (written at chunk c-1, visible since the last barrier) from slot (c+1) % 3 into the second
-// of two register sets, and runs chunk c's MFMAs on the first set, so the MFMAs after a barrier
-// never wait on LDS latency (kind 5: all waves read X(c) right after the barrier, an MFMA-pipe
-// bubble per chunk). One barrier per chunk; the slot written at chunk c was last read at chunk
-// c-2, before the barrier of chunk c-2. PF is the depth of both register rings (even, >= 4).
-// ------------------------------------------------------------------------------------------
-template <typename T, int MT, int NT, int NSRC, int PF, int VPL, int WAVES>
-__global__ __launch_bounds__(64 * WAVES) void k_ax_lds2(const T* __restrict__ A,
-                                                       const T* __restrict__ X0,
-                                                       const T* __restrict__ X1,
-                                                       const T* __restrict__ X2,
-                                                       T* __restrict__ P, int64_t m, int64_t n,
-                                                       int64_t chunks, int S, int gx, int xmap,
-                                                       const int* __restrict__ gate, int epoch) {
-  typedef MF<T> M;
-  typedef typename M::vec_t V;
-  typedef typename M::acc_t C;
-  constexpr int E = M::E;
-  constexpr int EL = VPL * E;
-  constexpr int CK = 4 * EL;
-  constexpr int L = 16 * NT;
-  constexpr int NC = NT * NSRC;
-  constexpr int LP = L + (sizeof(T) == 8 ? 4 : 2);
-  constexpr bool W16 = (LP * sizeof(T)) % 16 == 0;
-  constexpr int XCH = NSRC * CK * LP;
-  constexpr int NTHR = 64 * WAVES;
-  constexpr int XV = NSRC * CK * L / E;
-  constexpr int XPT = (XV + NTHR - 1) / NTHR;
-  constexpr bool XFULL = (XV % NTHR) == 0;
-  constexpr int VPR = L / E;
-  static_assert(PF >= 4 && PF % 2 == 0, "X(c+2) is written at chunk c; register sets alternate");
-  __shared__ __attribute__((aligned(16))) T xs[3][XCH];
-  if (!gate_live(gate, epoch)) return;
-  int bx, by;
-  if (!ax_block(xmap, gx, S, bx, by)) return;
-
-  const int lane = threadIdx.x & 63;
-  const int wave = threadIdx.x >> 6;
-  const int i = lane & 15, q = lane >> 4;
-  const int64_t row0 = (int64_t)bx * (16 * MT * WAVES) + (int64_t)wave * (16 * MT);
-  const int64_t cb = chunks * by / S, ce = chunks * (by + 1) / S;
-  const int64_t nch = ce - cb;
-  if (nch <= 0) return;   // block-uniform
-
-  const T* ap[MT];
-#pragma unroll
-  for (int mt = 0; mt < MT; ++mt) {
-    int64_t r = row0 + mt * 16 + i;
-    r = r < m ? r : m - 1;
-    ap[mt] = A + r * n + cb * CK + (int64_t)q * EL;
-  }
-  const T* xg[XPT];
-  int xo[XPT];
-  bool xon[XPT];
-#pragma unroll
-  for (int j = 0; j < XPT; ++j) {
-    const int v = threadIdx.x + NTHR * j;
-    xon[j] = XFULL || v < XV;
-    const int vv = xon[j] ? v : 0;
-    const int src = vv / (CK * VPR), rem = vv % (CK * VPR);
-    const int k = rem / VPR, c = (rem % VPR) * E;
-    const T* xb = src == 0 ? X0 : (src == 1 ? X1 : X2);
-    xg[j] = xb + (cb * CK + k) * L + c;
-    xo[j] = src * CK * LP + k * LP + c;
-  }
-
-  C acc[MT][NC];
-#pragma unroll
-  for (int mt = 0; mt < MT; ++mt)
-#pragma unroll
-    for (int c = 0; c < NC; ++c) acc[mt][c] = C{};
-
-  V a[PF][MT][VPL];
-  V xr[PF][XPT];
-  T xv[2][NC][EL];
-  auto load_x = [&](V (&dst)[XPT], int64_t off) {
-    off = off < nch ? off : nch - 1;
-#pragma unroll
-    for (int j = 0; j < XPT; ++j)
-      if (XFULL || xon[j]) dst[j] = *reinterpret_cast<const V*>(xg[j] + off * CK * L);
-  };
-  auto load_a_tile = [&](V (&dst)[VPL], int mt, int64_t off) {
-    off = off < nch ? off : nch - 1;
-#pragma unroll
-    for (int v = 0; v < VPL; ++v) dst[v] = load_vec<T, false>(ap[mt] + off * CK + v * E);
-  };
-  auto put_x = [&](int slot, const V (&src)[XPT]) {
-#pragma unroll
-    for (int j = 0; j < XPT; ++j)
-      if (XFULL || xon[j]) lds_put<T, W16>(&xs[slot][xo[j]], src[j]);
-  };
-  auto read_x = [&](int slot, T (&dst)[NC][EL]) {
-#pragma unroll
-    for (int cc = 0; cc < NC; ++cc) {
-      const int src = cc / NT, nt = cc % NT;
-      const T* xp = &xs[slot][src * CK * LP + q * EL * LP + nt * 16 + i];
-#pragma unroll
-      for (int e = 0; e < EL; ++e) dst[cc][e] = xp[e * LP];
-    }
-  };
-  auto mma_tile = [&](int mt, const V (&av)[VPL], const T (&x)[NC][EL]) {
-#pragma unroll
-    for (int v = 0; v < VPL; ++v)
-#pragma unroll
-      for (int e = 0; e < E; ++e)
-#pragma unroll
-        for (int cc = 0; cc < NC; ++cc)
-          acc[mt][cc] = M::mma(av[v][e], x[cc][v * E + e], acc[mt][cc]);
-  };
-
-  // prologue: rings hold chunks 0..PF-1; X(0), X(1) staged; X registers of those two slots
-  // refilled with X(PF), X(PF+1); X(0) read into register set 0
-#pragma unroll
-  for (int p = 0; p < PF; ++p) {
-    load_x(xr[p], p);
-#pragma unroll
-    for (int mt = 0; mt < MT; ++mt) load_a_tile(a[p][mt], mt, p);
-  }
-  put_x(0, xr[0]);
-  put_x(1, xr[1]);
-  load_x(xr[0], PF);
-  load_x(xr[1], PF + 1);
-  __syncthreads();
-  read_x(0, xv[0]);
-
-  int64_t c0 = 0;
-  for (; c0 + PF <= nch; c0 += PF) {
-#pragma unroll
-    for (int p = 0; p < PF; ++p) {
-      const int64_t c = c0 + p;
-      const int sw = (int)((c + 2) % 3), sr = (int)((c + 1) % 3);
-      put_x(sw, xr[(p + 2) % PF]);             // X(c+2); past the end: a harmless re-write
-      load_x(xr[(p + 2) % PF], c + 2 + PF);
-      read_x(sr, xv[(p + 1) & 1]);             // X(c+1) for the next chunk
-#pragma unroll
-      for (int mt = 0; mt < MT; ++mt) {
-        mma_tile(mt, a[p][mt], xv[p & 1]);
-        load_a_tile(a[p][mt], mt, c + PF);     // consumed in place, refilled in place
-      }
-      __syncthreads();
-    }
-  }
-#pragma unroll
-  for (int p = 0; p < PF - 1; ++p) {   // tail: fewer than PF chunks, data already in the rings
-    const int64_t c = c0 + p;
-    if (c < nch) {
-      if (c + 2 < nch) put_x((int)((c + 2) % 3), xr[(p + 2) % PF]);
-      if (c + 1 < nch) read_x((int)((c + 1) % 3), xv[(p + 1) & 1]);
-#pragma unroll
-      for (int mt = 0; mt < MT; ++mt) mma_tile(mt, a[p][mt], xv[p & 1]);
-      __syncthreads();
-    }
-  }
-
-#pragma unroll
-  for (int sr = 0; sr < NSRC; ++sr) {
-    T* pout = P + ((int64_t)sr * S + by) * m * L;
-#pragma unroll
-    for (int mt = 0; mt < MT; ++mt)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int64_t row = row0 + mt * 16 + M::row(lane, r);
-        if (row < m) {
-#pragma unroll
-          for (int nt = 0; nt < NT; ++nt) pout[row * L + nt * 16 + i] = acc[mt][sr * NT + nt][r];
-        }
-      }
-  }
-}
-
-// ------------------------------------------------------------------------------------------
-// A^T R on MFMA: a wave owns 64 columns of A (= 64 rows of G) x NT 16-col tiles of G.
-//   WL = 0: a block = one 64-column panel, its 4 waves split the block's rows (LDS-reduced);
-//   WL = 1: a block = four adjacent panels (256 columns) sharing one row range, so the four
-//           waves read the same R fragments (L1 hits) and write their slabs directly.
-// blockIdx.y = row split. Needs n % 64 == 0 (n % 256 for WL = 1), m % 4 == 0.
-// Gp[split][n][16*NT].
-// ------------------------------------------------------------------------------------------
-// A lane (i, q) of a row step feeds the four MFMAs e = 0..3 with row q of A at panel columns
-// atr_col(i, e); MFMA e's output row i is then G row col0 + atr_col(i, e). f64: columns
-// {2i, 2i+1} and {32 + 2i, 33 + 2i}, so each of the two 16-B loads of a wave-instruction covers
-// 256 contiguous bytes of each of its four rows (the streaming probe, scripts/stream_probe.hip:
-// 6.1 TB/s for the 4i..4i+3 form, whose loads leave every other 16 B of a 512-B span to the
-// next instruction, against 6.3-7.1 TB/s for contiguous 256/512-B pieces). f32: one 16-B load
-// already covers columns 4i..4i+3.
-template <typename T>
-__device__ inline int atr_col(int i, int e) {
-  if constexpr (sizeof(T) == 8) return (e >> 1) * 32 + 2 * i + (e & 1);
-  else return 4 * i + e;
-}
-template <typename T, bool NTL> struct Load4;
-template <bool NTL> struct Load4<double, NTL> {
-  __device__ static inline void go(const double* p, double (&a)[4]) {   // p = row + col0 + 2i
-    const d2_t v0 = load_vec<double, NTL>(p);
-    const d2_t v1 = load_vec<double, NTL>(p + 32);
-    a[0] = v0[0]; a[1] = v0[1]; a[2] = v1[0]; a[3] = v1[1];
-  }
-};
-template <bool NTL> struct Load4<float, NTL> {
-  __device__ static inline void go(const float* p, float (&a)[4]) {
-    const f4_t v = load_vec<float, NTL>(p);
-    a[0] = v[0]; a[1] = v[1]; a[2] = v[2]; a[3] = v[3];
-  }
-};
-
-// One 64-column panel of A^T R over this wave's (WL 1: this block's) row range; returns the
-// panel's first column. acc[e][nt] holds rows col0 + atr_col(M::row(lane, r), e). For WL 0 the
-// block's four waves split the rows (K) and are summed through LDS in the fixed order
-// ((w0 + w1) + w2) + w3; afterwards wave w holds the complete sum for e == w in acc[w][*]
-// (the other e of a wave are partial and unused), so the four waves share the epilogue.
-// (pbx, pby) = (panel, K split) of this block: (blockIdx.x, blockIdx.y) for k_atr_mfma.
-template <typename T, int NT, int PF, int WL, bool NTL>
-__device__ inline int64_t atr_panel(const T* __restrict__ A, const T* __restrict__ R, int64_t m,
-                                    int64_t n, int S, typename MF<T>::acc_t (&acc)[4][NT],
-                                    int64_t pbx, int64_t pby) {
-  typedef MF<T> M;
-  typedef typename M::acc_t C;
-  constexpr int L = 16 * NT;
-  __shared__ C red[WL == 0 ? 4 : 1][WL == 0 ? 4 * NT : 1][64];   // [wave][e * NT + nt][lane]
-
-  const int lane = threadIdx.x & 63;
-  const int wave = threadIdx.x >> 6;
-  const int i = lane & 15, q = lane >> 4;
-  const int64_t col0 = WL == 0 ? pbx * 64 : pbx * 256 + wave * 64;
-  const int64_t steps = m / 4;
-  const int64_t W = WL == 0 ? (int64_t)S * 4 : (int64_t)S;
-  const int64_t w = WL == 0 ? pby * 4 + wave : pby;
-  const int64_t sb = steps * w / W, se = steps * (w + 1) / W;
-
-  const T* ap = A + (sb * 4 + q) * n + col0 + atr_col<T>(i, 0);
-  const T* rp = R + (sb * 4 + q) * L + i;
-
-#pragma unroll
-  for (int e = 0; e < 4; ++e)
-#pragma unroll
-    for (int nt = 0; nt < NT; ++nt) acc[e][nt] = C{};
-
-  // Ring of PF row steps, consumed in place: a step's fragments feed its MFMAs and are then
-  // refilled with step s + PF in the same registers, at a clamped offset so that the main
-  // loop carries no load predicates (a predicate or a register copy at the loop's back edge
-  // makes the compiler drain vmcnt to 0 there). Lookahead = PF - 1 steps.
-  const int64_t nst = se - sb;
-  T a[PF][4], rb[PF][NT];
-  auto ld = [&](int p, int64_t off) {
-    off = off < nst ? off : nst - 1;
-    Load4<T, NTL>::go(ap + off * 4 * n, a[p]);
-#pragma unroll
-    for (int nt = 0; nt < NT; ++nt) rb[p][nt] = rp[off * 4 * L + nt * 16];
-  };
-  auto mma_step = [&](int p) {
-#pragma unroll
-    for (int e = 0; e < 4; ++e)
-#pragma unroll
-      for (int nt = 0; nt < NT; ++nt) acc[e][nt] = M::mma(a[p][e], rb[p][nt], acc[e][nt]);
-  };
-  if (nst > 0) {
-#pragma unroll
-    for (int p = 0; p < PF; ++p) ld(p, p);
-    int64_t s0 = 0;
-    for (; s0 + PF <= nst; s0 += PF) {
-#pragma unroll
-      for (int p = 0; p < PF; ++p) {
-        mma_step(p);
-        ld(p, s0 + p + PF);
-      }
-    }
-#pragma unroll
-    for (int p = 0; p < PF - 1; ++p)
-      if (s0 + p < nst) mma_step(p);
-  }
-
-  if (WL == 0) {
-#pragma unroll
-    for (int e = 0; e < 4; ++e)
-#pragma unroll
-      for (int nt = 0; nt < NT; ++nt) red[wave][e * NT + nt][lane] = acc[e][nt];
-    __syncthreads();
-#pragma unroll
-    for (int nt = 0; nt < NT; ++nt) {
-      C v = red[0][wave * NT + nt][lane];
-#pragma unroll
-      for (int s = 1; s < 4; ++s) v += red[s][wave * NT + nt][lane];
-#pragma unroll
-      for (int e = 0; e < 4; ++e)
-        if (e == wave) acc[e][nt] = v;   // static register index; e == wave selects one
-    }
-  }
-  return col0;
-}
-
-// K splits of a fused A^T R (WL 0, S > 1): a 1-D grid of n/64 panels x S splits (+ the
-// publisher). Every block stores its panel rows (wave w: rows e == w) into slab `split` of Gp;
-// the block that arrives last on its panel's counter sums the S slabs in slab order (the
-// order of slab_sum, so G is bit-identical to the unfused path) and runs the trial epilogue.
-// Hand-off: sc1 (agent-scope) stores, vmcnt(0), a workgroup barrier, one agent-scope add per
-// block; the last arriver loads with sc1 after a barrier (MI355X_MICROARCH.md "Valid forms",
-// row 1). Returns false in the blocks that are not last (they only join the grid reduction).
-// *slot = this block's grid-reduction slot, fixed whatever the arrival order: the panel's
-// trial sums (last arriver) at `panel`, the identity partials of the other S - 1 blocks at
-// n/64 + panel (S - 1) + their arrival index. So the trial's scalar sums come out in panel
-// order, bit-identical from run to run (a last arriver at its own block slot made their
-// summation order depend on timing).
-template <typename T, int NT>
-__device__ inline bool atr_split_combine(typename MF<T>::acc_t (&acc)[4][NT], T* __restrict__ Gp,
-                                         int64_t n, int S, int64_t panel, int64_t split,
-                                         unsigned* __restrict__ pcnt, int* slot) {
-  typedef MF<T> M;
-  constexpr int L = 16 * NT;
-  __shared__ int last;
-  __shared__ unsigned arrival;
-  const int lane = threadIdx.x & 63;
-  const int wave = threadIdx.x >> 6;
-  const int i = lane & 15;
-  const int64_t col0 = panel * 64;
-  const int64_t nl = n * L;
-#pragma unroll
-  for (int e = 0; e < 4; ++e) {
-    if (e != wave) continue;
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const int64_t row = col0 + atr_col<T>(M::row(lane, r), e);
-#pragma unroll
-      for (int nt = 0; nt < NT; ++nt)
-        __hip_atomic_store(Gp + split * nl + row * L + nt * 16 + i, acc[e][nt][r], __ATOMIC_RELAXED,
-                           __HIP_MEMORY_SCOPE_AGENT);
-    }
-  }
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    arrival = __hip_atomic_fetch_add(pcnt + panel, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    last = arrival == (unsigned)S - 1;
-  }
-  __syncthreads();
-  *slot = last ? (int)panel : (int)(n / 64 + panel * (S - 1) + arrival);
-  if (!last) return false;
-#pragma unroll
-  for (int e = 0; e < 4; ++e) {
-    if (e != wave) continue;
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const int64_t row = col0 + atr_col<T>(M::row(lane, r), e);
-#pragma unroll
-      for (int nt = 0; nt < NT; ++nt) {
-        const T* g = Gp + row * L + nt * 16 + i;
-        T v = __hip_atomic_load(g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        for (int k = 1; k < S; ++k)
-          v = v + __hip_atomic_load(g + (int64_t)k * nl, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        acc[e][nt][r] = v;
-      }
-    }
-  }
-  if (threadIdx.x == 0) __hip_atomic_store(pcnt + panel, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  return true;
-}
-
-template <typename T, int NT, int PF, int WL, bool NTL>
-__global__ __launch_bounds__(256) void k_atr_mfma(const T* __restrict__ A, const T* __restrict__ R,
-                                                  T* __restrict__ Gp, int64_t m, int64_t n, int S) {
-  typedef MF<T> M;
-  constexpr int L = 16 * NT;
-  const int lane = threadIdx.x & 63;
-  const int wave = threadIdx.x >> 6;
-  const int i = lane & 15;
-  typename M::acc_t acc[4][NT];
-  const int64_t col0 = atr_panel<T, NT, PF, WL, NTL>(A, R, m, n, S, acc, blockIdx.x, blockIdx.y);
-  T* gout = Gp + (int64_t)blockIdx.y * n * L;
-#pragma unroll
-  for (int e = 0; e < 4; ++e) {
-    if (WL == 0 && e != wave) continue;   // WL 0: wave w owns the rows e == w
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const int64_t grow = col0 + atr_col<T>(M::row(lane, r), e);
-#pragma unroll
-      for (int nt = 0; nt < NT; ++nt) gout[grow * L + nt * 16 + i] = acc[e][nt][r];
-    }
-  }
-}
-
-// ProxGD's line-search trial fused into A^T R (WL 0, one K split): once the block's LDS
-// reduction leaves each wave w the 16 gradient rows e == w of its panel — lane (i, q) holding
-// columns i and 16 + i of 4 rows, exactly the 16-lanes-per-row layout of k_prox_pgd — every
-// wave writes its rows of G and runs the trial on them (prox_pgd_row, the same arithmetic as
-// k_prox_pgd) with x = the thresholded iterate; the six trial sums are reduced over the grid.
-template <typename T, int NT, int PF, bool NTL, bool SPLIT>
-__global__ __launch_bounds__(256, sizeof(T) == 8 ? 2 : 1) void k_atr_prox(const T* __restrict__ A, const T* __restrict__ R,
-                                                  T* __restrict__ G, int64_t m, int64_t n,
-                                                  const T* __restrict__ x, T* __restrict__ p,
-                                                  T* __restrict__ pthr, T* __restrict__ z,
-                                                  double t_, double tmu_, double thres_, Red red,
-                                                  Pub pub, int S, T* __restrict__ Gp,
-                                                  unsigned* __restrict__ pcnt,
-                                                  uint8_t* __restrict__ zf) {
-  // Cancelled by a device-side decision (solver.cpp dc_run): nothing is computed or stored, no
-  // counter or ticket is touched. (Testing the flag after the main loop instead measured no
-  // faster and would spend a whole pass per cancelled launch.) The decision record still goes
-  // to the host: the cancelling decision's own.
-  if (red_skipped(red)) {
-    if (pub.host != nullptr && blockIdx.x == 0 && threadIdx.x == 0)
-      publish_packet(pub.s, pub.ns, pub.host, pub.host_seq, pub.seq);
-    return;
-  }
-  if (publisher_first<6, 0x8u>(pub, red)) return;   // the extra workgroup (n / 64 * S + 1 in all)
-  typedef MF<T> M;
-  constexpr int L = 16 * NT;
-  const int lane = threadIdx.x & 63;
-  const int wave = threadIdx.x >> 6;
-  const int i = lane & 15;
-  typename M::acc_t acc[4][NT];
-  const int64_t bid = (int64_t)blockIdx.x - (pub.host ? 1 : 0);
-  const int64_t panel = SPLIT ? bid / S : bid, split = SPLIT ? bid % S : 0;
-  const int64_t col0 = atr_panel<T, NT, PF, 0, NTL>(A, R, m, n, SPLIT ? S : 1, acc, panel, split);
-  double accr[6] = {0.0, 0.0, 0.0, -__builtin_inf(), 0.0, 0.0};
-  int slot = work_slot(pub);
-  if constexpr (SPLIT) {   // a separate instantiation: the S = 1 kernel keeps 2 blocks per CU
-    if (!atr_split_combine<T, NT>(acc, Gp, n, S, panel, split, pcnt, &slot)) {
-      grid_reduce<6, 0x8u>(accr, red, slot);
-      return;
-    }
-  }
-  const T t = (T)t_, tmu = (T)tmu_, thres = (T)thres_;
-#pragma unroll
-  for (int e = 0; e < 4; ++e) {
-    if (e != wave) continue;   // wave w owns the rows e == w (4 per lane group)
-    T xa[4][NT];
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const int64_t row = col0 + atr_col<T>(M::row(lane, r), e);
-#pragma unroll
-      for (int nt = 0; nt < NT; ++nt) xa[r][nt] = x[row * L + nt * 16 + i];
-    }
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const int64_t row = col0 + atr_col<T>(M::row(lane, r), e);
-      T gv[NT], pv[NT], pth[NT], zv[NT];
-      bool ok[NT];
-#pragma unroll
-      for (int nt = 0; nt < NT; ++nt) {
-        gv[nt] = acc[e][nt][r];
-        ok[nt] = true;
-        G[row * L + nt * 16 + i] = gv[nt];
-      }
-      const bool rowe =
-          prox_pgd_row<T, 16, NT>(xa[r], gv, ok, true, i, t, tmu, thres, pv, pth, zv, accr, zf != nullptr);
-      if (zf != nullptr && i == 0) zf[row] = rowe ? 1 : 0;
-#pragma unroll
-      for (int nt = 0; nt < NT; ++nt) {
-        p[row * L + nt * 16 + i] = pv[nt];
-        pthr[row * L + nt * 16 + i] = pth[nt];
-        z[row * L + nt * 16 + i] = zv[nt];
-      }
-    }
-  }
-  grid_reduce<6, 0x8u>(accr, red, slot);
-}
-
-// FISTA's backtracking trial fused into A^T R the same way (WL 0, one K split): each wave runs
-// fista_row (the arithmetic of k_fista_trial) on its 16 gradient rows, with y the extrapolated
-// point and xk the current iterate; writes G, xc, v_next, y_next and reduces the four sums.
-template <typename T, int NT, int PF, bool NTL, bool SPLIT>
-__global__ __launch_bounds__(256, sizeof(T) == 8 ? 2 : 1) void k_atr_fista(const T* __restrict__ A, const T* __restrict__ R,
-                                                   T* __restrict__ G, int64_t m, int64_t n,
-                                                   const T* __restrict__ y, const T* __restrict__ xk,
-                                                   T* __restrict__ xc, T* __restrict__ vnext,
-                                                   T* __restrict__ ynext, double t_, double tmu_,
-                                                   double thres_, double theta_, double a1_,
-                                                   double b1_, Red red, Pub pub, int S,
-                                                   T* __restrict__ Gp, unsigned* __restrict__ pcnt,
-                                                   T* __restrict__ ec, uint8_t* __restrict__ zf) {
-  if (publisher_first<4, 0x8u>(pub, red)) return;
-  typedef MF<T> M;
-  constexpr int L = 16 * NT;
-  const int lane = threadIdx.x & 63;
-  const int wave = threadIdx.x >> 6;
-  const int i = lane & 15;
-  typename M::acc_t acc[4][NT];
-  const int64_t bid = (int64_t)blockIdx.x - (pub.host ? 1 : 0);
-  const int64_t panel = SPLIT ? bid / S : bid, split = SPLIT ? bid % S : 0;
-  const int64_t col0 = atr_panel<T, NT, PF, 0, NTL>(A, R, m, n, SPLIT ? S : 1, acc, panel, split);
-  double accr[4] = {0.0, 0.0, 0.0, -__builtin_inf()};
-  int slot = work_slot(pub);
-  if constexpr (SPLIT) {   // fixed reduction slots, see atr_split_combine
-    if (!atr_split_combine<T, NT>(acc, Gp, n, S, panel, split, pcnt, &slot)) {
-      grid_reduce<4, 0x8u>(accr, red, slot);
-      return;
-    }
-  }
-  const T t = (T)t_, tmu = (T)tmu_, thres = (T)thres_, theta = (T)theta_, a1 = (T)a1_, b1 = (T)b1_;
-#pragma unroll
-  for (int e = 0; e < 4; ++e) {
-    if (e != wave) continue;   // wave w owns the rows e == w
-    T ya[4][NT], xa[4][NT];
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const int64_t row = col0 + atr_col<T>(M::row(lane, r), e);
-#pragma unroll
-      for (int nt = 0; nt < NT; ++nt) {
-        ya[r][nt] = y[row * L + nt * 16 + i];
-        xa[r][nt] = xk[row * L + nt * 16 + i];
-      }
-    }
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const int64_t row = col0 + atr_col<T>(M::row(lane, r), e);
-      T gv[NT], xcv[NT], vnv[NT], ynv[NT], ecv[NT];
-      bool ok[NT];
-#pragma unroll
-      for (int nt = 0; nt < NT; ++nt) {
-        gv[nt] = acc[e][nt][r];
-        ok[nt] = true;
-        G[row * L + nt * 16 + i] = gv[nt];
-      }
-      const bool rowe = fista_row<T, 16, NT, true>(ya[r], gv, xa[r], ok, true, i, t, tmu, thres, theta,
-                                                   a1, b1, T(0), T(0), xcv, vnv, ynv, accr,
-                                                   ec != nullptr ? ecv : nullptr);
-      if (zf != nullptr && i == 0) zf[row] = rowe ? 1 : 0;
-#pragma unroll
-      for (int nt = 0; nt < NT; ++nt) {
-        xc[row * L + nt * 16 + i] = xcv[nt];
-        vnext[row * L + nt * 16 + i] = vnv[nt];
-        ynext[row * L + nt * 16 + i] = ynv[nt];
-        if (ec != nullptr) ec[row * L + nt * 16 + i] = ecv[nt];
-      }
-    }
-  }
-  grid_reduce<4, 0x8u>(accr, red, slot);
-}
-
-// ------------------------------------------------------------------------------------------
-// VALU fallback for small l (GEMV-like, l <= 8 per pass) and ragged shapes.
-// A @ X: a wave owns RW rows and one K split; lanes stride the row with (16-byte) loads,
-// each X element is reused across the RW rows; columns [c0, c0+LB) of the output.
-// ------------------------------------------------------------------------------------------
-__device__ inline double wave_sum(double v) {
-#pragma unroll
-  for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off);
-  return v;
-}
-__device__ inline float wave_sum(float v) {
-#pragma unroll
-  for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off);
-  return v;
-}
 
 template <typename T, int LB, int RW, bool VEC, int NSRC>
 __global__ __launch_bounds__(256) void k_ax_valu(const T* __restrict__ A, const T* __restrict__ X0,
@@ -1326,88 +525,9 @@ __global__ __launch_bounds__(256) void k_ax_valu(const T* __restrict__ A, const 
   }
 }
 
-// A^T R on VALU: a thread owns E consecutive columns of A over a row range; R[row][c0..c0+LB)
-// is wave-uniform (scalar loads). Gp[blockIdx.y][n][l].
-template <typename T, int LB, bool VEC>
-__global__ __launch_bounds__(256) void k_atr_valu(const T* __restrict__ A, const T* __restrict__ R,
-                                                  T* __restrict__ Gp, int64_t m, int64_t n,
-                                                  int64_t l, int c0, int S) {
-  constexpr int E = VEC ? (16 / (int)sizeof(T)) : 1;
-  const int64_t col = ((int64_t)blockIdx.x * 256 + threadIdx.x) * E;
-  const int s = blockIdx.y;
-  const int64_t rb = m * s / S, re = m * (s + 1) / S;
-  const int nc = (int)((l - c0) < LB ? (l - c0) : LB);
-  const bool active = col < n;
-  const int64_t ccol = active ? col : 0;
-
-  T acc[E][LB];
-#pragma unroll
-  for (int e = 0; e < E; ++e)
-#pragma unroll
-    for (int c = 0; c < LB; ++c) acc[e][c] = T(0);
-
-  const T* ap = A + rb * n + ccol;
-  const T* rp = R + rb * l + c0;
-#pragma unroll 4
-  for (int64_t row = rb; row < re; ++row) {
-    T a[E];
-    if constexpr (VEC) {
-      typedef typename MF<T>::vec_t V;
-      const V v = *reinterpret_cast<const V*>(ap);
-#pragma unroll
-      for (int e = 0; e < E; ++e) a[e] = v[e];
-    } else {
-      a[0] = *ap;
-    }
-    T rv[LB];
-#pragma unroll
-    for (int c = 0; c < LB; ++c) rv[c] = (c < nc) ? rp[c] : T(0);
-#pragma unroll
-    for (int e = 0; e < E; ++e)
-#pragma unroll
-      for (int c = 0; c < LB; ++c) acc[e][c] = __builtin_fma(a[e], rv[c], acc[e][c]);
-    ap += n;
-    rp += l;
-  }
-  if (!active) return;
-  T* gout = Gp + (int64_t)s * n * l;
-#pragma unroll
-  for (int e = 0; e < E; ++e)
-#pragma unroll
-    for (int c = 0; c < LB; ++c)
-      if (c < nc) gout[(col + e) * l + c0 + c] = acc[e][c];
-}
-
 // ------------------------------------------------------------------------------------------
 // planning + launch
 // ------------------------------------------------------------------------------------------
-static inline int64_t cdiv(int64_t a, int64_t b) { return (a + b - 1) / b; }
-static inline int64_t clampi(int64_t v, int64_t lo, int64_t hi) {
-  return v < lo ? lo : (v > hi ? hi : v);
-}
-static constexpr int64_t kTargetWaves = 2048;   // 8 waves per CU on 256 CUs
-static constexpr int kMaxSplit = 64;
-
-static int env_int(const char* name, int dflt) {
-  const char* v = std::getenv(name);
-  return (v && *v) ? std::atoi(v) : dflt;
-}
-
-// Occupancy pad (tuning experiment, GLX_AX_LDS_PAD / GLX_ATR_LDS_PAD bytes): unused dynamic
-// LDS added to a launch so that at most one workgroup fits per CU — a 256-workgroup grid can
-// then not double up on some CUs while others idle. 0 = off (the default).
-template <typename K>
-static size_t lds_pad(K kernel, const char* env) {
-  const int pad = env_int(env, 0);
-  if (pad <= 0) return 0;
-  (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kernel),
-                            hipFuncAttributeMaxDynamicSharedMemorySize, pad);
-  return (size_t)pad;
-}
-
-// Defaults chosen by the sweep in scripts/kbench.py on MI355X.
-// ax code: kind*1000 + MT*100 + PF*10 + NTL (kind 1 = direct row loads, 2 = quad + bpermute).
-// kind 5 (X staged in LDS) code: 5 MT PF VPL WAVES. Kind-5 defaults fall back to the register
 // tiles below when the shape does not fit them (l not 16/32, n not a multiple of 4*E*VPL).
 static constexpr int kAxDefault = 52228;       // f64 single RHS: LDS, MT 2, PF 2, VPL 2, 8 waves
 static constexpr int kAxFallback = 21820;      // f64: VPL 2, direct loads, MT 8, PF 2
@@ -1428,20 +548,33 @@ static int axb_default(int nsrc, int esize) {
 }
 
 static constexpr int kLdsCodes[] = {52224, 52324, 52228, 52328, 52218, 54224, 52214, 54214,
-                                     51228, 51328, 51224,
-                                     52428, 54228, 54218, 62428, 62424, 62418, 72428, 72424,
-                                     72828};
-static bool lds_code_ok(int c, int64_t n, int64_t l, int esize) {
+                                     51228, 51328, 51224, 52428, 54228, 54218,
+                                     // kind 8 (LDS-DMA, f64): 8 NS KC/16 NTL WAVES
+                                     84208, 84218, 83208, 83218, 82408, 82418, 88108, 88118,
+                                     85208, 85218, 84204, 84214};
+static inline bool lds_kind(int c) { return c / 10000 == 5 || c / 10000 == 8; }
+static bool lds_code_ok(int c, int64_t n, int64_t l, int esize, int nsrc = 1) {
   bool known = false;
   for (int k : kLdsCodes) known |= (k == c);
   if (!known) return false;
+  if (c / 10000 == 8)
+    return esize == 8 && (l == 16 || l == 32) && n % (16 * ((c / 100) % 10)) == 0 &&
+           dma_lds_need(c, l, nsrc) <= 160 * 1024;
   const int E = 16 / esize, vpl = (c / 10) % 10;
   return (l == 16 || l == 32) && n % (4 * E * vpl) == 0;
 }
-// K split of a kind-5 launch: enough blocks for 2 (4-wave) blocks per CU
+// K split of a kind-5/8 launch: enough blocks for 2 (4-wave) blocks per CU
 static int lds_split(int esize, int64_t m, int64_t n, int code, int64_t target = 0) {
-  const int E = 16 / esize, mt = (code / 1000) % 10, vpl = (code / 10) % 10, waves = code % 10;
-  const int64_t rb = cdiv(m, 16 * mt * waves), chunks = n / (4 * E * vpl);
+  const int E = 16 / esize, waves = code % 10;
+  int64_t rb, chunks;
+  if (code / 10000 == 8) {   // one 16-row tile per wave, KC = 16 * digit-3 columns per chunk
+    rb = cdiv(m, 16 * waves);
+    chunks = n / (16 * ((code / 100) % 10));
+  } else {
+    const int mt = (code / 1000) % 10, vpl = (code / 10) % 10;
+    rb = cdiv(m, 16 * mt * waves);
+    chunks = n / (4 * E * vpl);
+  }
   if (target <= 0) target = env_int("GLX_AXL_BLOCKS", waves == 8 ? 256 : 512);
   return (int)clampi(cdiv(target, rb), 1, std::max<int64_t>(1, std::min<int64_t>(kMaxSplit, chunks / 8)));
 }
@@ -1539,7 +672,7 @@ GemmPlan make_plan(int esize, int64_t m, int64_t n, int64_t l, int ax_variant) {
   }
   const int s_ax = env_int("GLX_AX_S", 0);
   if (s_ax > 0) p.ax_S = (int)std::min<int64_t>(s_ax, kMaxSplit);
-  p.ax_xmap = env_int("GLX_AX_XCD", 1);
+  p.ax_xmap = (env_int("GLX_AX_XCD", 1) ? 1 : 0) | (env_int("GLX_AX_ROT", 1) ? 2 : 0);
   // batched right-hand sides
   p.axb_code[0] = p.axb_code[1] = p.ax_code;
   p.axb_S[0] = p.axb_S[1] = p.ax_S;
@@ -1548,14 +681,14 @@ GemmPlan make_plan(int esize, int64_t m, int64_t n, int64_t l, int ax_variant) {
     int S = p.ax_S;
     if (p.ax_kind == 3) {
       code = 0;
-    } else if (code / 10000 >= 5 && code / 10000 <= 7) {
-      if (lds_code_ok(code, n, l, esize)) lds_plan(esize, m, n, l, ns, code, S);
+    } else if (lds_kind(code)) {
+      if (lds_code_ok(code, n, l, esize, ns)) lds_plan(esize, m, n, l, ns, code, S);
       else code = ns == 2 ? 1420 : 1220;
     } else if (code >= 10000 && n % (4 * E * (code / 10000)) != 0) {
       code = ns == 2 ? 1420 : 1220;
     }
     const int s_axb = env_int("GLX_AXB_S", 0);
-    if (s_axb > 0 && code / 10000 >= 5 && code / 10000 <= 7) S = (int)std::min<int64_t>(s_axb, kMaxSplit);
+    if (s_axb > 0 && lds_kind(code)) S = (int)std::min<int64_t>(s_axb, kMaxSplit);
     p.axb_code[ns] = code;
     p.axb_S[ns] = S;
   }
@@ -1607,10 +740,11 @@ static std::string ax_name(const GemmPlan& p, int nsrc) {
   char buf[128];
   if (p.ax_kind == 3 || code == 0) {
     std::snprintf(buf, sizeof buf, "k_ax_valu<LB%d,VEC%d> S=%d", p.ax_lb, p.ax_vec, ax_split(p, nsrc));
-  } else if (code / 10000 >= 5 && code / 10000 <= 7) {
-    std::snprintf(buf, sizeof buf, "%s<MT%d,PF%d,VPL%d,W%d> S=%d",
-                  code / 10000 == 7 ? "k_ax_lds3" : (code / 10000 == 6 ? "k_ax_lds2" : "k_ax_lds"),
-                  (code / 1000) % 10,
+  } else if (code / 10000 == 8) {
+    std::snprintf(buf, sizeof buf, "k_ax_dma<NS%d,KC%d,NTL%d,W%d> S=%d", (code / 1000) % 10,
+                  16 * ((code / 100) % 10), (code / 10) % 10, code % 10, ax_split(p, nsrc));
+  } else if (code / 10000 == 5) {
+    std::snprintf(buf, sizeof buf, "k_ax_lds<MT%d,PF%d,VPL%d,W%d> S=%d", (code / 1000) % 10,
                   (code / 100) % 10, (code / 10) % 10, code % 10, ax_split(p, nsrc));
   } else {
     const int vpl = code / 10000 ? code / 10000 : 1;
@@ -1668,7 +802,7 @@ static void ax_mfma_go(const GemmPlan& p, const T* A, const T* const* X, T* P, c
                        int epoch, hipStream_t st) {
   constexpr int E = 16 / sizeof(T);
   const int gx = (int)cdiv(p.m, 16 * MT);
-  const int xmap = (p.ax_xmap && ax_xmap_ok(p.ax_S)) ? 1 : 0;
+  const int xmap = ((p.ax_xmap & 1) && ax_xmap_ok(p.ax_S)) ? 1 : 0;
   const dim3 grid((unsigned)ax_grid(xmap, gx, p.ax_S));
   hipLaunchKernelGGL((k_ax_mfma<T, MT, NT, NSRC, PF, QUAD, NTL, VPL>), grid, dim3(256), 0, st, A,
                      X[0], X[1], X[2], P, p.m, p.n, p.n / (4 * VPL * E), p.ax_S, gx, xmap, gate,
@@ -1681,7 +815,7 @@ static void ax_lds_go(const GemmPlan& p, int S, const T* A, const T* const* X, T
                       const uint8_t* sf = nullptr) {
   constexpr int E = 16 / sizeof(T);
   const int gx = (int)cdiv(p.m, 16 * MT * WAVES);
-  const int xmap = (p.ax_xmap && ax_xmap_ok(S)) ? 1 : 0;
+  const int xmap = ax_xmap_flags(p, S);
   const dim3 grid((unsigned)ax_grid(xmap, gx, S) + (pub.host ? 1u : 0u));
   if constexpr (NSRC == 2) {
     if (sf != nullptr) {
@@ -1697,42 +831,16 @@ static void ax_lds_go(const GemmPlan& p, int S, const T* A, const T* const* X, T
                      p.n / (4 * VPL * E), S, gx, xmap, gate, epoch, pub, nullptr);
 }
 
-template <typename T, int NT, int NSRC, int MT, int PF, int VPL, int WAVES, int BAR>
-static void ax_lds3_go(const GemmPlan& p, int S, const T* A, const T* const* X, T* P,
-                       const int* gate, int epoch, hipStream_t st) {
-  constexpr int E = 16 / sizeof(T);
-  const int gx = (int)cdiv(p.m, 16 * MT * WAVES);
-  const int xmap = (p.ax_xmap && ax_xmap_ok(S)) ? 1 : 0;
-  hipLaunchKernelGGL((k_ax_lds3<T, MT, NT, NSRC, PF, VPL, WAVES, BAR>),
-                     dim3((unsigned)ax_grid(xmap, gx, S)), dim3(64 * WAVES), 0, st, A, X[0], X[1],
-                     X[2], P, p.m, p.n, p.n / (4 * VPL * E), S, gx, xmap, gate, epoch);
-}
-
-template <typename T, int NT, int NSRC, int MT, int PF, int VPL, int WAVES>
-static void ax_lds2_go(const GemmPlan& p, int S, const T* A, const T* const* X, T* P,
-                       const int* gate, int epoch, hipStream_t st) {
-  constexpr int E = 16 / sizeof(T);
-  const int gx = (int)cdiv(p.m, 16 * MT * WAVES);
-  const int xmap = (p.ax_xmap && ax_xmap_ok(S)) ? 1 : 0;
-  hipLaunchKernelGGL((k_ax_lds2<T, MT, NT, NSRC, PF, VPL, WAVES>), dim3((unsigned)ax_grid(xmap, gx, S)),
-                     dim3(64 * WAVES), 0, st, A, X[0], X[1], X[2], P, p.m, p.n,
-                     p.n / (4 * VPL * E), S, gx, xmap, gate, epoch);
-}
-
-// kind 5 codes: 5 MT PF VPL WAVES; kind 6 (pipelined X): 6 MT PF VPL WAVES
 template <typename T, int NT, int NSRC>
 static void ax_lds_code(const GemmPlan& p, int code, int S, const T* A, const T* const* X, T* P,
                         const int* gate, int epoch, hipStream_t st, Pub pub,
                         const uint8_t* sf) {
-  if (pub.host != nullptr && code / 10000 != 5)
-    throw Error{GLX_E_INVALID, "A@X: only the kind-5 LDS tile carries the scalar packet"};
+  if (code / 10000 == 8) {
+    if (!launch_ax_dma<T>(p, code, NSRC, S, A, X, P, gate, epoch, st, pub))
+      throw Error{GLX_E_INVALID, "A@X: unknown LDS-DMA tile code"};
+    return;
+  }
   switch (code) {
-    case 62428: ax_lds2_go<T, NT, NSRC, 2, 4, 2, 8>(p, S, A, X, P, gate, epoch, st); return;
-    case 62424: ax_lds2_go<T, NT, NSRC, 2, 4, 2, 4>(p, S, A, X, P, gate, epoch, st); return;
-    case 62418: ax_lds2_go<T, NT, NSRC, 2, 4, 1, 8>(p, S, A, X, P, gate, epoch, st); return;
-    case 72428: ax_lds3_go<T, NT, NSRC, 2, 4, 2, 8, 2>(p, S, A, X, P, gate, epoch, st); return;   // barrier / 2
-    case 72424: ax_lds3_go<T, NT, NSRC, 2, 4, 2, 4, 2>(p, S, A, X, P, gate, epoch, st); return;
-    case 72828: ax_lds3_go<T, NT, NSRC, 2, 8, 2, 8, 4>(p, S, A, X, P, gate, epoch, st); return;   // barrier / 4
     case 52428: ax_lds_go<T, NT, NSRC, 2, 4, 2, 8>(p, S, A, X, P, gate, epoch, st, pub, sf); return;
     default: break;
   }
@@ -1761,7 +869,7 @@ template <typename T, int NT>
 static void ax_mfma_nt(const GemmPlan& p, int nsrc, const T* A, const T* const* X, T* P,
                        const int* gate, int epoch, hipStream_t st, Pub pub, const uint8_t* sf) {
   const int code = p.axb_code[nsrc];
-  if (code / 10000 >= 5 && code / 10000 <= 7) {
+  if (lds_kind(code)) {
     if (nsrc == 1) ax_lds_code<T, NT, 1>(p, code, p.axb_S[1], A, X, P, gate, epoch, st, pub, nullptr);
     else if (nsrc == 2) ax_lds_code<T, NT, 2>(p, code, p.axb_S[2], A, X, P, gate, epoch, st, pub, sf);
     else ax_lds_code<T, NT, 3>(p, code, p.axb_S[3], A, X, P, gate, epoch, st, pub, nullptr);
@@ -1822,7 +930,7 @@ static void ax_mfma_nt(const GemmPlan& p, int nsrc, const T* A, const T* const* 
 
 bool ax_pub_ok(const GemmPlan& p, int nsrc) {
   return p.ax_kind != 3 && (p.l == 16 || p.l == 32) && nsrc >= 1 && nsrc <= 3 &&
-         p.axb_code[nsrc] / 10000 == 5;
+         lds_kind(p.axb_code[nsrc]);
 }
 
 template <typename T>
@@ -1840,160 +948,6 @@ void launch_ax(const GemmPlan& p, int nsrc, const T* A, const T* const* X, T* P,
   else ax_mfma_nt<T, 2>(p, nsrc, A, X, P, gate, epoch, st, pub, sf);
 }
 
-template <typename T, int LB>
-static void atr_valu_lb(const GemmPlan& p, const T* A, const T* R, T* Gp, hipStream_t st) {
-  constexpr int E = 16 / sizeof(T);
-  const int64_t cols_per_block = 256 * (p.atr_vec ? E : 1);
-  const dim3 grid((unsigned)cdiv(p.n, cols_per_block), (unsigned)p.atr_S);
-  for (int64_t c0 = 0; c0 < p.l; c0 += LB) {
-    if (p.atr_vec)
-      hipLaunchKernelGGL((k_atr_valu<T, LB, true>), grid, dim3(256), 0, st, A, R, Gp, p.m, p.n,
-                         p.l, (int)c0, p.atr_S);
-    else
-      hipLaunchKernelGGL((k_atr_valu<T, LB, false>), grid, dim3(256), 0, st, A, R, Gp, p.m, p.n,
-                         p.l, (int)c0, p.atr_S);
-  }
-}
-
-template <typename T, int NT, int PF, int WL, bool NTL>
-static void atr_mfma_go(const GemmPlan& p, const T* A, const T* R, T* Gp, hipStream_t st) {
-  const dim3 grid((unsigned)(p.n / (WL ? 256 : 64)), (unsigned)p.atr_S);
-  static const size_t pad = lds_pad(k_atr_mfma<T, NT, PF, WL, NTL>, "GLX_ATR_LDS_PAD");
-  hipLaunchKernelGGL((k_atr_mfma<T, NT, PF, WL, NTL>), grid, dim3(256), pad, st, A, R, Gp, p.m, p.n, p.atr_S);
-}
-
-template <typename T, int NT>
-static void atr_mfma_nt(const GemmPlan& p, const T* A, const T* R, T* Gp, hipStream_t st) {
-  switch (p.atr_ntl * 100 + p.atr_wl * 10 + p.atr_pf) {
-    case 3: atr_mfma_go<T, NT, 3, 0, false>(p, A, R, Gp, st); break;
-    case 4: atr_mfma_go<T, NT, 4, 0, false>(p, A, R, Gp, st); break;
-    case 6: atr_mfma_go<T, NT, 6, 0, false>(p, A, R, Gp, st); break;
-    case 8: atr_mfma_go<T, NT, 8, 0, false>(p, A, R, Gp, st); break;
-    case 14: atr_mfma_go<T, NT, 4, 1, false>(p, A, R, Gp, st); break;
-    case 102: atr_mfma_go<T, NT, 2, 0, true>(p, A, R, Gp, st); break;
-    case 104: atr_mfma_go<T, NT, 4, 0, true>(p, A, R, Gp, st); break;
-    case 106: atr_mfma_go<T, NT, 6, 0, true>(p, A, R, Gp, st); break;
-    case 108: atr_mfma_go<T, NT, 8, 0, true>(p, A, R, Gp, st); break;
-    case 114: atr_mfma_go<T, NT, 4, 1, true>(p, A, R, Gp, st); break;
-    default: atr_mfma_go<T, NT, 2, 0, false>(p, A, R, Gp, st); break;
-  }
-}
-
-template <typename T>
-void launch_atr(const GemmPlan& p, const T* A, const T* R, T* Gp, hipStream_t st) {
-  if (p.atr_kind == 3) {
-    switch (p.atr_lb) {
-      case 1: atr_valu_lb<T, 1>(p, A, R, Gp, st); break;
-      case 2: atr_valu_lb<T, 2>(p, A, R, Gp, st); break;
-      case 4: atr_valu_lb<T, 4>(p, A, R, Gp, st); break;
-      default: atr_valu_lb<T, 8>(p, A, R, Gp, st); break;
-    }
-    return;
-  }
-  if (p.l == 16) atr_mfma_nt<T, 1>(p, A, R, Gp, st);
-  else atr_mfma_nt<T, 2>(p, A, R, Gp, st);
-}
-
 template void launch_ax<double>(const GemmPlan&, int, const double*, const double* const*, double*, const int*, int, hipStream_t, Pub, const uint8_t*);
 template void launch_ax<float>(const GemmPlan&, int, const float*, const float* const*, float*, const int*, int, hipStream_t, Pub, const uint8_t*);
-bool atr_prox_ok(const GemmPlan& p) {
-  return p.atr_kind == 1 && p.atr_wl == 0 && p.atr_S >= 1 && p.atr_S <= 8 &&
-         (p.l == 16 || p.l == 32) && p.n % 64 == 0 &&
-         (p.n / 64) * p.atr_S < kMaxBlocks &&   // + a publisher workgroup
-         (p.atr_S == 1 || env_int("GLX_ATR_FUSE_SPLIT", 1) != 0);
-}
-
-template <typename T, int NT, int PF, bool NTL>
-static void atr_prox_go(const GemmPlan& p, const T* A, const T* R, T* G, const T* x, T* pp,
-                        T* pthr, T* z, double t, double mu, double thres, Red red, hipStream_t st,
-                        Pub pub, T* Gp, unsigned* pcnt, uint8_t* zf) {
-  const dim3 grid((unsigned)(p.n / 64 * p.atr_S + (pub.host ? 1 : 0)));
-  if (p.atr_S > 1) {
-    hipLaunchKernelGGL((k_atr_prox<T, NT, PF, NTL, true>), grid, dim3(256), 0, st, A, R, G, p.m,
-                       p.n, x, pp, pthr, z, t, t * mu, thres, red, pub, p.atr_S, Gp, pcnt, zf);
-    return;
-  }
-  static const size_t pad = lds_pad(k_atr_prox<T, NT, PF, NTL, false>, "GLX_ATR_LDS_PAD");
-  hipLaunchKernelGGL((k_atr_prox<T, NT, PF, NTL, false>), grid, dim3(256), pad, st, A, R, G, p.m,
-                     p.n, x, pp, pthr, z, t, t * mu, thres, red, pub, 1, Gp, pcnt, zf);
-}
-template <typename T, int NT>
-static void atr_prox_nt(const GemmPlan& p, const T* A, const T* R, T* G, const T* x, T* pp,
-                        T* pthr, T* z, double t, double mu, double thres, Red red, hipStream_t st,
-                        Pub pub, T* Gp, unsigned* pcnt, uint8_t* zf) {
-  switch (p.atr_ntl * 100 + p.atr_pf) {
-    case 4: atr_prox_go<T, NT, 4, false>(p, A, R, G, x, pp, pthr, z, t, mu, thres, red, st, pub, Gp, pcnt, zf); break;
-    case 6: atr_prox_go<T, NT, 6, false>(p, A, R, G, x, pp, pthr, z, t, mu, thres, red, st, pub, Gp, pcnt, zf); break;
-    case 104: atr_prox_go<T, NT, 4, true>(p, A, R, G, x, pp, pthr, z, t, mu, thres, red, st, pub, Gp, pcnt, zf); break;
-    case 108: atr_prox_go<T, NT, 8, true>(p, A, R, G, x, pp, pthr, z, t, mu, thres, red, st, pub, Gp, pcnt, zf); break;
-    default: atr_prox_go<T, NT, 8, false>(p, A, R, G, x, pp, pthr, z, t, mu, thres, red, st, pub, Gp, pcnt, zf); break;
-  }
-}
-template <typename T>
-void launch_atr_prox(const GemmPlan& p, const T* A, const T* R, T* G, const T* x, T* pp, T* pthr,
-                     T* z, double t, double mu, double thres, Red red, hipStream_t st, Pub pub,
-                     T* Gp, unsigned* pcnt, uint8_t* zf) {
-  if (p.atr_S > 1 && (Gp == nullptr || pcnt == nullptr))
-    throw Error{GLX_E_INVALID, "fused A^T R with K splits needs slab and counter buffers"};
-  if (p.l == 16) atr_prox_nt<T, 1>(p, A, R, G, x, pp, pthr, z, t, mu, thres, red, st, pub, Gp, pcnt, zf);
-  else atr_prox_nt<T, 2>(p, A, R, G, x, pp, pthr, z, t, mu, thres, red, st, pub, Gp, pcnt, zf);
-}
-
-template <typename T, int NT, int PF, bool NTL>
-static void atr_fista_go(const GemmPlan& p, const T* A, const T* R, T* G, const T* y, const T* xk,
-                         T* xc, T* vn, T* yn, double t, double mu, double thres, double theta,
-                         double theta_next, Red red, hipStream_t st, Pub pub, T* Gp, unsigned* pcnt,
-                         T* ec, uint8_t* zf) {
-  const dim3 grid((unsigned)(p.n / 64 * p.atr_S + (pub.host ? 1 : 0)));
-  if (p.atr_S > 1) {
-    hipLaunchKernelGGL((k_atr_fista<T, NT, PF, NTL, true>), grid, dim3(256), 0, st, A, R, G, p.m,
-                       p.n, y, xk, xc, vn, yn, t, t * mu, thres, theta, 1.0 - theta_next,
-                       theta_next, red, pub, p.atr_S, Gp, pcnt, ec, zf);
-    return;
-  }
-  static const size_t pad = lds_pad(k_atr_fista<T, NT, PF, NTL, false>, "GLX_ATR_LDS_PAD");
-  hipLaunchKernelGGL((k_atr_fista<T, NT, PF, NTL, false>), grid, dim3(256), pad, st, A, R, G, p.m,
-                     p.n, y, xk, xc, vn, yn, t, t * mu, thres, theta, 1.0 - theta_next, theta_next,
-                     red, pub, 1, Gp, pcnt, ec, zf);
-}
-template <typename T, int NT>
-static void atr_fista_nt(const GemmPlan& p, const T* A, const T* R, T* G, const T* y, const T* xk,
-                         T* xc, T* vn, T* yn, double t, double mu, double thres, double theta,
-                         double theta_next, Red red, hipStream_t st, Pub pub, T* Gp, unsigned* pcnt,
-                         T* ec, uint8_t* zf) {
-  switch (p.atr_ntl * 100 + p.atr_pf) {
-    case 4: atr_fista_go<T, NT, 4, false>(p, A, R, G, y, xk, xc, vn, yn, t, mu, thres, theta, theta_next, red, st, pub, Gp, pcnt, ec, zf); break;
-    case 104: atr_fista_go<T, NT, 4, true>(p, A, R, G, y, xk, xc, vn, yn, t, mu, thres, theta, theta_next, red, st, pub, Gp, pcnt, ec, zf); break;
-    case 108: atr_fista_go<T, NT, 8, true>(p, A, R, G, y, xk, xc, vn, yn, t, mu, thres, theta, theta_next, red, st, pub, Gp, pcnt, ec, zf); break;
-    default: atr_fista_go<T, NT, 8, false>(p, A, R, G, y, xk, xc, vn, yn, t, mu, thres, theta, theta_next, red, st, pub, Gp, pcnt, ec, zf); break;
-  }
-}
-template <typename T>
-void launch_atr_fista(const GemmPlan& p, const T* A, const T* R, T* G, const T* y, const T* xk,
-                      T* xc, T* vn, T* yn, double t, double mu, double thres, double theta,
-                      double theta_next, Red red, hipStream_t st, Pub pub, T* Gp, unsigned* pcnt,
-                         T* ec, uint8_t* zf) {
-  if (p.atr_S > 1 && (Gp == nullptr || pcnt == nullptr))
-    throw Error{GLX_E_INVALID, "fused A^T R with K splits needs slab and counter buffers"};
-  if (p.l == 16) atr_fista_nt<T, 1>(p, A, R, G, y, xk, xc, vn, yn, t, mu, thres, theta, theta_next, red, st, pub, Gp, pcnt, ec, zf);
-  else atr_fista_nt<T, 2>(p, A, R, G, y, xk, xc, vn, yn, t, mu, thres, theta, theta_next, red, st, pub, Gp, pcnt, ec, zf);
-}
-
-template void launch_atr<double>(const GemmPlan&, const double*, const double*, double*, hipStream_t);
-template void launch_atr_fista<double>(const GemmPlan&, const double*, const double*, double*,
-                                       const double*, const double*, double*, double*, double*,
-                                       double, double, double, double, double, Red, hipStream_t, Pub,
-                                       double*, unsigned*, double*, uint8_t*);
-template void launch_atr_fista<float>(const GemmPlan&, const float*, const float*, float*,
-                                      const float*, const float*, float*, float*, float*, double,
-                                      double, double, double, double, Red, hipStream_t, Pub,
-                                      float*, unsigned*, float*, uint8_t*);
-template void launch_atr_prox<double>(const GemmPlan&, const double*, const double*, double*,
-                                      const double*, double*, double*, double*, double, double,
-                                      double, Red, hipStream_t, Pub, double*, unsigned*, uint8_t*);
-template void launch_atr_prox<float>(const GemmPlan&, const float*, const float*, float*,
-                                     const float*, float*, float*, float*, double, double, double,
-                                     Red, hipStream_t, Pub, float*, unsigned*, uint8_t*);
-template void launch_atr<float>(const GemmPlan&, const float*, const float*, float*, hipStream_t);
-
 }  // namespace glx

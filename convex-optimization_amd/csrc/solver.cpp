@@ -1777,15 +1777,22 @@ int glx_residual_gradient(int dtype, int64_t m, int64_t n, int64_t l, const void
     if (fused) {
       resgrad_reset(k.rg_ws, m, n, st);
       GLX_HIP(hipMemsetAsync(k.rg_err, 0, sizeof(int), st));
-      launch_resgrad((const double*)A, (const double*)X, (const double*)B, k.rg_s, k.rg_g, k.rg_ws, 1,
-                     m, n, k.rg_err, st);
-      double* rs[3] = {(double*)R, nullptr, nullptr};
-      launch_finalize_residual<double>(k.rg_s, 1, (const double*)B, 1, rs, m * l, nullptr, 0, 1,
-                                       nullptr, 0, nullptr, nullptr, 0.0, nullptr,
-                                       Red{k.part, k.ticket, k.scal}, st);
-      launch_sum_partials<double>(k.rg_g, resgrad_groups(n), (double*)G, n * l, st);
-      check_launch();
-      return;
+      if (launch_resgrad((const double*)A, (const double*)X, (const double*)B, k.rg_s, k.rg_g, k.rg_ws,
+                         1, m, n, k.rg_err, st)) {
+        double* rs[3] = {(double*)R, nullptr, nullptr};
+        launch_finalize_residual<double>(k.rg_s, 1, (const double*)B, 1, rs, m * l, nullptr, 0, 1,
+                                         nullptr, 0, nullptr, nullptr, 0.0, nullptr,
+                                         Red{k.part, k.ticket, k.scal}, st);
+        launch_sum_partials<double>(k.rg_g, resgrad_groups(n), (double*)G, n * l, st);
+        check_launch();
+        // the one-pass result is valid only if no hand-off wait timed out: read the flag back
+        // (this makes the one-pass call synchronous) and recompute with two passes otherwise
+        int herr = 0;
+        GLX_HIP(hipMemcpyAsync(&herr, k.rg_err, sizeof(int), hipMemcpyDeviceToHost, st));
+        GLX_HIP(hipStreamSynchronize(st));
+        if (herr == 0) return;
+      }
+      if (fused_out) *fused_out = 0;
     }
     const int es = dtype == GLX_F64 ? 8 : 4;
     (void)es;

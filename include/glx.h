@@ -168,8 +168,11 @@ int glx_prox(int dtype, int64_t n, int64_t l, const void* W, double t, double mu
  * `A.T @ (A @ x - b)`). one_pass = 0: A @ X, then A^T R (two passes over A, the faster path on
  * MI355X); one_pass = 1: the fused residual-gradient kernel reads A from HBM once
  *  where the shape and device allow it (fp64, l = 32, n = 512 P with P a power
- * of two in 2..128, m a multiple of 16 * 256 / P, >= 256 CUs), else two passes.
- * *one_pass_ran (may be NULL) = 1 when the fused kernel ran. */
+ * of two in 2..128, m a multiple of 16 * 256 / P, >= 256 CUs), else two passes. The one-pass
+ * kernel is a cooperative launch (its workgroups wait for each other); if the runtime refuses it,
+ * or a hand-off wait inside it times out (error flag read back: the one-pass call is synchronous),
+ * R and G are recomputed with two passes. *one_pass_ran (may be NULL) = 1 when the returned R
+ * and G come from the fused kernel. */
 int glx_residual_gradient(int dtype, int64_t m, int64_t n, int64_t l, const void* A, const void* X,
                           const void* B, void* R, void* G, void* workspace, size_t workspace_bytes,
                           int one_pass, int* one_pass_ran, void* stream);

@@ -41,6 +41,7 @@ def main():
     ap.add_argument("--splits", default="0,1,2,4,8,16")
     ap.add_argument("--axb", default="", help="batched (2-RHS) variants, e.g. 2420,1420,2220")
     ap.add_argument("--axb3", default="", help="batched (3-RHS) variants")
+    ap.add_argument("--no-ref", action="store_true", help="skip the torch streaming reference")
     args = ap.parse_args()
     from glx import kernels
     dt = torch.float64 if args.dtype == "f64" else torch.float32
@@ -53,7 +54,7 @@ def main():
     nbytes = es * (m * n + (m + n) * l)
     ref_r = (A.double() @ X.double() - B.double())
     ref_g = A.double().T @ R.double()
-    for v in [int(s) for s in args.ax.split(",")]:
+    for v in [int(s) for s in args.ax.split(",") if s]:
         for S in [int(s) for s in args.splits.split(",")]:
             os.environ["GLX_AX_S"] = str(S)
             got, _ = kernels.residual(A, X, B, variant=v)
@@ -68,7 +69,7 @@ def main():
         Xs = [X] + [torch.randn(n, l, device="cuda", dtype=dt) for _ in range(nsrc - 1)]
         refs = [(A.double() @ x.double() - B.double()) for x in Xs]
         nb = es * (m * n + (m + n) * l * nsrc)
-        for v in [int(s) for s in codes.split(",")]:
+        for v in [int(s) for s in codes.split(",") if s]:
             for S in [int(s) for s in args.splits.split(",")]:
                 os.environ["GLX_AXB_VARIANT"] = str(v)
                 os.environ["GLX_AX_S"] = str(S)
@@ -82,7 +83,7 @@ def main():
                                   "dtype": args.dtype, "shape": [m, n, l]}), flush=True)
     os.environ["GLX_AX_S"] = "0"
     os.environ["GLX_AXB_S"] = "0"
-    for v in [int(s) for s in args.atr.split(",")]:
+    for v in [int(s) for s in args.atr.split(",") if s]:
         for S in [int(s) for s in args.splits.split(",")]:
             os.environ["GLX_ATR_VARIANT"] = str(v)
             os.environ["GLX_ATR_S"] = str(S)
@@ -92,6 +93,8 @@ def main():
             print(json.dumps({"kernel": "atr", "variant": v, "split": S, "us": t * 1e6,
                               "GBs": nbytes / t / 1e9, "relerr": err, "dtype": args.dtype,
                               "shape": [m, n, l]}), flush=True)
+    if args.no_ref:
+        return
     # plain streaming reference: read A once with torch (sum) to calibrate achievable HBM
     t = timeit(lambda: A.sum(), args.reps)
     print(json.dumps({"kernel": "torch_sum_A", "us": t * 1e6, "GBs": es * m * n / t / 1e9}), flush=True)

@@ -1,7 +1,8 @@
 """Kernel-level numerics of the HIP path against an fp64 reference of the same op.
 
 A @ X - B, A^T R and the group prox, for every code path the planner can pick
-(MFMA direct loads, MFMA quad loads + bpermute, MFMA with X staged in LDS, VALU) at aligned,
+(MFMA direct loads, MFMA quad loads + bpermute, MFMA with X staged in LDS, MFMA with A and X
+staged by LDS-DMA, VALU) at aligned,
 ragged and GEMV shapes, single and batched right-hand sides.
 Tolerances: fp64 ≤ 1e-12 relative to the accumulated magnitude (sum |a||x|), fp32 ≤ 2e-5.
 """
@@ -32,7 +33,8 @@ SHAPES = [
 
 @pytest.mark.parametrize("dtype", ["f64", "f32"])
 @pytest.mark.parametrize("shape", SHAPES)
-@pytest.mark.parametrize("variant", [0, 2, 3, 21420, 41210, 52224, 54214, 52228, 62428])
+@pytest.mark.parametrize("variant", [0, 2, 3, 21420, 41210, 52224, 54214, 52228, 84208, 84218, 83218,
+                                     82418, 88118, 85218, 84214])
 def test_residual_and_gradient(shape, dtype, variant):
     k = _glx()
     m, n, l = shape
@@ -60,7 +62,8 @@ def test_residual_and_gradient(shape, dtype, variant):
     assert _rel_err(G, gref, gmag) < tolg
 
 
-BATCH_CODES = [0, 21420, 1220, 52224, 52324, 52228, 54224, 52214, 54214, 62428, 62424, 62418, 52428, 72428, 72424, 72828, 54228, 54218]
+BATCH_CODES = [0, 21420, 1220, 52224, 52324, 52228, 54224, 52214, 54214, 52428, 54228, 54218,
+               84208, 83208, 83218, 82408, 88108, 85208, 84204]
 
 
 @pytest.mark.parametrize("dtype", ["f64", "f32"])

@@ -76,3 +76,34 @@ def test_resgrad_unsupported_shape_falls_back():
     assert _rel(G3, A2.T @ R3, A2.abs().T @ R3.abs()) < 1e-13
     assert _rel(R, A @ X - B, A.abs() @ X.abs() + B.abs()) < 1e-13
     assert _rel(G, A.T @ R, A.abs().T @ R.abs()) < 1e-13
+
+
+def _check_forced_timeout(m, n):
+    """Every hand-off wait gives up at once (GLX_RG_SPIN=0): the kernel flags the error, the host
+    reads it back and recomputes R and G with two passes, and reports that the one-pass kernel's
+    result was not used."""
+    from glx import kernels
+    l = 32
+    g = torch.Generator(device="cuda").manual_seed(m + n)
+    A = torch.randn(m, n, device="cuda", dtype=torch.float64, generator=g)
+    X = torch.randn(n, l, device="cuda", dtype=torch.float64, generator=g)
+    B = torch.randn(m, l, device="cuda", dtype=torch.float64, generator=g)
+    R, G, fused = kernels.residual_gradient(A, X, B, one_pass=True)
+    torch.cuda.synchronize()
+    assert not fused, "a timed-out one-pass result was reported as used"
+    assert _rel(R, A @ X - B, A.abs() @ X.abs() + B.abs()) < 1e-13
+    assert _rel(G, A.T @ R, A.abs().T @ R.abs()) < 1e-13
+
+
+@pytest.mark.parametrize("xcd", ["1", "0"])
+def test_resgrad_timeout_falls_back(xcd):
+    import os
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    code = ("import sys; sys.path.insert(0, %r); import tests.test_gpu_resgrad as t; "
+            "t._check_forced_timeout(8192, 16384)" % root)
+    env = dict(os.environ, GLX_RG_SPIN="0", GLX_RG_XCD=xcd,
+               PYTHONPATH=os.pathsep.join([root, os.path.join(root, "convex-optimization_amd")]))
+    p = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=100)
+    assert p.returncode == 0, p.stdout[-2000:] + p.stderr[-2000:]
