@@ -53,7 +53,7 @@ constexpr int dma_lds_bytes() {
 template <int KC>
 __device__ inline int dma_sw(int i) { return KC >= 32 ? (i & 15) : ((i >> 1) & 7); }
 
-template <typename T, int NT, int NSRC, int NS, int KC, int WAVES, bool NTL>
+template <typename T, int NT, int NSRC, int NS, int KC, int WAVES, bool NTL, bool HOIST, bool PIPE>
 __global__ __launch_bounds__(64 * WAVES) void k_ax_dma(const T* __restrict__ A,
                                                       const T* __restrict__ X0,
                                                       const T* __restrict__ X1,
@@ -85,6 +85,9 @@ __global__ __launch_bounds__(64 * WAVES) void k_ax_dma(const T* __restrict__ A,
   static_assert(XS % 1024 == 0 && AW % 1024 == 0, "whole 1-KiB pieces");
   static_assert(D >= 1 && WAITN <= 63, "vmcnt range");
   static_assert(LDSB <= 160 * 1024, "LDS");
+  // s_waitcnt vmcnt(WAITN) expcnt(7) lgkmcnt(0) (gfx9 encoding: vmcnt[3:0] bits 3:0, expcnt
+  // bits 6:4, lgkmcnt bits 11:8, vmcnt[5:4] bits 15:14)
+  constexpr int kWaitVmLgkm0 = (WAITN & 15) | (7 << 4) | ((WAITN >> 4) << 14);
   __shared__ __attribute__((aligned(1024))) char lds[LDSB];
 
   if (pub.host != nullptr && blockIdx.x == 0) {   // as k_ax_lds: workgroup 0 carries the packet
@@ -156,6 +159,34 @@ __global__ __launch_bounds__(64 * WAVES) void k_ax_dma(const T* __restrict__ A,
     d2_t av[JN];
 #pragma unroll
     for (int j = 0; j < JN; ++j) av[j] = *reinterpret_cast<const d2_t*>(sb + asl[j]);
+    if constexpr (HOIST) {
+      // every LDS read of the chunk first, in MFMA order, then the MFMAs: the compiler's counted
+      // lgkmcnt waits then retire them progressively instead of a wait per small read group
+      T xv[JN][2][NSRC][NT];
+#pragma unroll
+      for (int j = 0; j < JN; ++j)
+#pragma unroll
+        for (int e = 0; e < 2; ++e)
+#pragma unroll
+          for (int src = 0; src < NSRC; ++src)
+#pragma unroll
+            for (int nt = 0; nt < NT; ++nt) {
+              const int k = 2 * (q + 4 * j) + e;
+              const int unit = (k * NT + nt) ^ (q & 1);
+              xv[j][e][src][nt] = *reinterpret_cast<const T*>(sb + xoff + src * XS + unit * 128);
+            }
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int j = 0; j < JN; ++j)
+#pragma unroll
+        for (int e = 0; e < 2; ++e)
+#pragma unroll
+          for (int src = 0; src < NSRC; ++src)
+#pragma unroll
+            for (int nt = 0; nt < NT; ++nt)
+              acc[src * NT + nt] = M::mma(av[j][e], xv[j][e][src][nt], acc[src * NT + nt]);
+      return;
+    }
 #pragma unroll
     for (int j = 0; j < JN; ++j)
 #pragma unroll
@@ -172,6 +203,75 @@ __global__ __launch_bounds__(64 * WAVES) void k_ax_dma(const T* __restrict__ A,
       }
   };
 
+  if constexpr (PIPE) {
+    // Software-pipelined: the operands of chunk c sit in registers (read one iteration earlier)
+    // when chunk c's MFMAs issue, so the MFMA pipe does not idle on the LDS read latency after
+    // each barrier (the two waves of a SIMD reach it in lockstep); chunk c + 1's reads are
+    // issued in front of those MFMAs and complete behind them. Same ring: after the barrier of
+    // iteration c every wave has landed chunk c + 1 and finished reading chunk c, whose slot
+    // takes chunk c + 1 + D.
+    // (fp64 MFMA on live data holds the clock near 2.05-2.2 GHz, where A@X's 2 m n l flops
+    // need ~125 us of MFMA pipe against ~158 us of streaming: scripts/axdma_ablate.hip.)
+    d2_t av[2][JN];
+    T xv[2][JN][2][NSRC][NT];
+    auto read_ops = [&](int slot, d2_t (&a)[JN], T (&x)[JN][2][NSRC][NT]) {
+      const char* sb = lds + slot * SLOT;
+#pragma unroll
+      for (int j = 0; j < JN; ++j) a[j] = *reinterpret_cast<const d2_t*>(sb + asl[j]);
+#pragma unroll
+      for (int j = 0; j < JN; ++j)
+#pragma unroll
+        for (int e = 0; e < 2; ++e)
+#pragma unroll
+          for (int src = 0; src < NSRC; ++src)
+#pragma unroll
+            for (int nt = 0; nt < NT; ++nt) {
+              const int k = 2 * (q + 4 * j) + e;
+              const int unit = (k * NT + nt) ^ (q & 1);
+              x[j][e][src][nt] = *reinterpret_cast<const T*>(sb + xoff + src * XS + unit * 128);
+            }
+    };
+    auto mma_ops = [&](const d2_t (&a)[JN], const T (&x)[JN][2][NSRC][NT]) {
+#pragma unroll
+      for (int j = 0; j < JN; ++j)
+#pragma unroll
+        for (int e = 0; e < 2; ++e)
+#pragma unroll
+          for (int src = 0; src < NSRC; ++src)
+#pragma unroll
+            for (int nt = 0; nt < NT; ++nt)
+              acc[src * NT + nt] = M::mma(a[j][e], x[j][e][src][nt], acc[src * NT + nt]);
+    };
+#pragma unroll
+    for (int d = 0; d < D; ++d) issue(d, d);
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(WAITN) : "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    issue(D, D);          // NS = D + 1: slot D is free
+    read_ops(0, av[0], xv[0]);
+    int cs = 1;           // slot of chunk c + 1
+    int64_t c = 0;
+    // two chunks per trip so the register sets keep static indices
+    for (; c + 1 < nch; c += 2) {
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        // chunk c + h + 1 landed everywhere, chunk c + h no longer read by anyone. The builtin
+        // (not inline asm) so that the compiler's own wait insertion knows the operand reads of
+        // the previous iteration are complete and adds no lgkmcnt(0) in front of the MFMAs
+        __builtin_amdgcn_sched_barrier(0);
+        __builtin_amdgcn_s_waitcnt(kWaitVmLgkm0);
+        __builtin_amdgcn_s_barrier();
+        __builtin_amdgcn_sched_barrier(0);
+        const int is = cs == 0 ? NS - 1 : cs - 1;   // slot of chunk c + h = slot of c + h + 1 + D
+        issue(c + h + 1 + D, is);
+        read_ops(cs, av[h ^ 1], xv[h ^ 1]);         // next chunk's operands ...
+        __builtin_amdgcn_sched_barrier(0);          // (DMA and reads issue before the MFMAs)
+        mma_ops(av[h], xv[h]);                      // ... in flight behind this chunk's MFMAs
+        cs = cs + 1 == NS ? 0 : cs + 1;
+      }
+    }
+    if (c < nch) mma_ops(av[0], xv[0]);   // odd count: the last chunk is in set 0
+  } else {
 #pragma unroll
   for (int d = 0; d < D; ++d) issue(d, d);
   int cs = 0;
@@ -185,6 +285,7 @@ __global__ __launch_bounds__(64 * WAVES) void k_ax_dma(const T* __restrict__ A,
     issue(c + D, is);
     compute(cs);
     cs = cs + 1 == NS ? 0 : cs + 1;
+  }
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the surplus re-issues, before exit
 
@@ -202,7 +303,8 @@ __global__ __launch_bounds__(64 * WAVES) void k_ax_dma(const T* __restrict__ A,
   }
 }
 
-template <typename T, int NT, int NSRC, int NS, int KC, int WAVES, bool NTL>
+template <typename T, int NT, int NSRC, int NS, int KC, int WAVES, bool NTL, bool HOIST = false,
+          bool PIPE = false>
 static void ax_dma_go(const GemmPlan& p, int S, const T* A, const T* const* X, T* P,
                       const int* gate, int epoch, hipStream_t st, Pub pub) {
   if constexpr (sizeof(T) != 8 || dma_lds_bytes<NT, NSRC, NS, KC, WAVES>() > 160 * 1024) {
@@ -211,7 +313,7 @@ static void ax_dma_go(const GemmPlan& p, int S, const T* A, const T* const* X, T
     const int gx = (int)cdiv(p.m, 16 * WAVES);
     const int xmap = ax_xmap_flags(p, S);
     const dim3 grid((unsigned)ax_grid(xmap, gx, S) + (pub.host ? 1u : 0u));
-    hipLaunchKernelGGL((k_ax_dma<T, NT, NSRC, NS, KC, WAVES, NTL>), grid, dim3(64 * WAVES), 0, st,
+    hipLaunchKernelGGL((k_ax_dma<T, NT, NSRC, NS, KC, WAVES, NTL, HOIST, PIPE>), grid, dim3(64 * WAVES), 0, st,
                        A, X[0], X[1], X[2], P, p.m, p.n, p.n / KC, S, gx, xmap, gate, epoch, pub);
   }
 }
@@ -234,12 +336,26 @@ static bool dma_code(const GemmPlan& p, int code, int S, const T* A, const T* co
     case 85218: ax_dma_go<T, NT, NSRC, 5, 32, 4, true>(p, S, A, X, P, gate, epoch, st, pub); return true;
     case 84204: ax_dma_go<T, NT, NSRC, 4, 32, 4, false>(p, S, A, X, P, gate, epoch, st, pub); return true;
     case 84214: ax_dma_go<T, NT, NSRC, 4, 32, 4, true>(p, S, A, X, P, gate, epoch, st, pub); return true;
+    // digit 4 = 2 | NTL: LDS reads hoisted ahead of the MFMAs; waves digit 1 = 16 waves
+    case 83238: ax_dma_go<T, NT, NSRC, 3, 32, 8, true, true>(p, S, A, X, P, gate, epoch, st, pub); return true;
+    case 84238: ax_dma_go<T, NT, NSRC, 4, 32, 8, true, true>(p, S, A, X, P, gate, epoch, st, pub); return true;
+    case 83228: ax_dma_go<T, NT, NSRC, 3, 32, 8, false, true>(p, S, A, X, P, gate, epoch, st, pub); return true;
+    case 84131: ax_dma_go<T, NT, NSRC, 4, 16, 16, true, true>(p, S, A, X, P, gate, epoch, st, pub); return true;
+    case 84111: ax_dma_go<T, NT, NSRC, 4, 16, 16, true, false>(p, S, A, X, P, gate, epoch, st, pub); return true;
+    case 82231: ax_dma_go<T, NT, NSRC, 2, 32, 16, true, true>(p, S, A, X, P, gate, epoch, st, pub); return true;
+    // digit 5 = 4 | NTL: software-pipelined operand reads
+    case 83258: ax_dma_go<T, NT, NSRC, 3, 32, 8, true, false, true>(p, S, A, X, P, gate, epoch, st, pub); return true;
+    case 84258: ax_dma_go<T, NT, NSRC, 4, 32, 8, true, false, true>(p, S, A, X, P, gate, epoch, st, pub); return true;
+    case 83248: ax_dma_go<T, NT, NSRC, 3, 32, 8, false, false, true>(p, S, A, X, P, gate, epoch, st, pub); return true;
+    case 84151: ax_dma_go<T, NT, NSRC, 4, 16, 16, true, false, true>(p, S, A, X, P, gate, epoch, st, pub); return true;
     default: return false;
   }
 }
 
+int dma_waves(int code) { return code % 10 == 1 ? 16 : code % 10; }
+
 int dma_lds_need(int code, int64_t l, int nsrc) {
-  const int ns = (code / 1000) % 10, kc = 16 * ((code / 100) % 10), waves = code % 10;
+  const int ns = (code / 1000) % 10, kc = 16 * ((code / 100) % 10), waves = dma_waves(code);
   const int xb = nsrc * kc * (int)l * 8;
   return ns * (waves * 16 * kc * 8 + xb) + ((xb / 1024) % waves ? 1024 : 0);
 }

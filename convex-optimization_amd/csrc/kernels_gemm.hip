@@ -551,7 +551,8 @@ static constexpr int kLdsCodes[] = {52224, 52324, 52228, 52328, 52218, 54224, 52
                                      51228, 51328, 51224, 52428, 54228, 54218,
                                      // kind 8 (LDS-DMA, f64): 8 NS KC/16 NTL WAVES
                                      84208, 84218, 83208, 83218, 82408, 82418, 88108, 88118,
-                                     85208, 85218, 84204, 84214};
+                                     84204, 84214, 83238, 84238, 83228, 84131, 84111, 82231,
+                                     83258, 84258, 83248, 84151};
 static inline bool lds_kind(int c) { return c / 10000 == 5 || c / 10000 == 8; }
 static bool lds_code_ok(int c, int64_t n, int64_t l, int esize, int nsrc = 1) {
   bool known = false;
@@ -568,14 +569,14 @@ static int lds_split(int esize, int64_t m, int64_t n, int code, int64_t target =
   const int E = 16 / esize, waves = code % 10;
   int64_t rb, chunks;
   if (code / 10000 == 8) {   // one 16-row tile per wave, KC = 16 * digit-3 columns per chunk
-    rb = cdiv(m, 16 * waves);
+    rb = cdiv(m, 16 * dma_waves(code));
     chunks = n / (16 * ((code / 100) % 10));
   } else {
     const int mt = (code / 1000) % 10, vpl = (code / 10) % 10;
     rb = cdiv(m, 16 * mt * waves);
     chunks = n / (4 * E * vpl);
   }
-  if (target <= 0) target = env_int("GLX_AXL_BLOCKS", waves == 8 ? 256 : 512);
+  if (target <= 0) target = env_int("GLX_AXL_BLOCKS", (waves == 8 || waves == 1) ? 256 : 512);
   return (int)clampi(cdiv(target, rb), 1, std::max<int64_t>(1, std::min<int64_t>(kMaxSplit, chunks / 8)));
 }
 // A K-split launch writes S partial slabs of m x (nsrc*l) that the finalize kernel reads back.
@@ -741,8 +742,10 @@ static std::string ax_name(const GemmPlan& p, int nsrc) {
   if (p.ax_kind == 3 || code == 0) {
     std::snprintf(buf, sizeof buf, "k_ax_valu<LB%d,VEC%d> S=%d", p.ax_lb, p.ax_vec, ax_split(p, nsrc));
   } else if (code / 10000 == 8) {
-    std::snprintf(buf, sizeof buf, "k_ax_dma<NS%d,KC%d,NTL%d,W%d> S=%d", (code / 1000) % 10,
-                  16 * ((code / 100) % 10), (code / 10) % 10, code % 10, ax_split(p, nsrc));
+    std::snprintf(buf, sizeof buf, "k_ax_dma<NS%d,KC%d,NTL%d,HOIST%d(2:PIPE),W%d> S=%d", (code / 1000) % 10,
+                  16 * ((code / 100) % 10), (code / 10) % 2, (code / 20) % 2 + 2 * ((code / 40) % 2),
+                  dma_waves(code),
+                  ax_split(p, nsrc));
   } else if (code / 10000 == 5) {
     std::snprintf(buf, sizeof buf, "k_ax_lds<MT%d,PF%d,VPL%d,W%d> S=%d", (code / 1000) % 10,
                   (code / 100) % 10, (code / 10) % 10, code % 10, ax_split(p, nsrc));

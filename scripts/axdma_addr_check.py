@@ -8,7 +8,8 @@ every ds_read inside the tile's LDS, before the kernel ever runs on a GPU.
 import itertools
 import sys
 
-CODES = [84208, 84218, 83208, 83218, 82408, 82418, 88108, 88118, 85208, 85218, 84204, 84214]
+CODES = [84208, 84218, 83208, 83218, 82408, 82418, 88108, 88118, 84204, 84214, 83238, 84238, 83228,
+         84131, 84111, 82231, 83258, 84258, 83248, 84151]
 SHAPES = [(512, 1024), (1000, 1024), (192, 4096), (129, 64), (64, 128), (4096, 8192), (129, 640),
           (8192, 16384), (1024, 16384), (2048, 16384), (256, 512)]
 
@@ -23,7 +24,7 @@ def lds_need(ns, kc, w, nt, nsrc):
 
 
 def check(code, m, n, nt, nsrc, S):
-    ns, kc, w = (code // 1000) % 10, 16 * ((code // 100) % 10), code % 10
+    ns, kc, w = (code // 1000) % 10, 16 * ((code // 100) % 10), (16 if code % 10 == 1 else code % 10)
     if n % kc or lds_need(ns, kc, w, nt, nsrc) > 160 * 1024:
         return None
     L = 16 * nt

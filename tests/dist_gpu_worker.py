@@ -34,6 +34,8 @@ def main():
     ap.add_argument("--csf", action="store_true", help="continuous_subgradient_flag (SGD/GD)")
     ap.add_argument("--alpha-scale", type=float, default=1.0,
                     help="alpha0 = scale / (sqrt(m) + sqrt(n))^2 (> 1: line-search rejections)")
+    ap.add_argument("--shm", action="store_true",
+                    help="one host copy of the instance in /dev/shm, each rank generating its own rows")
     ap.add_argument("--out", required=True)
     a = ap.parse_args()
 
@@ -47,10 +49,15 @@ def main():
     dist.init_process_group("gloo", rank=rank, world_size=world)
     comm = Comm.host_staged() if a.transport == "host" else Comm.from_torch_distributed()
 
-    A, b, u, x0, mu = numpy_ref.gen_data(a.m, a.n, a.l, 11)
+    r0, r1 = shard_rows(a.m, world, rank)
+    shm_path = None
+    if a.shm:
+        shm_path = "/dev/shm/glx_dist_%d_%s" % (world, os.environ.get("MASTER_PORT", "0"))
+        A, b, x0, mu = shm_instance(shm_path, a.m, a.n, a.l, 11, rank, r0, r1)
+    else:
+        A, b, u, x0, mu = numpy_ref.gen_data(a.m, a.n, a.l, 11)
     if a.dtype == "f32":
         A, b, x0 = (v.astype(np.float32) for v in (A, b, x0))
-    r0, r1 = shard_rows(a.m, world, rank)
     opts = {"alpha0": a.alpha_scale * numpy_ref.step_size_for(a.m, a.n), "maxit": a.maxit}
     if a.csf:
         opts["continuous_subgradient_flag"] = True
@@ -69,7 +76,41 @@ def main():
         with open(a.out, "w") as fh:
             json.dump(verdict, fh)
     comm.close()
+    if shm_path is not None:
+        dist.barrier()
+        if rank == 0:
+            os.unlink(shm_path)
     dist.destroy_process_group()
+
+
+def shm_instance(path, m, n, l, seed, rank, r0, r1):
+    """The instance as ONE host copy in shared memory (C5's global problem is 16 GiB of A): rank
+    0 creates the file, every rank fills its own rows of A from a per-shard seed (seed + rank,
+    SURVEY §8d's C5 recipe) and its rows of b = A u; u (10 % row-sparse) and x0 come from the
+    common seed, drawn in gen_data's order (main.py:41-47). Returns memory-mapped views."""
+    import torch.distributed as dist
+    nbytes = 8 * (m * n + m * l)
+    if rank == 0:
+        with open(path, "wb") as fh:
+            fh.truncate(nbytes)
+    dist.barrier()
+    mm = np.memmap(path, dtype=np.float64, mode="r+", shape=(m * n + m * l,))
+    A = mm[:m * n].reshape(m, n)
+    b = mm[m * n:].reshape(m, l)
+    gen = np.random.Generator(np.random.MT19937(seed=seed))
+    k = round(n * 0.1)
+    support = gen.permutation(n)[:k]
+    u = np.zeros(shape=(n, l))
+    u[support, :] = gen.standard_normal(size=(k, l))
+    x0 = gen.standard_normal(size=(n, l))
+    rows = np.random.Generator(np.random.MT19937(seed=seed * 1000 + 1 + rank))
+    for c0 in range(r0, r1, 1024):
+        c1 = min(r1, c0 + 1024)
+        rows.standard_normal(out=A[c0:c1])
+        b[c0:c1] = A[c0:c1] @ u
+    mm.flush()
+    dist.barrier()
+    return A, b, x0, 1e-2
 
 
 if __name__ == "__main__":

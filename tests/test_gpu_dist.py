@@ -125,3 +125,25 @@ def test_sharded_c5_shape_fprox_fp64(tmp_path):
     fh, fo = np.asarray(ranks[0]["f_hist"]), np.asarray(v["oracle_f_hist"])
     assert np.max(np.abs(fh - fo) / np.abs(fo)) < 1e-8
     assert v["x_maxdiff"] <= 1e-6 * v["x_scale"]
+
+
+@pytest.mark.timeout(400)
+def test_sharded_c5_global_world8(tmp_path):
+    """C5's global problem (131072 x 16384 x 32 fp64, 16 GiB of A; gl_FProxGD_primal.py:110-151
+    row-sharded) split the 8-GPU way: 8 ranks of 16384 rows, one iteration per continuation
+    phase, against the unsharded oracle on the same instance. The instance is ONE host copy in
+    /dev/shm (each rank generates its own rows), so host RAM holds A once; all 8 ranks share the
+    box's GPU through the host-staged transport."""
+    v = run_sharded(tmp_path, 8, "gl_FProxGD_primal", 131072, 16384, 32, maxit=1, threads=16,
+                    extra=("--shm",), timeout=380)
+    ranks = v["ranks"]
+    assert len(ranks) == 8
+    for r in ranks[1:]:
+        assert r["x_sha"] == ranks[0]["x_sha"] and r["k"] == ranks[0]["k"] and r["fval"] == ranks[0]["fval"]
+    assert ranks[0]["k"] == v["oracle_k"] == 3
+    rel = abs(ranks[0]["fval"] - v["oracle_fval"]) / abs(v["oracle_fval"])
+    assert rel < 1e-8, rel
+    fh, fo = np.asarray(ranks[0]["f_hist"]), np.asarray(v["oracle_f_hist"])
+    assert fh.shape == fo.shape
+    assert np.max(np.abs(fh - fo) / np.abs(fo)) < 1e-8
+    assert v["x_maxdiff"] <= 1e-6 * v["x_scale"]
