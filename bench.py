@@ -20,19 +20,21 @@ load run fast, then throttles (A@X 290 -> 400+ us) and recovers over ~30 ms
 (profiles/r2_power_probe.jsonl); a 20-step run would otherwise time that transient, not the
 solver. The timed session restarts from x0, so the iterations timed are the same ones.
 
-Also reported, for the dominant kernel (A@x with its batched right-hand sides, ~55-60% of the
-iteration):
+Also reported, for the dominant kernel (the dense A@X pass; at NS one right-hand side, A p_thr of
+the split-candidate trial, ~40 % of the iteration):
   roofline — the kernel's bound is whichever of MFMA time (flops / dense MFMA peak) and HBM time
-             (bytes / 8 TB/s) is larger for this (m, n, l, dtype): with l = 32 and two right-hand
-             sides it is MFMA-bound in fp64 and fp32 (BASELINE.json's metric is the MFMA roofline
-             %), with l = 1 (SGD) HBM-bound. achieved = algorithmic flops 2*m*n*l*rhs (or bytes
-             s*(m n + (m+n) l rhs)) per launch / average launch time from HIP events recorded on
-             the solver's stream over the timed region, around every 16th A@x / A^T r launch
-             (--profile 16: each timed event pair opens a few-us gap in the queue, 12 % of the
-             iteration at a 1024-row shard when every launch is timed). `pair_frac` is the same fraction for the
-             A@x + A^T r pair (the north-star target). `traffic` = HBM bytes per launch from
-             rocprofv3 PMC (profiles/pmc_traffic.json, 2*FETCH_SIZE + WRITE_SIZE per the gfx950
-             correction) when that file holds the same config, else null;
+             (bytes / 8 TB/s) is larger for this (m, n, l, dtype) and right-hand-side count: HBM
+             at NS (one right-hand side, l/4 flop/B in fp64) and for C4 (l = 1); MFMA for the
+             batched two-source passes (FProxGD without the split form, C3 in fp32). achieved =
+             algorithmic flops 2*m*n*l*rhs (or bytes s*(m n + (m+n) l rhs)) per launch / average
+             launch time from HIP events recorded on the solver's stream around every k-th dense
+             A@X / A^T r launch of the timed region (--profile k, default min(16, steps/8); each
+             event pair brackets exactly one kernel: the split-candidate A e gather is timed by
+             its own pair and reported apart). `pair_frac` / `pair4_frac` are the same fraction for
+             the A@x + A^T r pair (the north-star target), `pair4_frac_incl_gather` adds the
+             gather. `traffic` = HBM bytes per launch from rocprofv3 PMC (profiles/pmc_traffic.json,
+             2*FETCH_SIZE + WRITE_SIZE per the gfx950 correction) when that file holds the same
+             config and kernel, else null;
   cpu_baseline — the repo's NumPy oracle (oracle/numpy_ref.py) on the host cores, on a bounded
              sample of the same instance (rank 0, N = 1 only).
 """
@@ -266,17 +268,21 @@ def main():
     x = x0.clone()
     s = glx.Session(args.method, x, A, b, mu, opts, comm=comm)
     s.run(args.warmup)
-    s.kernel_time(0)
-    s.kernel_time(1)
+    for kind in (0, 1, 2):
+        s.kernel_time(kind)
     c0 = s.counters()
 
     if dist is not None:
         dist.barrier()
+    # marker kernels (torch's spin kernel) around the timed region, outside it: they delimit the
+    # timed launches in a rocprofv3 kernel trace of this command (scripts/prof_agree.py)
+    torch.cuda._sleep(1)
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     done = s.run(args.steps)
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
+    torch.cuda._sleep(1)
     if dist is not None:
         t = torch.tensor([elapsed], dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -286,6 +292,7 @@ def main():
     work = {k: c1[k] - c0[k] for k in c1}   # executed work of the timed region
     ax_n, ax_ms = s.kernel_time(0)
     atr_n, atr_ms = s.kernel_time(1)
+    ga_n, ga_ms = s.kernel_time(2)
     res = s.finish()
     s.close()
     if done != args.steps:
@@ -322,13 +329,19 @@ def main():
             gather_rows = st[5] / max(1.0, st[3] + st[4]) if split_cand else 0.0
         else:
             split_cand, sparse_rows, gather_rows = False, 0.0, 0.0
-        ax_bytes = es * (ml * n + (ml + n) * l * nsrc + (n * l if split_cand else 0) + ml * gather_rows)
+        # the dense A@X pass and the split-candidate gather are separate kernels, timed apart
+        ax_bytes = es * (ml * n + (ml + n) * l * nsrc)
+        ga_bytes = es * (n * l + ml * gather_rows) if split_cand else 0.0
         atr_bytes = es * (ml * n + (ml + n) * l)
-        ax_flops = 2.0 * ml * n * l * nsrc + 2.0 * ml * l * sparse_rows
+        ax_flops = 2.0 * ml * n * l * nsrc
+        ga_flops = 2.0 * ml * l * sparse_rows
         atr_flops = 2.0 * ml * n * l
+        ga_avg_s = (ga_ms / ga_n) / 1e3 if ga_n else 0.0
         ach = ax_bytes / ax_avg_s / 1e9 if ax_n else None
-        cfg_key = "%s_%s_%dx%dx%d_g%d%s" % (args.method, args.dtype, m, n, l, world,
-                                            "_sc" if split_cand and gather_rows else "")
+        ax_kname = ax_kernel_name(args.dtype, ml, n, l, nsrc)
+        # PMC entries are keyed by configuration AND the A@X tile the planner picks, so a
+        # measurement of another kernel is never reported as this one's traffic
+        cfg_key = "%s_%s_%dx%dx%d_g%d|%s" % (args.method, args.dtype, m, n, l, world, ax_kname)
         peak_tf = MFMA_PEAK_TFS[args.dtype]
         mfma_bound = ax_flops / (peak_tf * 1e12) >= ax_bytes / (HBM_PEAK_GBS * 1e9)
         ax_tf = ax_flops / ax_avg_s / 1e12 if ax_n else None
@@ -337,6 +350,9 @@ def main():
         # SURVEY §8d's literal pair: one A@x (l right-hand sides) + one A^T r = 4 m n l flops over
         # the same two launches (the batched second right-hand side is not counted)
         pair4_tf = ((4.0 * ml * n * l) / (ax_avg_s + atr_avg_s) / 1e12) if (ax_n and atr_n) else None
+        # the same with the split-candidate gather's time (and flops) added to the pair
+        pair4g_tf = (((4.0 * ml * n * l) + ga_flops) / (ax_avg_s + atr_avg_s + ga_avg_s) / 1e12
+                     if (ax_n and atr_n) else None)
         traffic, traffic_src = pmc_traffic(cfg_key)
         if mfma_bound:
             ach, peak, unit = ax_tf, peak_tf, "TFLOP/s"
@@ -344,9 +360,9 @@ def main():
             ach, peak, unit = ax_gbs, HBM_PEAK_GBS, "GB/s"
         roof = {"bound": "mfma" if mfma_bound else "hbm", "achieved": ach, "peak": peak,
                 "unit": unit, "frac": (ach / peak) if ach else None,
-                "traffic": traffic, "traffic_source": traffic_src,
+                "traffic": traffic, "traffic_source": traffic_src, "pmc_key": cfg_key,
                 "kernel": ("k_gemv_pair_fused: A@[x|thr(x)] and A^T r in ONE pass over A (l = 1)"
-                           if work["atr_calls"] == 0 else ax_kernel_name(args.dtype, ml, n, l, nsrc)),
+                           if work["atr_calls"] == 0 else ax_kname),
                 "flops_per_launch": ax_flops,
                 "bytes_per_launch": ax_bytes, "avg_launch_us": ax_avg_s * 1e6, "launches_timed": ax_n,
                 "timed_every": args.profile,
@@ -359,15 +375,20 @@ def main():
                 "atr_GBs": atr_bytes / atr_avg_s / 1e9 if atr_n else None,
                 "atr_mfma_frac": (atr_flops / atr_avg_s / 1e12) / peak_tf if atr_n else None,
                 "pair_tflops": pair_tf, "pair_frac": pair_tf / peak_tf if pair_tf else None,
-                "pair_definition": "pair_frac: algorithmic MFMA flops of the A@X launch (2 m n l "
-                                   "per dense right-hand side, 2 m l per flagged row of e) + "
-                                   "A^T r (2 m n l), over the two launches' time; the north-star "
-                                   "60 % target is read on this one. pair4_frac: SURVEY §8d's "
-                                   "literal 4 m n l over the same time",
+                "pair_definition": "pair_frac: algorithmic MFMA flops of the dense A@X launch "
+                                   "(2 m n l per dense right-hand side) + A^T r (2 m n l), over "
+                                   "the two launches' time (HIP events around each kernel); the "
+                                   "north-star 60 % target is read on this one. pair4_frac: "
+                                   "SURVEY §8d's literal 4 m n l over the same time. "
+                                   "pair4_frac_incl_gather: also counting the split-candidate A e "
+                                   "gather kernel's time (and its 2 m l flops per flagged row)",
                 "pair4_tflops": pair4_tf, "pair4_frac": pair4_tf / peak_tf if pair4_tf else None,
+                "gather_avg_launch_us": ga_avg_s * 1e6 if ga_n else None, "gather_launches_timed": ga_n,
+                "gather_bytes_per_launch": ga_bytes,
+                "pair4_frac_incl_gather": pair4g_tf / peak_tf if pair4g_tf else None,
                 # all MFMA flops issued in the timed region / its wall time (gaps, prox included)
                 "iter_frac": (2.0 * ml * n * l * work["ax_sources"] + work["atr_calls"] * atr_flops
-                              + 2.0 * ml * l * sparse_rows * work["ax_calls"])
+                              + ga_flops * work["ax_calls"])
                              / elapsed / 1e12 / peak_tf}
         steps = max(1, done)
         line = {

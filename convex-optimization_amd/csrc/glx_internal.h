@@ -134,7 +134,8 @@ template <typename T>
 bool launch_ax_dma(const GemmPlan& p, int code, int nsrc, int S, const T* A, const T* const* X, T* P,
                    const int* gate, int epoch, hipStream_t st, Pub pub);
 int dma_lds_need(int code, int64_t l, int nsrc);
-int dma_waves(int code);   // waves per workgroup of a kind-8 code (last digit; 1 = 16)
+int dma_waves(int code);   // waves per workgroup of a kind-8/9 code (last digit; 1 = 16)
+int dma_mt(int code);      // 16-row tiles per wave (kind 9: 2)
 template <typename T>
 void launch_atr(const GemmPlan& p, const T* A, const T* R, T* Gp, hipStream_t st);
 // ProxGD trial fused into A^T R (needs atr_prox_ok: MFMA panels, WL 0, at most 8 K splits):

@@ -552,13 +552,15 @@ static constexpr int kLdsCodes[] = {52224, 52324, 52228, 52328, 52218, 54224, 52
                                      // kind 8 (LDS-DMA, f64): 8 NS KC/16 NTL WAVES
                                      84208, 84218, 83208, 83218, 82408, 82418, 88108, 88118,
                                      84204, 84214, 83238, 84238, 83228, 84131, 84111, 82231,
-                                     83258, 84258, 83248, 84151};
-static inline bool lds_kind(int c) { return c / 10000 == 5 || c / 10000 == 8; }
+                                     83258, 84258, 83248, 84151, 94158, 94148, 93158, 92258,
+                                     83278, 93178, 92278, 93168, 92268, 94178, 94168};
+static inline bool dma_kind(int c) { return c / 10000 == 8 || c / 10000 == 9; }
+static inline bool lds_kind(int c) { return c / 10000 == 5 || dma_kind(c); }
 static bool lds_code_ok(int c, int64_t n, int64_t l, int esize, int nsrc = 1) {
   bool known = false;
   for (int k : kLdsCodes) known |= (k == c);
   if (!known) return false;
-  if (c / 10000 == 8)
+  if (dma_kind(c))
     return esize == 8 && (l == 16 || l == 32) && n % (16 * ((c / 100) % 10)) == 0 &&
            dma_lds_need(c, l, nsrc) <= 160 * 1024;
   const int E = 16 / esize, vpl = (c / 10) % 10;
@@ -568,8 +570,8 @@ static bool lds_code_ok(int c, int64_t n, int64_t l, int esize, int nsrc = 1) {
 static int lds_split(int esize, int64_t m, int64_t n, int code, int64_t target = 0) {
   const int E = 16 / esize, waves = code % 10;
   int64_t rb, chunks;
-  if (code / 10000 == 8) {   // one 16-row tile per wave, KC = 16 * digit-3 columns per chunk
-    rb = cdiv(m, 16 * dma_waves(code));
+  if (dma_kind(code)) {   // MT 16-row tiles per wave, KC = 16 * digit-3 columns per chunk
+    rb = cdiv(m, 16 * dma_mt(code) * dma_waves(code));
     chunks = n / (16 * ((code / 100) % 10));
   } else {
     const int mt = (code / 1000) % 10, vpl = (code / 10) % 10;
@@ -595,9 +597,29 @@ static int lds_split(int esize, int64_t m, int64_t n, int code, int64_t target =
 // One right-hand side at l = 32, f64 (round 2: the split-candidate trial's dense pass A p_thr is
 // HBM-bound): 51328 with its 4 K splits, A@X 246-250 vs 252-254 us incl. the A e gather, NS
 // ProxGD 2266-2269 vs 2231-2232 it/s on one box (profiles/r2_axtile/).
+//
+// Round 3, the LDS-DMA tile (kernels_axdma.hip): one right-hand side in fp64 with A beyond the
+// Infinity Cache (the split-candidate dense pass A p_thr at NS, FProxGD's A xc, C5's shard) takes
+// 92278 (two 16-row tiles per wave, 256-B row pieces, 2-slot ring, non-temporal A, DMA issues and
+// operand reads interleaved into the MFMA stream): NS 164 vs 193-196 us (6.57 TB/s), the 16384-row
+// shard 334 vs 399 us. fp64 C2 (two right-hand sides, l = 16, A in the Infinity Cache) takes
+// 92268 (default policy): 46.2 vs 49.3 us. Interleaved kernel-trace A/B, profiles/r3_axdma/.
 static void lds_plan(int esize, int64_t m, int64_t n, int64_t l, int nsrc, int& code, int& S) {
   S = lds_split(esize, m, n, code);
   if (std::getenv("GLX_AXL_BLOCKS") || std::getenv("GLX_AXB_VARIANT")) return;
+  const bool big = (double)m * (double)n * esize > kAtrNtBytes;
+  if (esize == 8 && nsrc == 1 && big && code == 52228 && lds_code_ok(92278, n, l, esize, 1) &&
+      env_int("GLX_AX_DMA", 1) != 0 && !std::getenv("GLX_AX_VARIANT")) {
+    code = 92278;
+    S = lds_split(esize, m, n, code);
+    return;
+  }
+  if (esize == 8 && nsrc == 2 && l == 16 && !big && code == 52228 &&
+      lds_code_ok(92268, n, l, esize, 2) && env_int("GLX_AX_DMA", 1) != 0) {
+    code = 92268;
+    S = lds_split(esize, m, n, code);
+    return;
+  }
   if (esize == 8 && nsrc == 1 && l == 32 && code == 52228 && lds_code_ok(51328, n, l, esize) &&
       !std::getenv("GLX_AX_VARIANT")) {
     code = 51328;
@@ -741,8 +763,8 @@ static std::string ax_name(const GemmPlan& p, int nsrc) {
   char buf[128];
   if (p.ax_kind == 3 || code == 0) {
     std::snprintf(buf, sizeof buf, "k_ax_valu<LB%d,VEC%d> S=%d", p.ax_lb, p.ax_vec, ax_split(p, nsrc));
-  } else if (code / 10000 == 8) {
-    std::snprintf(buf, sizeof buf, "k_ax_dma<NS%d,KC%d,NTL%d,HOIST%d(2:PIPE),W%d> S=%d", (code / 1000) % 10,
+  } else if (dma_kind(code)) {
+    std::snprintf(buf, sizeof buf, "k_ax_dma<MT%d,NS%d,KC%d,NTL%d,HOIST%d(2:PIPE),W%d> S=%d", dma_mt(code), (code / 1000) % 10,
                   16 * ((code / 100) % 10), (code / 10) % 2, (code / 20) % 2 + 2 * ((code / 40) % 2),
                   dma_waves(code),
                   ax_split(p, nsrc));
@@ -838,7 +860,7 @@ template <typename T, int NT, int NSRC>
 static void ax_lds_code(const GemmPlan& p, int code, int S, const T* A, const T* const* X, T* P,
                         const int* gate, int epoch, hipStream_t st, Pub pub,
                         const uint8_t* sf) {
-  if (code / 10000 == 8) {
+  if (dma_kind(code)) {
     if (!launch_ax_dma<T>(p, code, NSRC, S, A, X, P, gate, epoch, st, pub))
       throw Error{GLX_E_INVALID, "A@X: unknown LDS-DMA tile code"};
     return;

@@ -449,7 +449,8 @@ class Session : public SessionBase {
   }
 
   void kernel_time(int kind, int64_t* launches, double* ms) override {
-    if (kind < 0 || kind > 1) throw Error{GLX_E_INVALID, "kind must be 0 (A@x) or 1 (A^T r)"};
+    if (kind < 0 || kind > 2)
+      throw Error{GLX_E_INVALID, "kind must be 0 (A@x), 1 (A^T r) or 2 (split-candidate A e gather)"};
     auto& v = ev_[kind];
     double total = 0.0;
     if (!v.empty()) GLX_HIP(hipEventSynchronize(v.back().second));
@@ -568,19 +569,23 @@ class Session : public SessionBase {
   // are built on a side stream while the dense pass runs. Timed as one A@X (kind 0). pb: the
   // dense launch carries that scalar packet.
   void cand_ax(const T* const* xs, Pub pb = Pub{}) {
-    hipEvent_t e0 = prof_begin(0);
     const T* xd[3] = {xs[1], nullptr, nullptr};
     GLX_HIP(hipEventRecord(ev_trial_, st_));
     GLX_HIP(hipStreamWaitEvent(st2_, ev_trial_, 0));
     launch_e_lists<T>(xs[0], zf_, n_, l_, glists_, st2_);
     check_launch();
     GLX_HIP(hipEventRecord(ev_lists_, st2_));
+    // the dense pass and the gather are timed apart (kinds 0 and 2), so each event pair
+    // brackets one kernel of the trace
+    hipEvent_t e0 = prof_begin(0);
     launch_ax<T>(plan_, 1, A_, xd, Pp_ + (size_t)gsplit_ * ml_, nullptr, 0, st_, pb);
     check_launch();
+    prof_end(0, e0);
     GLX_HIP(hipStreamWaitEvent(st_, ev_lists_, 0));
+    hipEvent_t e2 = prof_begin(2);
     launch_at_gather<T>(At_, xs[0], m_, n_, l_, Pp_, glists_, st_);
     check_launch();
-    prof_end(0, e0);
+    prof_end(2, e2);
     ++ax_calls_;
     ax_cols_ += 1;
   }
@@ -1478,8 +1483,8 @@ class Session : public SessionBase {
   double tt_ = 0;
   int64_t ax_calls_ = 0, ax_cols_ = 0, atr_calls_ = 0, syncs_ = 0;
   double stats_[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-  std::vector<std::pair<hipEvent_t, hipEvent_t>> ev_[2];
-  int64_t prof_n_[2] = {0, 0};
+  std::vector<std::pair<hipEvent_t, hipEvent_t>> ev_[3];
+  int64_t prof_n_[3] = {0, 0, 0};
   std::vector<hipEvent_t> ev_pool_;
 };
 

@@ -171,7 +171,8 @@ class Session:
         return done.value
 
     def kernel_time(self, kind: int) -> Tuple[int, float]:
-        """(launches timed, total ms) of A@x (0) / A^T r (1): every k-th launch with opts profile=k."""
+        """(launches timed, total ms) of A@x (0: the dense pass) / A^T r (1) / the split-candidate
+        A e gather (2): every k-th launch of that kind with opts profile=k."""
         cnt = ctypes.c_int64(0)
         ms = ctypes.c_double(0)
         check(lib().glx_session_kernel_time(self.h, kind, ctypes.byref(cnt), ctypes.byref(ms)))

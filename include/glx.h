@@ -124,8 +124,9 @@ int  glx_session_create(glx_session** out, const glx_problem* prob, const glx_op
                         void* workspace, size_t workspace_bytes, void* stream);
 int  glx_session_run(glx_session* s, int64_t max_steps, int64_t* done, int32_t* finished);
 int  glx_session_finish(glx_session* s, glx_result* res);
-/* launches timed and their total device time (ms) for A@x (kind 0) / A^T r (kind 1), sampled
- * every opts.profile-th launch; resets the accumulators. */
+/* launches timed and their total device time (ms) for A@x (kind 0: the dense pass) / A^T r
+ * (kind 1) / the split-candidate A e gather (kind 2), sampled every opts.profile-th launch of that
+ * kind; resets the accumulators. */
 int  glx_session_kernel_time(glx_session* s, int kind, int64_t* launches, double* total_ms);
 /* executed-work counters since create: out = {A@x passes, right-hand sides in them, A^T r
  * passes, host readbacks} (cumulative; the caller differences them around a timed region). */

@@ -9,7 +9,8 @@ import itertools
 import sys
 
 CODES = [84208, 84218, 83208, 83218, 82408, 82418, 88108, 88118, 84204, 84214, 83238, 84238, 83228,
-         84131, 84111, 82231, 83258, 84258, 83248, 84151]
+         84131, 84111, 82231, 83258, 84258, 83248, 84151, 94158, 94148, 93158, 92258,
+         83278, 93178, 92278, 93168, 92268, 94178, 94168]
 SHAPES = [(512, 1024), (1000, 1024), (192, 4096), (129, 64), (64, 128), (4096, 8192), (129, 640),
           (8192, 16384), (1024, 16384), (2048, 16384), (256, 512)]
 
@@ -18,31 +19,32 @@ def sw(kc, i):
     return (i & 15) if kc >= 32 else ((i >> 1) & 7)
 
 
-def lds_need(ns, kc, w, nt, nsrc):
+def lds_need(ns, kc, w, nt, nsrc, mt=1):
     xb = nsrc * kc * 16 * nt * 8
-    return ns * (w * 16 * kc * 8 + xb) + (1024 if (xb // 1024) % w else 0)
+    return ns * (w * 16 * mt * kc * 8 + xb) + (1024 if (xb // 1024) % w else 0)
 
 
 def check(code, m, n, nt, nsrc, S):
     ns, kc, w = (code // 1000) % 10, 16 * ((code // 100) % 10), (16 if code % 10 == 1 else code % 10)
-    if n % kc or lds_need(ns, kc, w, nt, nsrc) > 160 * 1024:
+    mt = 2 if code // 10000 == 9 else 1
+    if n % kc or lds_need(ns, kc, w, nt, nsrc, mt) > 160 * 1024:
         return None
     L = 16 * nt
-    slr, aw = kc // 2, 16 * kc * 8
+    slr, aw = kc // 2, 16 * mt * kc * 8
     nia, xs = aw // 1024, kc * L * 8
     nxt = nsrc * xs // 1024
     nix = -(-nxt // w)
     slot = w * aw + nsrc * xs
-    ldsb = lds_need(ns, kc, w, nt, nsrc)
+    ldsb = lds_need(ns, kc, w, nt, nsrc, mt)
     chunks = n // kc
-    gx = -(-m // (16 * w))
+    gx = -(-m // (16 * mt * w))
     for bx, by in itertools.product(sorted({0, gx - 1}), range(S)):   # first and last row block
         cb, ce = chunks * by // S, chunks * (by + 1) // S
         nch = ce - cb
         if nch <= 0:
             continue
         for wave in range(w):
-            row0 = bx * 16 * w + wave * 16
+            row0 = bx * 16 * mt * w + wave * 16 * mt
             for c in (0, nch - 1):
                 for t in range(nia):
                     assert slot * (ns - 1) + wave * aw + t * 1024 + 1024 <= ldsb
@@ -50,7 +52,7 @@ def check(code, m, n, nt, nsrc, S):
                         ls = 64 * t + lane
                         ri, p = ls // slr, ls % slr
                         r = min(row0 + ri, m - 1)
-                        col = cb * kc + 2 * (p ^ sw(kc, ri)) + c * kc
+                        col = cb * kc + 2 * (p ^ sw(kc, ri & 15)) + c * kc
                         assert 0 <= col and col + 1 < n, (code, m, n, col)
                         assert 0 <= r < m
                 for rr in range(nix):
@@ -71,9 +73,10 @@ def check(code, m, n, nt, nsrc, S):
             # ds_reads
             for lane in range(64):
                 i, q = lane & 15, lane >> 4
-                for j in range(kc // 8):
-                    a = wave * aw + i * slr * 16 + 16 * ((q + 4 * j) ^ sw(kc, i))
-                    assert 0 <= a and a + 16 <= w * aw
+                for t in range(mt):
+                    for j in range(kc // 8):
+                        a = wave * aw + (16 * t + i) * slr * 16 + 16 * ((q + 4 * j) ^ sw(kc, i))
+                        assert wave * aw <= a and a + 16 <= (wave + 1) * aw
                 for j in range(kc // 8):
                     for e in range(2):
                         kk = 2 * (q + 4 * j) + e

@@ -11,7 +11,10 @@ ab() {  # name args...
   python3 scripts/ax_ab.py --summarize $O/$name > $O/$name.summary.jsonl || exit 1
   echo "== $name"; cat $O/$name.summary.jsonl
 }
-ab ns1 --codes 51328,83218,84238,83258,84258,84151 --rounds 5
-ab ns2 --nsrc 2 --codes 52228,83238,83258,83248 --rounds 4
-ab c2 --m 4096 --n 8192 --l 16 --nsrc 2 --codes 52228,83208,83248,83258 --rounds 4
+ab ns1 --codes 51328,92278,92268,93178,94178,94168 --rounds 5
+ab ns2 --nsrc 2 --codes 52228,92278,93178,94178 --rounds 4
+ab c2 --m 4096 --n 8192 --l 16 --nsrc 2 --codes 52228,93168,92268,94168 --rounds 4
+ab s1024 --m 1024 --nsrc 2 --codes 51328,52228,92268,94168,93168 --rounds 4
+ab s2048 --m 2048 --nsrc 2 --codes 51328,52228,92268,94168,93168 --rounds 4
+ab c5s --m 16384 --nsrc 1 --codes 51328,92278,94178 --rounds 3
 echo done

@@ -2,10 +2,12 @@
 
     python scripts/prof_agree.py --trace DIR --bench bench.json [--out summary.json]
 
-bench.py times the A@X and A^T R launches of the timed region with HIP events on the solver's
-stream (every `timed_every`-th launch); the trace holds every launch of the run (warmup
-included). The last launches_timed * timed_every A@X dispatches of the trace are the timed
-region's; their mean duration must agree with roofline.avg_launch_us (and likewise A^T R).
+bench.py times the dense A@X, A^T R and (split-candidate) A e gather launches of the timed region
+with HIP events on the solver's stream (every `timed_every`-th launch of each); the trace holds
+every launch of the run. bench.py brackets its timed region with two marker kernels (torch's
+spin kernel) launched outside it, so the trace's launches between the markers are exactly the
+timed region's; their mean duration must agree with the events' (roofline.avg_launch_us,
+atr_avg_launch_us, gather_avg_launch_us).
 """
 import argparse
 import csv
@@ -27,13 +29,25 @@ def main():
     for f in files:
         rows += list(csv.DictReader(open(f)))
     rows.sort(key=lambda r: int(r["Start_Timestamp"]))
-    out = {"bench_value": bench["value"], "bench_unit": bench["unit"]}
-    for kind, key, tag in (("ax", "avg_launch_us", "k_ax_"), ("atr", "atr_avg_launch_us", "k_atr_")):
-        durs = [(int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3 for r in rows if tag in r["Kernel_Name"]]
-        n = roof.get("launches_timed", roof.get("launches", 0)) * roof.get("timed_every", 1)
-        tail = durs[-n:] if len(durs) >= n else durs
-        avg = sum(tail) / max(1, len(tail))
-        out[kind] = {"trace_launches": len(durs), "compared": len(tail), "rocprof_avg_us": avg,
+    marks = [i for i, r in enumerate(rows) if "spin" in r["Kernel_Name"].lower() or "sleep" in r["Kernel_Name"].lower()]
+    if len(marks) >= 2:
+        region = rows[marks[-2] + 1:marks[-1]]
+        how = "launches between the two marker kernels"
+    else:
+        region = None
+        how = "no markers: the last launches_timed * timed_every launches of each kernel"
+    out = {"bench_value": bench["value"], "bench_unit": bench["unit"], "region": how}
+    for kind, key, tag in (("ax", "avg_launch_us", "k_ax_"), ("atr", "atr_avg_launch_us", "k_atr_"),
+                           ("gather", "gather_avg_launch_us", "k_at_gather")):
+        if roof.get(key) is None:
+            continue
+        src = region if region is not None else rows
+        durs = [(int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3 for r in src if tag in r["Kernel_Name"]]
+        if region is None:
+            n = roof.get("launches_timed", 0) * roof.get("timed_every", 1)
+            durs = durs[-n:] if len(durs) >= n else durs
+        avg = sum(durs) / max(1, len(durs))
+        out[kind] = {"trace_launches": len(durs), "rocprof_avg_us": avg,
                      "bench_events_avg_us": roof[key], "ratio": avg / roof[key] if roof[key] else None}
     print(json.dumps(out, indent=1))
     if a.out:
