@@ -136,6 +136,10 @@ bool launch_ax_dma(const GemmPlan& p, int code, int nsrc, int S, const T* A, con
 int dma_lds_need(int code, int64_t l, int nsrc);
 int dma_waves(int code);   // waves per workgroup of a kind-8/9 code (last digit; 1 = 16)
 int dma_mt(int code);      // 16-row tiles per wave (kind 9: 2)
+// Infinity-Cache hand-off between the passes (tuning experiment; MiB of A fetched with the
+// default policy at the end of a non-temporal pass; 0 = off): A@X (LDS-DMA tile) / A^T R
+void set_ax_keep_mib(int mib, hipStream_t st);
+void set_atr_keep_mib(int mib, hipStream_t st);
 template <typename T>
 void launch_atr(const GemmPlan& p, const T* A, const T* R, T* Gp, hipStream_t st);
 // ProxGD trial fused into A^T R (needs atr_prox_ok: MFMA panels, WL 0, at most 8 K splits):

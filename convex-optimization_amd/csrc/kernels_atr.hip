@@ -53,6 +53,17 @@ template <bool NTL> struct Load4<float, NTL> {
 // ((w0 + w1) + w2) + w3; afterwards wave w holds the complete sum for e == w in acc[w][*]
 // (the other e of a wave are partial and unused), so the four waves share the epilogue.
 // (pbx, pby) = (panel, K split) of this block: (blockIdx.x, blockIdx.y) for k_atr_mfma.
+// Infinity-Cache hand-off (tuning experiment, GLX_ATR_KEEP_MIB, default 0 = off): the last
+// rows a non-temporal A^T R pass reads are loaded with the default policy, so that about that many
+// MiB of A stay in the 256 MiB Infinity Cache for the next pass over A (A@X) to hit.
+__device__ int g_atr_keep_mib = 0;
+void set_atr_keep_mib(int mib, hipStream_t st) {
+  static int cur = -1;
+  if (mib == cur) return;
+  (void)hipMemcpyToSymbolAsync(HIP_SYMBOL(g_atr_keep_mib), &mib, sizeof(int), 0, hipMemcpyHostToDevice, st);
+  cur = mib;
+}
+
 template <typename T, int NT, int PF, int WL, bool NTL>
 __device__ inline int64_t atr_panel(const T* __restrict__ A, const T* __restrict__ R, int64_t m,
                                     int64_t n, int S, typename MF<T>::acc_t (&acc)[4][NT],
@@ -91,6 +102,20 @@ __device__ inline int64_t atr_panel(const T* __restrict__ A, const T* __restrict
 #pragma unroll
     for (int nt = 0; nt < NT; ++nt) rb[p][nt] = rp[off * 4 * L + nt * 16];
   };
+  auto ld_def = [&](int p, int64_t off) {   // default policy (the Infinity-Cache hand-off)
+    off = off < nst ? off : nst - 1;
+    Load4<T, false>::go(ap + off * 4 * n, a[p]);
+#pragma unroll
+    for (int nt = 0; nt < NT; ++nt) rb[p][nt] = rp[off * 4 * L + nt * 16];
+  };
+  // steps [kt, nst) load with the default policy: keep MiB over the grid's W * (n / 64) waves of
+  // 4 rows x 64 columns per step (WL 1: 4 x 256 columns per block step)
+  int64_t keep = 0;
+  if constexpr (NTL) {
+    const int64_t kb = (int64_t)g_atr_keep_mib << 20;
+    keep = kb / ((int64_t)(WL == 0 ? W * (n / 64) : W * (n / 256)) * 4 * (WL == 0 ? 64 : 256) * (int64_t)sizeof(T));
+  }
+  const int64_t kt = nst - keep;
   auto mma_step = [&](int p) {
 #pragma unroll
     for (int e = 0; e < 4; ++e)
@@ -101,11 +126,18 @@ __device__ inline int64_t atr_panel(const T* __restrict__ A, const T* __restrict
 #pragma unroll
     for (int p = 0; p < PF; ++p) ld(p, p);
     int64_t s0 = 0;
-    for (; s0 + PF <= nst; s0 += PF) {
+    for (; s0 + PF <= nst && (keep == 0 || s0 + 2 * PF <= kt); s0 += PF) {
 #pragma unroll
       for (int p = 0; p < PF; ++p) {
         mma_step(p);
         ld(p, s0 + p + PF);
+      }
+    }
+    for (; s0 + PF <= nst; s0 += PF) {   // the kept tail (only with keep > 0)
+#pragma unroll
+      for (int p = 0; p < PF; ++p) {
+        mma_step(p);
+        ld_def(p, s0 + p + PF);
       }
     }
 #pragma unroll

@@ -50,6 +50,17 @@ constexpr int dma_lds_bytes() {
          ((NSRC * KC * 16 * NT * 8 / 1024) % WAVES ? 1024 : 0);
 }
 
+// Infinity-Cache hand-off (tuning experiment, GLX_AX_KEEP_MIB, default 0 = off): with NTL, the
+// last chunks of every block's walk are fetched with the default policy instead, about that many
+// MiB of A over the grid, so they stay in the 256 MiB Infinity Cache for the next pass (A^T R).
+__device__ int g_ax_keep_mib = 0;
+void set_ax_keep_mib(int mib, hipStream_t st) {
+  static int cur = -1;
+  if (mib == cur) return;
+  (void)hipMemcpyToSymbolAsync(HIP_SYMBOL(g_ax_keep_mib), &mib, sizeof(int), 0, hipMemcpyHostToDevice, st);
+  cur = mib;
+}
+
 template <int KC>
 __device__ inline int dma_sw(int i) { return KC >= 32 ? (i & 15) : ((i >> 1) & 7); }
 
@@ -137,12 +148,24 @@ __global__ __launch_bounds__(64 * WAVES) void k_ax_dma(const T* __restrict__ A,
     xdst[r] = tx < NXT ? WAVES * AW + tx * 1024 : -1;
   }
   const int64_t rot = ax_rot(xmap, bx, gx, nch);
+  int64_t kt = nch;   // walk chunks [kt, nch) load with the default policy (the hand-off)
+  if constexpr (NTL) {
+    const int64_t kb = (int64_t)g_ax_keep_mib << 20;
+    if (kb > 0) kt = nch - kb / ((int64_t)gridDim.x * WAVES * AW);
+  }
   auto issue = [&](int64_t c, int slot) {
-    c = (c < nch ? c : nch - 1) + rot;   // the walk starts at chunk rot (mod nch)
+    c = c < nch ? c : nch - 1;
+    const bool nt = c < kt;
+    c += rot;                            // the walk starts at chunk rot (mod nch)
     c = c >= nch ? c - nch : c;
     char* sb = lds + slot * SLOT;
+    if (NTL && nt) {
 #pragma unroll
-    for (int t = 0; t < NIA; ++t) glds16<NTL>(asrc[t] + c * KC, sb + wave * AW + t * 1024);
+      for (int t = 0; t < NIA; ++t) glds16<NTL>(asrc[t] + c * KC, sb + wave * AW + t * 1024);
+    } else {
+#pragma unroll
+      for (int t = 0; t < NIA; ++t) glds16<false>(asrc[t] + c * KC, sb + wave * AW + t * 1024);
+    }
 #pragma unroll
     for (int r = 0; r < NIX; ++r)
       glds16<false>(xsrc[r] + c * KC * L, XDUP && xdst[r] < 0 ? lds + NS * SLOT : sb + xdst[r]);

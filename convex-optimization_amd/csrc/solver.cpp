@@ -83,6 +83,7 @@ constexpr int kBufs = 9;
 constexpr int kTailBytes = 64;   // behind each gradient set: scalars that ride its all-reduce
 constexpr int kRes = 4;
 constexpr int kDcWindow = 8;     // device-controlled ProxGD: iterations in flight (GLX_DC_BATCH)
+constexpr int kKeepMiB = 192;    // Infinity-Cache hand-off between the non-temporal passes
 
 static void validate(const glx_problem* P, const glx_opts* O) {
   if (!P || !O) throw Error{GLX_E_INVALID, "null problem/opts"};
@@ -321,6 +322,15 @@ class Session : public SessionBase {
                             hipHostMallocMapped | hipHostMallocCoherent));
       std::memset(dc_ring_, 0, sizeof(double) * kCtlRec * kCtlMaxBatch);   // tags start at 1
       GLX_HIP(hipHostGetDevicePointer(reinterpret_cast<void**>(&dc_ring_dev_), dc_ring_, 0));
+    }
+    {   // Infinity-Cache hand-off between the two non-temporal passes: the last ~192 MiB each
+        // pass reads stay in the 256 MiB Infinity Cache for the other pass. NS, same box, two
+        // interleaved rounds: 2307 / 2318 it/s against 2252 / 2272 with both off, either alone
+        // in between (profiles/r3_keep/). GLX_AX_KEEP_MIB / GLX_ATR_KEEP_MIB = 0: off.
+      const char* ka = std::getenv("GLX_AX_KEEP_MIB");
+      const char* kr = std::getenv("GLX_ATR_KEEP_MIB");
+      set_ax_keep_mib(ka ? std::atoi(ka) : kKeepMiB, st_);
+      set_atr_keep_mib(kr ? std::atoi(kr) : kKeepMiB, st_);
     }
     GLX_HIP(hipMemsetAsync(ticket_, 0, kTicketBytes, st_));
     GLX_HIP(hipMemsetAsync(pcnt_, 0, sizeof(unsigned) * (P.n / 64 + 64), st_));
