@@ -217,6 +217,11 @@ void launch_finalize_residual(const T* P, int S, const T* B, int nsrc, T* const*
                               double* snap_dst = nullptr, int nsnap = 0, int chain = 0, int S0 = 0,
                               Ctl ctl = Ctl{});
 // state[0..3] = s0..s3, *abort = 0 (one thread; the seed of a device-controlled batch)
+// the decision of a device-controlled ProxGD iteration with a communicator (one thread): out =
+// the all-reduced residual sums (a gradient set's tail); no-op once *c.abort != 0; the record
+// goes to c.rec and to the host ring (host[0..11), then *host_seq = seq)
+void launch_ctl_decide(const Ctl& c, const double* out, double* host, unsigned* host_seq,
+                       unsigned seq, hipStream_t st);
 void launch_ctl_seed(double* state, int* abort, double s0, double s1, double s2, double s3,
                      hipStream_t st);
 template <typename T>

@@ -110,6 +110,23 @@ __device__ inline void ctl_decide(const Ctl& c, const double* out, const double 
   for (int k = 0; k <= 10; ++k) c.rec[k] = rec[k];
 }
 
+// Device-controlled ProxGD with a communicator (solver.cpp dc_queue): the trial's residual sums
+// are final only after the gradient all-reduce that carries them (a gradient set's tail), so the
+// decision runs as its own one-thread launch right behind that all-reduce. Skipped once an earlier
+// decision of the batch has cancelled it; hands its record straight to the host ring.
+__global__ void k_ctl_decide(Ctl c, const double* __restrict__ out, double* host, unsigned* host_seq,
+                             unsigned seq) {
+  if (threadIdx.x != 0) return;
+  if (*c.abort != 0) return;
+  double pre[10];
+  for (int k = 0; k < 6; ++k) pre[k] = c.tr[k];
+  for (int k = 0; k < 4; ++k) pre[6 + k] = c.state[k];
+  double o[4];
+  for (int k = 0; k < 4; ++k) o[k] = out[k];
+  ctl_decide(c, o, pre);
+  publish_packet(c.rec, 11, host, host_seq, seq);
+}
+
 __global__ void k_ctl_seed(double* state, int* abort, double s0, double s1, double s2, double s3) {
   if (threadIdx.x == 0) {
     state[0] = s0;
@@ -738,6 +755,11 @@ void launch_record_f(const double* s, int i_sumsq, int i_reg, double mu, double*
                      hipStream_t st) {
   hipLaunchKernelGGL(k_record_f, dim3(1), dim3(64), 0, st, s, i_sumsq, i_reg, mu, fh, idx);
 }
+void launch_ctl_decide(const Ctl& c, const double* out, double* host, unsigned* host_seq,
+                       unsigned seq, hipStream_t st) {
+  hipLaunchKernelGGL(k_ctl_decide, dim3(1), dim3(64), 0, st, c, out, host, host_seq, seq);
+}
+
 void launch_ctl_seed(double* state, int* abort, double s0, double s1, double s2, double s3,
                      hipStream_t st) {
   hipLaunchKernelGGL(k_ctl_seed, dim3(1), dim3(64), 0, st, state, abort, s0, s1, s2, s3);

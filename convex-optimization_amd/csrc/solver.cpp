@@ -84,6 +84,17 @@ constexpr int kTailBytes = 64;   // behind each gradient set: scalars that ride 
 constexpr int kRes = 4;
 constexpr int kDcWindow = 8;     // device-controlled ProxGD: iterations in flight (GLX_DC_BATCH)
 constexpr int kKeepMiB = 192;    // Infinity-Cache hand-off between the non-temporal passes
+// gradient sets: 2 (current, speculative); with a communicator and device control a ring of
+// window + 2, so that the all-reduces queued behind a cancelling decision (they cannot be
+// gated) never land in the set the host resumes from
+constexpr int kMaxGSets = kCtlMaxBatch / 2 + 2;
+
+// device-controlled batches' window (GLX_DC_BATCH; 0 = the host decides every iteration)
+static int dc_window_env() {
+  const char* dc = std::getenv("GLX_DC_BATCH");
+  const int w = dc ? std::atoi(dc) : kDcWindow;
+  return std::max(0, std::min(w, kCtlMaxBatch / 2));
+}
 
 static void validate(const glx_problem* P, const glx_opts* O) {
   if (!P || !O) throw Error{GLX_E_INVALID, "null problem/opts"};
@@ -174,8 +185,8 @@ template <typename T>
 class Session : public SessionBase {
  public:
   // workspace layout; with ws == nullptr only computes the size
-  static size_t carve(const glx_problem& P, const GemmPlan& plan, int64_t fh_cap, int smode,
-                      void* ws, Session* s) {
+  static size_t carve(const glx_problem& P, const glx_opts& O, const GemmPlan& plan, int64_t fh_cap,
+                      int smode, void* ws, Session* s) {
     Carver c(ws);
     const int64_t nl = P.n * P.l, ml = P.m * P.l;
     const int nb = method_bufs(P.method);
@@ -183,10 +194,12 @@ class Session : public SessionBase {
     for (int i = 1; i < nb; ++i) bufs[i] = static_cast<T*>(c.take(sizeof(T) * nl));
     T* res[kRes];
     for (int i = 0; i < kRes; ++i) res[i] = static_cast<T*>(c.take(sizeof(T) * ml));
-    // two gradient sets (G, its split-K slabs): the current one and the speculative one
-    T* g[2];
-    T* gp[2];
-    for (int k = 0; k < 2; ++k) {
+    // gradient sets (G, its split-K slabs): the current one and the speculative one (a ring with
+    // a communicator and device control, gsets_for)
+    const int ngs = gsets_for(P, O);
+    T* g[kMaxGSets];
+    T* gp[kMaxGSets];
+    for (int k = 0; k < ngs; ++k) {
       g[k] = static_cast<T*>(c.take(sizeof(T) * nl + kTailBytes));   // + scalar tail (comm)
       gp[k] = plan.atr_S > 1 ? static_cast<T*>(c.take(sizeof(T) * nl * plan.atr_S)) : g[k];
     }
@@ -220,7 +233,8 @@ class Session : public SessionBase {
     if (s) {
       for (int i = 0; i < kBufs; ++i) s->X_[i] = bufs[i];
       for (int i = 0; i < kRes; ++i) s->R_[i] = res[i];
-      for (int k = 0; k < 2; ++k) { s->Gs_[k] = g[k]; s->Gps_[k] = gp[k]; }
+      for (int k = 0; k < ngs; ++k) { s->Gs_[k] = g[k]; s->Gps_[k] = gp[k]; }
+      s->nsets_ = ngs;
       s->G_ = g[0]; s->Gp_ = gp[0]; s->Pp_ = pp; s->At_ = at; s->glists_ = glists;
       s->scal_ = scal; s->part_ = part; s->ticket_ = ticket; s->flag_ = flag; s->fh_dev_ = fh;
       s->pcnt_ = pcnt;
@@ -246,6 +260,17 @@ class Session : public SessionBase {
     return gemv_fused_blocks((int)sizeof(T), P.m, P.n, P.l);
   }
 
+  // device control with a communicator: ProxGD, fp64 (the trial sums ride the gradient
+  // all-reduce), line search, fast objective mode
+  static bool dc_comm_ok(const glx_problem& P, const glx_opts& O) {
+    return P.comm != nullptr && P.method == GLX_PROXGD && P.dtype == GLX_F64 &&
+           O.step_type == GLX_STEP_LINE_SEARCH && O.ls_maxit > 0 && O.exact_objective == 0;
+  }
+  static int gsets_for(const glx_problem& P, const glx_opts& O) {
+    const int w = dc_window_env();
+    return (w > 0 && dc_comm_ok(P, O)) ? w + 2 : 2;
+  }
+
   static int64_t fh_capacity(const glx_problem& P, const glx_opts& O) {
     int64_t cap = 3 * (int64_t)O.maxit;
     if (O.max_total_iters > 0) cap = std::min<int64_t>(cap, O.max_total_iters);
@@ -260,10 +285,10 @@ class Session : public SessionBase {
     comm_ = static_cast<glx_comm*>(P.comm);
     fh_cap_ = fh_capacity(P, O);
     smode_ = split_mode(P, O);
-    const size_t need = carve(P, plan_, fh_cap_, smode_, nullptr, nullptr);
+    const size_t need = carve(P, O, plan_, fh_cap_, smode_, nullptr, nullptr);
     if (!ws || ws_bytes < need) throw Error{GLX_E_WORKSPACE, "workspace too small: need " + std::to_string(need) + " bytes"};
     if (reinterpret_cast<uintptr_t>(ws) & 255) throw Error{GLX_E_WORKSPACE, "workspace must be 256-byte aligned"};
-    carve(P, plan_, fh_cap_, smode_, ws, this);
+    carve(P, O, plan_, fh_cap_, smode_, ws, this);
     A_ = static_cast<const T*>(P.A);
     B_ = static_cast<const T*>(P.b);
     // scalar packet: host-mapped, coherent memory the GPU writes directly (k_publish)
@@ -309,13 +334,10 @@ class Session : public SessionBase {
     fused_fista_ok_ = fuse_any && P.method == GLX_FPROXGD;
     // device-controlled batches (dc_run): ProxGD with line search on the fused speculative path
     // of one GPU; GLX_DC_BATCH = iterations in flight (0: the host decides every iteration)
-    {
-      const char* dc = std::getenv("GLX_DC_BATCH");
-      const int w = dc ? std::atoi(dc) : kDcWindow;
-      dc_window_ = std::max(0, std::min(w, kCtlMaxBatch / 2));
-    }
-    if (!(fused_ok_ && comm_ == nullptr && spin_readback_ && O.exact_objective == 0 &&
-          O.step_type == GLX_STEP_LINE_SEARCH && O.ls_maxit > 0))
+    dc_window_ = dc_window_env();
+    if (!(fused_ok_ && spin_readback_ && O.exact_objective == 0 &&
+          O.step_type == GLX_STEP_LINE_SEARCH && O.ls_maxit > 0 &&
+          (comm_ == nullptr || (dc_comm_ok(P, O) && attach_ok_))))
       dc_window_ = 0;
     if (dc_window_ > 0) {
       GLX_HIP(hipHostMalloc(reinterpret_cast<void**>(&dc_ring_), sizeof(double) * kCtlRec * kCtlMaxBatch,
@@ -480,8 +502,9 @@ class Session : public SessionBase {
   // ------------------------------------------------------------------ helpers
   // while a device-controlled batch is queued every reduction carries its abort word: the launch
   // is skipped once a decision has cancelled the rest of the batch (*skip not 0 and not pass)
-  Red red(int slot, int pass = 0) {
-    Red r{part_, ticket_, scal_ + slot};
+  Red red(int slot, int pass = 0) { return red_to(scal_ + slot, pass); }
+  Red red_to(double* out, int pass = 0) {
+    Red r{part_, ticket_, out};
     r.skip = dc_gate_;
     r.skip_pass = pass;
     return r;
@@ -550,7 +573,7 @@ class Session : public SessionBase {
     launch_finalize_residual<T>(Pp_, gat ? ax_split(plan_, 1) : ax_split(plan_, nsrc), B_, nsrc, rsc,
                                 ml_, nullptr, 0, 1, cx,
                                 cx ? nl_ : 0, cmax, comm_ ? nullptr : fh, fh_mu, scal_ + S_DRN,
-                                defer ? Red{part_, ticket_, defer} : red(slot), st_,
+                                defer ? red_to(defer) : red(slot), st_,
                                 snap_trial ? scal_ + S_TR : nullptr,
                                 snap_trial ? scal_ + S_SNAP : nullptr, snap_trial ? 6 : 0,
                                 chain ? 1 : 0, gat ? gsplit_ : 0, dc_ctl_);
@@ -628,6 +651,7 @@ class Session : public SessionBase {
     return {G, 1};
   }
   void use_gset(int set) { gset_ = set; G_ = Gs_[set]; Gp_ = Gps_[set]; }
+  int nset(int set) const { return set + 1 == nsets_ ? 0 : set + 1; }   // the next set of the ring
   double* tail(int set) { return reinterpret_cast<double*>(Gs_[set] + nl_); }
   // merge a speculated trial's residual sums into the next gradient all-reduce
   bool merge_tail() const { return comm_ != nullptr && sizeof(T) == 8; }
@@ -861,13 +885,13 @@ class Session : public SessionBase {
         const bool axp = spec && fused_ok_ && comm_ != nullptr && late_pub && attach_ok_ &&
                          spec_ax_pub_ && ax_pub_ok(plan_, smode_ == 1 ? 1 : nsrc);
         residuals(nsrc, xs, rs, S_RT, X_[ip_], scal_ + S_TR + 3, nullptr, 0.0,
-                  late_pub ? nullptr : &seq, merge ? tail(1 - gset_) : nullptr, skip_ax, axp, emode_);
+                  late_pub ? nullptr : &seq, merge ? tail(nset(gset_)) : nullptr, skip_ax, axp, emode_);
         std::pair<const T*, int> sg;
         if (spec && fused_ok_) {
           // the next iteration's A^T r and first trial at the candidate p_thr, into the other
           // gradient set and the spare buffers (z is free once this trial's A@X has read it)
           Pub pbx;
-          atr_prox(R_[rpt], 1 - gset_, X_[ipt_], if1_, if2_, iz_, O_.alpha0, merge ? nsrc : 0,
+          atr_prox(R_[rpt], nset(gset_), X_[ipt_], if1_, if2_, iz_, O_.alpha0, merge ? nsrc : 0,
                    late_pub ? &seq : nullptr, axp ? &pbx : nullptr);
           spec_trial = true;
           if (axp) {
@@ -880,13 +904,13 @@ class Session : public SessionBase {
             ax_queued_ = true;
           }
         } else if (spec) {
-          sg = gradient(R_[rpt], 1 - gset_);   // gradient at the candidate p_thr
+          sg = gradient(R_[rpt], nset(gset_));   // gradient at the candidate p_thr
         }
         wait_readback(seq);
         const double gz = 0.5 * hs_[S_RT];
         if (gz <= gx_ - t * hs_[S_TR + 0] + 0.5 * t * hs_[S_TR + 1]) {
           accepted = true;
-          if (spec && !spec_trial) { spec_ready_ = true; spec_g_ = sg; spec_set_ = 1 - gset_; }
+          if (spec && !spec_trial) { spec_ready_ = true; spec_g_ = sg; spec_set_ = nset(gset_); }
           spec_on_ = (it == 0);
           break;
         }
@@ -939,7 +963,7 @@ class Session : public SessionBase {
     ix_ = ip_; ixt_ = ipt_; ip_ = if1_; ipt_ = if2_;
     if1_ = ox; if2_ = oxt;
     spec_trial_ready_ = true;
-    spec_set_ = 1 - gset_;
+    spec_set_ = nset(gset_);
     spec_trial_mu_ = mu_;
     spec_trial_t_ = O_.alpha0;
   }
@@ -959,13 +983,69 @@ class Session : public SessionBase {
   // the second trial; a stop ends the phase there. Results are bit-identical to host control.
   struct Roles { int ix, ixt, ip, ipt, if1, if2, iz, irg, gset; };
   bool dc_ready() const {
+    // (with a communicator the first trial's A@X is normally already queued: the batch uses it)
     return dc_window_ > 0 && spec_trial_ready_ && spec_trial_mu_ == mu_ &&
-           spec_trial_t_ == O_.alpha0 && want_spec(0) && !ax_queued_;
+           spec_trial_t_ == O_.alpha0 && want_spec(0) && (comm_ != nullptr || !ax_queued_);
   }
   // Gated (cancellable) launches: the finalize (it would overwrite the decision state and the
   // gradient residual of the iteration the host resumes) and the speculative fused kernel (the
   // next gradient set and iterate buffers). A@X and the gather only write the scratch slabs, so
   // a cancelled one runs to no effect instead of testing the flag.
+  Ctl dc_make_ctl(int64_t tag) const {
+    Ctl c{};
+    const int64_t slot = (tag % kCtlMaxBatch) * kCtlRec;
+    c.rec = dc_rec_ + slot;
+    c.state = dc_state_;
+    c.abort = dc_abort_;
+    c.tr = scal_ + S_TR;
+    c.tag = (double)tag;
+    c.t = O_.alpha0;
+    c.mu0 = P_.mu0;
+    c.ftol = O_.ftol;
+    c.nl = (double)nl_;
+    c.stable_thr = O_.stable_len_threshold;
+    c.use_sp = use_sparsity_ ? 1 : 0;
+    c.emode = emode_ ? 1 : 0;
+    c.pass = 1 + (int)(tag % 0x3FFFFFFF);
+    return c;
+  }
+  // With a communicator (f64): the trial's A@X is queued already (the previous segment, or the
+  // host path before the batch); its finalize defers the residual sums into the next gradient
+  // set's tail; A^T r of the candidate and the all-reduce of [G | tail] (not gated: a ring of
+  // gradient sets, kMaxGSets); the decision (k_ctl_decide, gated) from the all-reduced sums and
+  // the trial sums k_prox_pgd left in S_TR; then the next trial (k_prox_pgd, gated) and its
+  // A@X (not gated: scratch slabs). A stop cancels everything behind it too: the next phase
+  // starts from the gradient set the all-reduce in front of the decision completed.
+  void dc_queue_comm(Roles& q, int64_t tag, bool first) {
+    const int rz = (q.irg + 1) % kRes, rpt = (q.irg + 2) % kRes, rp = (q.irg + 3) % kRes;
+    const T* xs[3] = {X_[q.iz], X_[q.ipt], X_[q.ip]};
+    T* rs[3] = {R_[rz], R_[rpt], R_[rp]};
+    if (first && !ax_queued_) {
+      if (smode_ == 1) cand_ax(xs);
+      else spec_ax(2, xs, Pub{}, emode_ ? zf_ : nullptr);
+    }
+    dc_gate_ = dc_abort_;
+    const int ns = nset(q.gset);
+    residuals(2, xs, rs, S_RT, X_[q.ip], scal_ + S_TR + 3, nullptr, 0.0, nullptr, tail(ns), true,
+              false, emode_);
+    gradient(R_[rpt], ns, 2);
+    const int64_t slot = (tag % kCtlMaxBatch) * kCtlRec;
+    launch_ctl_decide(dc_make_ctl(tag), tail(ns), dc_ring_dev_ + slot,
+                      reinterpret_cast<unsigned*>(dc_ring_dev_ + slot + kCtlRec - 1), (unsigned)tag, st_);
+    check_launch();
+    launch_prox_pgd<T>(X_[q.ipt], Gs_[ns], 1, nullptr, X_[q.if1], X_[q.if2], X_[q.iz], n_, l_,
+                       O_.alpha0, mu_, O_.thres, red(S_TR), st_, Pub{}, ezf());
+    check_launch();
+    const T* sx[3] = {X_[q.iz], X_[q.if2], X_[q.if1]};   // [z | p_thr | p] of that trial
+    if (smode_ == 1) cand_ax(sx);
+    else spec_ax(2, sx, Pub{}, emode_ ? zf_ : nullptr);
+    dc_gate_ = nullptr;
+    q.irg = rpt;
+    const int ox = q.ix, oxt = q.ixt;
+    q.ix = q.ip; q.ixt = q.ipt; q.ip = q.if1; q.ipt = q.if2;
+    q.if1 = ox; q.if2 = oxt;
+    q.gset = ns;
+  }
   void dc_queue(Roles& q, int64_t tag) {
     const int rz = (q.irg + 1) % kRes, rpt = (q.irg + 2) % kRes, rp = (q.irg + 3) % kRes;
     const T* xs[3] = {X_[q.iz], X_[q.ipt], X_[q.ip]};
@@ -996,7 +1076,7 @@ class Session : public SessionBase {
     dc_pub_.host = dc_ring_dev_ + slot;
     dc_pub_.host_seq = reinterpret_cast<unsigned*>(dc_ring_dev_ + slot + kCtlRec - 1);
     dc_pub_.seq = (unsigned)tag;
-    atr_prox(R_[rpt], 1 - q.gset, X_[q.ipt], q.if1, q.if2, q.iz, O_.alpha0);
+    atr_prox(R_[rpt], nset(q.gset), X_[q.ipt], q.if1, q.if2, q.iz, O_.alpha0);
     dc_pub_ = Pub{};
     dc_pass_ = 0;
     dc_gate_ = nullptr;
@@ -1005,7 +1085,7 @@ class Session : public SessionBase {
     const int ox = q.ix, oxt = q.ixt;
     q.ix = q.ip; q.ixt = q.ipt; q.ip = q.if1; q.ipt = q.if2;
     q.if1 = ox; q.if2 = oxt;
-    q.gset = 1 - q.gset;
+    q.gset = nset(q.gset);
   }
   const double* dc_wait(int64_t tag) {
     const double* rec = dc_ring_ + (tag % kCtlMaxBatch) * kCtlRec;
@@ -1041,7 +1121,8 @@ class Session : public SessionBase {
     const int64_t w = std::min<int64_t>(dc_window_, budget);
     auto push = [&]() {   // tags are never reused: dc_tag_ = the last one queued
       dc_tag_ = tag0 + 1 + queued++;
-      dc_queue(q, dc_tag_);
+      if (comm_) dc_queue_comm(q, dc_tag_, queued == 1);
+      else dc_queue(q, dc_tag_);
     };
     while (queued < w) push();
     int prev = 0;
@@ -1078,6 +1159,8 @@ class Session : public SessionBase {
       proxgd_spec_rotate();
       prev = code;
     }
+    // with a communicator the last segment queued the next trial's A@X
+    ax_queued_ = comm_ != nullptr;
   }
 
   // A^T r fused with a ProxGD trial at x (gradient set `set`, outputs X_[op], X_[opt], X_[oz]).
@@ -1186,19 +1269,19 @@ class Session : public SessionBase {
         fs_batch = fsplit_ && kslot_ >= 0 && dense_left_ == 0;
         if (fs_batch) {   // A xc dense, A e_c gathered, A y_next by linearity
           fista_split_batch(R_[ryn], theta, theta_next, S_RT, X_[ic_], scal_ + S_TR + i_max,
-                            late_pub ? nullptr : &seq, merge ? tail(1 - gset_) : nullptr);
+                            late_pub ? nullptr : &seq, merge ? tail(nset(gset_)) : nullptr);
         } else {
           residuals(2, xs, rs, S_RT, X_[ic_], scal_ + S_TR + i_max, nullptr, 0.0,   // A @ [x | y_next]
-                    late_pub ? nullptr : &seq, merge ? tail(1 - gset_) : nullptr);
+                    late_pub ? nullptr : &seq, merge ? tail(nset(gset_)) : nullptr);
         }
         std::pair<const T*, int> sg;
         if (spec && fuse) {
           // the next iteration's gradient at y_next and its first trial (t, theta' = theta_next)
-          atr_fista(R_[ryn], 1 - gset_, X_[iyn_], X_[ic_], ff1_, ff2_, ff3_, t, theta_next,
+          atr_fista(R_[ryn], nset(gset_), X_[iyn_], X_[ic_], ff1_, ff2_, ff3_, t, theta_next,
                     2.0 / (double)(inner_ + 3), merge ? 2 : 0, late_pub ? &seq : nullptr);
           spec_trial = true;
         } else if (spec) {
-          sg = gradient(R_[ryn], 1 - gset_);   // gradient at the next y
+          sg = gradient(R_[ryn], nset(gset_));   // gradient at the next y
         }
         wait_readback(seq);
         if (gy_pending_) { gy_sq_ = hs_[S_RG]; gy_pending_ = false; }
@@ -1209,7 +1292,7 @@ class Session : public SessionBase {
         }
         if (gxc <= gy + hs_[S_TR + 0] + hs_[S_TR + 1] / (2 * t)) {
           accepted = true;
-          if (spec && !spec_trial) { spec_ready_ = true; spec_g_ = sg; spec_set_ = 1 - gset_; }
+          if (spec && !spec_trial) { spec_ready_ = true; spec_g_ = sg; spec_set_ = nset(gset_); }
           spec_on_ = (it == 0);
           break;
         }
@@ -1229,7 +1312,7 @@ class Session : public SessionBase {
       ic_ = ff1_; ivn_ = ff2_; iyn_ = ff3_;
       ff1_ = ox; ff2_ = ov; ff3_ = oy;
       spec_trial_ready_ = true;
-      spec_set_ = 1 - gset_;
+      spec_set_ = nset(gset_);
       spec_trial_mu_ = mu_;
       spec_trial_t_ = t;
       spec_trial_theta_ = theta_next;
@@ -1414,8 +1497,9 @@ class Session : public SessionBase {
   T* X_[kBufs] = {};
   T* R_[kRes] = {nullptr, nullptr, nullptr, nullptr};
   T *G_ = nullptr, *Gp_ = nullptr, *Pp_ = nullptr;
-  T* Gs_[2] = {nullptr, nullptr};
-  T* Gps_[2] = {nullptr, nullptr};
+  T* Gs_[kMaxGSets] = {};
+  T* Gps_[kMaxGSets] = {};
+  int nsets_ = 2;
   double *scal_ = nullptr, *part_ = nullptr, *fh_dev_ = nullptr;
   double *hs_ = nullptr, *hs_dev_ = nullptr;
   unsigned *hseq_ = nullptr, *hseq_dev_ = nullptr;
@@ -1502,8 +1586,8 @@ static size_t session_bytes(const glx_problem& P, const glx_opts& O) {
   const GemmPlan plan = session_plan(P, O);
   const int sm = split_mode(P, O);
   if (P.dtype == GLX_F64)
-    return Session<double>::carve(P, plan, Session<double>::fh_capacity(P, O), sm, nullptr, nullptr);
-  return Session<float>::carve(P, plan, Session<float>::fh_capacity(P, O), sm, nullptr, nullptr);
+    return Session<double>::carve(P, O, plan, Session<double>::fh_capacity(P, O), sm, nullptr, nullptr);
+  return Session<float>::carve(P, O, plan, Session<float>::fh_capacity(P, O), sm, nullptr, nullptr);
 }
 
 template <typename F>

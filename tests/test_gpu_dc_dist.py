@@ -1,0 +1,106 @@
+"""Device-controlled ProxGD with a communicator (solver.cpp dc_queue_comm, kernels_elem.hip
+k_ctl_decide): the world-2 twins of tests/test_gpu_dc.py.
+
+Two ranks share the box's GPU through the host-staged transport (RCCL needs one GPU per rank),
+each solving its row shard of the same instance; the decisions run on the device behind each
+gradient all-reduce. Every run must be bit-identical to host control (GLX_DC_BATCH=0) — same k,
+f_hist to the last bit, fval, iterate and threshold statistics — and identical on both ranks.
+fp32 keeps host control with a communicator (its trial sums do not ride the gradient
+all-reduce), so its twin checks that it stays host-controlled and identical.
+"""
+import json
+import os
+import socket
+import subprocess
+import sys
+
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _twin(tmp_path, shape, dtype="f64", scale=1.0, opts=None, env=None, windows="0,8", slices=0):
+    out = tmp_path / "dc_twin.json"
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes", "1", "--nproc-per-node", "2",
+           "--master-addr", "127.0.0.1", "--master-port", str(_port()),
+           os.path.join(ROOT, "tests", "dc_dist_worker.py"), "--shape", ",".join(map(str, shape)),
+           "--dtype", dtype, "--alpha-scale", str(scale), "--opts", json.dumps(opts or {}),
+           "--env", json.dumps(env or {}), "--windows", windows, "--slices", str(slices),
+           "--out", str(out)]
+    p = subprocess.run(cmd, env=dict(os.environ, OMP_NUM_THREADS="1"), capture_output=True,
+                       text=True, timeout=140)
+    assert p.returncode == 0, p.stdout[-3000:] + p.stderr[-3000:]
+    with open(out) as fh:
+        return json.load(fh)
+
+
+def _same(a, b):
+    assert a["k"] == b["k"]
+    assert a["f_hist"] == b["f_hist"]
+    assert a["fval"] == b["fval"]
+    assert a["x_sha"] == b["x_sha"]
+    assert a["stats"][:3] == b["stats"][:3]
+
+
+CASES = [   # the cases of test_gpu_dc.py
+    ((256, 16384, 32), "f64", 1.0, {"maxit": 300}, 0.5),
+    ((256, 16384, 32), "f64", 2.5, {"maxit": 120}, 0.0),
+    ((512, 1024, 16), "f64", 1.0, {}, 0.5),
+    ((512, 1024, 16), "f64", 2.5, {}, 1e-4),
+    ((512, 1024, 16), "f32", 1.0, {}, 0.0),
+    ((1024, 2048, 32), "f64", 1.0, {"maxit": 400}, 0.5),
+]
+
+
+@pytest.mark.parametrize("shape,dtype,scale,opts,frac", CASES)
+def test_device_control_world2_bit_identical(tmp_path, shape, dtype, scale, opts, frac):
+    r = _twin(tmp_path, shape, dtype, scale, opts)
+    host, dev = r["0"], r["8"]
+    for ranks in (host, dev):
+        for x in ranks[1:]:
+            _same(x, ranks[0])
+    _same(dev[0], host[0])
+    assert host[0]["stats"][7] == 0
+    d = dev[0]
+    if dtype == "f32":
+        assert d["stats"][7] == 0
+    else:
+        assert d["stats"][7] >= frac * d["k"], d["stats"]
+        if frac >= 0.5:
+            assert d["syncs"] < 0.1 * host[0]["syncs"]
+
+
+def test_world2_window_sizes(tmp_path):
+    r = _twin(tmp_path, (512, 1024, 16), scale=2.5, windows="0,1,3,32")
+    for w in ("1", "3", "32"):
+        _same(r[w][0], r["0"][0])
+        _same(r[w][1], r["0"][0])
+
+
+def test_world2_run_in_slices(tmp_path):
+    r = _twin(tmp_path, (512, 1024, 16), slices=7)
+    _same(r["8"][0], r["0"][0])
+
+
+def test_world2_split_candidate_gather_form(tmp_path):
+    r = _twin(tmp_path, (256, 16384, 32), scale=1.5, opts={"maxit": 150},
+              env={"GLX_SPLIT_CAND": "1"})
+    _same(r["8"][0], r["0"][0])
+    _same(r["8"][1], r["0"][0])
+    assert r["8"][0]["stats"][7] > 0
+
+
+def test_world2_max_total_iters(tmp_path):
+    r = _twin(tmp_path, (512, 1024, 16), opts={"max_total_iters": 37})
+    assert r["8"][0]["k"] == 37
+    _same(r["8"][0], r["0"][0])
