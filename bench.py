@@ -21,11 +21,12 @@ load run fast, then throttles (A@X 290 -> 400+ us) and recovers over ~30 ms
 solver. The timed session restarts from x0, so the iterations timed are the same ones.
 
 Also reported, for the dominant kernel (the dense A@X pass; at NS one right-hand side, A p_thr of
-the split-candidate trial, ~40 % of the iteration):
+the split-candidate trial, on the LDS-DMA tile, ~40 % of the iteration):
   roofline — the kernel's bound is whichever of MFMA time (flops / dense MFMA peak) and HBM time
              (bytes / 8 TB/s) is larger for this (m, n, l, dtype) and right-hand-side count: HBM
-             at NS (one right-hand side, l/4 flop/B in fp64) and for C4 (l = 1); MFMA for the
-             batched two-source passes (FProxGD without the split form, C3 in fp32). achieved =
+             at NS (one right-hand side: l/4 flop/B in fp64, 109 us of MFMA against 135 us of HBM),
+             at C2 and for C4 (l = 1); MFMA for the batched two-source passes (FProxGD's dense
+             batches, C3 in fp32). achieved =
              algorithmic flops 2*m*n*l*rhs (or bytes s*(m n + (m+n) l rhs)) per launch / average
              launch time from HIP events recorded on the solver's stream around every k-th dense
              A@X / A^T r launch of the timed region (--profile k, default min(16, steps/8); each
@@ -304,23 +305,21 @@ def main():
         ax_avg_s = (ax_ms / max(1, ax_n)) / 1e3
         atr_avg_s = (atr_ms / max(1, atr_n)) / 1e3
         # dense right-hand sides batched per A@x launch (e.g. A @ [z | p_thr | p] in exact mode).
-        # ProxGD's split-candidate mode batches [e | p_thr]: e = p - p_thr is nonzero only in the
-        # rows the hard threshold touched, its MFMAs run on flagged K chunks only, and it is not
-        # counted as a dense source; its algorithmic work is 2 m l flops per such row.
-        # Gather form (default): A e reads the flagged rows of a transposed copy of A (m values
-        # each) on top of the dense pass; the "sp" form skips unflagged K chunks in the tile.
+        # ProxGD's split-candidate mode: one dense pass A p_thr, and A e (e = p - p_thr, nonzero
+        # only in the rows the hard threshold touched) gathered from the flagged rows of a
+        # transposed copy of A (m values each); its algorithmic work is 2 m l flops per such row.
         nsrc = work["ax_sources"] / max(1, work["ax_calls"])
         # the solver's split-candidate rule (solver.cpp split_mode): fp64, not exact, A of this
-        # rank >= 768 MiB unless GLX_SPLIT_CAND=1/sp forces it; FProxGD only in the gather form
+        # rank >= 768 MiB unless GLX_SPLIT_CAND=1 forces it; l in {16, 32} and n < 65536 (gather)
         split_env = os.environ.get("GLX_SPLIT_CAND", "")
         split_on = (args.dtype == "f64" and not args.exact and split_env != "0" and
-                    (ml * n * 8 >= 768 * 2 ** 20 or split_env in ("1", "sp")))
+                    (ml * n * 8 >= 768 * 2 ** 20 or split_env == "1"))
         gather_fits = l in (16, 32) and n <= 65535
         st = res["stats"]
         if args.method == "gl_ProxGD_primal":
-            split_cand = split_on
+            split_cand = split_on and gather_fits
             sparse_rows = st[1] / max(1.0, st[2]) if split_cand else 0.0
-            gather_rows = sparse_rows if (split_cand and split_env != "sp" and gather_fits) else 0.0
+            gather_rows = sparse_rows
         elif args.method == "gl_FProxGD_primal":
             split_cand = (split_on and gather_fits and
                           os.environ.get("GLX_SPLIT_FISTA", "") != "0")
@@ -367,8 +366,7 @@ def main():
                 "bytes_per_launch": ax_bytes, "avg_launch_us": ax_avg_s * 1e6, "launches_timed": ax_n,
                 "timed_every": args.profile,
                 "rhs_per_launch": nsrc,
-                "split_candidate": (False if not split_cand else
-                                    ("sp" if (split_env == "sp" or not gather_fits) else "gather")),
+                "split_candidate": "gather" if split_cand else False,
                 "sparse_rows_per_launch": sparse_rows, "hbm_GBs": ax_gbs, "hbm_frac": ax_gbs / HBM_PEAK_GBS if ax_n else None,
                 "mfma_tflops": ax_tf, "mfma_frac": ax_tf / peak_tf if ax_n else None,
                 "atr_avg_launch_us": atr_avg_s * 1e6,

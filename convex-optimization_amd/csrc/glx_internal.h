@@ -46,20 +46,30 @@ struct Red {
 //   state[0..3] = gx (1/2 ||A thr(x) - b||^2), f and sparsity of the last record, stable count
 //   tr = the trial's six sums (k_prox_pgd / k_atr_prox), t = the trial's step
 // On acceptance the next record (f, s) and the stop rule are evaluated and the state advances.
-// *abort = 0 (accepted), pass (accepted, the next record stops the phase), -1 (rejected):
+// *abort = 0 (accepted), pass (accepted, the next record stops the phase, or code 3), -1 (rejected):
 // the speculative gradient queued right behind this decision runs on 0 and on this tag
-// (Red::skip_pass), the rest of the batch only on 0. ring[10] = 0, 1 (stop), 2 (rejected).
+// (Red::skip_pass), the rest of the batch only on 0. ring[10] = 0, 1 (stop), 2 (rejected),
+// 3 (FProxGD: accepted, nnz budget exceeded).
 // rec[0..10] (device) = the four residual sums, the six trial sums and the code as a double.
 // The speculative kernel queued behind the decision hands rec to the host from its publisher
 // workgroup (Pub), also when the decision cancels it, so the PCIe write latency stays off the
 // finalize's critical path.
+//
+// mode 1 = FProxGD's backtracking test (gl_FProxGD_primal.py:89-103): state[0] = ||A y - b||^2 of
+// the current y (not halved), the test g(xc) <= g(y) + <g, xc - y> + ||xc - y||^2 / (2t) from the
+// batch's residual sums and the trial's four sums, and on acceptance state[0] = ||A y_next - b||^2.
+// A gathered (split-candidate) batch also checks nnz(e_c) = out[2] against nnz_budget (>= 0): above
+// it the next batches are dense on the host path (solver.cpp kFistaDenseRun), so the decision
+// cancels the batch behind it like a stop (code 3: accepted, the speculative kernel runs).
 struct Ctl {
   double* rec = nullptr;
   double* state = nullptr;
   int* abort = nullptr;
   const double* tr = nullptr;
   double tag = 0.0, t = 0.0, mu0 = 0.0, ftol = 0.0, nl = 1.0;
+  double nnz_budget = -1.0;
   int stable_thr = 0, use_sp = 1, emode = 0;
+  int mode = 0;    // 0 ProxGD, 1 FProxGD
   int pass = 0;    // nonzero; the abort word's value for "stop" (Red::skip_pass of the kernel behind)
 };
 constexpr int kCtlRec = 16;        // doubles per ring record
@@ -121,13 +131,10 @@ std::string describe_plan(const GemmPlan& p);
 // P[src][ax_split(p, nsrc)][m][l]; skipped entirely unless gate == NULL or *gate == epoch.
 // pub.host != NULL: the launch also hands that scalar packet to the host from its first
 // workgroup (needs ax_pub_ok: the kind-5 LDS tile for nsrc).
-// sf != NULL: n row flags of X[0] (sf[k] == 0 => row k of X[0] is exactly zero); the kind-5
-// tile then skips the MFMAs of X[0] on K chunks without a flagged row (same result: the
-// skipped products are exact zeros). Other tiles ignore it.
 bool ax_pub_ok(const GemmPlan& p, int nsrc);
 template <typename T>
 void launch_ax(const GemmPlan& p, int nsrc, const T* A, const T* const* X, T* P, const int* gate,
-               int epoch, hipStream_t st, Pub pub = Pub{}, const uint8_t* sf = nullptr);
+               int epoch, hipStream_t st, Pub pub = Pub{});
 // the kind-8 (LDS-DMA, f64) A @ X tile of `code` (kernels_axdma.hip); false: unknown code.
 // dma_lds_need: its LDS bytes for l columns and nsrc right-hand sides (<= 160 KiB to launch).
 template <typename T>
@@ -253,7 +260,7 @@ template <typename T>
 void launch_finalize_fista(const T* P, int S, const T* Pe, int S0, const T* B, T* Ry, const T* sxo,
                            T* sxo_out, int64_t ml, double a1, double b1, double theta, const T* cx,
                            int64_t cn, const double* cmax, const unsigned* counts, int nl, Red red,
-                           hipStream_t st);
+                           hipStream_t st, Ctl ctl = Ctl{});
 // plain prox of W (glx_prox): out: [sum ||x_i||, max |x|]
 template <typename T>
 void launch_prox_plain(const T* w, T* x, int64_t n, int64_t l, double t, double mu, double thres,

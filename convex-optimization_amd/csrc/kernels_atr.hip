@@ -343,6 +343,11 @@ __global__ __launch_bounds__(256, sizeof(T) == 8 ? 2 : 1) void k_atr_fista(const
                                                    double b1_, Red red, Pub pub, int S,
                                                    T* __restrict__ Gp, unsigned* __restrict__ pcnt,
                                                    T* __restrict__ ec, uint8_t* __restrict__ zf) {
+  if (red_skipped(red)) {   // cancelled by a device-side decision (as k_atr_prox)
+    if (pub.host != nullptr && blockIdx.x == 0 && threadIdx.x == 0)
+      publish_packet(pub.s, pub.ns, pub.host, pub.host_seq, pub.seq);
+    return;
+  }
   if (publisher_first<4, 0x8u>(pub, red)) return;
   typedef MF<T> M;
   constexpr int L = 16 * NT;

@@ -375,49 +375,17 @@ static void ax_dma_go(const GemmPlan& p, int S, const T* A, const T* const* X, T
   }
 }
 
-// kind 5 codes: 5 MT PF VPL WAVES; kind 8 (LDS-DMA): 8 NS KC/16 NTL WAVES
-// kind-8 code: 8 NS KC/16 NTL WAVES (LDS slots, chunk columns, non-temporal A, waves per block)
+// The planner's LDS-DMA tiles (kernels_gemm.hip lds_plan). Code: 9 NS KC/16 flags WAVES, kind 9 =
+// two 16-row tiles per wave; flags 7 = non-temporal A + hoisted, pipelined operand reads with the
+// DMA issues interleaved into the MFMAs, 6 = the same with the default load policy. The round-3
+// sweep's other forms (one row tile per wave, 3-4 ring slots, 16-wave blocks, 16-column chunks,
+// no hoisting / pipelining) measured slower and are no longer instantiated.
 template <typename T, int NT, int NSRC>
 static bool dma_code(const GemmPlan& p, int code, int S, const T* A, const T* const* X, T* P,
                      const int* gate, int epoch, hipStream_t st, Pub pub) {
   switch (code) {
-    case 84208: ax_dma_go<T, NT, NSRC, 4, 32, 8, false>(p, S, A, X, P, gate, epoch, st, pub); return true;
-    case 84218: ax_dma_go<T, NT, NSRC, 4, 32, 8, true>(p, S, A, X, P, gate, epoch, st, pub); return true;
-    case 83208: ax_dma_go<T, NT, NSRC, 3, 32, 8, false>(p, S, A, X, P, gate, epoch, st, pub); return true;
-    case 83218: ax_dma_go<T, NT, NSRC, 3, 32, 8, true>(p, S, A, X, P, gate, epoch, st, pub); return true;
-    case 82408: ax_dma_go<T, NT, NSRC, 2, 64, 8, false>(p, S, A, X, P, gate, epoch, st, pub); return true;
-    case 82418: ax_dma_go<T, NT, NSRC, 2, 64, 8, true>(p, S, A, X, P, gate, epoch, st, pub); return true;
-    case 88108: ax_dma_go<T, NT, NSRC, 8, 16, 8, false>(p, S, A, X, P, gate, epoch, st, pub); return true;
-    case 88118: ax_dma_go<T, NT, NSRC, 8, 16, 8, true>(p, S, A, X, P, gate, epoch, st, pub); return true;
-    case 85208: ax_dma_go<T, NT, NSRC, 5, 32, 4, false>(p, S, A, X, P, gate, epoch, st, pub); return true;
-    case 85218: ax_dma_go<T, NT, NSRC, 5, 32, 4, true>(p, S, A, X, P, gate, epoch, st, pub); return true;
-    case 84204: ax_dma_go<T, NT, NSRC, 4, 32, 4, false>(p, S, A, X, P, gate, epoch, st, pub); return true;
-    case 84214: ax_dma_go<T, NT, NSRC, 4, 32, 4, true>(p, S, A, X, P, gate, epoch, st, pub); return true;
-    // digit 4 = 2 | NTL: LDS reads hoisted ahead of the MFMAs; waves digit 1 = 16 waves
-    case 83238: ax_dma_go<T, NT, NSRC, 3, 32, 8, true, true>(p, S, A, X, P, gate, epoch, st, pub); return true;
-    case 84238: ax_dma_go<T, NT, NSRC, 4, 32, 8, true, true>(p, S, A, X, P, gate, epoch, st, pub); return true;
-    case 83228: ax_dma_go<T, NT, NSRC, 3, 32, 8, false, true>(p, S, A, X, P, gate, epoch, st, pub); return true;
-    case 84131: ax_dma_go<T, NT, NSRC, 4, 16, 16, true, true>(p, S, A, X, P, gate, epoch, st, pub); return true;
-    case 84111: ax_dma_go<T, NT, NSRC, 4, 16, 16, true, false>(p, S, A, X, P, gate, epoch, st, pub); return true;
-    case 82231: ax_dma_go<T, NT, NSRC, 2, 32, 16, true, true>(p, S, A, X, P, gate, epoch, st, pub); return true;
-    // digit 5 = 4 | NTL: software-pipelined operand reads
-    case 83258: ax_dma_go<T, NT, NSRC, 3, 32, 8, true, false, true>(p, S, A, X, P, gate, epoch, st, pub); return true;
-    case 84258: ax_dma_go<T, NT, NSRC, 4, 32, 8, true, false, true>(p, S, A, X, P, gate, epoch, st, pub); return true;
-    case 83248: ax_dma_go<T, NT, NSRC, 3, 32, 8, false, false, true>(p, S, A, X, P, gate, epoch, st, pub); return true;
-    case 84151: ax_dma_go<T, NT, NSRC, 4, 16, 16, true, false, true>(p, S, A, X, P, gate, epoch, st, pub); return true;
-    // digit 7 / 6 = pipelined with the DMAs and reads interleaved into the MFMAs (NTL / not)
-    case 83278: ax_dma_go<T, NT, NSRC, 3, 32, 8, true, true, true>(p, S, A, X, P, gate, epoch, st, pub); return true;
-    case 93178: ax_dma_go<T, NT, NSRC, 3, 16, 8, true, true, true, 2>(p, S, A, X, P, gate, epoch, st, pub); return true;
     case 92278: ax_dma_go<T, NT, NSRC, 2, 32, 8, true, true, true, 2>(p, S, A, X, P, gate, epoch, st, pub); return true;
-    case 93168: ax_dma_go<T, NT, NSRC, 3, 16, 8, false, true, true, 2>(p, S, A, X, P, gate, epoch, st, pub); return true;
     case 92268: ax_dma_go<T, NT, NSRC, 2, 32, 8, false, true, true, 2>(p, S, A, X, P, gate, epoch, st, pub); return true;
-    case 94178: ax_dma_go<T, NT, NSRC, 4, 16, 8, true, true, true, 2>(p, S, A, X, P, gate, epoch, st, pub); return true;
-    case 94168: ax_dma_go<T, NT, NSRC, 4, 16, 8, false, true, true, 2>(p, S, A, X, P, gate, epoch, st, pub); return true;
-    // kind 9: two 16-row tiles per wave (X reads shared by both), pipelined
-    case 94158: ax_dma_go<T, NT, NSRC, 4, 16, 8, true, false, true, 2>(p, S, A, X, P, gate, epoch, st, pub); return true;
-    case 94148: ax_dma_go<T, NT, NSRC, 4, 16, 8, false, false, true, 2>(p, S, A, X, P, gate, epoch, st, pub); return true;
-    case 93158: ax_dma_go<T, NT, NSRC, 3, 16, 8, true, false, true, 2>(p, S, A, X, P, gate, epoch, st, pub); return true;
-    case 92258: ax_dma_go<T, NT, NSRC, 2, 32, 8, true, false, true, 2>(p, S, A, X, P, gate, epoch, st, pub); return true;
     default: return false;
   }
 }

@@ -73,8 +73,9 @@ __device__ inline T group_slab_sum(const T* __restrict__ P, int S, int64_t ml, i
   return v;
 }
 
-// Device-side control of a ProxGD line-search iteration (struct Ctl, solver.cpp dc_batch): the
-// Armijo test of gl_ProxGD_primal.py:89-92 with t = the trial's step, then — on acceptance — the
+// Device-side control of a ProxGD (mode 0) / FProxGD (mode 1) line-search iteration (struct Ctl,
+// solver.cpp dc_run / fista_dc_run): the Armijo test of gl_ProxGD_primal.py:89-92 (FProxGD's
+// backtracking test, gl_FProxGD_primal.py:92-97) with t = the trial's step, then — on acceptance — the
 // next record's objective and sparsity (:132-133 via the split-candidate/dense residual sums) and
 // the stop rule of :118-125. The expressions are the host's (solver.cpp iter_proxgd, stop_rule)
 // term for term, so with -ffp-contract=off the decision is the host's bit for bit; the host
@@ -87,25 +88,36 @@ __device__ inline void ctl_decide(const Ctl& c, const double* out, const double 
   double rec[kCtlRec];
   for (int k = 0; k < 4; ++k) rec[k] = out[k];
   for (int k = 0; k < 6; ++k) rec[4 + k] = tr[k];
-  const double gz = 0.5 * out[0];
-  const double gx = pre[6];
-  const bool acc = gz <= gx - c.t * tr[0] + 0.5 * c.t * tr[1];
+  bool acc;
+  if (c.mode == 1) {   // FProxGD (solver.cpp fista_trials): g(xc) <= g(y) + <g, xc - y> + |xc - y|^2/(2t)
+    const double gy = 0.5 * pre[6], gxc = 0.5 * out[0];
+    acc = gxc <= gy + tr[0] + tr[1] / (2 * c.t);
+  } else {             // ProxGD (iter_proxgd): g(z) <= g(x) - t <g, G_t> + t/2 |G_t|^2
+    const double gz = 0.5 * out[0];
+    acc = gz <= pre[6] - c.t * tr[0] + 0.5 * c.t * tr[1];
+  }
   int code = 2;
   if (acc) {
-    const double sqx = (c.emode || tr[4] != 0) ? out[0] : out[1];
-    const double f = 0.5 * sqx + c.mu0 * tr[2];
+    double f;
+    if (c.mode == 1) {
+      f = 0.5 * out[0] + c.mu0 * tr[2];
+    } else {
+      const double sqx = (c.emode || tr[4] != 0) ? out[0] : out[1];
+      f = 0.5 * sqx + c.mu0 * tr[2];
+    }
     const double s = out[3] / c.nl;
     const double fl = pre[7], sl = pre[8];
     bool ok = fabs(f - fl) / fabs(fl) < c.ftol;
     if (ok && c.use_sp) ok = fabs(s - sl) / fabs(sl) < c.ftol;
     const double stable = ok ? pre[9] + 1.0 : 0.0;
-    st[0] = 0.5 * out[1];
+    st[0] = c.mode == 1 ? out[1] : 0.5 * out[1];
     st[1] = f;
     st[2] = s;
     st[3] = stable;
     code = stable > (double)c.stable_thr ? 1 : 0;
+    if (code == 0 && c.nnz_budget >= 0.0 && out[2] > c.nnz_budget) code = 3;
   }
-  *c.abort = code == 0 ? 0 : (code == 1 ? c.pass : -1);
+  *c.abort = code == 0 ? 0 : (code == 2 ? -1 : c.pass);
   rec[10] = (double)code;
   for (int k = 0; k <= 10; ++k) c.rec[k] = rec[k];
 }
@@ -212,7 +224,13 @@ __global__ __launch_bounds__(256) void k_finalize_fista(
     const T* __restrict__ P, int S, const T* __restrict__ Pe, int S0, const T* __restrict__ B,
     T* __restrict__ Ry, const T* __restrict__ sxo, T* __restrict__ sxo_out, int64_t ml, double a1_,
     double b1_, double theta_, const T* __restrict__ cx, int64_t cn, const double* __restrict__ cmax,
-    const unsigned* __restrict__ counts, int nl, Red red) {
+    const unsigned* __restrict__ counts, int nl, Red red, Ctl ctl) {
+  const bool skipped = red_skipped(red);   // cancelled in a device-controlled batch
+  double pre[10];
+  if (ctl.rec != nullptr && threadIdx.x == 0) {
+    for (int k = 0; k < 6; ++k) pre[k] = ctl.tr[k];
+    for (int k = 0; k < 4; ++k) pre[6 + k] = ctl.state[k];
+  }
   const T a1 = (T)a1_, b1 = (T)b1_, theta = (T)theta_;
   double v[4] = {0.0, 0.0, 0.0, 0.0};
   if (blockIdx.x == 0 && (int)threadIdx.x < nl) v[2] = (double)counts[threadIdx.x];
@@ -228,6 +246,7 @@ __global__ __launch_bounds__(256) void k_finalize_fista(
     const T avn = so + (sx - so) / theta;
     const T ry = (a1 * apt + b1 * avn) - bv;
     const T rx = sx - bv;
+    if (skipped) return;
     if (sub == 0) {
       Ry[idx] = ry;
       sxo_out[idx] = apt;
@@ -235,9 +254,11 @@ __global__ __launch_bounds__(256) void k_finalize_fista(
       v[1] += (double)(ry * ry);
     }
   }
+  if (skipped) return;
   if (cx != nullptr)
     for (int64_t idx = tid; idx < cn; idx += stride) v[3] += (tabs(cx[idx]) > thr) ? 1.0 : 0.0;
-  grid_reduce<4, 0u>(v, red);
+  const bool last = grid_reduce<4, 0u>(v, red);
+  if (last && ctl.rec != nullptr && threadIdx.x == 0) ctl_decide(ctl, red.out, pre);
 }
 
 template <typename T>
@@ -279,6 +300,13 @@ __global__ __launch_bounds__(256) void k_prox_pgd(const T* __restrict__ x, const
                                                   uint8_t* __restrict__ zf, int64_t n,
                                                   int64_t l, double t_, double tmu_, double thres_,
                                                   Red red, Pub pub) {
+  // a launch of a device-controlled batch cancelled by an earlier decision (communicator path,
+  // solver.cpp dc_queue_comm): nothing is written, no ticket touched (uniform over the grid)
+  if (red_skipped(red)) {
+    if (pub.host != nullptr && blockIdx.x == gridDim.x - 1 && threadIdx.x == 0)
+      publish_packet(pub.s, pub.ns, pub.host, pub.host_seq, pub.seq);
+    return;
+  }
   if (publisher_last<6, 0x8u>(pub, red)) return;
   const T t = (T)t_, tmu = (T)tmu_, thres = (T)thres_;
   const int64_t nl = n * l;
@@ -326,6 +354,11 @@ __global__ __launch_bounds__(256) void k_fista_trial(
     double b1_, double dd_, double delta_, Red red, Pub pub, T* __restrict__ ec,
     uint8_t* __restrict__ zf) {
   constexpr int NV = PROX ? 4 : 5;
+  if (red_skipped(red)) {   // cancelled in a device-controlled batch (as k_prox_pgd)
+    if (pub.host != nullptr && blockIdx.x == gridDim.x - 1 && threadIdx.x == 0)
+      publish_packet(pub.s, pub.ns, pub.host, pub.host_seq, pub.seq);
+    return;
+  }
   if (publisher_last<NV, (1u << (NV - 1))>(pub, red)) return;
   const T t = (T)t_, tmu = (T)tmu_, thres = (T)thres_, theta = (T)theta_, a1 = (T)a1_, b1 = (T)b1_;
   const T dd = (T)dd_, delta = (T)delta_;
@@ -648,14 +681,14 @@ template <typename T>
 void launch_finalize_fista(const T* P, int S, const T* Pe, int S0, const T* B, T* Ry, const T* sxo,
                            T* sxo_out, int64_t ml, double a1, double b1, double theta, const T* cx,
                            int64_t cn, const double* cmax, const unsigned* counts, int nl, Red red,
-                           hipStream_t st) {
+                           hipStream_t st, Ctl ctl) {
   const int G = finalize_groups(S > S0 ? S : S0);
   if (G > 8) throw Error{GLX_E_INVALID, "finalize: more than 64 K-split slabs"};
   const int64_t work = ml * G > cn ? ml * G : cn;
   const dim3 grid(grid_for(work, 256 * 2));
   auto go = [&](auto g) {
     hipLaunchKernelGGL((k_finalize_fista<T, decltype(g)::value>), grid, dim3(256), 0, st, P, S, Pe,
-                       S0, B, Ry, sxo, sxo_out, ml, a1, b1, theta, cx, cn, cmax, counts, nl, red);
+                       S0, B, Ry, sxo, sxo_out, ml, a1, b1, theta, cx, cn, cmax, counts, nl, red, ctl);
   };
   if (G == 1) go(std::integral_constant<int, 1>{});
   else if (G == 2) go(std::integral_constant<int, 2>{});
@@ -779,7 +812,7 @@ void launch_publish(const double* s, int ns, double* host, unsigned* host_seq, u
   template void launch_sum_partials<T>(const T*, int, T*, int64_t, hipStream_t);                    \
   template void launch_finalize_fista<T>(const T*, int, const T*, int, const T*, T*, const T*, T*,  \
                                          int64_t, double, double, double, const T*, int64_t,        \
-                                         const double*, const unsigned*, int, Red, hipStream_t);    \
+                                         const double*, const unsigned*, int, Red, hipStream_t, Ctl);\
   template void launch_prox_pgd<T>(const T*, const T*, int, T*, T*, T*, T*, int64_t, int64_t,       \
                                    double, double, double, Red, hipStream_t, Pub, uint8_t*);        \
   template void launch_fista_trial<T>(bool, const T*, const T*, int, T*, const T*, T*, T*, T*,      \

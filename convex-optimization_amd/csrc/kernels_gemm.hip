@@ -203,12 +203,7 @@ __device__ inline void lds_put(T* dst, typename MF<T>::vec_t v) {
   }
 }
 
-//
-// SP (split-candidate mode, NSRC = 2): X0 = e is zero except in the rows sf flags, so the MFMAs
-// of source 0 run only on chunks with a flagged row (one uniform branch per chunk; the flags
-// of chunk c + PF are fetched with its A refill). Skipped chunks contribute exact zeros, so the
-// partials equal the dense product's.
-template <typename T, int MT, int NT, int NSRC, int PF, int VPL, int WAVES, bool SP = false>
+template <typename T, int MT, int NT, int NSRC, int PF, int VPL, int WAVES>
 __global__ __launch_bounds__(64 * WAVES) void k_ax_lds(const T* __restrict__ A,
                                                       const T* __restrict__ X0,
                                                       const T* __restrict__ X1,
@@ -216,8 +211,7 @@ __global__ __launch_bounds__(64 * WAVES) void k_ax_lds(const T* __restrict__ A,
                                                       T* __restrict__ P, int64_t m, int64_t n,
                                                       int64_t chunks, int S, int gx, int xmap,
                                                       const int* __restrict__ gate, int epoch,
-                                                      Pub pub, const uint8_t* __restrict__ sf) {
-  static_assert(!SP || NSRC == 2, "split-candidate mode has two sources");
+                                                      Pub pub) {
   typedef MF<T> M;
   typedef typename M::vec_t V;
   typedef typename M::acc_t C;
@@ -338,24 +332,13 @@ __global__ __launch_bounds__(64 * WAVES) void k_ax_lds(const T* __restrict__ A,
           if (cc >= c0 && cc < c1) acc[mt][cc] = M::mma(av[v][e], xv[cc][v * E + e], acc[mt][cc]);
   };
   auto mma_tile = [&](int mt, const V (&av)[VPL], const T (&xv)[NC][EL]) {
-    mma_cols(mt, av, xv, SP ? NT : 0, NC);
+    mma_cols(mt, av, xv, 0, NC);
   };
-  // SP: does chunk `off` hold a flagged row of X0 (CK flag bytes, OR-ed as words)?
-  auto flag_of = [&](int64_t off) -> unsigned {
-    off = kch(off);
-    const unsigned* fp = reinterpret_cast<const unsigned*>(sf + (cb + off) * CK);
-    unsigned f = 0;
-#pragma unroll
-    for (int j = 0; j < CK / 4; ++j) f |= fp[j];
-    return __builtin_amdgcn_readfirstlane(f);
-  };
-  unsigned fl[PF];
 
 #pragma unroll
   for (int p = 0; p < PF; ++p) {   // X first, then A, in every ring step (see header)
     load_x(xr[p], p);
     load_a(a[p], p);
-    if constexpr (SP) fl[p] = flag_of(p);
   }
   put_x(0, xr[0]);                 // chunk 0 -> slot 0
   __syncthreads();
@@ -374,31 +357,11 @@ __global__ __launch_bounds__(64 * WAVES) void k_ax_lds(const T* __restrict__ A,
       T xv[NC][EL];
       read_x(slot, xv);
       const int64_t off = kch(c + PF);
-      if constexpr (SP) {
-        // two straight-line bodies, so an active chunk runs exactly the dense schedule
-        if (fl[p] != 0) {
 #pragma unroll
-          for (int mt = 0; mt < MT; ++mt) {
-            mma_cols(mt, a[p][mt], xv, 0, NC);
+      for (int mt = 0; mt < MT; ++mt) {
+        mma_tile(mt, a[p][mt], xv);
 #pragma unroll
-            for (int v = 0; v < VPL; ++v) a[p][mt][v] = load_vec<T, false>(ap[mt] + off * CK + v * E);
-          }
-        } else {
-#pragma unroll
-          for (int mt = 0; mt < MT; ++mt) {
-            mma_cols(mt, a[p][mt], xv, NT, NC);
-#pragma unroll
-            for (int v = 0; v < VPL; ++v) a[p][mt][v] = load_vec<T, false>(ap[mt] + off * CK + v * E);
-          }
-        }
-        fl[p] = flag_of(c + PF);
-      } else {
-#pragma unroll
-        for (int mt = 0; mt < MT; ++mt) {
-          mma_tile(mt, a[p][mt], xv);
-#pragma unroll
-          for (int v = 0; v < VPL; ++v) a[p][mt][v] = load_vec<T, false>(ap[mt] + off * CK + v * E);
-        }
+        for (int v = 0; v < VPL; ++v) a[p][mt][v] = load_vec<T, false>(ap[mt] + off * CK + v * E);
       }
       __syncthreads();
     }
@@ -414,12 +377,6 @@ __global__ __launch_bounds__(64 * WAVES) void k_ax_lds(const T* __restrict__ A,
       read_x(slot, xv);
 #pragma unroll
       for (int mt = 0; mt < MT; ++mt) mma_tile(mt, a[p][mt], xv);
-      if constexpr (SP) {
-        if (fl[p] != 0) {
-#pragma unroll
-          for (int mt = 0; mt < MT; ++mt) mma_cols(mt, a[p][mt], xv, 0, NT);
-        }
-      }
       __syncthreads();
     }
   }
@@ -547,13 +504,10 @@ static int axb_default(int nsrc, int esize) {
   return esize == 8 ? 52228 : 52324;
 }
 
-static constexpr int kLdsCodes[] = {52224, 52324, 52228, 52328, 52218, 54224, 52214, 54214,
-                                     51228, 51328, 51224, 52428, 54228, 54218,
-                                     // kind 8 (LDS-DMA, f64): 8 NS KC/16 NTL WAVES
-                                     84208, 84218, 83208, 83218, 82408, 82418, 88108, 88118,
-                                     84204, 84214, 83238, 84238, 83228, 84131, 84111, 82231,
-                                     83258, 84258, 83248, 84151, 94158, 94148, 93158, 92258,
-                                     83278, 93178, 92278, 93168, 92268, 94178, 94168};
+// the tiles the planner picks (lds_plan); the LDS-DMA sweep's other codes are in DESIGN.md
+static constexpr int kLdsCodes[] = {52224, 52324, 52228, 51328,
+                                     // kind 9 (LDS-DMA, f64, two row tiles per wave): 9 NS KC/16 flags WAVES
+                                     92278, 92268};
 static inline bool dma_kind(int c) { return c / 10000 == 8 || c / 10000 == 9; }
 static inline bool lds_kind(int c) { return c / 10000 == 5 || dma_kind(c); }
 static bool lds_code_ok(int c, int64_t n, int64_t l, int esize, int nsrc = 1) {
@@ -639,15 +593,7 @@ static void lds_plan(int esize, int64_t m, int64_t n, int64_t l, int nsrc, int& 
   if (S4 < S) { code = c4; S = S4; }
 }
 
-static bool valid_ax_code(int c) {
-  switch (c) {
-    case 1410: case 1420: case 1421: case 1430: case 1431: case 1820: case 1821: case 1810:
-    case 1811: case 2410: case 2420: case 2421: case 2820: case 2821: case 1220: case 1221:
-    case 21420: case 22420: case 21410: case 41220: case 41210: case 41410: case 21820:
-      return true;
-    default: return false;
-  }
-}
+static bool valid_ax_code(int c) { return c == 21820 || c == 21410 || c == 1820; }
 
 GemmPlan make_plan(int esize, int64_t m, int64_t n, int64_t l, int ax_variant) {
   GemmPlan p{};
@@ -657,9 +603,7 @@ GemmPlan make_plan(int esize, int64_t m, int64_t n, int64_t l, int ax_variant) {
   const bool mfma_l = (l == 16 || l == 32);
   // ---- A @ X ----
   if (ax_variant == 0) ax_variant = env_int("GLX_AX_VARIANT", 0);
-  if (ax_variant == 1) ax_variant = 1410;
-  if (ax_variant == 2) ax_variant = 2410;
-  if (ax_variant >= 100 && ax_variant < 1000) ax_variant = ax_variant * 10;  // legacy 3-digit codes
+  if (ax_variant == 1 || ax_variant == 2) ax_variant = esize == 8 ? kAxFallback : kAxDefault32;
   const bool ax_mfma_ok = mfma_l && (n % (4 * E) == 0);
   if (ax_variant == 3 || !ax_mfma_ok) {
     p.ax_kind = 3;
@@ -792,7 +736,7 @@ std::string describe_plan(const GemmPlan& p) {
 
 int max_ax_split(int esize, int64_t m, int64_t n, int64_t l) {
   int s = 1;
-  for (int v : {0, 3, 1220, 1410, 1820}) s = std::max(s, ax_split_max(make_plan(esize, m, n, l, v)));
+  for (int v : {0, 3, 1820, 21820, 21410}) s = std::max(s, ax_split_max(make_plan(esize, m, n, l, v)));
   for (int v : kLdsCodes) s = std::max(s, ax_split_max(make_plan(esize, m, n, l, v)));
   return s;
 }
@@ -836,120 +780,63 @@ static void ax_mfma_go(const GemmPlan& p, const T* A, const T* const* X, T* P, c
 
 template <typename T, int NT, int NSRC, int MT, int PF, int VPL, int WAVES>
 static void ax_lds_go(const GemmPlan& p, int S, const T* A, const T* const* X, T* P,
-                      const int* gate, int epoch, hipStream_t st, Pub pub = Pub{},
-                      const uint8_t* sf = nullptr) {
+                      const int* gate, int epoch, hipStream_t st, Pub pub = Pub{}) {
   constexpr int E = 16 / sizeof(T);
   const int gx = (int)cdiv(p.m, 16 * MT * WAVES);
   const int xmap = ax_xmap_flags(p, S);
   const dim3 grid((unsigned)ax_grid(xmap, gx, S) + (pub.host ? 1u : 0u));
-  if constexpr (NSRC == 2) {
-    if (sf != nullptr) {
-      hipLaunchKernelGGL((k_ax_lds<T, MT, NT, NSRC, PF, VPL, WAVES, true>), grid, dim3(64 * WAVES), 0,
-                         st, A, X[0], X[1], X[2], P, p.m, p.n, p.n / (4 * VPL * E), S, gx, xmap,
-                         gate, epoch, pub, sf);
-      return;
-    }
-  }
   static const size_t pad = lds_pad(k_ax_lds<T, MT, NT, NSRC, PF, VPL, WAVES>, "GLX_AX_LDS_PAD");
   hipLaunchKernelGGL((k_ax_lds<T, MT, NT, NSRC, PF, VPL, WAVES>), grid,
                      dim3(64 * WAVES), pad, st, A, X[0], X[1], X[2], P, p.m, p.n,
-                     p.n / (4 * VPL * E), S, gx, xmap, gate, epoch, pub, nullptr);
+                     p.n / (4 * VPL * E), S, gx, xmap, gate, epoch, pub);
 }
 
+// the planner's kind-5 tiles (lds_plan): 52228 (f64 batched / one RHS in the Infinity Cache),
+// 52224 (its 4-wave form for deep-split shards), 51328 (one 16-row tile per wave: the
+// one-RHS and shard tile at l = 32), 52324 (f32 batched)
 template <typename T, int NT, int NSRC>
 static void ax_lds_code(const GemmPlan& p, int code, int S, const T* A, const T* const* X, T* P,
-                        const int* gate, int epoch, hipStream_t st, Pub pub,
-                        const uint8_t* sf) {
+                        const int* gate, int epoch, hipStream_t st, Pub pub) {
   if (dma_kind(code)) {
     if (!launch_ax_dma<T>(p, code, NSRC, S, A, X, P, gate, epoch, st, pub))
       throw Error{GLX_E_INVALID, "A@X: unknown LDS-DMA tile code"};
     return;
   }
   switch (code) {
-    case 52428: ax_lds_go<T, NT, NSRC, 2, 4, 2, 8>(p, S, A, X, P, gate, epoch, st, pub, sf); return;
-    default: break;
-  }
-  switch (code) {
-    case 52324: ax_lds_go<T, NT, NSRC, 2, 3, 2, 4>(p, S, A, X, P, gate, epoch, st, pub, sf); break;
-    case 54228: ax_lds_go<T, NT, NSRC, 4, 2, 2, 8>(p, S, A, X, P, gate, epoch, st, pub, sf); break;
-    case 54218: ax_lds_go<T, NT, NSRC, 4, 2, 1, 8>(p, S, A, X, P, gate, epoch, st, pub, sf); break;
-    case 52228: ax_lds_go<T, NT, NSRC, 2, 2, 2, 8>(p, S, A, X, P, gate, epoch, st, pub, sf); break;
-    // one 16-row tile per wave: twice the row tiles, half the K splits and partial slabs
-    case 51228: ax_lds_go<T, NT, NSRC, 1, 2, 2, 8>(p, S, A, X, P, gate, epoch, st, pub, sf); break;
-    case 51328: ax_lds_go<T, NT, NSRC, 1, 3, 2, 8>(p, S, A, X, P, gate, epoch, st, pub, sf); break;
-    case 51224: ax_lds_go<T, NT, NSRC, 1, 2, 2, 4>(p, S, A, X, P, gate, epoch, st, pub, sf); break;
-    case 52328: ax_lds_go<T, NT, NSRC, 2, 3, 2, 8>(p, S, A, X, P, gate, epoch, st, pub, sf); break;
-    case 52218: ax_lds_go<T, NT, NSRC, 2, 2, 1, 8>(p, S, A, X, P, gate, epoch, st, pub, sf); break;
-    case 54224: ax_lds_go<T, NT, NSRC, 4, 2, 2, 4>(p, S, A, X, P, gate, epoch, st, pub, sf); break;
-    case 52214: ax_lds_go<T, NT, NSRC, 2, 2, 1, 4>(p, S, A, X, P, gate, epoch, st, pub, sf); break;
-    case 54214: ax_lds_go<T, NT, NSRC, 4, 2, 1, 4>(p, S, A, X, P, gate, epoch, st, pub, sf); break;
-    default:   // 52224
-      ax_lds_go<T, NT, NSRC, 2, 2, 2, 4>(p, S, A, X, P, gate, epoch, st, pub, sf);
-      break;
+    case 52228: ax_lds_go<T, NT, NSRC, 2, 2, 2, 8>(p, S, A, X, P, gate, epoch, st, pub); break;
+    case 51328: ax_lds_go<T, NT, NSRC, 1, 3, 2, 8>(p, S, A, X, P, gate, epoch, st, pub); break;
+    case 52324: ax_lds_go<T, NT, NSRC, 2, 3, 2, 4>(p, S, A, X, P, gate, epoch, st, pub); break;
+    case 52224: ax_lds_go<T, NT, NSRC, 2, 2, 2, 4>(p, S, A, X, P, gate, epoch, st, pub); break;
+    default: throw Error{GLX_E_INVALID, "A@X: unknown LDS tile code"};
   }
 }
 
-// One source: the swept variant. Batched sources (2, 3) use fixed register-feasible tiles.
+// Direct-load tiles (kinds 1/2) only where no LDS tile fits the shape (lds_code_ok: l not 16/32
+// is VALU; n not a multiple of the LDS chunk): 21820 / 1820 (f64, or any n % 4E), 21410 (f32),
+// and for batched sources 1420 / 1220.
 template <typename T, int NT>
 static void ax_mfma_nt(const GemmPlan& p, int nsrc, const T* A, const T* const* X, T* P,
-                       const int* gate, int epoch, hipStream_t st, Pub pub, const uint8_t* sf) {
+                       const int* gate, int epoch, hipStream_t st, Pub pub) {
   const int code = p.axb_code[nsrc];
   if (lds_kind(code)) {
-    if (nsrc == 1) ax_lds_code<T, NT, 1>(p, code, p.axb_S[1], A, X, P, gate, epoch, st, pub, nullptr);
-    else if (nsrc == 2) ax_lds_code<T, NT, 2>(p, code, p.axb_S[2], A, X, P, gate, epoch, st, pub, sf);
-    else ax_lds_code<T, NT, 3>(p, code, p.axb_S[3], A, X, P, gate, epoch, st, pub, nullptr);
+    if (nsrc == 1) ax_lds_code<T, NT, 1>(p, code, p.axb_S[1], A, X, P, gate, epoch, st, pub);
+    else if (nsrc == 2) ax_lds_code<T, NT, 2>(p, code, p.axb_S[2], A, X, P, gate, epoch, st, pub);
+    else ax_lds_code<T, NT, 3>(p, code, p.axb_S[3], A, X, P, gate, epoch, st, pub);
     return;
   }
   if (pub.host != nullptr) throw Error{GLX_E_INVALID, "A@X: this tile cannot carry the scalar packet"};
   if (nsrc == 2) {
-    switch (code) {
-      case 1220: ax_mfma_go<T, NT, 2, 2, 2, false, false>(p, A, X, P, gate, epoch, st); break;
-      case 1420: ax_mfma_go<T, NT, 2, 4, 2, false, false>(p, A, X, P, gate, epoch, st); break;
-      case 1430: ax_mfma_go<T, NT, 2, 4, 3, false, false>(p, A, X, P, gate, epoch, st); break;
-      case 2220: ax_mfma_go<T, NT, 2, 2, 2, true, false>(p, A, X, P, gate, epoch, st); break;
-      case 2230: ax_mfma_go<T, NT, 2, 2, 3, true, false>(p, A, X, P, gate, epoch, st); break;
-      case 2421: ax_mfma_go<T, NT, 2, 4, 2, true, true>(p, A, X, P, gate, epoch, st); break;
-      case 2430: ax_mfma_go<T, NT, 2, 4, 3, true, false>(p, A, X, P, gate, epoch, st); break;
-      case 2420: ax_mfma_go<T, NT, 2, 4, 2, true, false>(p, A, X, P, gate, epoch, st); break;
-      case 21420: ax_mfma_go<T, NT, 2, 4, 2, false, false, 2>(p, A, X, P, gate, epoch, st); break;
-      case 21410: ax_mfma_go<T, NT, 2, 4, 1, false, false, 2>(p, A, X, P, gate, epoch, st); break;
-      case 41210: ax_mfma_go<T, NT, 2, 2, 1, false, false, 4>(p, A, X, P, gate, epoch, st); break;
-      default: ax_mfma_go<T, NT, 2, 4, 2, false, false>(p, A, X, P, gate, epoch, st); break;
-    }
+    ax_mfma_go<T, NT, 2, 4, 2, false, false>(p, A, X, P, gate, epoch, st);
     return;
   }
   if (nsrc == 3) {
-    switch (code) {
-      case 2220: ax_mfma_go<T, NT, 3, 2, 2, true, false>(p, A, X, P, gate, epoch, st); break;
-      case 2230: ax_mfma_go<T, NT, 3, 2, 3, true, false>(p, A, X, P, gate, epoch, st); break;
-      default: ax_mfma_go<T, NT, 3, 2, 2, false, false>(p, A, X, P, gate, epoch, st); break;
-    }
+    ax_mfma_go<T, NT, 3, 2, 2, false, false>(p, A, X, P, gate, epoch, st);
     return;
   }
   switch (p.ax_code) {
-    case 1410: ax_mfma_go<T, NT, 1, 4, 1, false, false>(p, A, X, P, gate, epoch, st); break;
-    case 1420: ax_mfma_go<T, NT, 1, 4, 2, false, false>(p, A, X, P, gate, epoch, st); break;
-    case 1421: ax_mfma_go<T, NT, 1, 4, 2, false, true>(p, A, X, P, gate, epoch, st); break;
-    case 1430: ax_mfma_go<T, NT, 1, 4, 3, false, false>(p, A, X, P, gate, epoch, st); break;
-    case 1431: ax_mfma_go<T, NT, 1, 4, 3, false, true>(p, A, X, P, gate, epoch, st); break;
-    case 1810: ax_mfma_go<T, NT, 1, 8, 1, false, false>(p, A, X, P, gate, epoch, st); break;
-    case 1811: ax_mfma_go<T, NT, 1, 8, 1, false, true>(p, A, X, P, gate, epoch, st); break;
-    case 1820: ax_mfma_go<T, NT, 1, 8, 2, false, false>(p, A, X, P, gate, epoch, st); break;
-    case 1821: ax_mfma_go<T, NT, 1, 8, 2, false, true>(p, A, X, P, gate, epoch, st); break;
-    case 2410: ax_mfma_go<T, NT, 1, 4, 1, true, false>(p, A, X, P, gate, epoch, st); break;
-    case 2420: ax_mfma_go<T, NT, 1, 4, 2, true, false>(p, A, X, P, gate, epoch, st); break;
-    case 2820: ax_mfma_go<T, NT, 1, 8, 2, true, false>(p, A, X, P, gate, epoch, st); break;
-    case 2821: ax_mfma_go<T, NT, 1, 8, 2, true, true>(p, A, X, P, gate, epoch, st); break;
-    case 1220: ax_mfma_go<T, NT, 1, 2, 2, false, false>(p, A, X, P, gate, epoch, st); break;
-    case 1221: ax_mfma_go<T, NT, 1, 2, 2, false, true>(p, A, X, P, gate, epoch, st); break;
-    case 21420: ax_mfma_go<T, NT, 1, 4, 2, false, false, 2>(p, A, X, P, gate, epoch, st); break;
-    case 22420: ax_mfma_go<T, NT, 1, 4, 2, true, false, 2>(p, A, X, P, gate, epoch, st); break;
-    case 21410: ax_mfma_go<T, NT, 1, 4, 1, false, false, 2>(p, A, X, P, gate, epoch, st); break;
-    case 41220: ax_mfma_go<T, NT, 1, 2, 2, false, false, 4>(p, A, X, P, gate, epoch, st); break;
-    case 41210: ax_mfma_go<T, NT, 1, 2, 1, false, false, 4>(p, A, X, P, gate, epoch, st); break;
-    case 41410: ax_mfma_go<T, NT, 1, 4, 1, false, false, 4>(p, A, X, P, gate, epoch, st); break;
     case 21820: ax_mfma_go<T, NT, 1, 8, 2, false, false, 2>(p, A, X, P, gate, epoch, st); break;
-    default: ax_mfma_go<T, NT, 1, 4, 2, true, true>(p, A, X, P, gate, epoch, st); break;
+    case 21410: ax_mfma_go<T, NT, 1, 4, 1, false, false, 2>(p, A, X, P, gate, epoch, st); break;
+    default: ax_mfma_go<T, NT, 1, 8, 2, false, false>(p, A, X, P, gate, epoch, st); break;   // 1820
   }
 }
 
@@ -960,7 +847,7 @@ bool ax_pub_ok(const GemmPlan& p, int nsrc) {
 
 template <typename T>
 void launch_ax(const GemmPlan& p, int nsrc, const T* A, const T* const* X, T* P, const int* gate,
-               int epoch, hipStream_t st, Pub pub, const uint8_t* sf) {
+               int epoch, hipStream_t st, Pub pub) {
   if (pub.host != nullptr && !ax_pub_ok(p, nsrc))
     throw Error{GLX_E_INVALID, "A@X: this plan cannot carry the scalar packet"};
   if (p.ax_kind == 3) {
@@ -969,10 +856,10 @@ void launch_ax(const GemmPlan& p, int nsrc, const T* A, const T* const* X, T* P,
     else ax_valu_src<T, 3>(p, A, X, P, gate, epoch, st);
     return;
   }
-  if (p.l == 16) ax_mfma_nt<T, 1>(p, nsrc, A, X, P, gate, epoch, st, pub, sf);
-  else ax_mfma_nt<T, 2>(p, nsrc, A, X, P, gate, epoch, st, pub, sf);
+  if (p.l == 16) ax_mfma_nt<T, 1>(p, nsrc, A, X, P, gate, epoch, st, pub);
+  else ax_mfma_nt<T, 2>(p, nsrc, A, X, P, gate, epoch, st, pub);
 }
 
-template void launch_ax<double>(const GemmPlan&, int, const double*, const double* const*, double*, const int*, int, hipStream_t, Pub, const uint8_t*);
-template void launch_ax<float>(const GemmPlan&, int, const float*, const float* const*, float*, const int*, int, hipStream_t, Pub, const uint8_t*);
+template void launch_ax<double>(const GemmPlan&, int, const double*, const double* const*, double*, const int*, int, hipStream_t, Pub);
+template void launch_ax<float>(const GemmPlan&, int, const float*, const float* const*, float*, const int*, int, hipStream_t, Pub);
 }  // namespace glx

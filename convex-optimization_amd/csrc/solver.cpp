@@ -89,10 +89,15 @@ constexpr int kKeepMiB = 192;    // Infinity-Cache hand-off between the non-temp
 // gated) never land in the set the host resumes from
 constexpr int kMaxGSets = kCtlMaxBatch / 2 + 2;
 
-// device-controlled batches' window (GLX_DC_BATCH; 0 = the host decides every iteration)
-static int dc_window_env() {
-  const char* dc = std::getenv("GLX_DC_BATCH");
-  const int w = dc ? std::atoi(dc) : kDcWindow;
+// device-controlled batches' window: opts.dc_window (> 0: that window, < 0: off), else
+// GLX_DC_BATCH, else kDcWindow (0 = the host decides every iteration)
+static int dc_window_opt(const glx_opts& O) {
+  int w = kDcWindow;
+  if (O.dc_window != 0) {
+    w = O.dc_window;
+  } else if (const char* dc = std::getenv("GLX_DC_BATCH")) {
+    w = std::atoi(dc);
+  }
   return std::max(0, std::min(w, kCtlMaxBatch / 2));
 }
 
@@ -121,9 +126,9 @@ static void validate(const glx_problem* P, const glx_opts* O) {
 // FProxGD 3669–3691 → 3743–3749 it/s, ProxGD 3654–3657 → 3744–3752, FProxGD at (4096,8192,16)
 // 11 362–11 366 → 13 200–13 215 (profiles/r1_tuning/small_kernels/atr_f32_fused.log).
 // Split-candidate ProxGD (the fast objective mode, see iter_proxgd): 0 = off (exact mode, other
-// methods, or GLX_SPLIT_CAND=0: the dense [z | p_thr] batch of round 1); 1 = A e from the
-// transposed copy of A (kernels_gather.hip, the default); 2 = A e by skipping unflagged K
-// chunks inside the batched A@X tile (GLX_SPLIT_CAND=sp).
+// methods, shapes the gather does not cover, or GLX_SPLIT_CAND=0 / glx_opts.split_cand = 0: the
+// dense [z | p_thr] batch of round 1); 1 = A e from the transposed copy of A (kernels_gather.hip;
+// costs an extra m x n copy of A in the workspace, glx_session_workspace_bytes).
 // fp64 only: in fp32 the regrouped sum (A p_thr - b) + A e moves f by ~1e-6 relative on short
 // unconverged runs (measured 1.5e-6 on mid_384x640x16 against the 1e-6 fp32 bar), and no fp32
 // ProxGD configuration is on the benchmark path.
@@ -138,9 +143,10 @@ static constexpr double kSplitMinBytes = 768.0 * 1024 * 1024;
 static int split_mode(const glx_problem& P, const glx_opts& O) {
   if (O.exact_objective != 0 || P.dtype != GLX_F64) return 0;
   if (P.method != GLX_PROXGD && P.method != GLX_FPROXGD) return 0;
-  const char* sc = std::getenv("GLX_SPLIT_CAND");
+  if (O.split_cand == 2) return 0;
+  const char* sc = O.split_cand == 0 ? std::getenv("GLX_SPLIT_CAND") : nullptr;
   if (sc && std::strcmp(sc, "0") == 0) return 0;
-  const bool force = sc && (std::strcmp(sc, "1") == 0 || std::strcmp(sc, "sp") == 0);
+  const bool force = O.split_cand == 1 || (sc && std::strcmp(sc, "1") == 0);
   if (!force && (double)P.m * (double)P.n * 8.0 < kSplitMinBytes) return 0;
   if (P.method == GLX_FPROXGD) {
     const char* sf = std::getenv("GLX_SPLIT_FISTA");
@@ -148,8 +154,7 @@ static int split_mode(const glx_problem& P, const glx_opts& O) {
     const bool ls = O.step_type == GLX_STEP_LINE_SEARCH && O.ls_maxit > 0;
     return (ls && gather_ok(P.n, P.l)) ? 1 : 0;
   }
-  if (sc && std::strcmp(sc, "sp") == 0) return 2;
-  return gather_ok(P.n, P.l) ? 1 : 2;
+  return gather_ok(P.n, P.l) ? 1 : 0;
 }
 
 static GemmPlan session_plan(const glx_problem& P, const glx_opts& O) {
@@ -263,11 +268,11 @@ class Session : public SessionBase {
   // device control with a communicator: ProxGD, fp64 (the trial sums ride the gradient
   // all-reduce), line search, fast objective mode
   static bool dc_comm_ok(const glx_problem& P, const glx_opts& O) {
-    return P.comm != nullptr && P.method == GLX_PROXGD && P.dtype == GLX_F64 &&
+    return P.comm != nullptr && (P.method == GLX_PROXGD || P.method == GLX_FPROXGD) && P.dtype == GLX_F64 &&
            O.step_type == GLX_STEP_LINE_SEARCH && O.ls_maxit > 0 && O.exact_objective == 0;
   }
   static int gsets_for(const glx_problem& P, const glx_opts& O) {
-    const int w = dc_window_env();
+    const int w = dc_window_opt(O);
     return (w > 0 && dc_comm_ok(P, O)) ? w + 2 : 2;
   }
 
@@ -332,10 +337,11 @@ class Session : public SessionBase {
       GLX_HIP(hipEventCreateWithFlags(&ev_lists_, hipEventDisableTiming));
     }
     fused_fista_ok_ = fuse_any && P.method == GLX_FPROXGD;
-    // device-controlled batches (dc_run): ProxGD with line search on the fused speculative path
-    // of one GPU; GLX_DC_BATCH = iterations in flight (0: the host decides every iteration)
-    dc_window_ = dc_window_env();
-    if (!(fused_ok_ && spin_readback_ && O.exact_objective == 0 &&
+    // device-controlled batches (dc_run / fista_dc_run): ProxGD / FProxGD with line search on
+    // the fused speculative path; GLX_DC_BATCH = iterations in flight (0: the host decides every
+    // iteration). With a communicator fp64 only (the trial sums ride the gradient all-reduce).
+    dc_window_ = dc_window_opt(O);
+    if (!((fused_ok_ || fused_fista_ok_) && spin_readback_ && O.exact_objective == 0 &&
           O.step_type == GLX_STEP_LINE_SEARCH && O.ls_maxit > 0 &&
           (comm_ == nullptr || (dc_comm_ok(P, O) && attach_ok_))))
       dc_window_ = 0;
@@ -456,6 +462,7 @@ class Session : public SessionBase {
     for (int i = 0; i < 8; ++i) res->stats[i] = stats_[i];
     res->atr_calls = atr_calls_;
     res->syncs = syncs_;
+    res->record_waits = record_waits_;
     // finish() overwrote residual buffers: rebuild the iteration state if run() is called again
     state_valid_ = false;
     y_ready_ = false;
@@ -567,7 +574,7 @@ class Session : public SessionBase {
     const bool gat = chain && smode_ == 1;
     if (!skip_ax) {
       if (gat) cand_ax(xs);
-      else spec_ax(nsrc, xs, Pub{}, chain ? zf_ : nullptr);
+      else spec_ax(nsrc, xs);
     }
     T* rsc[3] = {chain ? nullptr : rs[0], rs[1], rs[2]};
     launch_finalize_residual<T>(Pp_, gat ? ax_split(plan_, 1) : ax_split(plan_, nsrc), B_, nsrc, rsc,
@@ -589,13 +596,13 @@ class Session : public SessionBase {
     if (pub_seq != nullptr) *pub_seq = post_readback();
   }
   // A @ [xs] into the slabs Pp_; pb: the launch also carries that scalar packet (ax_pub_ok)
-  void spec_ax(int nsrc, const T* const* xs, Pub pb = Pub{}, const uint8_t* sf = nullptr) {
+  void spec_ax(int nsrc, const T* const* xs, Pub pb = Pub{}) {
     hipEvent_t e0 = prof_begin(0);
-    launch_ax<T>(plan_, nsrc, A_, xs, Pp_, nullptr, 0, st_, pb, sf);
+    launch_ax<T>(plan_, nsrc, A_, xs, Pp_, nullptr, 0, st_, pb);
     check_launch();
     prof_end(0, e0);
     ++ax_calls_;
-    ax_cols_ += sf ? nsrc - 1 : nsrc;   // dense right-hand sides (the flagged e is counted apart)
+    ax_cols_ += nsrc;   // dense right-hand sides
   }
   // Split-candidate trial, gather form: A p_thr (one dense source, slabs behind the A e slab)
   // and A e from the transposed copy (one slab at Pp_); xs = [e | p_thr]. The column lists of e
@@ -900,7 +907,7 @@ class Session : public SessionBase {
             pbx.n3 = 6;
             const T* sx[3] = {X_[iz_], X_[if2_], X_[if1_]};   // [z | p_thr | p] of that trial
             if (smode_ == 1) cand_ax(sx, pbx);
-            else spec_ax(nsrc, sx, pbx, ezf());
+            else spec_ax(nsrc, sx, pbx);
             ax_queued_ = true;
           }
         } else if (spec) {
@@ -1022,7 +1029,7 @@ class Session : public SessionBase {
     T* rs[3] = {R_[rz], R_[rpt], R_[rp]};
     if (first && !ax_queued_) {
       if (smode_ == 1) cand_ax(xs);
-      else spec_ax(2, xs, Pub{}, emode_ ? zf_ : nullptr);
+      else spec_ax(2, xs);
     }
     dc_gate_ = dc_abort_;
     const int ns = nset(q.gset);
@@ -1038,7 +1045,7 @@ class Session : public SessionBase {
     check_launch();
     const T* sx[3] = {X_[q.iz], X_[q.if2], X_[q.if1]};   // [z | p_thr | p] of that trial
     if (smode_ == 1) cand_ax(sx);
-    else spec_ax(2, sx, Pub{}, emode_ ? zf_ : nullptr);
+    else spec_ax(2, sx);
     dc_gate_ = nullptr;
     q.irg = rpt;
     const int ox = q.ix, oxt = q.ixt;
@@ -1051,21 +1058,8 @@ class Session : public SessionBase {
     const T* xs[3] = {X_[q.iz], X_[q.ipt], X_[q.ip]};
     T* rs[3] = {R_[rz], R_[rpt], R_[rp]};
     dc_gate_ = dc_abort_;
-    dc_ctl_ = Ctl{};
+    dc_ctl_ = dc_make_ctl(tag);
     const int64_t slot = (tag % kCtlMaxBatch) * kCtlRec;
-    dc_ctl_.rec = dc_rec_ + slot;
-    dc_ctl_.state = dc_state_;
-    dc_ctl_.abort = dc_abort_;
-    dc_ctl_.tr = scal_ + S_TR;
-    dc_ctl_.tag = (double)tag;
-    dc_ctl_.t = O_.alpha0;
-    dc_ctl_.mu0 = P_.mu0;
-    dc_ctl_.ftol = O_.ftol;
-    dc_ctl_.nl = (double)nl_;
-    dc_ctl_.stable_thr = O_.stable_len_threshold;
-    dc_ctl_.use_sp = use_sparsity_ ? 1 : 0;
-    dc_ctl_.emode = emode_ ? 1 : 0;
-    dc_ctl_.pass = 1 + (int)(tag % 0x3FFFFFFF);
     residuals(2, xs, rs, S_RT, X_[q.ip], scal_ + S_TR + 3, nullptr, 0.0, nullptr, nullptr, false,
               false, emode_);
     dc_ctl_ = Ctl{};
@@ -1135,6 +1129,7 @@ class Session : public SessionBase {
         if (stop) { end_phase(true); return; }
       }
       const double* rec = dc_wait(tag0 + 1 + d);
+      ++record_waits_;
       if (queued < budget) push();
       for (int i = 0; i < 4; ++i) hs_[S_RT + i] = rec[i];
       for (int i = 0; i < 6; ++i) hs_[S_TR + i] = rec[4 + i];
@@ -1214,6 +1209,7 @@ class Session : public SessionBase {
     const double t0 = ls ? tk_ : schedule(inner_);
     const bool fuse = fused_fista_ok_ && !smooth;
     if (fsplit_ && ls && kslot_ < 0 && dense_left_ == 0) fista_split_prologue();
+    if (!smooth && fista_dc_ready(t0, theta)) { fista_dc_run(); return; }
     // first trial: from the previous iteration's speculative fused kernel, fused into this
     // iteration's A^T r, or (FGD / unfusable plans) the gradient and k_fista_trial
     std::pair<const T*, int> g{nullptr, 0};
@@ -1238,6 +1234,16 @@ class Session : public SessionBase {
         g = take_gradient(R_[iry_]);
       }
     }
+    fista_trials(g, first_done, t0, 0, theta, theta_next, smooth);
+  }
+
+  // The backtracking search from trial it0 (it0 = 1: the first trial was rejected by a
+  // device-side decision, fista_dc_run; t0 is then already tk * ls_coeff), or the untested
+  // step, and the update (x_k, v_k, y and the split-candidate bookkeeping).
+  void fista_trials(std::pair<const T*, int> g, bool first_done, double t0, int it0, double theta,
+                    double theta_next, bool smooth) {
+    const bool ls = O_.step_type == GLX_STEP_LINE_SEARCH && O_.ls_maxit > 0;
+    const bool fuse = fused_fista_ok_ && !smooth;
     const T* y = X_[iy_];
     if (smooth) {                                         // G = A^T r + mu y / sqrt(|y_i|^2 + d^2)
       launch_fgd_grad<T>(y, g.first, g.second, G_, n_, l_, mu_, O_.delta, red(S_REGY), st_);
@@ -1258,7 +1264,7 @@ class Session : public SessionBase {
     bool fs_batch = false;
     if (ls) {
       t = t0;
-      for (int it = 0; it < O_.ls_maxit; ++it) {
+      for (int it = it0; it < O_.ls_maxit; ++it) {
         if (!(it == 0 && first_done)) trial(t, it == 0);
         const T* xs[3] = {X_[ic_], X_[iyn_], nullptr};
         T* rs[3] = {R_[rc], R_[ryn], nullptr};
@@ -1305,7 +1311,14 @@ class Session : public SessionBase {
       t = t0;
       if (!first_done) trial(t, true);
     }
-    // x_k <- x, v_k <- v (:145, :147), y <- y_next
+    fista_update(accepted, spec_trial, t, fs_batch, theta_next, ryn, i_rn);
+  }
+
+  // After the search: x_k <- x, v_k <- v (:145, :147), y <- y_next; the packet (hs_) holds the
+  // last trial's sums. spec_trial: the speculative fused kernel left the next first trial.
+  void fista_update(bool accepted, bool spec_trial, double t, bool fs_batch, double theta_next,
+                    int ryn, int i_rn) {
+    const bool ls = O_.step_type == GLX_STEP_LINE_SEARCH && O_.ls_maxit > 0;
     if (spec_trial) {   // the speculative outputs become the next iteration's trial buffers
       const int ox = ix_, ov = iv_, oy = iy_;
       ix_ = ic_; iv_ = ivn_; iy_ = iyn_;
@@ -1343,6 +1356,145 @@ class Session : public SessionBase {
     } else {
       y_ready_ = false;
       f_known_ = false;
+    }
+  }
+
+  // ------------------------------------------------------------------ device-controlled FProxGD
+  // SURVEY 8f row 2 for FISTA (round 3), the counterpart of dc_run. In the speculative steady
+  // state (the previous first trial accepted, the step t unchanged, theta = 2/(k+1) known ahead)
+  // every iteration launches the same kernels on rotating roles: the trial's batch (A@[xc |
+  // y_next] and its finalize, or the split-candidate A xc + A e_c gather and k_finalize_fista),
+  // then the fused A^T r at y_next + the next first trial (k_atr_fista). The backtracking test
+  // (gl_FProxGD_primal.py:92-97), the next record and the stop rule (:127-134) run in the
+  // finalize's last block (ctl_decide, mode 1); with a communicator in k_ctl_decide behind the
+  // gradient all-reduce that carries the trial's residual sums, followed by k_fista_trial. A
+  // gathered batch whose nnz(e_c) exceeds the budget ends the device batch (code 3): the host
+  // path then runs kFistaDenseRun dense batches, which device control queues again (each batch
+  // at most until the A thr(x_k) restore). The host re-derives every decision from the records
+  // and checks it; results are bit-identical to host control.
+  struct FRoles { int ix, iv, iy, ic, ivn, iyn, f1, f2, f3, iry, gset, ks; };
+  bool fista_dc_ready(double t0, double theta) const {
+    return dc_window_ > 0 && method_ == GLX_FPROXGD && fused_fista_ok_ && spec_trial_ready_ &&
+           y_ready_ && !gy_pending_ && spec_trial_mu_ == mu_ && spec_trial_t_ == t0 &&
+           spec_trial_theta_ == theta && want_spec(0) && !(fsplit_ && kslot_ < 0 && dense_left_ == 0);
+  }
+  // one segment of a device-controlled FISTA batch; th = theta of the iteration, thn / thnn the
+  // next two (the speculative trial's theta and theta_next)
+  void fista_dc_queue(FRoles& q, int64_t tag, bool split, double t, double th, double thn,
+                      double thnn) {
+    const int rc = (q.iry + 1) % kRes, ryn = (q.iry + 2) % kRes;
+    Ctl c = dc_make_ctl(tag);
+    c.mode = 1;
+    c.t = t;
+    c.nnz_budget = split ? nnz_budget_ : -1.0;
+    dc_gate_ = dc_abort_;
+    const int ns = nset(q.gset);
+    double* defer = comm_ ? tail(ns) : nullptr;
+    if (split) {
+      const T* xs[3] = {E_, X_[q.ic], nullptr};
+      cand_ax(xs);
+      launch_finalize_fista<T>(Pp_ + (size_t)gsplit_ * ml_, ax_split(plan_, 1), Pp_, gsplit_, B_,
+                               R_[ryn], SXO_[q.ks], SXO_[(q.ks + 1) % 3], ml_, 1.0 - thn, thn, th,
+                               X_[q.ic], nl_, scal_ + S_TR + 3, gather_counts(glists_, n_), (int)l_,
+                               defer ? red_to(defer) : red(S_RT), st_, comm_ ? Ctl{} : c);
+      check_launch();
+      q.ks = (q.ks + 1) % 3;
+    } else {
+      const T* xs[3] = {X_[q.ic], X_[q.iyn], nullptr};
+      T* rs[3] = {R_[rc], R_[ryn], nullptr};
+      if (!comm_) dc_ctl_ = c;
+      residuals(2, xs, rs, S_RT, X_[q.ic], scal_ + S_TR + 3, nullptr, 0.0, nullptr, defer);
+      dc_ctl_ = Ctl{};
+    }
+    if (comm_) {
+      gradient(R_[ryn], ns, 2);
+      const int64_t slot = (tag % kCtlMaxBatch) * kCtlRec;
+      launch_ctl_decide(c, tail(ns), dc_ring_dev_ + slot,
+                        reinterpret_cast<unsigned*>(dc_ring_dev_ + slot + kCtlRec - 1), (unsigned)tag, st_);
+      check_launch();
+      // the next first trial runs also behind a stop / budget decision (the host path needs it)
+      launch_fista_trial<T>(true, X_[q.iyn], Gs_[ns], 1, nullptr, X_[q.ic], X_[q.f1], X_[q.f2],
+                            X_[q.f3], n_, l_, t, mu_, O_.thres, thn, thnn, O_.delta,
+                            red(S_TR, c.pass), st_, Pub{}, fec(), fzf());
+      check_launch();
+    } else {
+      dc_pass_ = c.pass;
+      dc_pub_ = Pub{};
+      const int64_t slot = (tag % kCtlMaxBatch) * kCtlRec;
+      dc_pub_.s = dc_rec_ + slot;
+      dc_pub_.ns = 11;
+      dc_pub_.host = dc_ring_dev_ + slot;
+      dc_pub_.host_seq = reinterpret_cast<unsigned*>(dc_ring_dev_ + slot + kCtlRec - 1);
+      dc_pub_.seq = (unsigned)tag;
+      atr_fista(R_[ryn], ns, X_[q.iyn], X_[q.ic], q.f1, q.f2, q.f3, t, thn, thnn);
+      dc_pub_ = Pub{};
+      dc_pass_ = 0;
+    }
+    dc_gate_ = nullptr;
+    q.iry = ryn;
+    const int ox = q.ix, ov = q.iv, oy = q.iy;
+    q.ix = q.ic; q.iv = q.ivn; q.iy = q.iyn;
+    q.ic = q.f1; q.ivn = q.f2; q.iyn = q.f3;
+    q.f1 = ox; q.f2 = ov; q.f3 = oy;
+    q.gset = ns;
+  }
+  void fista_dc_run() {
+    int64_t budget = O_.maxit - inner_ + 1;
+    if (O_.max_total_iters > 0) budget = std::min<int64_t>(budget, O_.max_total_iters - k_ + 1);
+    budget = std::max<int64_t>(1, std::min<int64_t>(budget, step_room_));
+    const bool split = fsplit_ && kslot_ >= 0 && dense_left_ == 0;
+    // dense batches: at most until the A thr(x_k) restore the host path runs after the last one
+    if (fsplit_ && dense_left_ > 0) budget = std::min<int64_t>(budget, dense_left_);
+    ++syncs_;   // the host's one drain point per batch (its records are read while it runs)
+    launch_ctl_seed(dc_state_, dc_abort_, gy_sq_, f_cur_, s_cur_, (double)stable_, st_);
+    check_launch();
+    FRoles q{ix_, iv_, iy_, ic_, ivn_, iyn_, ff1_, ff2_, ff3_, iry_, spec_set_, kslot_};
+    const int64_t tag0 = dc_tag_, in0 = inner_;
+    const double t = tk_;
+    int64_t queued = 0;
+    const int64_t w = std::min<int64_t>(dc_window_, budget);
+    auto push = [&]() {
+      const int64_t d = queued;
+      dc_tag_ = tag0 + 1 + queued++;
+      fista_dc_queue(q, dc_tag_, split, t, 2.0 / (double)(in0 + d + 1), 2.0 / (double)(in0 + d + 2),
+                     2.0 / (double)(in0 + d + 3));
+    };
+    while (queued < w) push();
+    int prev = 0;
+    for (int64_t d = 0; d < budget; ++d) {
+      if (d > 0) {
+        record(f_cur_, s_cur_);
+        const bool stop = stop_rule();
+        if (stop != (prev == 1))
+          throw Error{GLX_E_STATE, "device-controlled batch: stop rule differs from the host's"};
+        if (stop) { end_phase(true); return; }
+      }
+      const double* rec = dc_wait(tag0 + 1 + d);
+      ++record_waits_;
+      if (queued < budget) push();
+      for (int i = 0; i < 4; ++i) hs_[S_RT + i] = rec[i];
+      for (int i = 0; i < 6; ++i) hs_[S_TR + i] = rec[4 + i];
+      const int code = (int)rec[10];
+      spec_trial_ready_ = false;
+      use_gset(spec_set_);
+      const double theta = 2.0 / (double)(inner_ + 1), theta_next = 2.0 / (double)(inner_ + 2);
+      const double gy = 0.5 * gy_sq_, gxc = 0.5 * hs_[S_RT];
+      const bool acc = gxc <= gy + hs_[S_TR + 0] + hs_[S_TR + 1] / (2 * t);
+      if (acc != (code != 2))
+        throw Error{GLX_E_STATE, "device-controlled batch: backtracking decision differs from the host's"};
+      stats_[7] += 1;
+      if (!acc) {   // everything behind this decision was cancelled on the device
+        spec_on_ = false;
+        fista_trials({G_, 1}, true, t * O_.ls_coeff, 1, theta, theta_next, false);
+        return;
+      }
+      spec_on_ = true;
+      const bool trip = split && hs_[S_RT + 2] > nnz_budget_;
+      if ((code == 3) != (trip && code != 1))
+        throw Error{GLX_E_STATE, "device-controlled batch: nnz budget decision differs from the host's"};
+      fista_update(true, true, t, split, theta_next, (iry_ + 2) % kRes, 2);
+      prev = code;
+      if (code == 3) return;   // the batch behind was cancelled; dense batches follow
     }
   }
 
@@ -1407,11 +1559,11 @@ class Session : public SessionBase {
       check_launch();
       return;
     }
-    Pub pb;
+    Pub pb = dc_pub_;   // in a device-controlled batch: the decision record (fista_dc_queue)
     if (pub_seq) pb = make_pub(extra, pub_seq);
     hipEvent_t e0 = prof_begin(1);
     launch_atr_fista<T>(plan_, A_, r, Gs_[set], yv, xk, X_[oc], X_[ov], X_[oy], t, mu_, O_.thres,
-                        theta, theta_next, red(S_TR), st_, pb, Gps_[set], pcnt_, fec(), fzf());
+                        theta, theta_next, red(S_TR, dc_pass_), st_, pb, Gps_[set], pcnt_, fec(), fzf());
     check_launch();
     prof_end(1, e0);
     ++atr_calls_;
@@ -1575,7 +1727,10 @@ class Session : public SessionBase {
   int64_t phase_start_[3] = {-1, -1, -1};
   int64_t phase_break_[3] = {0, 0, 0};
   double tt_ = 0;
-  int64_t ax_calls_ = 0, ax_cols_ = 0, atr_calls_ = 0, syncs_ = 0;
+  // syncs_: host readbacks the queue drains behind (the host decides before queuing more; one
+  // per device-controlled batch); record_waits_: decision records read while the device keeps
+  // later iterations queued (device-controlled batches)
+  int64_t ax_calls_ = 0, ax_cols_ = 0, atr_calls_ = 0, syncs_ = 0, record_waits_ = 0;
   double stats_[8] = {0, 0, 0, 0, 0, 0, 0, 0};
   std::vector<std::pair<hipEvent_t, hipEvent_t>> ev_[3];
   int64_t prof_n_[3] = {0, 0, 0};

@@ -29,7 +29,7 @@ class GlxOpts(ctypes.Structure):
                 ("ls_coeff", c_double), ("ls_maxit", c_int32), ("delta", c_double),
                 ("continuous_subgradient", c_int32), ("exact_objective", c_int32),
                 ("profile", c_int32), ("max_total_iters", c_int64), ("ax_variant", c_int32),
-                ("reserved", c_int32 * 7)]
+                ("split_cand", c_int32), ("dc_window", c_int32), ("reserved", c_int32 * 5)]
 
 
 class GlxProblem(ctypes.Structure):
@@ -43,7 +43,7 @@ class GlxResult(ctypes.Structure):
                 ("f_hist", POINTER(c_double)), ("f_hist_best", POINTER(c_double)),
                 ("f_cap", c_int64), ("n_fhist", c_int64), ("ax_calls", c_int64),
                 ("atr_calls", c_int64), ("syncs", c_int64), ("ax_sources", c_int64),
-                ("stats", c_double * 8)]
+                ("stats", c_double * 8), ("record_waits", c_int64)]
 
 
 class GlxError(RuntimeError):
@@ -112,7 +112,7 @@ def lib():
             fn = getattr(h, name)
             fn.restype = res
             fn.argtypes = args
-        if h.glx_abi_version() != 1:
+        if h.glx_abi_version() != 2:
             raise RuntimeError("libglx ABI mismatch")
         _LIB = h
     return _LIB

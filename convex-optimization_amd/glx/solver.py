@@ -15,7 +15,8 @@ provides device memory, the stream and the multi-process bootstrap. There is no 
 
 Build-only option keys (ignored by the reference): ``exact_objective`` (ProxGD: recompute
 A@x for every objective instead of reusing the accepted trial residual), ``profile``,
-``max_total_iters``, ``ax_variant``, ``device``, ``comm``.
+``max_total_iters``, ``ax_variant``, ``split_cand`` (0 auto, 1 on, 2 off), ``dc_window``
+(device-controlled line search: 0 auto, -1 off, k iterations in flight), ``device``, ``comm``.
 """
 from __future__ import annotations
 
@@ -37,7 +38,8 @@ _REF_KEYS = {
     "line_search_attenuation_coeffi": "ls_coeff", "maxit_line_search_iter": "ls_maxit",
     "delta": "delta",
 }
-_BUILD_KEYS = {"exact_objective", "profile", "max_total_iters", "ax_variant"}
+_BUILD_KEYS = {"exact_objective", "profile", "max_total_iters", "ax_variant", "split_cand",
+               "dc_window"}
 
 
 def _device(opts: Dict[str, Any]) -> torch.device:
@@ -212,6 +214,7 @@ class Session:
                 "f_hist_best": [np.float64(v) for v in fb[:n]],
                 "ax_calls": int(res.ax_calls), "atr_calls": int(res.atr_calls),
                 "syncs": int(res.syncs), "ax_sources": int(res.ax_sources),
+                "record_waits": int(res.record_waits),
                 "stats": [float(v) for v in res.stats]}
 
     def close(self):

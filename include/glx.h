@@ -35,7 +35,7 @@
 extern "C" {
 #endif
 
-#define GLX_ABI_VERSION 1
+#define GLX_ABI_VERSION 2
 
 enum glx_dtype { GLX_F32 = 0, GLX_F64 = 1 };
 enum glx_method { GLX_PROXGD = 0, GLX_FPROXGD = 1, GLX_SGD = 2, GLX_GD = 3, GLX_FGD = 4 };
@@ -69,7 +69,15 @@ typedef struct glx_opts {
   int32_t profile;                /* k > 0: time every k-th A@x / A^T r launch (HIP events) */
   int64_t max_total_iters;        /* stop after this many iterations in total (0 = off)     */
   int32_t ax_variant;             /* A@x kernel variant for A/B tests (0 = auto)            */
-  int32_t reserved[7];
+  int32_t split_cand;             /* fp64 ProxGD / FProxGD split-candidate trial (A p = A p_thr
+                                     + A e, A e gathered from a transposed copy of A): 0 = auto
+                                     (on when this rank's A is >= 768 MiB; GLX_SPLIT_CAND env
+                                     overrides), 1 = on at any size, 2 = off. On adds an m x n
+                                     copy of A to the workspace (glx_workspace_bytes counts it) */
+  int32_t dc_window;              /* device-controlled line search (ProxGD / FProxGD): 0 = auto
+                                     (GLX_DC_BATCH env, else off), -1 = off, k in 1..32 = up to
+                                     k iterations queued ahead of the host                      */
+  int32_t reserved[5];
 } glx_opts;
 
 /* One problem instance. For multi-GPU runs A and b are this rank's row shard
@@ -96,12 +104,16 @@ typedef struct glx_result {
   int64_t n_fhist;      /* entries written                                           */
   int64_t ax_calls;     /* passes of A@x issued (executed-work accounting)            */
   int64_t atr_calls;    /* passes of A^T r issued                                     */
-  int64_t syncs;        /* host<->device synchronisations                             */
+  int64_t syncs;        /* host readbacks the device queue drains behind (the host decides
+                           before queuing more work; a device-controlled batch counts one) */
   int64_t ax_sources;   /* right-hand sides batched into those A@x passes (>= ax_calls) */
   double stats[8];      /* diagnostics: [0] threshold-changed entries and [1] rows summed over
                            accepted ProxGD steps, [2] accepted steps; split-candidate
                            FProxGD: [3] gathered batches, [4] dense batches, [5] nnz(e_c)
-                           summed over the gathered ones, [6] A thr(x_k) restores       */
+                           summed over the gathered ones, [6] A thr(x_k) restores;
+                           [7] iterations whose line-search decision ran on the device  */
+  int64_t record_waits; /* device-controlled batches: decision records the host read while
+                           later iterations stayed queued on the device                   */
 } glx_result;
 
 typedef struct glx_session glx_session;
@@ -111,7 +123,10 @@ int         glx_abi_version(void);
 const char* glx_last_error(void);
 int         glx_default_opts(int method, glx_opts* out);
 
-/* Workspace (device bytes) a session needs for this problem. */
+/* Workspace (device bytes) a session needs for this problem and these options (includes the
+ * transposed copy of A of the split-candidate trial, opts.split_cand, and the gradient-set ring
+ * of device control with a communicator, opts.dc_window). Environment overrides (GLX_*) are read
+ * here and at create: keep them unchanged in between. */
 int glx_workspace_bytes(const glx_problem* prob, const glx_opts* opts, size_t* bytes);
 
 /* Session API: the reference loop split so that a caller can time exactly K iterations.
@@ -129,7 +144,8 @@ int  glx_session_finish(glx_session* s, glx_result* res);
  * kind; resets the accumulators. */
 int  glx_session_kernel_time(glx_session* s, int kind, int64_t* launches, double* total_ms);
 /* executed-work counters since create: out = {A@x passes, right-hand sides in them, A^T r
- * passes, host readbacks} (cumulative; the caller differences them around a timed region). */
+ * passes, host readbacks (glx_result.syncs)} (cumulative; the caller differences them around a
+ * timed region). */
 int  glx_session_counters(glx_session* s, int64_t out[4]);
 /* After glx_session_finish: what the reference's 'opt' logger prints, so a host can replay it
  * without touching the hot loop (gl_ProxGD_primal.py:54 `new mu=` per phase, :134-136 the line

@@ -27,10 +27,12 @@ def main():
     ap.add_argument("--n", type=int, default=16384)
     ap.add_argument("--l", type=int, default=32)
     ap.add_argument("--maxit", type=int, default=0, help="per phase (0 = the method's default)")
+    ap.add_argument("--dtype", default="f64", choices=["f64", "f32"])
     a = ap.parse_args()
     import glx
     dev = torch.device("cuda", 0)
-    A, b, x0 = bench.make_instance(a.m, a.n, a.l, 0, a.m, torch.float64, dev)
+    dt = torch.float64 if a.dtype == "f64" else torch.float32
+    A, b, x0 = bench.make_instance(a.m, a.n, a.l, 0, a.m, dt, dev)
     alpha0 = float(1.0 / (math.sqrt(a.m) + math.sqrt(a.n)) ** 2)
     opts = {"alpha0": alpha0}
     if a.maxit:
@@ -42,9 +44,10 @@ def main():
     x, k, out = glx.solve(a.method, x0.clone(), A, b, 1e-2, dict(opts))
     torch.cuda.synchronize()
     wall = time.perf_counter() - t0
-    print(json.dumps({"method": a.method, "k": int(k), "tt": out["tt"], "wall": wall,
+    print(json.dumps({"method": a.method, "dtype": a.dtype, "shape": [a.m, a.n, a.l], "k": int(k), "tt": out["tt"], "wall": wall,
                       "its": k / out["tt"], "fval": float(out["fval"]), "stats": out.get("stats"),
                       "ax_calls": out.get("ax_calls"), "ax_sources": out.get("ax_sources"),
+                      "syncs": out.get("glx", {}).get("syncs"),
                       "env": {k2: v for k2, v in os.environ.items() if k2.startswith("GLX_")}}))
 
 

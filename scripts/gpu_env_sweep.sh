@@ -10,6 +10,6 @@ while IFS='|' read -r tag envs args; do
   python - "$O/$tag.json" "$tag" "$envs" <<'PY'
 import json, sys
 d = json.loads(open(sys.argv[1]).read().strip().splitlines()[-1]); r = d["roofline"]
-print("%-16s %-40s %8.1f it/s ax %6.1fus atr %6.1fus  %s" % (sys.argv[2], sys.argv[3], d["value"], r["avg_launch_us"], r["atr_avg_launch_us"], r["kernel"]))
+print("%-16s %-40s %8.1f it/s ax %6.1fus atr %6.1fus syncs/it %.3f  %s" % (sys.argv[2], sys.argv[3], d["value"], r["avg_launch_us"], r["atr_avg_launch_us"], d["work"]["syncs_per_iter"], r["kernel"]))
 PY
 done < "$2"

@@ -30,6 +30,7 @@ def main():
     ap.add_argument("--windows", default="0,8")
     ap.add_argument("--slices", type=int, default=0)
     ap.add_argument("--out", required=True)
+    ap.add_argument("--method", default="gl_ProxGD_primal")
     a = ap.parse_args()
 
     import glx
@@ -53,7 +54,7 @@ def main():
         os.environ["GLX_DC_BATCH"] = str(w)
         At, bt, xt = (torch.from_numpy(np.ascontiguousarray(v.astype(dt))).cuda()
                       for v in (A[r0:r1], b[r0:r1], x0))
-        s = glx.Session("gl_ProxGD_primal", xt, At, bt, mu, dict(opts), comm=comm)
+        s = glx.Session(a.method, xt, At, bt, mu, dict(opts), comm=comm)
         if a.slices:
             while not s.finished:
                 s.run(a.slices)

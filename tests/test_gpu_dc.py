@@ -25,7 +25,7 @@ def _instance(m, n, l, seed=2024):
 
 
 def _run(monkeypatch, window, shape, dtype=np.float64, alpha_scale=1.0, opts=None, slices=0,
-         env=None):
+         env=None, method="gl_ProxGD_primal"):
     import glx
     monkeypatch.setenv("GLX_DC_BATCH", str(window))
     for k, v in (env or {}).items():
@@ -34,7 +34,7 @@ def _run(monkeypatch, window, shape, dtype=np.float64, alpha_scale=1.0, opts=Non
     o = {"alpha0": alpha0 * alpha_scale}
     o.update(opts or {})
     At, bt, xt = (torch.from_numpy(a.astype(dtype)).cuda() for a in (A, b, x0))
-    s = glx.Session("gl_ProxGD_primal", xt, At, bt, mu, o)
+    s = glx.Session(method, xt, At, bt, mu, o)
     if slices:
         while not s.finished:
             s.run(slices)
@@ -52,7 +52,7 @@ def _same(a, b):
     assert np.array_equal(np.asarray(r_a["f_hist"]), np.asarray(r_b["f_hist"]))
     assert r_a["fval"] == r_b["fval"]
     assert np.array_equal(x_a, x_b)
-    assert r_a["stats"][:3] == r_b["stats"][:3]   # thresholded entries / rows, accepted trials
+    assert r_a["stats"][:7] == r_b["stats"][:7]   # threshold / split-candidate statistics
 
 
 CASES = [
@@ -115,6 +115,61 @@ def test_oracle_parity_with_device_control(monkeypatch):
     A, b, x0, mu, alpha0 = _instance(*shape)
     x, r = _run(monkeypatch, 8, shape, alpha_scale=2.5)
     xr, kr, outr = numpy_ref.gl_ProxGD_primal(x0, A, b, mu, {"alpha0": alpha0 * 2.5})
+    assert r["k"] == kr
+    assert abs(r["fval"] - outr["fval"]) <= 1e-10 * abs(outr["fval"])
+    assert r["stats"][7] > 0
+
+
+# ---- FProxGD (solver.cpp fista_dc_run): the backtracking test (gl_FProxGD_primal.py:92-97), the
+# next record and the stop rule on the device; split-candidate batches also check nnz(e_c)
+# against the budget (code 3 ends the device batch, dense batches follow on the host path and
+# are device-controlled again up to the A thr(x_k) restore).
+FISTA_CASES = [
+    ((512, 1024, 16), np.float64, 1.0, {}, {}, 0.5),
+    ((512, 1024, 16), np.float64, 3.0, {}, {}, 0.3),      # backtracking rejections
+    ((512, 1024, 16), np.float32, 1.0, {}, {}, 0.5),      # fp32 (C3's dtype)
+    ((256, 16384, 32), np.float64, 1.0, {"maxit": 300}, {}, 0.5),
+    ((256, 16384, 32), np.float64, 1.5, {"maxit": 200}, {"GLX_SPLIT_CAND": "1"}, 0.5),
+    # a tight nnz budget: gathered batches trip it, dense runs and restores alternate
+    ((256, 16384, 32), np.float64, 1.0, {"maxit": 400}, {"GLX_SPLIT_CAND": "1", "GLX_SPLIT_NNZ": "0.002"}, 0.3),
+]
+
+
+@pytest.mark.parametrize("shape,dtype,scale,opts,env,frac", FISTA_CASES)
+def test_fista_device_control_bit_identical(monkeypatch, shape, dtype, scale, opts, env, frac):
+    m = "gl_FProxGD_primal"
+    host = _run(monkeypatch, 0, shape, dtype, scale, opts, env=env, method=m)
+    dev = _run(monkeypatch, 8, shape, dtype, scale, opts, env=env, method=m)
+    _same(dev, host)
+    r_h, r_d = host[1], dev[1]
+    assert r_h["stats"][7] == 0
+    assert r_d["stats"][7] >= frac * r_d["k"], r_d["stats"]
+    assert r_d["syncs"] < 0.5 * r_h["syncs"], (r_d["syncs"], r_h["syncs"])
+    if env.get("GLX_SPLIT_NNZ"):
+        assert r_d["stats"][3] > 0 and r_d["stats"][4] > 0 and r_d["stats"][6] > 1, r_d["stats"]
+
+
+@pytest.mark.parametrize("window", [1, 3, 32])
+def test_fista_window_sizes(monkeypatch, window):
+    m, shape = "gl_FProxGD_primal", (512, 1024, 16)
+    _same(_run(monkeypatch, window, shape, alpha_scale=3.0, method=m),
+          _run(monkeypatch, 0, shape, alpha_scale=3.0, method=m))
+
+
+def test_fista_run_in_slices_and_max_total(monkeypatch):
+    m, shape = "gl_FProxGD_primal", (512, 1024, 16)
+    _same(_run(monkeypatch, 8, shape, slices=7, method=m), _run(monkeypatch, 0, shape, method=m))
+    dev = _run(monkeypatch, 8, shape, opts={"max_total_iters": 41}, method=m)
+    assert dev[1]["k"] == 41
+    _same(dev, _run(monkeypatch, 0, shape, opts={"max_total_iters": 41}, method=m))
+
+
+def test_fista_oracle_parity_with_device_control(monkeypatch):
+    from oracle import numpy_ref
+    shape = (512, 1024, 16)
+    A, b, x0, mu, alpha0 = _instance(*shape)
+    x, r = _run(monkeypatch, 8, shape, alpha_scale=3.0, method="gl_FProxGD_primal")
+    xr, kr, outr = numpy_ref.gl_FProxGD_primal(x0, A, b, mu, {"alpha0": alpha0 * 3.0})
     assert r["k"] == kr
     assert abs(r["fval"] - outr["fval"]) <= 1e-10 * abs(outr["fval"])
     assert r["stats"][7] > 0

@@ -29,14 +29,15 @@ def _port():
     return p
 
 
-def _twin(tmp_path, shape, dtype="f64", scale=1.0, opts=None, env=None, windows="0,8", slices=0):
+def _twin(tmp_path, shape, dtype="f64", scale=1.0, opts=None, env=None, windows="0,8", slices=0,
+          method="gl_ProxGD_primal"):
     out = tmp_path / "dc_twin.json"
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes", "1", "--nproc-per-node", "2",
            "--master-addr", "127.0.0.1", "--master-port", str(_port()),
            os.path.join(ROOT, "tests", "dc_dist_worker.py"), "--shape", ",".join(map(str, shape)),
            "--dtype", dtype, "--alpha-scale", str(scale), "--opts", json.dumps(opts or {}),
            "--env", json.dumps(env or {}), "--windows", windows, "--slices", str(slices),
-           "--out", str(out)]
+           "--out", str(out), "--method", method]
     p = subprocess.run(cmd, env=dict(os.environ, OMP_NUM_THREADS="1"), capture_output=True,
                        text=True, timeout=140)
     assert p.returncode == 0, p.stdout[-3000:] + p.stderr[-3000:]
@@ -49,7 +50,7 @@ def _same(a, b):
     assert a["f_hist"] == b["f_hist"]
     assert a["fval"] == b["fval"]
     assert a["x_sha"] == b["x_sha"]
-    assert a["stats"][:3] == b["stats"][:3]
+    assert a["stats"][:7] == b["stats"][:7]
 
 
 CASES = [   # the cases of test_gpu_dc.py
@@ -103,4 +104,40 @@ def test_world2_split_candidate_gather_form(tmp_path):
 def test_world2_max_total_iters(tmp_path):
     r = _twin(tmp_path, (512, 1024, 16), opts={"max_total_iters": 37})
     assert r["8"][0]["k"] == 37
+    _same(r["8"][0], r["0"][0])
+
+
+FISTA_CASES = [   # the FProxGD cases of test_gpu_dc.py (fp32 stays host-controlled at N > 1)
+    ((512, 1024, 16), "f64", 1.0, {}, {}, 0.5),
+    ((512, 1024, 16), "f64", 3.0, {}, {}, 0.3),
+    ((512, 1024, 16), "f32", 1.0, {}, {}, 0.0),
+    ((256, 16384, 32), "f64", 1.0, {"maxit": 300}, {}, 0.5),
+    ((256, 16384, 32), "f64", 1.5, {"maxit": 200}, {"GLX_SPLIT_CAND": "1"}, 0.5),
+    ((256, 16384, 32), "f64", 1.0, {"maxit": 400}, {"GLX_SPLIT_CAND": "1", "GLX_SPLIT_NNZ": "0.002"}, 0.3),
+]
+
+
+@pytest.mark.parametrize("shape,dtype,scale,opts,env,frac", FISTA_CASES)
+def test_fista_device_control_world2_bit_identical(tmp_path, shape, dtype, scale, opts, env, frac):
+    r = _twin(tmp_path, shape, dtype, scale, opts, env=env, method="gl_FProxGD_primal")
+    host, dev = r["0"], r["8"]
+    for ranks in (host, dev):
+        for x in ranks[1:]:
+            _same(x, ranks[0])
+    _same(dev[0], host[0])
+    assert host[0]["stats"][7] == 0
+    d = dev[0]
+    if dtype == "f32":
+        assert d["stats"][7] == 0
+    else:
+        assert d["stats"][7] >= frac * d["k"], d["stats"]
+        assert d["syncs"] < 0.5 * host[0]["syncs"]
+
+
+def test_fista_world2_windows_and_slices(tmp_path):
+    m = "gl_FProxGD_primal"
+    r = _twin(tmp_path, (512, 1024, 16), scale=3.0, windows="0,1,3,32", method=m)
+    for w in ("1", "3", "32"):
+        _same(r[w][0], r["0"][0])
+    r = _twin(tmp_path, (512, 1024, 16), slices=7, method=m)
     _same(r["8"][0], r["0"][0])

@@ -33,10 +33,8 @@ SHAPES = [
 
 @pytest.mark.parametrize("dtype", ["f64", "f32"])
 @pytest.mark.parametrize("shape", SHAPES)
-@pytest.mark.parametrize("variant", [0, 2, 3, 21420, 41210, 52224, 54214, 52228, 84208, 84218, 83218,
-                                     82418, 88118, 84214, 83238, 84131, 84111, 82231, 83258,
-                                     84258, 83248, 84151, 94158, 94148, 93158, 92258, 83278,
-                                     93178, 92278, 93168, 92268, 94178, 94168])
+@pytest.mark.parametrize("variant", [0, 2, 3, 1820, 21820, 21410, 52224, 52228, 51328, 52324, 92278,
+                                     92268])
 def test_residual_and_gradient(shape, dtype, variant):
     k = _glx()
     m, n, l = shape
@@ -64,9 +62,7 @@ def test_residual_and_gradient(shape, dtype, variant):
     assert _rel_err(G, gref, gmag) < tolg
 
 
-BATCH_CODES = [0, 21420, 1220, 52224, 52324, 52228, 54224, 52214, 54214, 52428, 54228, 54218,
-               84208, 83208, 83218, 82408, 88108, 84204, 83238, 84131, 82231, 83258, 83248,
-               84151, 94158, 93158, 93178, 83278, 93168, 92278, 94168]
+BATCH_CODES = [0, 1420, 52224, 52324, 52228, 51328, 92278, 92268]
 
 
 @pytest.mark.parametrize("dtype", ["f64", "f32"])

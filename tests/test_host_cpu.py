@@ -24,7 +24,7 @@ def test_library_loads_and_exports_header_symbols():
     for name in sorted(declared):
         assert hasattr(h, name), name
     assert set(_lib.EXPORTED) == declared
-    assert h.glx_abi_version() == 1
+    assert h.glx_abi_version() == 2
 
 
 def test_single_hip_runtime_in_process():
@@ -44,9 +44,10 @@ def test_struct_layout_matches_c():
 #include <stddef.h>
 #include "glx.h"
 int main(void) {
-  printf("%zu %zu %zu %zu %zu %zu %zu\n", sizeof(glx_opts), sizeof(glx_problem), sizeof(glx_result),
-         offsetof(glx_opts, max_total_iters), offsetof(glx_problem, mu0), offsetof(glx_result, syncs),
-         offsetof(glx_opts, ax_variant));
+  printf("%zu %zu %zu %zu %zu %zu %zu %zu %zu %zu\n", sizeof(glx_opts), sizeof(glx_problem),
+         sizeof(glx_result), offsetof(glx_opts, max_total_iters), offsetof(glx_problem, mu0),
+         offsetof(glx_result, syncs), offsetof(glx_opts, ax_variant), offsetof(glx_opts, split_cand),
+         offsetof(glx_opts, dc_window), offsetof(glx_result, record_waits));
   return 0;
 }'''
     with tempfile.TemporaryDirectory() as d:
@@ -57,7 +58,8 @@ int main(void) {
         got = [int(v) for v in subprocess.run([exe], capture_output=True, text=True, check=True).stdout.split()]
     want = [ctypes.sizeof(_lib.GlxOpts), ctypes.sizeof(_lib.GlxProblem), ctypes.sizeof(_lib.GlxResult),
             _lib.GlxOpts.max_total_iters.offset, _lib.GlxProblem.mu0.offset, _lib.GlxResult.syncs.offset,
-            _lib.GlxOpts.ax_variant.offset]
+            _lib.GlxOpts.ax_variant.offset, _lib.GlxOpts.split_cand.offset,
+            _lib.GlxOpts.dc_window.offset, _lib.GlxResult.record_waits.offset]
     assert got == want
 
 
