@@ -214,6 +214,12 @@ __device__ inline double row_allsum(double v) {
   return v;
 }
 template <int LPR>
+__device__ inline unsigned row_or(unsigned v) {
+#pragma unroll
+  for (int off = LPR / 2; off > 0; off >>= 1) v |= __shfl_xor(v, off);
+  return v;
+}
+template <int LPR>
 __device__ inline float row_allsum(float v) {
 #pragma unroll
   for (int off = LPR / 2; off > 0; off >>= 1) v += __shfl_xor(v, off);
@@ -232,11 +238,12 @@ __device__ inline float row_allsum(float v) {
 // emode (the split-candidate form of the fast objective mode, see solver.cpp iter_proxgd):
 // instead of z the third output is e = p - p_thr, i.e. p where the threshold zeroed it and 0
 // elsewhere (exact: p_thr is either p or 0, and NaN is never "small"), so A p = A p_thr + A e
-// with e nonzero only in the rows the threshold touched. Returns whether this row of e is
-// nonzero (every lane of the row gets the same answer).
+// with e nonzero only in the rows the threshold touched. Returns the row's column mask of e
+// (bit j = e[j] != 0, columns j < 32; every lane of the row gets the same mask), which the
+// split-candidate gather's column lists are built from (kernels_gather.hip k_e_lists).
 // ------------------------------------------------------------------------------------------
 template <typename T, int LPR, int EPL>
-__device__ inline bool prox_pgd_row(const T (&xv)[EPL], const T (&gv)[EPL], const bool (&ok)[EPL],
+__device__ inline unsigned prox_pgd_row(const T (&xv)[EPL], const T (&gv)[EPL], const bool (&ok)[EPL],
                                     bool rv, int sub, T t, T tmu, T thres, T (&pv)[EPL],
                                     T (&pth)[EPL], T (&zv)[EPL], double (&acc)[6],
                                     bool emode = false) {
@@ -253,6 +260,7 @@ __device__ inline bool prox_pgd_row(const T (&xv)[EPL], const T (&gv)[EPL], cons
   const T d = ((nrm < thres) ? T(1) : T(0)) + nrm;
   T psq = T(0);
   bool rch = false;
+  unsigned mk = 0;
 #pragma unroll
   for (int e = 0; e < EPL; ++e) {
     pv[e] = (w[e] * c) / d;
@@ -267,6 +275,7 @@ __device__ inline bool prox_pgd_row(const T (&xv)[EPL], const T (&gv)[EPL], cons
       const bool ch = small && pv[e] != T(0);
       acc[4] += ch ? 1.0 : 0.0;
       rch = rch || ch;
+      if (ch && sub + e * LPR < 32) mk |= 1u << (sub + e * LPR);
       psq = psq + pv[e] * pv[e];
     }
   }
@@ -276,7 +285,7 @@ __device__ inline bool prox_pgd_row(const T (&xv)[EPL], const T (&gv)[EPL], cons
     acc[2] += (double)pn;
     acc[5] += rowch > 0.0 ? 1.0 : 0.0;
   }
-  return rowch > 0.0;
+  return emode ? row_or<LPR>(mk) : 0u;
 }
 
 // ------------------------------------------------------------------------------------------
@@ -287,9 +296,9 @@ __device__ inline bool prox_pgd_row(const T (&xv)[EPL], const T (&gv)[EPL], cons
 //      FGD  [sum g*(xc-y), sum (xc-y)^2, sum (sqrt(||xc_i||^2+d^2)-d), sum ||xc_i||, max |xc|].
 // ------------------------------------------------------------------------------------------
 // ecv (split form, when non-null): e_c = xc - thr(xc), i.e. xc where the threshold zeroes it and
-// 0 elsewhere; returns whether this row of e_c is nonzero (same answer on every lane of the row).
+// 0 elsewhere; returns the row's column mask of e_c (as prox_pgd_row; 0 without ecv).
 template <typename T, int LPR, int EPL, bool PROX>
-__device__ inline bool fista_row(const T (&yv)[EPL], const T (&gv)[EPL], const T (&xkv)[EPL],
+__device__ inline unsigned fista_row(const T (&yv)[EPL], const T (&gv)[EPL], const T (&xkv)[EPL],
                                  const bool (&ok)[EPL], bool rv, int sub, T t, T tmu, T thres,
                                  T theta, T a1, T b1, T dd, T delta, T (&xcv)[EPL],
                                  T (&vnv)[EPL], T (&ynv)[EPL], double (&acc)[PROX ? 4 : 5],
@@ -310,7 +319,7 @@ __device__ inline bool fista_row(const T (&yv)[EPL], const T (&gv)[EPL], const T
     d = ((nrm < thres) ? T(1) : T(0)) + nrm;
   }
   T psq = T(0);
-  bool rch = false;
+  unsigned mk = 0;
 #pragma unroll
   for (int e = 0; e < EPL; ++e) {
     const T pv = PROX ? (w[e] * c) / d : w[e];
@@ -325,7 +334,7 @@ __device__ inline bool fista_row(const T (&yv)[EPL], const T (&gv)[EPL], const T
     ynv[e] = a1 * pt + b1 * vn;
     if (ecv != nullptr) {
       ecv[e] = small ? pv : T(0);
-      if (ok[e] && small && pv != T(0)) rch = true;
+      if (ok[e] && small && pv != T(0) && sub + e * LPR < 32) mk |= 1u << (sub + e * LPR);
     }
     if (ok[e]) {
       acc[0] += (double)(gv[e] * dl);
@@ -343,7 +352,7 @@ __device__ inline bool fista_row(const T (&yv)[EPL], const T (&gv)[EPL], const T
       acc[3] += (double)__builtin_sqrt(ps);
     }
   }
-  return ecv != nullptr && row_allsum<LPR>(rch ? 1.0 : 0.0) > 0.0;
+  return ecv != nullptr ? row_or<LPR>(mk) : 0u;
 }
 
 }  // namespace glx

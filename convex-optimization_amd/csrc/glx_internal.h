@@ -159,7 +159,7 @@ bool atr_prox_ok(const GemmPlan& p);
 template <typename T>
 void launch_atr_prox(const GemmPlan& p, const T* A, const T* R, T* G, const T* x, T* pp, T* pthr,
                      T* z, double t, double mu, double thres, Red red, hipStream_t st, Pub pub = Pub{},
-                     T* Gp = nullptr, unsigned* pcnt = nullptr, uint8_t* zf = nullptr);
+                     T* Gp = nullptr, unsigned* pcnt = nullptr, unsigned* zf = nullptr);
 // FISTA trial fused into A^T R (same plan condition): G = A^T R, then xc, v_next, y_next and the
 // four trial sums of k_fista_trial (PROX) into red (ec, zf: as launch_fista_trial).
 template <typename T>
@@ -167,7 +167,7 @@ void launch_atr_fista(const GemmPlan& p, const T* A, const T* R, T* G, const T* 
                       T* xc, T* vn, T* yn, double t, double mu, double thres, double theta,
                       double theta_next, Red red, hipStream_t st, Pub pub = Pub{},
                       T* Gp = nullptr, unsigned* pcnt = nullptr, T* ec = nullptr,
-                      uint8_t* zf = nullptr);
+                      unsigned* zf = nullptr);
 
 // ---- split-candidate A e from a transposed copy of A (kernels_gather.hip) ----
 // gather_ok: the shape supports it (l in {16, 32}, n < 65536); gather_split: K splits of the
@@ -177,14 +177,13 @@ int gather_split(int64_t m);
 // At (n x m) = A^T
 template <typename T>
 void launch_transpose(const T* A, T* At, int64_t m, int64_t n, hipStream_t st);
-// launch_e_lists: per column c the ascending k with zf[k] != 0 and E[k][c] != 0, into lists_ws
-// (gather_lists_bytes(n)); launch_at_gather: P[r][c] = sum over column c's list of
-// At[k][r] E[k][c] (one slab)
+// launch_e_lists: per column c the ascending k with bit c of zm[k] set (zm: the per-row column
+// masks of e the trial kernels write), into lists_ws (gather_lists_bytes(n));
+// launch_at_gather: P[r][c] = sum over column c's list of At[k][r] E[k][c] (one slab)
 size_t gather_lists_bytes(int64_t n);
 // the l per-column list lengths inside lists_ws (device)
 const unsigned* gather_counts(const void* lists_ws, int64_t n);
-template <typename T>
-void launch_e_lists(const T* E, const uint8_t* zf, int64_t n, int64_t l, void* lists_ws, hipStream_t st,
+void launch_e_lists(const unsigned* zm, int64_t n, int64_t l, void* lists_ws, hipStream_t st,
                     const int* skip = nullptr);
 template <typename T>
 void launch_at_gather(const T* At, const T* E, int64_t m, int64_t n, int64_t l, T* P, void* lists_ws,
@@ -235,23 +234,23 @@ template <typename T>
 void launch_sum_partials(const T* Gp, int S, T* G, int64_t nl, hipStream_t st);
 // ProxGD trial: p = prox(x - t g, t), G_t = (x - p)/t, z = x - t G_t, pthr = p thresholded.
 // out: [sum g*G_t, sum G_t^2, sum_i ||p_i||, max |p|, #changed by the threshold]
-// zf != NULL (split-candidate mode): z receives e = p - p_thr instead and zf[i] (n bytes) = row
-// i of e is nonzero.
+// zf != NULL (split-candidate mode): z receives e = p - p_thr instead and zf[i] = the column mask
+// of row i of e (bit c = e[i][c] != 0).
 template <typename T>
 void launch_prox_pgd(const T* x, const T* g, int S, T* gout, T* p, T* pthr, T* z, int64_t n,
                      int64_t l, double t, double mu, double thres, Red red, hipStream_t st,
-                     Pub pub = Pub{}, uint8_t* zf = nullptr);
+                     Pub pub = Pub{}, unsigned* zf = nullptr);
 // FISTA (prox = true) / FGD (prox = false: identity) trial fused with the next combine:
 // xc = prox(y - t g, t); vnext = thr(xk) + (xc - thr(xk))/theta;
 // ynext = (1 - theta_next) thr(xc) + theta_next vnext.
 // out: prox: [sum g*(xc-y), sum (xc-y)^2, sum ||xc_i||, max |xc|]
 //      FGD : [sum g*(xc-y), sum (xc-y)^2, sum (sqrt(||xc_i||^2+d^2)-d), sum ||xc_i||, max |xc|]
-// ec != NULL (split-candidate mode): ec = xc - thr(xc) and zf[i] (n bytes) = row i of ec is nonzero.
+// ec != NULL (split-candidate mode): ec = xc - thr(xc) and zf[i] = the column mask of row i of ec.
 template <typename T>
 void launch_fista_trial(bool prox, const T* y, const T* g, int S, T* gout, const T* xk, T* xc,
                         T* vnext, T* ynext, int64_t n, int64_t l, double t, double mu, double thres,
                         double theta, double theta_next, double delta, Red red, hipStream_t st,
-                        Pub pub = Pub{}, T* ec = nullptr, uint8_t* zf = nullptr);
+                        Pub pub = Pub{}, T* ec = nullptr, unsigned* zf = nullptr);
 // split-candidate FISTA batch finalize (k_finalize_fista): P = S slabs of A xc, Pe = S0 slabs of
 // A e_c, sxo = A thr(xk); Ry = A y_next - b with y_next = a1 thr(xc) + b1 (thr(xk) + (xc -
 // thr(xk)) / theta), sxo_out = A thr(xc). out: [sum (A xc - b)^2, sum Ry^2,

@@ -266,7 +266,7 @@ __global__ __launch_bounds__(256, sizeof(T) == 8 ? 2 : 1) void k_atr_prox(const 
                                                   double t_, double tmu_, double thres_, Red red,
                                                   Pub pub, int S, T* __restrict__ Gp,
                                                   unsigned* __restrict__ pcnt,
-                                                  uint8_t* __restrict__ zf) {
+                                                  unsigned* __restrict__ zf) {
   // Cancelled by a device-side decision (solver.cpp dc_run): nothing is computed or stored, no
   // counter or ticket is touched. (Testing the flag after the main loop instead measured no
   // faster and would spend a whole pass per cancelled launch.) The decision record still goes
@@ -316,9 +316,9 @@ __global__ __launch_bounds__(256, sizeof(T) == 8 ? 2 : 1) void k_atr_prox(const 
         ok[nt] = true;
         G[row * L + nt * 16 + i] = gv[nt];
       }
-      const bool rowe =
+      const unsigned rowe =
           prox_pgd_row<T, 16, NT>(xa[r], gv, ok, true, i, t, tmu, thres, pv, pth, zv, accr, zf != nullptr);
-      if (zf != nullptr && i == 0) zf[row] = rowe ? 1 : 0;
+      if (zf != nullptr && i == 0) zf[row] = rowe;
 #pragma unroll
       for (int nt = 0; nt < NT; ++nt) {
         p[row * L + nt * 16 + i] = pv[nt];
@@ -342,7 +342,7 @@ __global__ __launch_bounds__(256, sizeof(T) == 8 ? 2 : 1) void k_atr_fista(const
                                                    double thres_, double theta_, double a1_,
                                                    double b1_, Red red, Pub pub, int S,
                                                    T* __restrict__ Gp, unsigned* __restrict__ pcnt,
-                                                   T* __restrict__ ec, uint8_t* __restrict__ zf) {
+                                                   T* __restrict__ ec, unsigned* __restrict__ zf) {
   if (red_skipped(red)) {   // cancelled by a device-side decision (as k_atr_prox)
     if (pub.host != nullptr && blockIdx.x == 0 && threadIdx.x == 0)
       publish_packet(pub.s, pub.ns, pub.host, pub.host_seq, pub.seq);
@@ -391,10 +391,10 @@ __global__ __launch_bounds__(256, sizeof(T) == 8 ? 2 : 1) void k_atr_fista(const
         ok[nt] = true;
         G[row * L + nt * 16 + i] = gv[nt];
       }
-      const bool rowe = fista_row<T, 16, NT, true>(ya[r], gv, xa[r], ok, true, i, t, tmu, thres, theta,
+      const unsigned rowe = fista_row<T, 16, NT, true>(ya[r], gv, xa[r], ok, true, i, t, tmu, thres, theta,
                                                    a1, b1, T(0), T(0), xcv, vnv, ynv, accr,
                                                    ec != nullptr ? ecv : nullptr);
-      if (zf != nullptr && i == 0) zf[row] = rowe ? 1 : 0;
+      if (zf != nullptr && i == 0) zf[row] = rowe;
 #pragma unroll
       for (int nt = 0; nt < NT; ++nt) {
         xc[row * L + nt * 16 + i] = xcv[nt];
@@ -525,7 +525,7 @@ bool atr_prox_ok(const GemmPlan& p) {
 template <typename T, int NT, int PF, bool NTL>
 static void atr_prox_go(const GemmPlan& p, const T* A, const T* R, T* G, const T* x, T* pp,
                         T* pthr, T* z, double t, double mu, double thres, Red red, hipStream_t st,
-                        Pub pub, T* Gp, unsigned* pcnt, uint8_t* zf) {
+                        Pub pub, T* Gp, unsigned* pcnt, unsigned* zf) {
   const dim3 grid((unsigned)(p.n / 64 * p.atr_S + (pub.host ? 1 : 0)));
   if (p.atr_S > 1) {
     hipLaunchKernelGGL((k_atr_prox<T, NT, PF, NTL, true>), grid, dim3(256), 0, st, A, R, G, p.m,
@@ -539,7 +539,7 @@ static void atr_prox_go(const GemmPlan& p, const T* A, const T* R, T* G, const T
 template <typename T, int NT>
 static void atr_prox_nt(const GemmPlan& p, const T* A, const T* R, T* G, const T* x, T* pp,
                         T* pthr, T* z, double t, double mu, double thres, Red red, hipStream_t st,
-                        Pub pub, T* Gp, unsigned* pcnt, uint8_t* zf) {
+                        Pub pub, T* Gp, unsigned* pcnt, unsigned* zf) {
   switch (p.atr_ntl * 100 + p.atr_pf) {
     case 4: atr_prox_go<T, NT, 4, false>(p, A, R, G, x, pp, pthr, z, t, mu, thres, red, st, pub, Gp, pcnt, zf); break;
     case 6: atr_prox_go<T, NT, 6, false>(p, A, R, G, x, pp, pthr, z, t, mu, thres, red, st, pub, Gp, pcnt, zf); break;
@@ -551,7 +551,7 @@ static void atr_prox_nt(const GemmPlan& p, const T* A, const T* R, T* G, const T
 template <typename T>
 void launch_atr_prox(const GemmPlan& p, const T* A, const T* R, T* G, const T* x, T* pp, T* pthr,
                      T* z, double t, double mu, double thres, Red red, hipStream_t st, Pub pub,
-                     T* Gp, unsigned* pcnt, uint8_t* zf) {
+                     T* Gp, unsigned* pcnt, unsigned* zf) {
   if (p.atr_S > 1 && (Gp == nullptr || pcnt == nullptr))
     throw Error{GLX_E_INVALID, "fused A^T R with K splits needs slab and counter buffers"};
   if (p.l == 16) atr_prox_nt<T, 1>(p, A, R, G, x, pp, pthr, z, t, mu, thres, red, st, pub, Gp, pcnt, zf);
@@ -562,7 +562,7 @@ template <typename T, int NT, int PF, bool NTL>
 static void atr_fista_go(const GemmPlan& p, const T* A, const T* R, T* G, const T* y, const T* xk,
                          T* xc, T* vn, T* yn, double t, double mu, double thres, double theta,
                          double theta_next, Red red, hipStream_t st, Pub pub, T* Gp, unsigned* pcnt,
-                         T* ec, uint8_t* zf) {
+                         T* ec, unsigned* zf) {
   const dim3 grid((unsigned)(p.n / 64 * p.atr_S + (pub.host ? 1 : 0)));
   if (p.atr_S > 1) {
     hipLaunchKernelGGL((k_atr_fista<T, NT, PF, NTL, true>), grid, dim3(256), 0, st, A, R, G, p.m,
@@ -579,7 +579,7 @@ template <typename T, int NT>
 static void atr_fista_nt(const GemmPlan& p, const T* A, const T* R, T* G, const T* y, const T* xk,
                          T* xc, T* vn, T* yn, double t, double mu, double thres, double theta,
                          double theta_next, Red red, hipStream_t st, Pub pub, T* Gp, unsigned* pcnt,
-                         T* ec, uint8_t* zf) {
+                         T* ec, unsigned* zf) {
   switch (p.atr_ntl * 100 + p.atr_pf) {
     case 4: atr_fista_go<T, NT, 4, false>(p, A, R, G, y, xk, xc, vn, yn, t, mu, thres, theta, theta_next, red, st, pub, Gp, pcnt, ec, zf); break;
     case 104: atr_fista_go<T, NT, 4, true>(p, A, R, G, y, xk, xc, vn, yn, t, mu, thres, theta, theta_next, red, st, pub, Gp, pcnt, ec, zf); break;
@@ -591,7 +591,7 @@ template <typename T>
 void launch_atr_fista(const GemmPlan& p, const T* A, const T* R, T* G, const T* y, const T* xk,
                       T* xc, T* vn, T* yn, double t, double mu, double thres, double theta,
                       double theta_next, Red red, hipStream_t st, Pub pub, T* Gp, unsigned* pcnt,
-                         T* ec, uint8_t* zf) {
+                         T* ec, unsigned* zf) {
   if (p.atr_S > 1 && (Gp == nullptr || pcnt == nullptr))
     throw Error{GLX_E_INVALID, "fused A^T R with K splits needs slab and counter buffers"};
   if (p.l == 16) atr_fista_nt<T, 1>(p, A, R, G, y, xk, xc, vn, yn, t, mu, thres, theta, theta_next, red, st, pub, Gp, pcnt, ec, zf);
@@ -602,17 +602,17 @@ template void launch_atr<double>(const GemmPlan&, const double*, const double*, 
 template void launch_atr_fista<double>(const GemmPlan&, const double*, const double*, double*,
                                        const double*, const double*, double*, double*, double*,
                                        double, double, double, double, double, Red, hipStream_t, Pub,
-                                       double*, unsigned*, double*, uint8_t*);
+                                       double*, unsigned*, double*, unsigned*);
 template void launch_atr_fista<float>(const GemmPlan&, const float*, const float*, float*,
                                       const float*, const float*, float*, float*, float*, double,
                                       double, double, double, double, Red, hipStream_t, Pub,
-                                      float*, unsigned*, float*, uint8_t*);
+                                      float*, unsigned*, float*, unsigned*);
 template void launch_atr_prox<double>(const GemmPlan&, const double*, const double*, double*,
                                       const double*, double*, double*, double*, double, double,
-                                      double, Red, hipStream_t, Pub, double*, unsigned*, uint8_t*);
+                                      double, Red, hipStream_t, Pub, double*, unsigned*, unsigned*);
 template void launch_atr_prox<float>(const GemmPlan&, const float*, const float*, float*,
                                      const float*, float*, float*, float*, double, double, double,
-                                     Red, hipStream_t, Pub, float*, unsigned*, uint8_t*);
+                                     Red, hipStream_t, Pub, float*, unsigned*, unsigned*);
 template void launch_atr<float>(const GemmPlan&, const float*, const float*, float*, hipStream_t);
 
 

@@ -297,7 +297,7 @@ template <typename T, int LPR, int EPL>
 __global__ __launch_bounds__(256) void k_prox_pgd(const T* __restrict__ x, const T* __restrict__ g,
                                                   int S, T* __restrict__ gout, T* __restrict__ p,
                                                   T* __restrict__ pthr, T* __restrict__ z,
-                                                  uint8_t* __restrict__ zf, int64_t n,
+                                                  unsigned* __restrict__ zf, int64_t n,
                                                   int64_t l, double t_, double tmu_, double thres_,
                                                   Red red, Pub pub) {
   // a launch of a device-controlled batch cancelled by an earlier decision (communicator path,
@@ -322,9 +322,9 @@ __global__ __launch_bounds__(256) void k_prox_pgd(const T* __restrict__ x, const
     gv[e] = ok[e] ? slab_sum(g, S, nl, base + j) : T(0);
     if (ok[e] && gout != nullptr) gout[base + j] = gv[e];
   }
-  const bool rowe = prox_pgd_row<T, LPR, EPL>(xv, gv, ok, rv, sub, t, tmu, thres, pv, pth, zv, acc,
+  const unsigned rowe = prox_pgd_row<T, LPR, EPL>(xv, gv, ok, rv, sub, t, tmu, thres, pv, pth, zv, acc,
                                               zf != nullptr);
-  if (zf != nullptr && rv && sub == 0) zf[row] = rowe ? 1 : 0;
+  if (zf != nullptr && rv && sub == 0) zf[row] = rowe;
 #pragma unroll
   for (int e = 0; e < EPL; ++e) {
     const int64_t j = sub + (int64_t)e * LPR;
@@ -352,7 +352,7 @@ __global__ __launch_bounds__(256) void k_fista_trial(
     const T* __restrict__ xk, T* __restrict__ xc, T* __restrict__ vnext, T* __restrict__ ynext,
     int64_t n, int64_t l, double t_, double tmu_, double thres_, double theta_, double a1_,
     double b1_, double dd_, double delta_, Red red, Pub pub, T* __restrict__ ec,
-    uint8_t* __restrict__ zf) {
+    unsigned* __restrict__ zf) {
   constexpr int NV = PROX ? 4 : 5;
   if (red_skipped(red)) {   // cancelled in a device-controlled batch (as k_prox_pgd)
     if (pub.host != nullptr && blockIdx.x == gridDim.x - 1 && threadIdx.x == 0)
@@ -379,10 +379,10 @@ __global__ __launch_bounds__(256) void k_fista_trial(
     xkv[e] = ok[e] ? xk[base + j] : T(0);
     if (ok[e] && gout != nullptr) gout[base + j] = gv[e];
   }
-  const bool rowe = fista_row<T, LPR, EPL, PROX>(yv, gv, xkv, ok, rv, sub, t, tmu, thres, theta, a1,
+  const unsigned rowe = fista_row<T, LPR, EPL, PROX>(yv, gv, xkv, ok, rv, sub, t, tmu, thres, theta, a1,
                                                   b1, dd, delta, xcv, vnv, ynv, acc,
                                                   ec != nullptr ? ecv : nullptr);
-  if (zf != nullptr && rv && sub == 0) zf[row] = rowe ? 1 : 0;
+  if (zf != nullptr && rv && sub == 0) zf[row] = rowe;
 #pragma unroll
   for (int e = 0; e < EPL; ++e) {
     const int64_t j = sub + (int64_t)e * LPR;
@@ -634,10 +634,13 @@ static void dispatch_row(int64_t l, F&& f) {
 }
 static inline unsigned row_grid(int64_t n, int lpr) { return grid_for(n, 256 / lpr); }
 // + one publisher workgroup when the launch carries the scalar packet (the grid reduction's
-// partials hold at most kMaxBlocks workgroups)
+// partials hold at most kMaxBlocks workgroups). The work workgroups are capped at kMaxBlocks - 1
+// with or without the packet, so the rows each workgroup sums, and with them the rounding of the
+// trial's sums, do not depend on whether the launch carries it (a device-controlled batch runs
+// the same trial without a packet: at n >= 16368 the two grids used to differ by one workgroup
+// and the sums by an ulp)
 static inline unsigned row_grid_pub(int64_t n, int lpr, const Pub& pub) {
-  if (pub.host == nullptr) return row_grid(n, lpr);
-  return std::min<unsigned>(row_grid(n, lpr), (unsigned)kMaxBlocks - 1) + 1;
+  return std::min<unsigned>(row_grid(n, lpr), (unsigned)kMaxBlocks - 1) + (pub.host ? 1u : 0u);
 }
 
 template <typename T>
@@ -702,7 +705,7 @@ void launch_sum_partials(const T* Gp, int S, T* G, int64_t nl, hipStream_t st) {
 template <typename T>
 void launch_prox_pgd(const T* x, const T* g, int S, T* gout, T* p, T* pthr, T* z, int64_t n,
                      int64_t l, double t, double mu, double thres, Red red, hipStream_t st, Pub pub,
-                     uint8_t* zf) {
+                     unsigned* zf) {
   dispatch_row(l, [&](auto lpr, auto epl) {
     hipLaunchKernelGGL((k_prox_pgd<T, decltype(lpr)::value, decltype(epl)::value>),
                        dim3(row_grid_pub(n, lpr, pub)), dim3(256), 0, st, x, g, S, gout, p, pthr, z, zf,
@@ -713,7 +716,7 @@ template <typename T>
 void launch_fista_trial(bool prox, const T* y, const T* g, int S, T* gout, const T* xk, T* xc,
                         T* vnext, T* ynext, int64_t n, int64_t l, double t, double mu, double thres,
                         double theta, double theta_next, double delta, Red red, hipStream_t st,
-                        Pub pub, T* ec, uint8_t* zf) {
+                        Pub pub, T* ec, unsigned* zf) {
   dispatch_row(l, [&](auto lpr, auto epl) {
     if (prox)
       hipLaunchKernelGGL((k_fista_trial<T, decltype(lpr)::value, decltype(epl)::value, true>),
@@ -814,10 +817,10 @@ void launch_publish(const double* s, int ns, double* host, unsigned* host_seq, u
                                          int64_t, double, double, double, const T*, int64_t,        \
                                          const double*, const unsigned*, int, Red, hipStream_t, Ctl);\
   template void launch_prox_pgd<T>(const T*, const T*, int, T*, T*, T*, T*, int64_t, int64_t,       \
-                                   double, double, double, Red, hipStream_t, Pub, uint8_t*);        \
+                                   double, double, double, Red, hipStream_t, Pub, unsigned*);       \
   template void launch_fista_trial<T>(bool, const T*, const T*, int, T*, const T*, T*, T*, T*,      \
                                       int64_t, int64_t, double, double, double, double, double,     \
-                                      double, Red, hipStream_t, Pub, T*, uint8_t*);                 \
+                                      double, Red, hipStream_t, Pub, T*, unsigned*);                \
   template void launch_prox_plain<T>(const T*, T*, int64_t, int64_t, double, double, double, Red,   \
                                      hipStream_t);                                                  \
   template void launch_rownorm_max<T>(const T*, int64_t, int64_t, Red, hipStream_t);                \

@@ -53,91 +53,66 @@ __global__ __launch_bounds__(256) void k_transpose(const T* __restrict__ A, T* _
   }
 }
 
-// Column lists of e (one workgroup per column c): the ascending k with zf[k] != 0 and
-// e[k][c] != 0 -> lists[c * n ...], counts[c]. First the flagged rows (a 256-thread scan of the
-// n flags into LDS), then their e[k][c] (loads issued 16 at a time), then a second scan.
-template <typename T, int L>
-__global__ __launch_bounds__(kGThreads) void k_e_lists(const T* __restrict__ E,
-                                                       const uint8_t* __restrict__ zf, int64_t n,
+// Column lists of e (one workgroup per column c): the ascending k whose column mask zm[k] (written
+// by the trial kernels, bit c = e[k][c] != 0) has bit c. Thread t owns the masks
+// [t * per, (t + 1) * per) as 16-B vectors, up to 16 in flight; a count, one block scan, and a
+// write pass over the same vectors (L1/L2 hits). (Round 2 scanned the byte row flags, then loaded
+// e[k][c] of every flagged row, 8 B per 256-B row: under the concurrent dense pass that chain of
+// dependent loads took ~155 us a trial, as long as the pass it hides behind.)
+__global__ __launch_bounds__(kGThreads) void k_e_lists(const unsigned* __restrict__ zm, int64_t n,
                                                        unsigned short* __restrict__ lists,
                                                        unsigned* __restrict__ counts,
                                                        const int* __restrict__ skip) {
   if (skip != nullptr && *skip != 0) return;
-  extern __shared__ unsigned short fl[];             // the flagged rows (n entries worst case)
   __shared__ unsigned wsum[kGW];
   const int tid = threadIdx.x;
   const int lane = tid & 63, wave = tid >> 6;
-  const int c = (int)blockIdx.x;
-  auto scan = [&](unsigned cntl, unsigned& base, unsigned& total) {
-    unsigned inc = cntl;
-#pragma unroll
-    for (int off = 1; off < 64; off <<= 1) {
-      const unsigned v = __shfl_up(inc, off);
-      if (lane >= off) inc += v;
-    }
-    __syncthreads();
-    if (lane == 63) wsum[wave] = inc;
-    __syncthreads();
-    base = 0;
-    total = 0;
-#pragma unroll
-    for (int w = 0; w < kGW; ++w) {
-      if (w < wave) base += wsum[w];
-      total += wsum[w];
-    }
-    base += inc - cntl;
-  };
-  // 1. flagged rows: thread t owns flags [t * per, (t + 1) * per) (16-B vectors; the buffer is
-  //    padded to 256 B, bytes at k >= n are ignored)
-  const int64_t per = (((n + kGThreads - 1) / kGThreads) + 15) & ~int64_t(15);
+  const unsigned c = blockIdx.x;
+  constexpr int V = 16;   // vectors in flight per thread
+  const int64_t per = (((n + kGThreads - 1) / kGThreads) + 3) & ~int64_t(3);
   const int64_t f0 = tid * per;
-  const int64_t f1 = (f0 + per < n) ? f0 + per : (f0 < n ? n : f0);
-  unsigned cnt1 = 0;
-  for (int64_t k = f0; k < f1; k += 16) {
-    const uint4 v = *reinterpret_cast<const uint4*>(zf + k);
-    const unsigned w[4] = {v.x, v.y, v.z, v.w};
+  const int64_t f1 = f0 + per < n ? f0 + per : (f0 < n ? n : f0);
+  auto chunk = [&](int64_t k0, unsigned (&w)[4 * V]) {
 #pragma unroll
-    for (int j = 0; j < 16; ++j)
-      if (k + j < f1 && ((w[j >> 2] >> (8 * (j & 3))) & 0xffu) != 0) ++cnt1;
-  }
-  unsigned pos, nf;
-  scan(cnt1, pos, nf);
-  if (cnt1 != 0)
-    for (int64_t k = f0; k < f1; k += 16) {   // the same 16-B vectors again (L1/L2 hits)
-      const uint4 v = *reinterpret_cast<const uint4*>(zf + k);
-      const unsigned w[4] = {v.x, v.y, v.z, v.w};
-#pragma unroll
-      for (int j = 0; j < 16; ++j)
-        if (k + j < f1 && ((w[j >> 2] >> (8 * (j & 3))) & 0xffu) != 0) fl[pos++] = (unsigned short)(k + j);
+    for (int u = 0; u < V; ++u) {
+      const int64_t k = k0 + 4 * u;
+      const uint4 v = k < f1 ? *reinterpret_cast<const uint4*>(zm + k) : uint4{0u, 0u, 0u, 0u};
+      w[4 * u] = v.x; w[4 * u + 1] = v.y; w[4 * u + 2] = v.z; w[4 * u + 3] = v.w;
     }
+  };
+  unsigned cnt = 0;
+  for (int64_t k0 = f0; k0 < f1; k0 += 4 * V) {
+    unsigned w[4 * V];
+    chunk(k0, w);
+#pragma unroll
+    for (int j = 0; j < 4 * V; ++j)
+      if (k0 + j < f1 && ((w[j] >> c) & 1u)) ++cnt;
+  }
+  // block-exclusive scan of the counts
+  unsigned inc = cnt;
+#pragma unroll
+  for (int off = 1; off < 64; off <<= 1) {
+    const unsigned v = __shfl_up(inc, off);
+    if (lane >= off) inc += v;
+  }
+  if (lane == 63) wsum[wave] = inc;
   __syncthreads();
-  // 2. thread t takes flagged entries [t * q, (t + 1) * q) in order, so the list stays ascending
-  const unsigned q = (nf + kGThreads - 1) / kGThreads;
-  const unsigned g0 = tid * q, g1 = (g0 + q < nf) ? g0 + q : (g0 < nf ? nf : g0);
-  // nonzero bits of this thread's entries, 64 at a time (q <= 64 when n <= 16384; larger n
-  // takes a second round of loads in the write pass)
-  unsigned cnt2 = 0;
-  unsigned long long nzb = 0;
-  for (unsigned g = g0; g < g1; g += 16) {
-    T ev[16];
+  unsigned pos = inc - cnt, total = 0;
 #pragma unroll
-    for (int u = 0; u < 16; ++u) ev[u] = (g + u < g1) ? E[(int64_t)fl[g + u] * L + c] : T(0);
-#pragma unroll
-    for (int u = 0; u < 16; ++u)
-      if (ev[u] != T(0)) {
-        ++cnt2;
-        if (g - g0 + u < 64) nzb |= 1ull << (g - g0 + u);
-      }
+  for (int w = 0; w < kGW; ++w) {
+    if (w < wave) pos += wsum[w];
+    total += wsum[w];
   }
-  unsigned p2, nc;
-  scan(cnt2, p2, nc);
   unsigned short* out = lists + (int64_t)c * n;
-  for (unsigned g = g0; g < g1; ++g) {
-    const unsigned o = g - g0;
-    const bool nz = o < 64 ? ((nzb >> o) & 1ull) != 0 : E[(int64_t)fl[g] * L + c] != T(0);
-    if (nz) out[p2++] = fl[g];
-  }
-  if (tid == 0) counts[c] = nc;
+  if (cnt != 0)
+    for (int64_t k0 = f0; k0 < f1; k0 += 4 * V) {
+      unsigned w[4 * V];
+      chunk(k0, w);
+#pragma unroll
+      for (int j = 0; j < 4 * V; ++j)
+        if (k0 + j < f1 && ((w[j] >> c) & 1u)) out[pos++] = (unsigned short)(k0 + j);
+    }
+  if (tid == 0) counts[c] = total;
 }
 
 // One workgroup per (256-row block, column c) of A e. e has few nonzeros per flagged row (about
@@ -205,22 +180,11 @@ const unsigned* gather_counts(const void* lists_ws, int64_t n) {
   return list_counts(const_cast<void*>(lists_ws), n);
 }
 
-template <typename T>
-void launch_e_lists(const T* E, const uint8_t* zf, int64_t n, int64_t l, void* lists_ws, hipStream_t st,
+void launch_e_lists(const unsigned* zm, int64_t n, int64_t l, void* lists_ws, hipStream_t st,
                     const int* skip) {
   if (!gather_ok(n, l)) throw Error{GLX_E_INVALID, "A e gather: needs l in {16, 32}, n < 65536"};
-  const size_t lds = sizeof(unsigned short) * (size_t)n;
-  auto go = [&](auto kern) {
-    // the flagged-row list exceeds the default 64 KiB of dynamic LDS only past n = 32768; the
-    // attribute is set on every such launch (cheap), since it is per kernel AND per device
-    if (lds > 64 * 1024)
-      (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kern),
-                                hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024 - 64);
-    hipLaunchKernelGGL(kern, dim3((unsigned)l), dim3(kGThreads), lds, st, E, zf, n,
-                       static_cast<unsigned short*>(lists_ws), list_counts(lists_ws, n), skip);
-  };
-  if (l == 32) go(k_e_lists<T, 32>);
-  else go(k_e_lists<T, 16>);
+  hipLaunchKernelGGL(k_e_lists, dim3((unsigned)l), dim3(kGThreads), 0, st, zm, n,
+                     static_cast<unsigned short*>(lists_ws), list_counts(lists_ws, n), skip);
 }
 
 template <typename T>
@@ -246,10 +210,6 @@ size_t gather_lists_bytes(int64_t n) { return (((size_t)32 * n * 2 + 255) & ~siz
 
 template void launch_transpose<double>(const double*, double*, int64_t, int64_t, hipStream_t);
 template void launch_transpose<float>(const float*, float*, int64_t, int64_t, hipStream_t);
-template void launch_e_lists<double>(const double*, const uint8_t*, int64_t, int64_t, void*, hipStream_t,
-                                     const int*);
-template void launch_e_lists<float>(const float*, const uint8_t*, int64_t, int64_t, void*, hipStream_t,
-                                    const int*);
 template void launch_at_gather<double>(const double*, const double*, int64_t, int64_t, int64_t, double*,
                                        void*, hipStream_t, const int*);
 template void launch_at_gather<float>(const float*, const float*, int64_t, int64_t, int64_t, float*,

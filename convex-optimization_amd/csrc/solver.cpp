@@ -82,7 +82,7 @@ static int method_bufs(int method) {
 constexpr int kBufs = 9;
 constexpr int kTailBytes = 64;   // behind each gradient set: scalars that ride its all-reduce
 constexpr int kRes = 4;
-constexpr int kDcWindow = 8;     // device-controlled ProxGD: iterations in flight (GLX_DC_BATCH)
+constexpr int kDcWindow = 8;     // device-controlled line search: iterations in flight (GLX_DC_BATCH)
 constexpr int kKeepMiB = 192;    // Infinity-Cache hand-off between the non-temporal passes
 // gradient sets: 2 (current, speculative); with a communicator and device control a ring of
 // window + 2, so that the all-reduces queued behind a cancelling decision (they cannot be
@@ -90,9 +90,15 @@ constexpr int kKeepMiB = 192;    // Infinity-Cache hand-off between the non-temp
 constexpr int kMaxGSets = kCtlMaxBatch / 2 + 2;
 
 // device-controlled batches' window: opts.dc_window (> 0: that window, < 0: off), else
-// GLX_DC_BATCH, else kDcWindow (0 = the host decides every iteration)
-static int dc_window_opt(const glx_opts& O) {
-  int w = kDcWindow;
+// GLX_DC_BATCH, else the measured default (0 = the host decides every iteration): kDcWindow for
+// FProxGD, off for ProxGD. Same box, 200-step windows, host control against window 8
+// (profiles/r3_dc/): ProxGD NS 2374-2382 vs 2344-2354 it/s, C2 9003-9010 vs 8894-8910, the
+// comm-path shards 6922-11023 vs 6735-10612 (its speculative A@X already hides the host's turn);
+// FProxGD NS 2454-2478 vs 2456-2465, C3 3702 vs 3687-3703, C5's shard 1227-1231 vs 1230-1234, the
+// 1024-row comm shard 9802-9829 vs 10517-10587 (+7.5 %: the host path leaves the GPU idle while
+// it decides behind the short speculative trial).
+static int dc_window_opt(const glx_problem& P, const glx_opts& O) {
+  int w = P.method == GLX_FPROXGD ? kDcWindow : 0;
   if (O.dc_window != 0) {
     w = O.dc_window;
   } else if (const char* dc = std::getenv("GLX_DC_BATCH")) {
@@ -229,8 +235,8 @@ class Session : public SessionBase {
     // device-controlled batches: Ctl::state (4 doubles) and the abort word; decision records
     double* dcs = static_cast<double*>(c.take(256));
     double* dcr = static_cast<double*>(c.take(sizeof(double) * kCtlRec * kCtlMaxBatch));
-    // split-candidate mode: row flags of e = p - p_thr (z's buffer), read in chunks of up to 32
-    uint8_t* zf = static_cast<uint8_t*>(c.take((size_t)((P.n + 255) / 256) * 256));
+    // split-candidate mode: per-row column masks of e = p - p_thr (z's buffer; bit c = e[k][c] != 0)
+    unsigned* zf = static_cast<unsigned*>(c.take((size_t)((P.n * 4 + 255) / 256) * 256));
     double* fh = static_cast<double*>(c.take(sizeof(double) * (fh_cap + 1)));
     double* sp100 = static_cast<double*>(c.take(sizeof(double) * (fh_cap / 100 + 2)));
     const int gb = gemv_blocks_for(P);
@@ -272,7 +278,7 @@ class Session : public SessionBase {
            O.step_type == GLX_STEP_LINE_SEARCH && O.ls_maxit > 0 && O.exact_objective == 0;
   }
   static int gsets_for(const glx_problem& P, const glx_opts& O) {
-    const int w = dc_window_opt(O);
+    const int w = dc_window_opt(P, O);
     return (w > 0 && dc_comm_ok(P, O)) ? w + 2 : 2;
   }
 
@@ -340,7 +346,7 @@ class Session : public SessionBase {
     // device-controlled batches (dc_run / fista_dc_run): ProxGD / FProxGD with line search on
     // the fused speculative path; GLX_DC_BATCH = iterations in flight (0: the host decides every
     // iteration). With a communicator fp64 only (the trial sums ride the gradient all-reduce).
-    dc_window_ = dc_window_opt(O);
+    dc_window_ = dc_window_opt(P, O);
     if (!((fused_ok_ || fused_fista_ok_) && spin_readback_ && O.exact_objective == 0 &&
           O.step_type == GLX_STEP_LINE_SEARCH && O.ls_maxit > 0 &&
           (comm_ == nullptr || (dc_comm_ok(P, O) && attach_ok_))))
@@ -612,7 +618,7 @@ class Session : public SessionBase {
     const T* xd[3] = {xs[1], nullptr, nullptr};
     GLX_HIP(hipEventRecord(ev_trial_, st_));
     GLX_HIP(hipStreamWaitEvent(st2_, ev_trial_, 0));
-    launch_e_lists<T>(xs[0], zf_, n_, l_, glists_, st2_);
+    launch_e_lists(zf_, n_, l_, glists_, st2_);
     check_launch();
     GLX_HIP(hipEventRecord(ev_lists_, st2_));
     // the dense pass and the gather are timed apart (kinds 0 and 2), so each event pair
@@ -1657,14 +1663,14 @@ class Session : public SessionBase {
   unsigned *hseq_ = nullptr, *hseq_dev_ = nullptr;
   unsigned* ticket_ = nullptr;
   unsigned* pcnt_ = nullptr;   // per-panel counters (fused A^T R with K splits)
-  uint8_t* zf_ = nullptr;      // row flags of e (split-candidate ProxGD)
+  unsigned* zf_ = nullptr;     // per-row column masks of e (split-candidate mode)
   T* At_ = nullptr;            // A^T (split-candidate gather form)
   void* glists_ = nullptr;     // its per-column index lists of e
   hipStream_t st2_ = nullptr;  // side stream: the lists, beside the dense A@X
   hipEvent_t ev_trial_ = nullptr, ev_lists_ = nullptr;
   int smode_ = 0, gsplit_ = 1;
   bool emode_ = false;         // split-candidate ProxGD: trials write e = p - p_thr, not z
-  uint8_t* ezf() const { return emode_ ? zf_ : nullptr; }
+  unsigned* ezf() const { return emode_ ? zf_ : nullptr; }
   // split-candidate FProxGD (iter_fista): trials also write e_c = xc - thr(xc) to E_ and its
   // row flags to zf_; SXO_[kslot_] = A thr(x_k) (kslot_ < 0: not known)
   bool fsplit_ = false;
@@ -1674,7 +1680,7 @@ class Session : public SessionBase {
   double nnz_budget_ = 0;      // nnz(e_c) above which the dense batch is cheaper
   int dense_left_ = 0;         // dense batches before the gather form is tried again
   T* fec() const { return fsplit_ ? E_ : nullptr; }
-  uint8_t* fzf() const { return fsplit_ ? zf_ : nullptr; }
+  unsigned* fzf() const { return fsplit_ ? zf_ : nullptr; }
   int* flag_ = nullptr;
   // device-controlled ProxGD batches (dc_run)
   double* dc_state_ = nullptr;    // Ctl::state

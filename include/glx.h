@@ -75,8 +75,9 @@ typedef struct glx_opts {
                                      overrides), 1 = on at any size, 2 = off. On adds an m x n
                                      copy of A to the workspace (glx_workspace_bytes counts it) */
   int32_t dc_window;              /* device-controlled line search (ProxGD / FProxGD): 0 = auto
-                                     (GLX_DC_BATCH env, else off), -1 = off, k in 1..32 = up to
-                                     k iterations queued ahead of the host                      */
+                                     (GLX_DC_BATCH env, else the measured default: 8 for
+                                     FProxGD, off for ProxGD), -1 = off, k in 1..32 = up to k
+                                     iterations queued ahead of the host                        */
   int32_t reserved[5];
 } glx_opts;
 
