@@ -218,7 +218,7 @@ __global__ __launch_bounds__(256) void k_finalize_residual(
 //   A thr(xc) = A xc - A e_c,   A y_next = a1 A thr(xc) + b1 (A thr(xk) + (A xc - A thr(xk)) / theta)
 // with A thr(xk) (sxo) kept from the previous accepted trial. Writes R_y = A y_next - b and
 // sxo_out = A thr(xc); out: [sum (A xc - b)^2, sum R_y^2, nnz(e_c) = sum of the nl list
-// lengths `counts` (k_e_lists), count(|cx| > 1e-6 *cmax)].
+// lengths `counts` (written by k_at_gather), count(|cx| > 1e-6 *cmax)].
 template <typename T, int G>
 __global__ __launch_bounds__(256) void k_finalize_fista(
     const T* __restrict__ P, int S, const T* __restrict__ Pe, int S0, const T* __restrict__ B,

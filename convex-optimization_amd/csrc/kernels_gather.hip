@@ -56,9 +56,13 @@ __global__ __launch_bounds__(256) void k_transpose(const T* __restrict__ A, T* _
 // Column lists of e (one workgroup per column c): the ascending k whose column mask zm[k] (written
 // by the trial kernels, bit c = e[k][c] != 0) has bit c. Thread t owns the masks
 // [t * per, (t + 1) * per) as 16-B vectors, up to 16 in flight; a count, one block scan, and a
-// write pass over the same vectors (L1/L2 hits). (Round 2 scanned the byte row flags, then loaded
-// e[k][c] of every flagged row, 8 B per 256-B row: under the concurrent dense pass that chain of
-// dependent loads took ~155 us a trial, as long as the pass it hides behind.)
+// write pass over the same vectors (L1/L2 hits); no LDS beyond the scan's 16 B. It runs on the
+// solver's stream right before the dense pass. Round 2 ran the lists on a side stream beside the
+// dense pass (byte row flags, then e[k][c] of every flagged row, 32 KiB of LDS): the kernel trace
+// showed them getting CUs only once the dense pass drained (the LDS-DMA tile fills every CU's
+// LDS), and the cross-stream wait ordering the gather behind them left 11-19 us idle per trial.
+// Building each column's list inside every gather workgroup instead made the gather 40 us
+// instead of 13 (profiles/r3_gather/).
 __global__ __launch_bounds__(kGThreads) void k_e_lists(const unsigned* __restrict__ zm, int64_t n,
                                                        unsigned short* __restrict__ lists,
                                                        unsigned* __restrict__ counts,

@@ -91,14 +91,14 @@ constexpr int kMaxGSets = kCtlMaxBatch / 2 + 2;
 
 // device-controlled batches' window: opts.dc_window (> 0: that window, < 0: off), else
 // GLX_DC_BATCH, else the measured default (0 = the host decides every iteration): kDcWindow for
-// FProxGD, off for ProxGD. Same box, 200-step windows, host control against window 8
-// (profiles/r3_dc/): ProxGD NS 2374-2382 vs 2344-2354 it/s, C2 9003-9010 vs 8894-8910, the
-// comm-path shards 6922-11023 vs 6735-10612 (its speculative A@X already hides the host's turn);
-// FProxGD NS 2454-2478 vs 2456-2465, C3 3702 vs 3687-3703, C5's shard 1227-1231 vs 1230-1234, the
-// 1024-row comm shard 9802-9829 vs 10517-10587 (+7.5 %: the host path leaves the GPU idle while
-// it decides behind the short speculative trial).
+// FProxGD with a communicator, off elsewhere. Same box, 200-step windows, host control against
+// window 8 (profiles/r3_dc/): ProxGD NS 2374-2382 vs 2344-2354 it/s, C2 9003-9010 vs 8894-8910,
+// the comm-path shards 6922-11023 vs 6735-10612 (its speculative A@X already hides the host's
+// turn); FProxGD NS 2454-2478 vs 2456-2465 (whole solve 2058-2060 vs 2036-2038), C3 3702 vs
+// 3687-3703, C5's shard 1227-1231 vs 1230-1234, the 1024-row comm shard 9802-9829 vs 10517-10587
+// (+7.5 %: the host path leaves the GPU idle while it decides behind the short speculative trial).
 static int dc_window_opt(const glx_problem& P, const glx_opts& O) {
-  int w = P.method == GLX_FPROXGD ? kDcWindow : 0;
+  int w = (P.method == GLX_FPROXGD && P.comm != nullptr) ? kDcWindow : 0;
   if (O.dc_window != 0) {
     w = O.dc_window;
   } else if (const char* dc = std::getenv("GLX_DC_BATCH")) {
@@ -338,9 +338,6 @@ class Session : public SessionBase {
     gsplit_ = gather_split(m_);
     if (smode_ == 1) {
       launch_transpose<T>(static_cast<const T*>(P.A), At_, m_, n_, st_);   // once
-      GLX_HIP(hipStreamCreateWithFlags(&st2_, hipStreamNonBlocking));
-      GLX_HIP(hipEventCreateWithFlags(&ev_trial_, hipEventDisableTiming));
-      GLX_HIP(hipEventCreateWithFlags(&ev_lists_, hipEventDisableTiming));
     }
     fused_fista_ok_ = fuse_any && P.method == GLX_FPROXGD;
     // device-controlled batches (dc_run / fista_dc_run): ProxGD / FProxGD with line search on
@@ -384,12 +381,6 @@ class Session : public SessionBase {
   }
 
   ~Session() override {
-    if (st2_) {
-      (void)hipStreamSynchronize(st2_);
-      (void)hipStreamDestroy(st2_);
-    }
-    if (ev_trial_) (void)hipEventDestroy(ev_trial_);
-    if (ev_lists_) (void)hipEventDestroy(ev_lists_);
     if (hs_) (void)hipHostFree(hs_);
     if (dc_ring_) (void)hipHostFree(dc_ring_);
     if (rb_event_) (void)hipEventDestroy(rb_event_);
@@ -602,9 +593,13 @@ class Session : public SessionBase {
     if (pub_seq != nullptr) *pub_seq = post_readback();
   }
   // A @ [xs] into the slabs Pp_; pb: the launch also carries that scalar packet (ax_pub_ok)
+  // In a device-controlled batch the A@X passes, the column lists and the gather are gated by the
+  // abort word too (live only while it is 0): after a rejection, stop or nnz-budget decision the
+  // queued passes of the cancelled iterations would otherwise stream A for nothing (up to
+  // window - 1 dense passes per cancellation).
   void spec_ax(int nsrc, const T* const* xs, Pub pb = Pub{}) {
     hipEvent_t e0 = prof_begin(0);
-    launch_ax<T>(plan_, nsrc, A_, xs, Pp_, nullptr, 0, st_, pb);
+    launch_ax<T>(plan_, nsrc, A_, xs, Pp_, dc_gate_, 0, st_, pb);
     check_launch();
     prof_end(0, e0);
     ++ax_calls_;
@@ -612,24 +607,21 @@ class Session : public SessionBase {
   }
   // Split-candidate trial, gather form: A p_thr (one dense source, slabs behind the A e slab)
   // and A e from the transposed copy (one slab at Pp_); xs = [e | p_thr]. The column lists of e
-  // are built on a side stream while the dense pass runs. Timed as one A@X (kind 0). pb: the
-  // dense launch carries that scalar packet.
+  // are built first on the same stream, from the row masks the trial wrote (a few us; round 2 ran
+  // them on a side stream beside the dense pass, where they waited for CUs until the pass drained
+  // and the cross-stream wait left the queue idle, see kernels_gather.hip). The dense pass and the
+  // gather are timed apart (kinds 0 and 2), so each event pair brackets one kernel of the trace.
+  // pb: the dense launch carries that scalar packet.
   void cand_ax(const T* const* xs, Pub pb = Pub{}) {
     const T* xd[3] = {xs[1], nullptr, nullptr};
-    GLX_HIP(hipEventRecord(ev_trial_, st_));
-    GLX_HIP(hipStreamWaitEvent(st2_, ev_trial_, 0));
-    launch_e_lists(zf_, n_, l_, glists_, st2_);
+    launch_e_lists(zf_, n_, l_, glists_, st_, dc_gate_);
     check_launch();
-    GLX_HIP(hipEventRecord(ev_lists_, st2_));
-    // the dense pass and the gather are timed apart (kinds 0 and 2), so each event pair
-    // brackets one kernel of the trace
     hipEvent_t e0 = prof_begin(0);
-    launch_ax<T>(plan_, 1, A_, xd, Pp_ + (size_t)gsplit_ * ml_, nullptr, 0, st_, pb);
+    launch_ax<T>(plan_, 1, A_, xd, Pp_ + (size_t)gsplit_ * ml_, dc_gate_, 0, st_, pb);
     check_launch();
     prof_end(0, e0);
-    GLX_HIP(hipStreamWaitEvent(st_, ev_lists_, 0));
     hipEvent_t e2 = prof_begin(2);
-    launch_at_gather<T>(At_, xs[0], m_, n_, l_, Pp_, glists_, st_);
+    launch_at_gather<T>(At_, xs[0], m_, n_, l_, Pp_, glists_, st_, dc_gate_);
     check_launch();
     prof_end(2, e2);
     ++ax_calls_;
@@ -1665,9 +1657,7 @@ class Session : public SessionBase {
   unsigned* pcnt_ = nullptr;   // per-panel counters (fused A^T R with K splits)
   unsigned* zf_ = nullptr;     // per-row column masks of e (split-candidate mode)
   T* At_ = nullptr;            // A^T (split-candidate gather form)
-  void* glists_ = nullptr;     // its per-column index lists of e
-  hipStream_t st2_ = nullptr;  // side stream: the lists, beside the dense A@X
-  hipEvent_t ev_trial_ = nullptr, ev_lists_ = nullptr;
+  void* glists_ = nullptr;     // the gather's per-column index lists of e
   int smode_ = 0, gsplit_ = 1;
   bool emode_ = false;         // split-candidate ProxGD: trials write e = p - p_thr, not z
   unsigned* ezf() const { return emode_ ? zf_ : nullptr; }

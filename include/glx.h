@@ -76,8 +76,8 @@ typedef struct glx_opts {
                                      copy of A to the workspace (glx_workspace_bytes counts it) */
   int32_t dc_window;              /* device-controlled line search (ProxGD / FProxGD): 0 = auto
                                      (GLX_DC_BATCH env, else the measured default: 8 for
-                                     FProxGD, off for ProxGD), -1 = off, k in 1..32 = up to k
-                                     iterations queued ahead of the host                        */
+                                     FProxGD with a communicator, off otherwise), -1 = off,
+                                     k in 1..32 = up to k iterations queued ahead of the host   */
   int32_t reserved[5];
 } glx_opts;
 
