@@ -84,6 +84,12 @@ typedef unsigned long long u64;
 // grouping is taken from HW_REG_XCC_ID at run time, see k_resgrad), so a plain 8-byte store,
 // which keeps the line in that XCD's L2, is enough: the readers' sc1 loads bypass their L1 and
 // are served by the same L2. Otherwise sc1 (write-through) stores, visible on every XCD.
+// Architecture dependence: the HIP memory model does not promise that a
+// workgroup-scope store becomes visible to another workgroup. XL relies on two gfx950 facts:
+// the vector L1 is write-through (a store reaches the XCD's L2 without a writeback), and every
+// reader is on the writer's XCD and loads with sc1 (L1 bypass). Each granule carries its own tag,
+// so there is no separate flag whose ordering a fence would have to provide. The solver never
+// launches this kernel (glx_residual_gradient(one_pass = 1) only); the portable form is XL = 0.
 template <bool XL>
 __device__ inline void put_value(u64* g, unsigned tag, double v) {
   const u64 u = (u64)__double_as_longlong(v);
