@@ -39,8 +39,11 @@ __device__ inline bool red_skipped(const Red& red) {
 // MAXMASK bit v = max op. slot = this block's partials slot (default blockIdx.x): a launch
 // whose first workgroup is a publisher (publisher_first) puts that one last and the others at
 // blockIdx.x - 1, so the sums come out bit-identical with and without the packet.
+// nparts >= 0: only nparts workgroups of the launch take part, each with a distinct slot in
+// [0, nparts) (the K-split A^T R kernels: one per panel + the publisher, so the split count is
+// not bounded by the partials row); the arrival shards are then keyed by slot, not blockIdx.
 template <int NV, unsigned MAXMASK, int NW = 4>
-__device__ bool grid_reduce(double (&v)[NV], const Red& red, int slot = -1) {
+__device__ bool grid_reduce(double (&v)[NV], const Red& red, int slot = -1, int nparts = -1) {
   static_assert(NW == 4 || NW == 8, "4- or 8-wave blocks");
   constexpr int NTHR = 64 * NW;
   __shared__ double sh[NV][NW];
@@ -74,8 +77,8 @@ __device__ bool grid_reduce(double (&v)[NV], const Red& red, int slot = -1) {
     // arrive on the counter of their shard (blockIdx % 8, i.e. their XCD under round-robin
     // dispatch); the last arriver of each shard, whose add returned after every add of its
     // shard, arrives on the final counter, and the last arriver there owns the sum.
-    const unsigned G = gridDim.x;
-    const unsigned sh = blockIdx.x & (kTicketShards - 1);
+    const unsigned G = nparts >= 0 ? (unsigned)nparts : gridDim.x;
+    const unsigned sh = (nparts >= 0 ? (unsigned)slot : blockIdx.x) & (kTicketShards - 1);
     const unsigned nsh = G < (unsigned)kTicketShards ? G : (unsigned)kTicketShards;
     const unsigned cnt = (G - sh + kTicketShards - 1) / kTicketShards;
     const unsigned prev = __hip_atomic_fetch_add(red.ticket + (1 + sh) * kTicketStride, 1u,
@@ -91,13 +94,14 @@ __device__ bool grid_reduce(double (&v)[NV], const Red& red, int slot = -1) {
   // are issued before the first is consumed (clamped index, select afterwards), so the last
   // block pays one round trip instead of one per partial.
   constexpr int PER = kMaxBlocks / NTHR;
+  const unsigned np = nparts >= 0 ? (unsigned)nparts : gridDim.x;
   double pv[NV][PER];
 #pragma unroll
   for (int j = 0; j < NV; ++j)
 #pragma unroll
     for (int t = 0; t < PER; ++t) {
       const unsigned b = threadIdx.x + (unsigned)NTHR * t;
-      const unsigned bc = b < gridDim.x ? b : gridDim.x - 1;
+      const unsigned bc = b < np ? b : np - 1;
       pv[j][t] = __hip_atomic_load(&red.part[j * kMaxBlocks + bc], __ATOMIC_RELAXED,
                                    __HIP_MEMORY_SCOPE_AGENT);
     }
@@ -108,7 +112,7 @@ __device__ bool grid_reduce(double (&v)[NV], const Red& red, int slot = -1) {
     acc[j] = identity(op);
 #pragma unroll
     for (int t = 0; t < PER; ++t)
-      if (threadIdx.x + (unsigned)NTHR * t < gridDim.x) acc[j] = combine(op, acc[j], pv[j][t]);
+      if (threadIdx.x + (unsigned)NTHR * t < np) acc[j] = combine(op, acc[j], pv[j][t]);
 #pragma unroll
     for (int off = 32; off > 0; off >>= 1) acc[j] = combine(op, acc[j], __shfl_xor(acc[j], off));
   }
@@ -161,8 +165,9 @@ __device__ inline void publish_packet(const double* s, int ns, double* host, uns
 // kernel's other workgroups work, instead of as a separate k_publish launch in front of it —
 // also when only one workgroup fits per CU (a last-index publisher then waited for the first
 // workgroups to retire: a 4 us gap before the next kernel). Returns true in the publisher.
+// nparts >= 0: the launch reduces over nparts slots (grid_reduce); the publisher takes the last.
 template <int NV, unsigned MAXMASK, int NW = 4>
-__device__ inline bool publisher_first(const Pub& pub, const Red& red) {
+__device__ inline bool publisher_first(const Pub& pub, const Red& red, int nparts = -1) {
   if (pub.host == nullptr || blockIdx.x != 0) return false;
   if (threadIdx.x == 0)
     publish_packet(pub.s, pub.ns, pub.host, pub.host_seq, pub.seq, pub.s2, pub.off2, pub.n2,
@@ -170,7 +175,7 @@ __device__ inline bool publisher_first(const Pub& pub, const Red& red) {
   double v[NV];
 #pragma unroll
   for (int j = 0; j < NV; ++j) v[j] = identity((MAXMASK >> j) & 1);
-  grid_reduce<NV, MAXMASK, NW>(v, red, (int)gridDim.x - 1);
+  grid_reduce<NV, MAXMASK, NW>(v, red, (nparts >= 0 ? nparts : (int)gridDim.x) - 1, nparts);
   return true;
 }
 // partials slot of a non-publisher workgroup of such a launch

@@ -170,12 +170,12 @@ __device__ inline int64_t atr_panel(const T* __restrict__ A, const T* __restrict
 // order of slab_sum, so G is bit-identical to the unfused path) and runs the trial epilogue.
 // Hand-off: sc1 (agent-scope) stores, vmcnt(0), a workgroup barrier, one agent-scope add per
 // block; the last arriver loads with sc1 after a barrier (MI355X_MICROARCH.md "Valid forms",
-// row 1). Returns false in the blocks that are not last (they only join the grid reduction).
-// *slot = this block's grid-reduction slot, fixed whatever the arrival order: the panel's
-// trial sums (last arriver) at `panel`, the identity partials of the other S - 1 blocks at
-// n/64 + panel (S - 1) + their arrival index. So the trial's scalar sums come out in panel
-// order, bit-identical from run to run (a last arriver at its own block slot made their
-// summation order depend on timing).
+// row 1). Returns false in the blocks that are not last: they leave the kernel without joining
+// the grid reduction, which counts only the n/64 panel owners (+ the publisher; grid_reduce's
+// nparts), so S is not bounded by the kMaxBlocks partials row (round 3: C2 takes more splits).
+// *slot = the panel: the trial's scalar sums come out in panel order, bit-identical from run to
+// run whatever the arrival order (a last arriver at its own block slot made their summation
+// order depend on timing), and equal to the earlier form that also reduced identity partials.
 template <typename T, int NT>
 __device__ inline bool atr_split_combine(typename MF<T>::acc_t (&acc)[4][NT], T* __restrict__ Gp,
                                          int64_t n, int S, int64_t panel, int64_t split,
@@ -208,8 +208,8 @@ __device__ inline bool atr_split_combine(typename MF<T>::acc_t (&acc)[4][NT], T*
     last = arrival == (unsigned)S - 1;
   }
   __syncthreads();
-  *slot = last ? (int)panel : (int)(n / 64 + panel * (S - 1) + arrival);
   if (!last) return false;
+  *slot = (int)panel;
 #pragma unroll
   for (int e = 0; e < 4; ++e) {
     if (e != wave) continue;
@@ -276,7 +276,10 @@ __global__ __launch_bounds__(256, sizeof(T) == 8 ? 2 : 1) void k_atr_prox(const 
       publish_packet(pub.s, pub.ns, pub.host, pub.host_seq, pub.seq);
     return;
   }
-  if (publisher_first<6, 0x8u>(pub, red)) return;   // the extra workgroup (n / 64 * S + 1 in all)
+  // the extra workgroup (n / 64 * S + 1 in all); with K splits only the panel owners and the
+  // publisher reduce (nparts)
+  const int nparts = SPLIT ? (int)(n / 64) + (pub.host ? 1 : 0) : -1;
+  if (publisher_first<6, 0x8u>(pub, red, nparts)) return;
   typedef MF<T> M;
   constexpr int L = 16 * NT;
   const int lane = threadIdx.x & 63;
@@ -289,10 +292,7 @@ __global__ __launch_bounds__(256, sizeof(T) == 8 ? 2 : 1) void k_atr_prox(const 
   double accr[6] = {0.0, 0.0, 0.0, -__builtin_inf(), 0.0, 0.0};
   int slot = work_slot(pub);
   if constexpr (SPLIT) {   // a separate instantiation: the S = 1 kernel keeps 2 blocks per CU
-    if (!atr_split_combine<T, NT>(acc, Gp, n, S, panel, split, pcnt, &slot)) {
-      grid_reduce<6, 0x8u>(accr, red, slot);
-      return;
-    }
+    if (!atr_split_combine<T, NT>(acc, Gp, n, S, panel, split, pcnt, &slot)) return;
   }
   const T t = (T)t_, tmu = (T)tmu_, thres = (T)thres_;
 #pragma unroll
@@ -327,7 +327,7 @@ __global__ __launch_bounds__(256, sizeof(T) == 8 ? 2 : 1) void k_atr_prox(const 
       }
     }
   }
-  grid_reduce<6, 0x8u>(accr, red, slot);
+  grid_reduce<6, 0x8u>(accr, red, slot, nparts);
 }
 
 // FISTA's backtracking trial fused into A^T R the same way (WL 0, one K split): each wave runs
@@ -348,7 +348,8 @@ __global__ __launch_bounds__(256, sizeof(T) == 8 ? 2 : 1) void k_atr_fista(const
       publish_packet(pub.s, pub.ns, pub.host, pub.host_seq, pub.seq);
     return;
   }
-  if (publisher_first<4, 0x8u>(pub, red)) return;
+  const int nparts = SPLIT ? (int)(n / 64) + (pub.host ? 1 : 0) : -1;   // see k_atr_prox
+  if (publisher_first<4, 0x8u>(pub, red, nparts)) return;
   typedef MF<T> M;
   constexpr int L = 16 * NT;
   const int lane = threadIdx.x & 63;
@@ -361,10 +362,7 @@ __global__ __launch_bounds__(256, sizeof(T) == 8 ? 2 : 1) void k_atr_fista(const
   double accr[4] = {0.0, 0.0, 0.0, -__builtin_inf()};
   int slot = work_slot(pub);
   if constexpr (SPLIT) {   // fixed reduction slots, see atr_split_combine
-    if (!atr_split_combine<T, NT>(acc, Gp, n, S, panel, split, pcnt, &slot)) {
-      grid_reduce<4, 0x8u>(accr, red, slot);
-      return;
-    }
+    if (!atr_split_combine<T, NT>(acc, Gp, n, S, panel, split, pcnt, &slot)) return;
   }
   const T t = (T)t_, tmu = (T)tmu_, thres = (T)thres_, theta = (T)theta_, a1 = (T)a1_, b1 = (T)b1_;
 #pragma unroll
@@ -404,7 +402,7 @@ __global__ __launch_bounds__(256, sizeof(T) == 8 ? 2 : 1) void k_atr_fista(const
       }
     }
   }
-  grid_reduce<4, 0x8u>(accr, red, slot);
+  grid_reduce<4, 0x8u>(accr, red, slot, nparts);
 }
 
 // A^T R on VALU: a thread owns E consecutive columns of A over a row range; R[row][c0..c0+LB)
@@ -518,7 +516,7 @@ void launch_atr(const GemmPlan& p, const T* A, const T* R, T* Gp, hipStream_t st
 bool atr_prox_ok(const GemmPlan& p) {
   return p.atr_kind == 1 && p.atr_wl == 0 && p.atr_S >= 1 && p.atr_S <= 8 &&
          (p.l == 16 || p.l == 32) && p.n % 64 == 0 &&
-         (p.n / 64) * p.atr_S < kMaxBlocks &&   // + a publisher workgroup
+         p.n / 64 < kMaxBlocks &&   // reducing slots (one per panel) + the publisher
          (p.atr_S == 1 || env_int("GLX_ATR_FUSE_SPLIT", 1) != 0);
 }
 

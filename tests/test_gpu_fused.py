@@ -85,3 +85,47 @@ def test_fused_trial_fixed_step(monkeypatch, method):
     x_u, r_u = _run(monkeypatch, False, False, opts, method)
     assert r_f["k"] == r_u["k"]
     assert np.array_equal(x_f, x_u)
+
+
+# K-split fused kernels (round 3): with S > 1 only the panel owners (the last arriver of each
+# panel's S blocks) and the publisher join the trial's grid reduction, so S is no longer bounded
+# by the 1024-slot partials row (C2 = 128 panels could not take 8 splits before). G is summed
+# over the S slabs in slab order in both paths, so the iterate is bit-identical to the unfused
+# kernels at the same S; the scalars' panel order is fixed whatever the arrival order.
+SPLIT_SHAPE = (1024, 8192, 16)
+
+
+@pytest.mark.parametrize("method", METHODS)
+@pytest.mark.parametrize("S", [2, 4, 8])
+@pytest.mark.parametrize("dc", [0, 8])
+def test_fused_trial_k_splits(monkeypatch, method, S, dc):
+    import glx
+    from oracle import numpy_ref
+    m, n, l = SPLIT_SHAPE
+    A, b, u, x0, mu = numpy_ref.gen_data(m, n, l, 77)
+    opts = {"alpha0": numpy_ref.step_size_for(m, n), "maxit": 30, "dc_window": dc}
+    monkeypatch.setenv("GLX_ATR_S", str(S))
+    from glx import _lib
+    assert _lib.plan_describe(_lib.GLX_F64, m, n, l).rstrip().endswith("S=%d" % S)
+
+    def run(fused):
+        monkeypatch.setenv("GLX_FUSED_TRIAL", "1" if fused else "0")
+        At, bt, xt = (torch.from_numpy(a).cuda() for a in (A, b, x0))
+        s = glx.Session(method, xt, At, bt, mu, opts)
+        s.run(0)
+        res = s.finish()
+        s.close()
+        torch.cuda.synchronize()
+        return xt.cpu().numpy(), res
+
+    x_f, r_f = run(True)
+    x_u, r_u = run(False)
+    assert r_f["k"] == r_u["k"]
+    assert np.array_equal(x_f, x_u)
+    np.testing.assert_allclose(np.asarray(r_f["f_hist"]), np.asarray(r_u["f_hist"]), rtol=1e-13)
+    x_2, r_2 = run(True)   # run to run: bit-identical scalars and iterate
+    assert np.array_equal(x_f, x_2) and list(r_f["f_hist"]) == list(r_2["f_hist"])
+    x_r, k_r, out_r = numpy_ref.SOLVERS[method](x0.copy(), A, b, mu, {k: v for k, v in opts.items() if k != "dc_window"})
+    assert r_f["k"] == k_r
+    f_g, f_r = np.asarray(r_f["f_hist"], dtype=float), np.asarray(out_r["f_hist"], dtype=float)
+    assert np.max(np.abs(f_g - f_r) / np.abs(f_r)) < 1e-8
