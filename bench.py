@@ -28,10 +28,11 @@ the split-candidate trial, on the LDS-DMA tile, ~40 % of the iteration):
              at C2 and for C4 (l = 1); MFMA for the batched two-source passes (FProxGD's dense
              batches, C3 in fp32). achieved =
              algorithmic flops 2*m*n*l*rhs (or bytes s*(m n + (m+n) l rhs)) per launch / average
-             launch time from HIP events recorded on the solver's stream around every k-th dense
-             A@X / A^T r launch of the timed region (--profile k, default min(16, steps/8); each
-             event pair brackets exactly one kernel: the split-candidate A e gather is timed by
-             its own pair and reported apart). `pair_frac` / `pair4_frac` are the same fraction for
+             launch time from HIP events on every k-th dense A@X / A^T r launch of the timed
+             region (--profile k, default min(16, steps/4)), attached to the kernel itself
+             (hipExtLaunchKernel: the pair is stamped with that kernel's start and end on the
+             solver's stream); the split-candidate A e gather is timed by its own pair and
+             reported apart. `pair_frac` / `pair4_frac` are the same fraction for
              the A@x + A^T r pair (the north-star target), `pair4_frac_incl_gather` adds the
              gather. `traffic` = HBM bytes per launch from rocprofv3 PMC (profiles/pmc_traffic.json,
              2*FETCH_SIZE + WRITE_SIZE per the gfx950 correction) when that file holds the same
@@ -190,8 +191,8 @@ def main():
     ap.add_argument("--variant", type=int, default=0)
     ap.add_argument("--exact", type=int, default=0)
     ap.add_argument("--profile", type=int, default=None,
-                    help="HIP events around every k-th A@x / A^T r launch (0 = off; default: "
-                         "min(16, steps // 8), so at least 8 launches of each are timed)")
+                    help="HIP events on every k-th A@x / A^T r / gather launch (0 = off; default: "
+                         "min(16, steps // 4), so at least 4 launches of each are timed)")
     ap.add_argument("--prewarm-s", type=float, default=0.5,
                     help="seconds of a throwaway solver session before the warmup (0 = off)")
     ap.add_argument("--dry-run-launch", action="store_true",
@@ -206,7 +207,9 @@ def main():
                          "performance number)")
     args = ap.parse_args()
     if args.profile is None:
-        args.profile = max(1, min(16, args.steps // 8))
+        # a timed launch still costs ~11 us of queue gaps around it (profiles/r3_evt/): the
+        # driver's 20-step form times 4 launches of each kind, not 10
+        args.profile = max(1, min(16, args.steps // 4))
 
     if "WORLD_SIZE" not in os.environ and (args.gpus > 1 or args.dry_run_launch):
         sys.exit(launch_ranks(args))

@@ -1,11 +1,14 @@
 // glx_internal.h — declarations shared by the HIP kernels and the host-side driver.
 #pragma once
 
+#include <hip/hip_ext.h>
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include <stddef.h>
 
 #include <string>
+#include <tuple>
+#include <utility>
 
 namespace glx {
 
@@ -15,6 +18,41 @@ struct Error {
   std::string msg;
 };
 extern thread_local std::string g_last_error;
+
+// Kernel-attached HIP-event timing (solver.cpp prof_begin / prof_end). A sampled A@X / A^T R /
+// gather launch sets this slot; the next glx_launch on the thread hands the two events to
+// hipExtLaunchKernel, which stamps them with that kernel's own start and end, and clears it.
+// Round 3: hipEventRecord around the launch instead put two marker packets in the queue, each
+// opening a ~6 us gap before the next kernel (profiles/r3_timeline/: the driver-form command,
+// every second launch timed, ran 5 gaps per two iterations, ~3-4 % of its time).
+struct LaunchTiming {
+  hipEvent_t start = nullptr, stop = nullptr;
+};
+extern thread_local LaunchTiming g_launch_timing;
+
+template <typename... P, std::size_t... I>
+inline void ext_launch(void (*kern)(P...), dim3 g, dim3 b, uint32_t sh, hipStream_t st,
+                       std::tuple<P...>& t, std::index_sequence<I...>, hipEvent_t e0,
+                       hipEvent_t e1) {
+  void* args[sizeof...(P) > 0 ? sizeof...(P) : 1] = {static_cast<void*>(&std::get<I>(t))...};
+  (void)hipExtLaunchKernel(reinterpret_cast<const void*>(kern), g, b, args, sh, st, e0, e1, 0);
+}
+// hipLaunchKernelGGL, or the timed form when a timing slot is pending. The arguments are
+// converted to the kernel's own parameter types first (hipExtLaunchKernel takes raw pointers
+// to them, so an int passed for an int64_t must not reach it unconverted).
+template <typename... P, typename... A>
+inline void glx_launch(void (*kern)(P...), dim3 g, dim3 b, uint32_t sh, hipStream_t st, A&&... a) {
+  static_assert(sizeof...(P) == sizeof...(A), "argument count");
+  LaunchTiming& lt = g_launch_timing;
+  if (lt.start != nullptr) {
+    std::tuple<P...> t(static_cast<P>(std::forward<A>(a))...);
+    const hipEvent_t e0 = lt.start, e1 = lt.stop;
+    lt = LaunchTiming{};
+    ext_launch(kern, g, b, sh, st, t, std::index_sequence_for<P...>{}, e0, e1);
+    return;
+  }
+  hipLaunchKernelGGL(kern, g, b, sh, st, std::forward<A>(a)...);
+}
 
 constexpr int kMaxBlocks = 1024;   // grid cap of every reducing kernel (size of a partials row)
 constexpr int kMaxRedVals = 6;     // max scalars one reducing kernel produces

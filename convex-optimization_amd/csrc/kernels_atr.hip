@@ -465,10 +465,10 @@ static void atr_valu_lb(const GemmPlan& p, const T* A, const T* R, T* Gp, hipStr
   const dim3 grid((unsigned)cdiv(p.n, cols_per_block), (unsigned)p.atr_S);
   for (int64_t c0 = 0; c0 < p.l; c0 += LB) {
     if (p.atr_vec)
-      hipLaunchKernelGGL((k_atr_valu<T, LB, true>), grid, dim3(256), 0, st, A, R, Gp, p.m, p.n,
+      glx_launch((k_atr_valu<T, LB, true>), grid, dim3(256), 0, st, A, R, Gp, p.m, p.n,
                          p.l, (int)c0, p.atr_S);
     else
-      hipLaunchKernelGGL((k_atr_valu<T, LB, false>), grid, dim3(256), 0, st, A, R, Gp, p.m, p.n,
+      glx_launch((k_atr_valu<T, LB, false>), grid, dim3(256), 0, st, A, R, Gp, p.m, p.n,
                          p.l, (int)c0, p.atr_S);
   }
 }
@@ -477,7 +477,7 @@ template <typename T, int NT, int PF, int WL, bool NTL>
 static void atr_mfma_go(const GemmPlan& p, const T* A, const T* R, T* Gp, hipStream_t st) {
   const dim3 grid((unsigned)(p.n / (WL ? 256 : 64)), (unsigned)p.atr_S);
   static const size_t pad = lds_pad(k_atr_mfma<T, NT, PF, WL, NTL>, "GLX_ATR_LDS_PAD");
-  hipLaunchKernelGGL((k_atr_mfma<T, NT, PF, WL, NTL>), grid, dim3(256), pad, st, A, R, Gp, p.m, p.n, p.atr_S);
+  glx_launch((k_atr_mfma<T, NT, PF, WL, NTL>), grid, dim3(256), pad, st, A, R, Gp, p.m, p.n, p.atr_S);
 }
 
 template <typename T, int NT>
@@ -526,12 +526,12 @@ static void atr_prox_go(const GemmPlan& p, const T* A, const T* R, T* G, const T
                         Pub pub, T* Gp, unsigned* pcnt, unsigned* zf) {
   const dim3 grid((unsigned)(p.n / 64 * p.atr_S + (pub.host ? 1 : 0)));
   if (p.atr_S > 1) {
-    hipLaunchKernelGGL((k_atr_prox<T, NT, PF, NTL, true>), grid, dim3(256), 0, st, A, R, G, p.m,
+    glx_launch((k_atr_prox<T, NT, PF, NTL, true>), grid, dim3(256), 0, st, A, R, G, p.m,
                        p.n, x, pp, pthr, z, t, t * mu, thres, red, pub, p.atr_S, Gp, pcnt, zf);
     return;
   }
   static const size_t pad = lds_pad(k_atr_prox<T, NT, PF, NTL, false>, "GLX_ATR_LDS_PAD");
-  hipLaunchKernelGGL((k_atr_prox<T, NT, PF, NTL, false>), grid, dim3(256), pad, st, A, R, G, p.m,
+  glx_launch((k_atr_prox<T, NT, PF, NTL, false>), grid, dim3(256), pad, st, A, R, G, p.m,
                      p.n, x, pp, pthr, z, t, t * mu, thres, red, pub, 1, Gp, pcnt, zf);
 }
 template <typename T, int NT>
@@ -563,13 +563,13 @@ static void atr_fista_go(const GemmPlan& p, const T* A, const T* R, T* G, const 
                          T* ec, unsigned* zf) {
   const dim3 grid((unsigned)(p.n / 64 * p.atr_S + (pub.host ? 1 : 0)));
   if (p.atr_S > 1) {
-    hipLaunchKernelGGL((k_atr_fista<T, NT, PF, NTL, true>), grid, dim3(256), 0, st, A, R, G, p.m,
+    glx_launch((k_atr_fista<T, NT, PF, NTL, true>), grid, dim3(256), 0, st, A, R, G, p.m,
                        p.n, y, xk, xc, vn, yn, t, t * mu, thres, theta, 1.0 - theta_next,
                        theta_next, red, pub, p.atr_S, Gp, pcnt, ec, zf);
     return;
   }
   static const size_t pad = lds_pad(k_atr_fista<T, NT, PF, NTL, false>, "GLX_ATR_LDS_PAD");
-  hipLaunchKernelGGL((k_atr_fista<T, NT, PF, NTL, false>), grid, dim3(256), pad, st, A, R, G, p.m,
+  glx_launch((k_atr_fista<T, NT, PF, NTL, false>), grid, dim3(256), pad, st, A, R, G, p.m,
                      p.n, y, xk, xc, vn, yn, t, t * mu, thres, theta, 1.0 - theta_next, theta_next,
                      red, pub, 1, Gp, pcnt, ec, zf);
 }

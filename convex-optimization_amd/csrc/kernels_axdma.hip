@@ -370,7 +370,7 @@ static void ax_dma_go(const GemmPlan& p, int S, const T* A, const T* const* X, T
     const int gx = (int)cdiv(p.m, 16 * MT * WAVES);
     const int xmap = ax_xmap_flags(p, S);
     const dim3 grid((unsigned)ax_grid(xmap, gx, S) + (pub.host ? 1u : 0u));
-    hipLaunchKernelGGL((k_ax_dma<T, NT, NSRC, NS, KC, WAVES, NTL, HOIST, PIPE, MT>), grid, dim3(64 * WAVES), 0, st,
+    glx_launch((k_ax_dma<T, NT, NSRC, NS, KC, WAVES, NTL, HOIST, PIPE, MT>), grid, dim3(64 * WAVES), 0, st,
                        A, X[0], X[1], X[2], P, p.m, p.n, p.n / KC, S, gx, xmap, gate, epoch, pub);
   }
 }

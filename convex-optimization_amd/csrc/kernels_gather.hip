@@ -202,7 +202,7 @@ void launch_at_gather(const T* At, const T* E, int64_t m, int64_t n, int64_t l, 
     return !(e && std::strcmp(e, "0") == 0);
   }();
   auto go = [&](auto kern) {
-    hipLaunchKernelGGL(kern, dim3((unsigned)(gx * l)), dim3(kGThreads), 0, st, At, E, lists,
+    glx_launch(kern, dim3((unsigned)(gx * l)), dim3(kGThreads), 0, st, At, E, lists,
                        list_counts(lists_ws, n), m, n, P, gx, skip);
   };
   if (l == 32) nt ? go(k_at_gather<T, 32, true>) : go(k_at_gather<T, 32, false>);

@@ -747,10 +747,10 @@ static void ax_valu_lb(const GemmPlan& p, const T* A, const T* const* X, T* P, c
   const dim3 grid((unsigned)cdiv(cdiv(p.m, 4), 4), (unsigned)p.ax_S);
   for (int64_t c0 = 0; c0 < p.l; c0 += LB) {
     if (p.ax_vec)
-      hipLaunchKernelGGL((k_ax_valu<T, LB, 4, true, NSRC>), grid, dim3(256), 0, st, A, X[0], X[1],
+      glx_launch((k_ax_valu<T, LB, 4, true, NSRC>), grid, dim3(256), 0, st, A, X[0], X[1],
                          X[2], P, p.m, p.n, p.l, (int)c0, p.ax_S, gate, epoch);
     else
-      hipLaunchKernelGGL((k_ax_valu<T, LB, 4, false, NSRC>), grid, dim3(256), 0, st, A, X[0], X[1],
+      glx_launch((k_ax_valu<T, LB, 4, false, NSRC>), grid, dim3(256), 0, st, A, X[0], X[1],
                          X[2], P, p.m, p.n, p.l, (int)c0, p.ax_S, gate, epoch);
   }
 }
@@ -773,7 +773,7 @@ static void ax_mfma_go(const GemmPlan& p, const T* A, const T* const* X, T* P, c
   const int gx = (int)cdiv(p.m, 16 * MT);
   const int xmap = ((p.ax_xmap & 1) && ax_xmap_ok(p.ax_S)) ? 1 : 0;
   const dim3 grid((unsigned)ax_grid(xmap, gx, p.ax_S));
-  hipLaunchKernelGGL((k_ax_mfma<T, MT, NT, NSRC, PF, QUAD, NTL, VPL>), grid, dim3(256), 0, st, A,
+  glx_launch((k_ax_mfma<T, MT, NT, NSRC, PF, QUAD, NTL, VPL>), grid, dim3(256), 0, st, A,
                      X[0], X[1], X[2], P, p.m, p.n, p.n / (4 * VPL * E), p.ax_S, gx, xmap, gate,
                      epoch);
 }
@@ -786,7 +786,7 @@ static void ax_lds_go(const GemmPlan& p, int S, const T* A, const T* const* X, T
   const int xmap = ax_xmap_flags(p, S);
   const dim3 grid((unsigned)ax_grid(xmap, gx, S) + (pub.host ? 1u : 0u));
   static const size_t pad = lds_pad(k_ax_lds<T, MT, NT, NSRC, PF, VPL, WAVES>, "GLX_AX_LDS_PAD");
-  hipLaunchKernelGGL((k_ax_lds<T, MT, NT, NSRC, PF, VPL, WAVES>), grid,
+  glx_launch((k_ax_lds<T, MT, NT, NSRC, PF, VPL, WAVES>), grid,
                      dim3(64 * WAVES), pad, st, A, X[0], X[1], X[2], P, p.m, p.n,
                      p.n / (4 * VPL * E), S, gx, xmap, gate, epoch, pub);
 }

@@ -205,10 +205,10 @@ static void gemv_go(int blocks, const T* A, const T* x, const T* xt, const T* b,
   }();
   const bool nt = nt_env >= 0 ? nt_env != 0 : (double)m * n * sizeof(T) > kGemvNtBytes;
   if (nt)
-    hipLaunchKernelGGL((k_gemv_pair_fused<T, VPT, RB, true>), dim3((unsigned)blocks),
+    glx_launch((k_gemv_pair_fused<T, VPT, RB, true>), dim3((unsigned)blocks),
                        dim3(kGemvThreads), 0, st, A, x, xt, b, Gp, m, n, fh, fh_mu, rn, red);
   else
-    hipLaunchKernelGGL((k_gemv_pair_fused<T, VPT, RB, false>), dim3((unsigned)blocks),
+    glx_launch((k_gemv_pair_fused<T, VPT, RB, false>), dim3((unsigned)blocks),
                        dim3(kGemvThreads), 0, st, A, x, xt, b, Gp, m, n, fh, fh_mu, rn, red);
 }
 

@@ -31,6 +31,7 @@
 namespace glx {
 
 thread_local std::string g_last_error;
+thread_local LaunchTiming g_launch_timing;
 
 #define GLX_HIP(expr)                                                                          \
   do {                                                                                         \
@@ -514,22 +515,30 @@ class Session : public SessionBase {
     return r;
   }
 
-  // HIP-event timing of A@X (kind 0) / A^T R (kind 1) launches. opts.profile = k > 0 times every
-  // k-th launch of each kind: a timed event pair opens a gap of a few us in the queue, so
-  // sampling keeps the measured run close to an unprofiled one.
+  // HIP-event timing of A@X (kind 0) / A^T R (kind 1) / gather (kind 2) launches. opts.profile =
+  // k > 0 times every k-th launch of each kind. The events ride on the kernel itself
+  // (hipExtLaunchKernel through glx_launch, see LaunchTiming): the next glx_launch takes them, so
+  // the pair brackets exactly that kernel and adds nothing to the queue.
   hipEvent_t prof_begin(int kind) {
     if (O_.profile <= 0 || (prof_n_[kind]++ % O_.profile) != 0) return nullptr;
     hipEvent_t e0 = get_event();
-    GLX_HIP(hipEventRecord(e0, st_));
+    prof_stop_ = get_event();
+    g_launch_timing = LaunchTiming{e0, prof_stop_};
     return e0;
   }
   void prof_end(int kind, hipEvent_t e0) {
     if (e0 == nullptr) return;
-    hipEvent_t e1 = get_event();
-    GLX_HIP(hipEventRecord(e1, st_));
-    ev_[kind].push_back({e0, e1});
+    const LaunchTiming lt = g_launch_timing;
+    g_launch_timing = LaunchTiming{};
+    if (lt.start == nullptr) {   // taken by the launch: keep the sample
+      ev_[kind].push_back({e0, prof_stop_});
+    } else {                     // the launch path had no timed kernel: no sample
+      ev_pool_.push_back(lt.start);
+      ev_pool_.push_back(lt.stop);
+    }
   }
 
+  hipEvent_t prof_stop_ = nullptr;   // the stop event of the open prof_begin
   hipEvent_t get_event() {
     if (ev_pool_.empty()) {   // grow in batches: never create events inside a timed loop's steady state
       for (int i = 0; i < 256; ++i) {

@@ -15,10 +15,16 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("trace")
     ap.add_argument("--last", type=int, default=2000)
+    ap.add_argument("--markers", action="store_true",
+                    help="use the launches between the last two marker kernels (bench.py's timed region)")
     a = ap.parse_args()
     rows = list(csv.DictReader(open(a.trace)))
     ks = sorted(((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), r["Kernel_Name"]) for r in rows))
-    ks = ks[-a.last:]
+    marks = [i for i, k in enumerate(ks) if "spin" in k[2].lower() or "sleep" in k[2].lower()]
+    if a.markers and len(marks) >= 2:
+        ks = ks[marks[-2] + 1:marks[-1]]
+    else:
+        ks = ks[-a.last:]
     span = ks[-1][1] - ks[0][0]
     busy = collections.defaultdict(lambda: [0, 0])
     gaps = collections.defaultdict(list)
