@@ -127,11 +127,14 @@ static void validate(const glx_problem* P, const glx_opts* O) {
 
 // ------------------------------------------------------------------------------------------
 // The solver's plan: the shape's GEMM plan, plus one method-level choice. fp32 ProxGD/FProxGD
-// on one GPU take the 4-wave panel AᵀR with 2 K splits (code 1104) instead of the 4-panel
+// on one GPU take the 4-wave panel AᵀR with 2 K splits (code 1008) instead of the 4-panel
 // tile (1114), so that the line-search trial fuses into it (atr_split_combine): the AᵀR pass
 // is ≈13 µs slower but the trial launch and its boundary go. Same box: C3 (8192,16384,32)
 // FProxGD 3669–3691 → 3743–3749 it/s, ProxGD 3654–3657 → 3744–3752, FProxGD at (4096,8192,16)
 // 11 362–11 366 → 13 200–13 215 (profiles/r1_tuning/small_kernels/atr_f32_fused.log).
+// Round 3: with the PF 8 ring (1008) instead of PF 4 the C3 pass reads 5.0 instead of 4.7 TB/s
+// (A^T R 106.6–107.1 vs 113–114.5 us), FProxGD 3627–3680 → 3725–3763 it/s over 200 steps;
+// S = 1 / 4 and the default load policy measured level or slower (profiles/r3_c3atr/sweep.txt).
 // Split-candidate ProxGD (the fast objective mode, see iter_proxgd): 0 = off (exact mode, other
 // methods, shapes the gather does not cover, or GLX_SPLIT_CAND=0 / glx_opts.split_cand = 0: the
 // dense [z | p_thr] batch of round 1); 1 = A e from the transposed copy of A (kernels_gather.hip;
@@ -176,7 +179,7 @@ static GemmPlan session_plan(const glx_problem& P, const glx_opts& O) {
     GemmPlan f = p;
     f.atr_wl = 0;
     f.atr_ntl = 1;
-    f.atr_pf = 4;
+    f.atr_pf = 8;   // round 3: the PF 8 ring (1008), see above
     f.atr_S = 2;
     if (atr_prox_ok(f)) return f;   // only where the trial actually fuses (GLX_ATR_FUSE_SPLIT)
   }
