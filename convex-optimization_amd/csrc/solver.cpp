@@ -391,6 +391,13 @@ class Session : public SessionBase {
     for (auto& v : ev_)
       for (auto& p : v) { (void)hipEventDestroy(p.first); (void)hipEventDestroy(p.second); }
     for (hipEvent_t e : ev_pool_) (void)hipEventDestroy(e);
+    // a timing slot this session opened whose launch threw: never hand its events to a later
+    // launch on this thread
+    if (g_launch_timing.stop != nullptr && g_launch_timing.stop == prof_stop_) {
+      (void)hipEventDestroy(g_launch_timing.start);
+      (void)hipEventDestroy(g_launch_timing.stop);
+      g_launch_timing = LaunchTiming{};
+    }
   }
 
   // ------------------------------------------------------------------ run loop
