@@ -84,8 +84,15 @@ __global__ __launch_bounds__(kGThreads) void k_e_lists(const unsigned* __restric
       w[4 * u] = v.x; w[4 * u + 1] = v.y; w[4 * u + 2] = v.z; w[4 * u + 3] = v.w;
     }
   };
+  // the first 4V masks of the thread's range stay in registers for the write pass (the whole
+  // range at n <= 4V * 256 = 16384: one load round per kernel instead of two)
+  unsigned w0[4 * V];
+  chunk(f0, w0);
   unsigned cnt = 0;
-  for (int64_t k0 = f0; k0 < f1; k0 += 4 * V) {
+#pragma unroll
+  for (int j = 0; j < 4 * V; ++j)
+    if (f0 + j < f1 && ((w0[j] >> c) & 1u)) ++cnt;
+  for (int64_t k0 = f0 + 4 * V; k0 < f1; k0 += 4 * V) {
     unsigned w[4 * V];
     chunk(k0, w);
 #pragma unroll
@@ -108,14 +115,18 @@ __global__ __launch_bounds__(kGThreads) void k_e_lists(const unsigned* __restric
     total += wsum[w];
   }
   unsigned short* out = lists + (int64_t)c * n;
-  if (cnt != 0)
-    for (int64_t k0 = f0; k0 < f1; k0 += 4 * V) {
+  if (cnt != 0) {
+#pragma unroll
+    for (int j = 0; j < 4 * V; ++j)
+      if (f0 + j < f1 && ((w0[j] >> c) & 1u)) out[pos++] = (unsigned short)(f0 + j);
+    for (int64_t k0 = f0 + 4 * V; k0 < f1; k0 += 4 * V) {
       unsigned w[4 * V];
       chunk(k0, w);
 #pragma unroll
       for (int j = 0; j < 4 * V; ++j)
         if (k0 + j < f1 && ((w[j] >> c) & 1u)) out[pos++] = (unsigned short)(k0 + j);
     }
+  }
   if (tid == 0) counts[c] = total;
 }
 
