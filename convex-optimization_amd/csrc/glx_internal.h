@@ -10,6 +10,8 @@
 #include <tuple>
 #include <utility>
 
+#include "glx.h"
+
 namespace glx {
 
 // error carried to the C ABI boundary (never crosses it)
@@ -35,7 +37,8 @@ inline void ext_launch(void (*kern)(P...), dim3 g, dim3 b, uint32_t sh, hipStrea
                        std::tuple<P...>& t, std::index_sequence<I...>, hipEvent_t e0,
                        hipEvent_t e1) {
   void* args[sizeof...(P) > 0 ? sizeof...(P) : 1] = {static_cast<void*>(&std::get<I>(t))...};
-  (void)hipExtLaunchKernel(reinterpret_cast<const void*>(kern), g, b, args, sh, st, e0, e1, 0);
+  const hipError_t e = hipExtLaunchKernel(reinterpret_cast<const void*>(kern), g, b, args, sh, st, e0, e1, 0);
+  if (e != hipSuccess) throw Error{GLX_E_HIP, std::string("timed kernel launch: ") + hipGetErrorString(e)};
 }
 // hipLaunchKernelGGL, or the timed form when a timing slot is pending. The arguments are
 // converted to the kernel's own parameter types first (hipExtLaunchKernel takes raw pointers
