@@ -130,33 +130,6 @@ __global__ __launch_bounds__(kGThreads) void k_e_lists(const unsigned* __restric
   if (tid == 0) counts[c] = total;
 }
 
-// Per-panel column lists (round 3; n <= kPlMaxN, n % 64 == 0): one wave per 64-row panel of e.
-// Lane j holds row 64 p + j's mask; per column c a ballot gives the panel's flagged rows, and
-// each flagged lane writes its row at its rank among them (mbcnt), so the panel's list of
-// column c is ascending. The gather concatenates the n/64 panel lists in panel order (ascending
-// k, the order of k_e_lists' column lists: bit-identical sums). One load round over the whole
-// grid instead of k_e_lists' 32 workgroups each scanning all n masks (8.3 us at NS).
-constexpr int64_t kPlMaxN = 16384;   // the gather's LDS list (32 KiB) and one panel per thread
-__global__ __launch_bounds__(64) void k_e_plists(const unsigned* __restrict__ zm, int l,
-                                                 unsigned short* __restrict__ plist,
-                                                 unsigned char* __restrict__ pcnt,
-                                                 const int* __restrict__ skip) {
-  if (skip != nullptr && *skip != 0) return;
-  const int lane = threadIdx.x;
-  const int64_t panel = blockIdx.x;
-  const unsigned msk = zm[panel * 64 + lane];
-  for (int c = 0; c < l; ++c) {
-    const bool f = ((msk >> c) & 1u) != 0u;
-    const uint64_t bits = __builtin_amdgcn_ballot_w64(f);
-    if (f) {
-      const unsigned pos = __builtin_amdgcn_mbcnt_hi((unsigned)(bits >> 32),
-                                                     __builtin_amdgcn_mbcnt_lo((unsigned)bits, 0u));
-      plist[(panel * l + c) * 64 + pos] = (unsigned short)(panel * 64 + lane);
-    }
-    if (lane == 0) pcnt[panel * l + c] = (unsigned char)__builtin_popcountll(bits);
-  }
-}
-
 // One workgroup per (256-row block, column c) of A e. e has few nonzeros per flagged row (about
 // one of the 32 columns at the north-star size), so a dense 16x16x4 MFMA over all 32 columns
 // would spend ~97 % of its flops on zeros: here every output element is a fp64 VALU dot product
@@ -165,52 +138,17 @@ __global__ __launch_bounds__(64) void k_e_plists(const unsigned* __restrict__ zm
 // of one At row. out[r][c] = the sum (one slab: no K split).
 // NT: At read with the non-temporal policy (each of its rows is read at most once per trial;
 // GLX_GATHER_NT)
-// PL: the lists are k_e_plists' per-panel lists (pcnt / plist): the workgroup first concatenates
-// column c's n/64 panel lists into LDS (a block scan of the panel counts, one panel per thread)
-// and reads the indices from there; row block 0 also writes the column's total to counts[c]
-// (nnz(e_c) for FISTA's budget, as k_e_lists did).
-template <typename T, int L, bool NT, bool PL>
+template <typename T, int L, bool NT>
 __global__ __launch_bounds__(kGThreads) void k_at_gather(const T* __restrict__ At,
                                                          const T* __restrict__ E,
                                                          const unsigned short* __restrict__ lists,
-                                                         unsigned* __restrict__ counts,
+                                                         const unsigned* __restrict__ counts,
                                                          int64_t m, int64_t n, T* __restrict__ P,
-                                                         int gx, const int* __restrict__ skip,
-                                                         const unsigned char* __restrict__ pcnt) {
+                                                         int gx, const int* __restrict__ skip) {
   if (skip != nullptr && *skip != 0) return;
   const int rb = (int)blockIdx.x % gx, c = (int)blockIdx.x / gx;
-  int total;
-  const unsigned short* lst;
-  __shared__ unsigned short slist[PL ? kPlMaxN : 1];
-  __shared__ unsigned wtot[kGW];
-  if constexpr (PL) {
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    const int np = (int)(n / 64);
-    const unsigned cp = tid < np ? (unsigned)pcnt[(int64_t)tid * L + c] : 0u;
-    unsigned inc = cp;
-#pragma unroll
-    for (int off = 1; off < 64; off <<= 1) {
-      const unsigned v = __shfl_up(inc, off);
-      if (lane >= off) inc += v;
-    }
-    if (lane == 63) wtot[wave] = inc;
-    __syncthreads();
-    unsigned pos = inc - cp, tot = 0;
-#pragma unroll
-    for (int w = 0; w < kGW; ++w) {
-      if (w < wave) pos += wtot[w];
-      tot += wtot[w];
-    }
-    const unsigned short* src = lists + ((int64_t)tid * L + c) * 64;
-    for (unsigned j = 0; j < cp; ++j) slist[pos + j] = src[j];
-    __syncthreads();
-    total = (int)tot;
-    lst = slist;
-    if (rb == 0 && tid == 0) counts[c] = tot;
-  } else {
-    total = (int)counts[c];
-    lst = lists + (int64_t)c * n;
-  }
+  const int total = (int)counts[c];
+  const unsigned short* lst = lists + (int64_t)c * n;
   const int64_t r = (int64_t)rb * kGThreads + threadIdx.x;
   const int64_t rr = r < m ? r : m - 1;
   constexpr int U = 8;
@@ -257,26 +195,9 @@ const unsigned* gather_counts(const void* lists_ws, int64_t n) {
   return list_counts(const_cast<void*>(lists_ws), n);
 }
 
-static bool plists_on(int64_t n) {
-  static const bool env = [] {   // GLX_PLISTS=1: on (validation pending: off by default)
-    const char* e = std::getenv("GLX_PLISTS");
-    return e && std::strcmp(e, "1") == 0;
-  }();
-  return env && n <= kPlMaxN && n % 64 == 0;
-}
-// per-panel counts behind the index lists (gather_lists_bytes)
-static unsigned char* plist_counts(void* lists_ws, int64_t n) {
-  return static_cast<unsigned char*>(lists_ws) + (((size_t)32 * n * 2 + 255) & ~size_t(255));
-}
-
 void launch_e_lists(const unsigned* zm, int64_t n, int64_t l, void* lists_ws, hipStream_t st,
                     const int* skip) {
   if (!gather_ok(n, l)) throw Error{GLX_E_INVALID, "A e gather: needs l in {16, 32}, n < 65536"};
-  if (plists_on(n)) {
-    hipLaunchKernelGGL(k_e_plists, dim3((unsigned)(n / 64)), dim3(64), 0, st, zm, (int)l,
-                       static_cast<unsigned short*>(lists_ws), plist_counts(lists_ws, n), skip);
-    return;
-  }
   hipLaunchKernelGGL(k_e_lists, dim3((unsigned)l), dim3(kGThreads), 0, st, zm, n,
                      static_cast<unsigned short*>(lists_ws), list_counts(lists_ws, n), skip);
 }
@@ -291,26 +212,16 @@ void launch_at_gather(const T* At, const T* E, int64_t m, int64_t n, int64_t l, 
     const char* e = std::getenv("GLX_GATHER_NT");
     return !(e && std::strcmp(e, "0") == 0);
   }();
-  const unsigned char* pc = plist_counts(lists_ws, n);
   auto go = [&](auto kern) {
     glx_launch(kern, dim3((unsigned)(gx * l)), dim3(kGThreads), 0, st, At, E, lists,
-               list_counts(lists_ws, n), m, n, P, gx, skip, pc);
+                       list_counts(lists_ws, n), m, n, P, gx, skip);
   };
-  const bool pl = plists_on(n);
-  if (l == 32) {
-    if (pl) nt ? go(k_at_gather<T, 32, true, true>) : go(k_at_gather<T, 32, false, true>);
-    else nt ? go(k_at_gather<T, 32, true, false>) : go(k_at_gather<T, 32, false, false>);
-  } else {
-    if (pl) nt ? go(k_at_gather<T, 16, true, true>) : go(k_at_gather<T, 16, false, true>);
-    else nt ? go(k_at_gather<T, 16, true, false>) : go(k_at_gather<T, 16, false, false>);
-  }
+  if (l == 32) nt ? go(k_at_gather<T, 32, true>) : go(k_at_gather<T, 32, false>);
+  else nt ? go(k_at_gather<T, 16, true>) : go(k_at_gather<T, 16, false>);
 }
 
-// workspace of the column lists: l * n indices (column lists, or the per-panel lists), the
-// per-panel counts (n / 64 panels x 32 columns, one byte each) and 256 B of column counts
-size_t gather_lists_bytes(int64_t n) {
-  return (((size_t)32 * n * 2 + 255) & ~size_t(255)) + (((size_t)(n / 64 + 1) * 32 + 255) & ~size_t(255)) + 256;
-}
+// workspace of the column lists: l * n indices + 256 B of counts
+size_t gather_lists_bytes(int64_t n) { return (((size_t)32 * n * 2 + 255) & ~size_t(255)) + 256; }
 
 template void launch_transpose<double>(const double*, double*, int64_t, int64_t, hipStream_t);
 template void launch_transpose<float>(const float*, float*, int64_t, int64_t, hipStream_t);
