@@ -33,12 +33,11 @@ struct LaunchTiming {
 extern thread_local LaunchTiming g_launch_timing;
 
 template <typename... P, std::size_t... I>
-inline void ext_launch(void (*kern)(P...), dim3 g, dim3 b, uint32_t sh, hipStream_t st,
-                       std::tuple<P...>& t, std::index_sequence<I...>, hipEvent_t e0,
-                       hipEvent_t e1) {
+inline hipError_t ext_launch(void (*kern)(P...), dim3 g, dim3 b, uint32_t sh, hipStream_t st,
+                             std::tuple<P...>& t, std::index_sequence<I...>, hipEvent_t e0,
+                             hipEvent_t e1) {
   void* args[sizeof...(P) > 0 ? sizeof...(P) : 1] = {static_cast<void*>(&std::get<I>(t))...};
-  const hipError_t e = hipExtLaunchKernel(reinterpret_cast<const void*>(kern), g, b, args, sh, st, e0, e1, 0);
-  if (e != hipSuccess) throw Error{GLX_E_HIP, std::string("timed kernel launch: ") + hipGetErrorString(e)};
+  return hipExtLaunchKernel(reinterpret_cast<const void*>(kern), g, b, args, sh, st, e0, e1, 0);
 }
 // hipLaunchKernelGGL, or the timed form when a timing slot is pending. The arguments are
 // converted to the kernel's own parameter types first (hipExtLaunchKernel takes raw pointers
@@ -51,7 +50,13 @@ inline void glx_launch(void (*kern)(P...), dim3 g, dim3 b, uint32_t sh, hipStrea
     std::tuple<P...> t(static_cast<P>(std::forward<A>(a))...);
     const hipEvent_t e0 = lt.start, e1 = lt.stop;
     lt = LaunchTiming{};
-    ext_launch(kern, g, b, sh, st, t, std::index_sequence_for<P...>{}, e0, e1);
+    const hipError_t e = ext_launch(kern, g, b, sh, st, t, std::index_sequence_for<P...>{}, e0, e1);
+    if (e != hipSuccess) {
+      // the events were not taken: hand the slot back, so prof_end (or the session's destructor)
+      // returns them to the pool instead of losing them
+      lt = LaunchTiming{e0, e1};
+      throw Error{GLX_E_HIP, std::string("timed kernel launch: ") + hipGetErrorString(e)};
+    }
     return;
   }
   hipLaunchKernelGGL(kern, g, b, sh, st, std::forward<A>(a)...);
@@ -152,6 +157,10 @@ struct GemmPlan {
   int atr_ntl;      // non-temporal A loads
   int atr_S;        // M (= m) splits across workgroups
   int atr_lb, atr_vec;
+  // Infinity-Cache hand-off between the two non-temporal passes (Session sets them; 0 = off):
+  // the last ~that many MiB a pass reads load with the default policy (kernel arguments, so
+  // every session and device gets its own value)
+  int ax_keep_mib = 0, atr_keep_mib = 0;
 };
 
 GemmPlan make_plan(int esize, int64_t m, int64_t n, int64_t l, int ax_variant);
@@ -186,8 +195,6 @@ int dma_waves(int code);   // waves per workgroup of a kind-8/9 code (last digit
 int dma_mt(int code);      // 16-row tiles per wave (kind 9: 2)
 // Infinity-Cache hand-off between the passes (tuning experiment; MiB of A fetched with the
 // default policy at the end of a non-temporal pass; 0 = off): A@X (LDS-DMA tile) / A^T R
-void set_ax_keep_mib(int mib, hipStream_t st);
-void set_atr_keep_mib(int mib, hipStream_t st);
 template <typename T>
 void launch_atr(const GemmPlan& p, const T* A, const T* R, T* Gp, hipStream_t st);
 // ProxGD trial fused into A^T R (needs atr_prox_ok: MFMA panels, WL 0, at most 8 K splits):

@@ -53,21 +53,15 @@ template <bool NTL> struct Load4<float, NTL> {
 // ((w0 + w1) + w2) + w3; afterwards wave w holds the complete sum for e == w in acc[w][*]
 // (the other e of a wave are partial and unused), so the four waves share the epilogue.
 // (pbx, pby) = (panel, K split) of this block: (blockIdx.x, blockIdx.y) for k_atr_mfma.
-// Infinity-Cache hand-off (tuning experiment, GLX_ATR_KEEP_MIB, default 0 = off): the last
-// rows a non-temporal A^T R pass reads are loaded with the default policy, so that about that many
-// MiB of A stay in the 256 MiB Infinity Cache for the next pass over A (A@X) to hit.
-__device__ int g_atr_keep_mib = 0;
-void set_atr_keep_mib(int mib, hipStream_t st) {
-  static int cur = -1;
-  if (mib == cur) return;
-  (void)hipMemcpyToSymbolAsync(HIP_SYMBOL(g_atr_keep_mib), &mib, sizeof(int), 0, hipMemcpyHostToDevice, st);
-  cur = mib;
-}
+// Infinity-Cache hand-off (GemmPlan::atr_keep_mib, a kernel argument; the solver's default is
+// kKeepMiB = 192, GLX_ATR_KEEP_MIB overrides it, 0 = off): the last rows a non-temporal A^T R
+// pass reads are loaded with the default policy, so that about that many MiB of A stay in the
+// 256 MiB Infinity Cache for the next pass over A (A@X) to hit.
 
 template <typename T, int NT, int PF, int WL, bool NTL>
 __device__ inline int64_t atr_panel(const T* __restrict__ A, const T* __restrict__ R, int64_t m,
                                     int64_t n, int S, typename MF<T>::acc_t (&acc)[4][NT],
-                                    int64_t pbx, int64_t pby) {
+                                    int64_t pbx, int64_t pby, int keep_mib) {
   typedef MF<T> M;
   typedef typename M::acc_t C;
   constexpr int L = 16 * NT;
@@ -112,7 +106,7 @@ __device__ inline int64_t atr_panel(const T* __restrict__ A, const T* __restrict
   // 4 rows x 64 columns per step (WL 1: 4 x 256 columns per block step)
   int64_t keep = 0;
   if constexpr (NTL) {
-    const int64_t kb = (int64_t)g_atr_keep_mib << 20;
+    const int64_t kb = (int64_t)keep_mib << 20;
     keep = kb / ((int64_t)(WL == 0 ? W * (n / 64) : W * (n / 256)) * 4 * (WL == 0 ? 64 : 256) * (int64_t)sizeof(T));
   }
   const int64_t kt = nst - keep;
@@ -232,14 +226,15 @@ __device__ inline bool atr_split_combine(typename MF<T>::acc_t (&acc)[4][NT], T*
 
 template <typename T, int NT, int PF, int WL, bool NTL>
 __global__ __launch_bounds__(256) void k_atr_mfma(const T* __restrict__ A, const T* __restrict__ R,
-                                                  T* __restrict__ Gp, int64_t m, int64_t n, int S) {
+                                                  T* __restrict__ Gp, int64_t m, int64_t n, int S,
+                                                  int keep_mib) {
   typedef MF<T> M;
   constexpr int L = 16 * NT;
   const int lane = threadIdx.x & 63;
   const int wave = threadIdx.x >> 6;
   const int i = lane & 15;
   typename M::acc_t acc[4][NT];
-  const int64_t col0 = atr_panel<T, NT, PF, WL, NTL>(A, R, m, n, S, acc, blockIdx.x, blockIdx.y);
+  const int64_t col0 = atr_panel<T, NT, PF, WL, NTL>(A, R, m, n, S, acc, blockIdx.x, blockIdx.y, keep_mib);
   T* gout = Gp + (int64_t)blockIdx.y * n * L;
 #pragma unroll
   for (int e = 0; e < 4; ++e) {
@@ -266,7 +261,7 @@ __global__ __launch_bounds__(256, sizeof(T) == 8 ? 2 : 1) void k_atr_prox(const 
                                                   double t_, double tmu_, double thres_, Red red,
                                                   Pub pub, int S, T* __restrict__ Gp,
                                                   unsigned* __restrict__ pcnt,
-                                                  unsigned* __restrict__ zf) {
+                                                  unsigned* __restrict__ zf, int keep_mib) {
   // Cancelled by a device-side decision (solver.cpp dc_run): nothing is computed or stored, no
   // counter or ticket is touched. (Testing the flag after the main loop instead measured no
   // faster and would spend a whole pass per cancelled launch.) The decision record still goes
@@ -288,7 +283,7 @@ __global__ __launch_bounds__(256, sizeof(T) == 8 ? 2 : 1) void k_atr_prox(const 
   typename M::acc_t acc[4][NT];
   const int64_t bid = (int64_t)blockIdx.x - (pub.host ? 1 : 0);
   const int64_t panel = SPLIT ? bid / S : bid, split = SPLIT ? bid % S : 0;
-  const int64_t col0 = atr_panel<T, NT, PF, 0, NTL>(A, R, m, n, SPLIT ? S : 1, acc, panel, split);
+  const int64_t col0 = atr_panel<T, NT, PF, 0, NTL>(A, R, m, n, SPLIT ? S : 1, acc, panel, split, keep_mib);
   double accr[6] = {0.0, 0.0, 0.0, -__builtin_inf(), 0.0, 0.0};
   int slot = work_slot(pub);
   if constexpr (SPLIT) {   // a separate instantiation: the S = 1 kernel keeps 2 blocks per CU
@@ -342,7 +337,8 @@ __global__ __launch_bounds__(256, sizeof(T) == 8 ? 2 : 1) void k_atr_fista(const
                                                    double thres_, double theta_, double a1_,
                                                    double b1_, Red red, Pub pub, int S,
                                                    T* __restrict__ Gp, unsigned* __restrict__ pcnt,
-                                                   T* __restrict__ ec, unsigned* __restrict__ zf) {
+                                                   T* __restrict__ ec, unsigned* __restrict__ zf,
+                                                   int keep_mib) {
   if (red_skipped(red)) {   // cancelled by a device-side decision (as k_atr_prox)
     if (pub.host != nullptr && blockIdx.x == 0 && threadIdx.x == 0)
       publish_packet(pub.s, pub.ns, pub.host, pub.host_seq, pub.seq);
@@ -358,7 +354,7 @@ __global__ __launch_bounds__(256, sizeof(T) == 8 ? 2 : 1) void k_atr_fista(const
   typename M::acc_t acc[4][NT];
   const int64_t bid = (int64_t)blockIdx.x - (pub.host ? 1 : 0);
   const int64_t panel = SPLIT ? bid / S : bid, split = SPLIT ? bid % S : 0;
-  const int64_t col0 = atr_panel<T, NT, PF, 0, NTL>(A, R, m, n, SPLIT ? S : 1, acc, panel, split);
+  const int64_t col0 = atr_panel<T, NT, PF, 0, NTL>(A, R, m, n, SPLIT ? S : 1, acc, panel, split, keep_mib);
   double accr[4] = {0.0, 0.0, 0.0, -__builtin_inf()};
   int slot = work_slot(pub);
   if constexpr (SPLIT) {   // fixed reduction slots, see atr_split_combine
@@ -477,7 +473,8 @@ template <typename T, int NT, int PF, int WL, bool NTL>
 static void atr_mfma_go(const GemmPlan& p, const T* A, const T* R, T* Gp, hipStream_t st) {
   const dim3 grid((unsigned)(p.n / (WL ? 256 : 64)), (unsigned)p.atr_S);
   static const size_t pad = lds_pad(k_atr_mfma<T, NT, PF, WL, NTL>, "GLX_ATR_LDS_PAD");
-  glx_launch((k_atr_mfma<T, NT, PF, WL, NTL>), grid, dim3(256), pad, st, A, R, Gp, p.m, p.n, p.atr_S);
+  glx_launch((k_atr_mfma<T, NT, PF, WL, NTL>), grid, dim3(256), pad, st, A, R, Gp, p.m, p.n, p.atr_S,
+             p.atr_keep_mib);
 }
 
 template <typename T, int NT>
@@ -527,12 +524,12 @@ static void atr_prox_go(const GemmPlan& p, const T* A, const T* R, T* G, const T
   const dim3 grid((unsigned)(p.n / 64 * p.atr_S + (pub.host ? 1 : 0)));
   if (p.atr_S > 1) {
     glx_launch((k_atr_prox<T, NT, PF, NTL, true>), grid, dim3(256), 0, st, A, R, G, p.m,
-                       p.n, x, pp, pthr, z, t, t * mu, thres, red, pub, p.atr_S, Gp, pcnt, zf);
+                       p.n, x, pp, pthr, z, t, t * mu, thres, red, pub, p.atr_S, Gp, pcnt, zf, p.atr_keep_mib);
     return;
   }
   static const size_t pad = lds_pad(k_atr_prox<T, NT, PF, NTL, false>, "GLX_ATR_LDS_PAD");
   glx_launch((k_atr_prox<T, NT, PF, NTL, false>), grid, dim3(256), pad, st, A, R, G, p.m,
-                     p.n, x, pp, pthr, z, t, t * mu, thres, red, pub, 1, Gp, pcnt, zf);
+                     p.n, x, pp, pthr, z, t, t * mu, thres, red, pub, 1, Gp, pcnt, zf, p.atr_keep_mib);
 }
 template <typename T, int NT>
 static void atr_prox_nt(const GemmPlan& p, const T* A, const T* R, T* G, const T* x, T* pp,
@@ -565,13 +562,13 @@ static void atr_fista_go(const GemmPlan& p, const T* A, const T* R, T* G, const 
   if (p.atr_S > 1) {
     glx_launch((k_atr_fista<T, NT, PF, NTL, true>), grid, dim3(256), 0, st, A, R, G, p.m,
                        p.n, y, xk, xc, vn, yn, t, t * mu, thres, theta, 1.0 - theta_next,
-                       theta_next, red, pub, p.atr_S, Gp, pcnt, ec, zf);
+                       theta_next, red, pub, p.atr_S, Gp, pcnt, ec, zf, p.atr_keep_mib);
     return;
   }
   static const size_t pad = lds_pad(k_atr_fista<T, NT, PF, NTL, false>, "GLX_ATR_LDS_PAD");
   glx_launch((k_atr_fista<T, NT, PF, NTL, false>), grid, dim3(256), pad, st, A, R, G, p.m,
                      p.n, y, xk, xc, vn, yn, t, t * mu, thres, theta, 1.0 - theta_next, theta_next,
-                     red, pub, 1, Gp, pcnt, ec, zf);
+                     red, pub, 1, Gp, pcnt, ec, zf, p.atr_keep_mib);
 }
 template <typename T, int NT>
 static void atr_fista_nt(const GemmPlan& p, const T* A, const T* R, T* G, const T* y, const T* xk,

@@ -50,16 +50,10 @@ constexpr int dma_lds_bytes() {
          ((NSRC * KC * 16 * NT * 8 / 1024) % WAVES ? 1024 : 0);
 }
 
-// Infinity-Cache hand-off (tuning experiment, GLX_AX_KEEP_MIB, default 0 = off): with NTL, the
-// last chunks of every block's walk are fetched with the default policy instead, about that many
-// MiB of A over the grid, so they stay in the 256 MiB Infinity Cache for the next pass (A^T R).
-__device__ int g_ax_keep_mib = 0;
-void set_ax_keep_mib(int mib, hipStream_t st) {
-  static int cur = -1;
-  if (mib == cur) return;
-  (void)hipMemcpyToSymbolAsync(HIP_SYMBOL(g_ax_keep_mib), &mib, sizeof(int), 0, hipMemcpyHostToDevice, st);
-  cur = mib;
-}
+// Infinity-Cache hand-off (GemmPlan::ax_keep_mib, a kernel argument; the solver's default is
+// kKeepMiB = 192, GLX_AX_KEEP_MIB overrides it, 0 = off): with NTL, the last chunks of every
+// block's walk are fetched with the default policy instead, about that many MiB of A over the
+// grid, so they stay in the 256 MiB Infinity Cache for the next pass (A^T R).
 
 template <int KC>
 __device__ inline int dma_sw(int i) { return KC >= 32 ? (i & 15) : ((i >> 1) & 7); }
@@ -73,7 +67,7 @@ __global__ __launch_bounds__(64 * WAVES) void k_ax_dma(const T* __restrict__ A,
                                                       T* __restrict__ P, int64_t m, int64_t n,
                                                       int64_t chunks, int S, int gx, int xmap,
                                                       const int* __restrict__ gate, int epoch,
-                                                      Pub pub) {
+                                                      Pub pub, int keep_mib) {
   static_assert(sizeof(T) == 8, "f64 tile");
   typedef MF<T> M;
   typedef typename M::acc_t C;
@@ -150,7 +144,7 @@ __global__ __launch_bounds__(64 * WAVES) void k_ax_dma(const T* __restrict__ A,
   const int64_t rot = ax_rot(xmap, bx, gx, nch);
   int64_t kt = nch;   // walk chunks [kt, nch) load with the default policy (the hand-off)
   if constexpr (NTL) {
-    const int64_t kb = (int64_t)g_ax_keep_mib << 20;
+    const int64_t kb = (int64_t)keep_mib << 20;
     if (kb > 0) kt = nch - kb / ((int64_t)gridDim.x * WAVES * AW);
   }
   auto issue = [&](int64_t c, int slot) {
@@ -371,7 +365,8 @@ static void ax_dma_go(const GemmPlan& p, int S, const T* A, const T* const* X, T
     const int xmap = ax_xmap_flags(p, S);
     const dim3 grid((unsigned)ax_grid(xmap, gx, S) + (pub.host ? 1u : 0u));
     glx_launch((k_ax_dma<T, NT, NSRC, NS, KC, WAVES, NTL, HOIST, PIPE, MT>), grid, dim3(64 * WAVES), 0, st,
-                       A, X[0], X[1], X[2], P, p.m, p.n, p.n / KC, S, gx, xmap, gate, epoch, pub);
+                       A, X[0], X[1], X[2], P, p.m, p.n, p.n / KC, S, gx, xmap, gate, epoch, pub,
+                       p.ax_keep_mib);
   }
 }
 

@@ -211,7 +211,7 @@ class Session : public SessionBase {
     for (int i = 0; i < kRes; ++i) res[i] = static_cast<T*>(c.take(sizeof(T) * ml));
     // gradient sets (G, its split-K slabs): the current one and the speculative one (a ring with
     // a communicator and device control, gsets_for)
-    const int ngs = gsets_for(P, O);
+    const int ngs = gsets_for(P, O, plan);
     T* g[kMaxGSets];
     T* gp[kMaxGSets];
     for (int k = 0; k < ngs; ++k) {
@@ -281,8 +281,30 @@ class Session : public SessionBase {
     return P.comm != nullptr && (P.method == GLX_PROXGD || P.method == GLX_FPROXGD) && P.dtype == GLX_F64 &&
            O.step_type == GLX_STEP_LINE_SEARCH && O.ls_maxit > 0 && O.exact_objective == 0;
   }
-  static int gsets_for(const glx_problem& P, const glx_opts& O) {
-    const int w = dc_window_opt(P, O);
+  static bool env_is(const char* name, const char* v) {
+    const char* e = std::getenv(name);
+    return e && std::strcmp(e, v) == 0;
+  }
+  // the device-control window that takes effect for this plan: the requested one
+  // (dc_window_opt) where the fused speculative path, the spinning readback and, with a
+  // communicator, the attached packet are all on; else 0 (the host decides)
+  static int dc_window_eff(const glx_problem& P, const glx_opts& O, const GemmPlan& plan) {
+    const bool ls = O.step_type == GLX_STEP_LINE_SEARCH && O.ls_maxit > 0;
+    const bool spin = !env_is("GLX_READBACK", "sync");
+    const bool attach = spin && !env_is("GLX_ATTACH_PUB", "0");
+    const bool fuse_any = (P.comm != nullptr || atr_prox_ok(plan)) &&
+                          (O.step_type == GLX_STEP_LINE_SEARCH || O.step_type == GLX_STEP_FIXED) &&
+                          !env_is("GLX_FUSED_TRIAL", "0");
+    const bool method = P.method == GLX_PROXGD || P.method == GLX_FPROXGD;
+    if (!(fuse_any && method && spin && O.exact_objective == 0 && ls &&
+          (P.comm == nullptr || (dc_comm_ok(P, O) && attach))))
+      return 0;
+    return dc_window_opt(P, O);
+  }
+  // a ring of window + 2 gradient sets only where device control with a communicator actually
+  // runs (it was sized on the request, not on the window that takes effect)
+  static int gsets_for(const glx_problem& P, const glx_opts& O, const GemmPlan& plan) {
+    const int w = dc_window_eff(P, O, plan);
     return (w > 0 && dc_comm_ok(P, O)) ? w + 2 : 2;
   }
 
@@ -297,6 +319,16 @@ class Session : public SessionBase {
     m_ = P.m; n_ = P.n; l_ = P.l;
     nl_ = n_ * l_; ml_ = m_ * l_;
     plan_ = session_plan(P, O);
+    {   // Infinity-Cache hand-off between the two non-temporal passes: the last ~192 MiB each
+        // pass reads stay in the 256 MiB Infinity Cache for the other pass. NS, same box, two
+        // interleaved rounds: 2307 / 2318 it/s against 2252 / 2272 with both off, either alone
+        // in between (profiles/r3_keep/). GLX_AX_KEEP_MIB / GLX_ATR_KEEP_MIB = 0: off. Kernel
+        // arguments through the plan, so every session and device has its own value.
+      const char* ka = std::getenv("GLX_AX_KEEP_MIB");
+      const char* kr = std::getenv("GLX_ATR_KEEP_MIB");
+      plan_.ax_keep_mib = std::max(0, ka ? std::atoi(ka) : kKeepMiB);
+      plan_.atr_keep_mib = std::max(0, kr ? std::atoi(kr) : kKeepMiB);
+    }
     comm_ = static_cast<glx_comm*>(P.comm);
     fh_cap_ = fh_capacity(P, O);
     smode_ = split_mode(P, O);
@@ -347,25 +379,14 @@ class Session : public SessionBase {
     // device-controlled batches (dc_run / fista_dc_run): ProxGD / FProxGD with line search on
     // the fused speculative path; GLX_DC_BATCH = iterations in flight (0: the host decides every
     // iteration). With a communicator fp64 only (the trial sums ride the gradient all-reduce).
-    dc_window_ = dc_window_opt(P, O);
-    if (!((fused_ok_ || fused_fista_ok_) && spin_readback_ && O.exact_objective == 0 &&
-          O.step_type == GLX_STEP_LINE_SEARCH && O.ls_maxit > 0 &&
-          (comm_ == nullptr || (dc_comm_ok(P, O) && attach_ok_))))
-      dc_window_ = 0;
+    dc_window_ = dc_window_eff(P, O, plan_);
+    if (dc_window_ > 0 && !((fused_ok_ || fused_fista_ok_) && spin_readback_ && (comm_ == nullptr || attach_ok_)))
+      throw Error{GLX_E_STATE, "device-control window and the session's fused path disagree"};
     if (dc_window_ > 0) {
       GLX_HIP(hipHostMalloc(reinterpret_cast<void**>(&dc_ring_), sizeof(double) * kCtlRec * kCtlMaxBatch,
                             hipHostMallocMapped | hipHostMallocCoherent));
       std::memset(dc_ring_, 0, sizeof(double) * kCtlRec * kCtlMaxBatch);   // tags start at 1
       GLX_HIP(hipHostGetDevicePointer(reinterpret_cast<void**>(&dc_ring_dev_), dc_ring_, 0));
-    }
-    {   // Infinity-Cache hand-off between the two non-temporal passes: the last ~192 MiB each
-        // pass reads stay in the 256 MiB Infinity Cache for the other pass. NS, same box, two
-        // interleaved rounds: 2307 / 2318 it/s against 2252 / 2272 with both off, either alone
-        // in between (profiles/r3_keep/). GLX_AX_KEEP_MIB / GLX_ATR_KEEP_MIB = 0: off.
-      const char* ka = std::getenv("GLX_AX_KEEP_MIB");
-      const char* kr = std::getenv("GLX_ATR_KEEP_MIB");
-      set_ax_keep_mib(ka ? std::atoi(ka) : kKeepMiB, st_);
-      set_atr_keep_mib(kr ? std::atoi(kr) : kKeepMiB, st_);
     }
     GLX_HIP(hipMemsetAsync(ticket_, 0, kTicketBytes, st_));
     GLX_HIP(hipMemsetAsync(pcnt_, 0, sizeof(unsigned) * (P.n / 64 + 64), st_));
@@ -389,7 +410,7 @@ class Session : public SessionBase {
     if (dc_ring_) (void)hipHostFree(dc_ring_);
     if (rb_event_) (void)hipEventDestroy(rb_event_);
     for (auto& v : ev_)
-      for (auto& p : v) { (void)hipEventDestroy(p.first); (void)hipEventDestroy(p.second); }
+      for (auto& p : v) { (void)hipEventDestroy(p.a); (void)hipEventDestroy(p.b); }
     for (hipEvent_t e : ev_pool_) (void)hipEventDestroy(e);
     // a timing slot this session opened whose launch threw: never hand its events to a later
     // launch on this thread
@@ -500,13 +521,13 @@ class Session : public SessionBase {
       throw Error{GLX_E_INVALID, "kind must be 0 (A@x), 1 (A^T r) or 2 (split-candidate A e gather)"};
     auto& v = ev_[kind];
     double total = 0.0;
-    if (!v.empty()) GLX_HIP(hipEventSynchronize(v.back().second));
+    if (!v.empty()) GLX_HIP(hipEventSynchronize(v.back().b));
     for (auto& p : v) {
       float t = 0.f;
-      GLX_HIP(hipEventElapsedTime(&t, p.first, p.second));
+      GLX_HIP(hipEventElapsedTime(&t, p.a, p.b));
       total += t;
-      ev_pool_.push_back(p.first);
-      ev_pool_.push_back(p.second);
+      ev_pool_.push_back(p.a);
+      ev_pool_.push_back(p.b);
     }
     if (launches) *launches = (int64_t)v.size();
     if (ms) *ms = total;
@@ -529,19 +550,38 @@ class Session : public SessionBase {
   // k > 0 times every k-th launch of each kind. The events ride on the kernel itself
   // (hipExtLaunchKernel through glx_launch, see LaunchTiming): the next glx_launch takes them, so
   // the pair brackets exactly that kernel and adds nothing to the queue.
+  // Launches queued inside a device-controlled batch carry the batch segment's tag; when a
+  // decision cancels segments, their samples are dropped (prof_drop_from): a cancelled launch
+  // exits at once and would report a near-zero kernel time.
   hipEvent_t prof_begin(int kind) {
     if (O_.profile <= 0 || (prof_n_[kind]++ % O_.profile) != 0) return nullptr;
     hipEvent_t e0 = get_event();
     prof_stop_ = get_event();
+    prof_tag_ = dc_gate_ != nullptr ? dc_tag_ : 0;
     g_launch_timing = LaunchTiming{e0, prof_stop_};
     return e0;
+  }
+  // drop the samples of batch segments tagged >= tag (those a device-side decision cancelled)
+  void prof_drop_from(int64_t tag) {
+    for (auto& v : ev_) {
+      size_t keep = 0;
+      for (size_t i = 0; i < v.size(); ++i) {
+        if (v[i].tag != 0 && v[i].tag >= tag) {
+          ev_pool_.push_back(v[i].a);
+          ev_pool_.push_back(v[i].b);
+        } else {
+          v[keep++] = v[i];
+        }
+      }
+      v.resize(keep);
+    }
   }
   void prof_end(int kind, hipEvent_t e0) {
     if (e0 == nullptr) return;
     const LaunchTiming lt = g_launch_timing;
     g_launch_timing = LaunchTiming{};
     if (lt.start == nullptr) {   // taken by the launch: keep the sample
-      ev_[kind].push_back({e0, prof_stop_});
+      ev_[kind].push_back({e0, prof_stop_, prof_tag_});
     } else {                     // the launch path had no timed kernel: no sample
       ev_pool_.push_back(lt.start);
       ev_pool_.push_back(lt.stop);
@@ -549,6 +589,7 @@ class Session : public SessionBase {
   }
 
   hipEvent_t prof_stop_ = nullptr;   // the stop event of the open prof_begin
+  int64_t prof_tag_ = 0;             // its batch segment (0: not in a device-controlled batch)
   hipEvent_t get_event() {
     if (ev_pool_.empty()) {   // grow in batches: never create events inside a timed loop's steady state
       for (int i = 0; i < 256; ++i) {
@@ -1143,7 +1184,19 @@ class Session : public SessionBase {
         const bool stop = stop_rule();
         if (stop != (prev == 1))
           throw Error{GLX_E_STATE, "device-controlled batch: stop rule differs from the host's"};
-        if (stop) { end_phase(true); return; }
+        if (stop) {
+          // With a communicator the stopping decision cancelled the next trial (its gated
+          // k_prox_pgd and everything behind it), which proxgd_spec_rotate declared ready: keep
+          // its gradient set (the all-reduce in front of the decision completed) but never its
+          // trial, even where the next phase's mu equals this one's (mu0 = 0).
+          if (comm_) {
+            spec_trial_mu_ = NAN;
+            ax_queued_ = false;
+          }
+          prof_drop_from(tag0 + d + 1);   // the segments behind the stopping decision
+          end_phase(true);
+          return;
+        }
       }
       const double* rec = dc_wait(tag0 + 1 + d);
       ++record_waits_;
@@ -1161,6 +1214,7 @@ class Session : public SessionBase {
         throw Error{GLX_E_STATE, "device-controlled batch: Armijo decision differs from the host's"};
       stats_[7] += 1;
       if (!acc) {   // everything queued behind this decision was cancelled on the device
+        prof_drop_from(tag0 + 1 + d);
         spec_on_ = false;
         ax_queued_ = false;
         proxgd_trials({G_, 1}, true, t * O_.ls_coeff, 1);
@@ -1484,7 +1538,11 @@ class Session : public SessionBase {
         const bool stop = stop_rule();
         if (stop != (prev == 1))
           throw Error{GLX_E_STATE, "device-controlled batch: stop rule differs from the host's"};
-        if (stop) { end_phase(true); return; }
+        if (stop) {
+          prof_drop_from(tag0 + d + 1);   // the segments behind the stopping decision
+          end_phase(true);
+          return;
+        }
       }
       const double* rec = dc_wait(tag0 + 1 + d);
       ++record_waits_;
@@ -1501,6 +1559,7 @@ class Session : public SessionBase {
         throw Error{GLX_E_STATE, "device-controlled batch: backtracking decision differs from the host's"};
       stats_[7] += 1;
       if (!acc) {   // everything behind this decision was cancelled on the device
+        prof_drop_from(tag0 + 1 + d);
         spec_on_ = false;
         fista_trials({G_, 1}, true, t * O_.ls_coeff, 1, theta, theta_next, false);
         return;
@@ -1511,7 +1570,10 @@ class Session : public SessionBase {
         throw Error{GLX_E_STATE, "device-controlled batch: nnz budget decision differs from the host's"};
       fista_update(true, true, t, split, theta_next, (iry_ + 2) % kRes, 2);
       prev = code;
-      if (code == 3) return;   // the batch behind was cancelled; dense batches follow
+      if (code == 3) {   // the batch behind was cancelled; dense batches follow
+        prof_drop_from(tag0 + 2 + d);
+        return;
+      }
     }
   }
 
@@ -1747,7 +1809,8 @@ class Session : public SessionBase {
   // later iterations queued (device-controlled batches)
   int64_t ax_calls_ = 0, ax_cols_ = 0, atr_calls_ = 0, syncs_ = 0, record_waits_ = 0;
   double stats_[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-  std::vector<std::pair<hipEvent_t, hipEvent_t>> ev_[3];
+  struct EvSample { hipEvent_t a, b; int64_t tag; };
+  std::vector<EvSample> ev_[3];
   int64_t prof_n_[3] = {0, 0, 0};
   std::vector<hipEvent_t> ev_pool_;
 };

@@ -31,6 +31,7 @@ def main():
     ap.add_argument("--slices", type=int, default=0)
     ap.add_argument("--out", required=True)
     ap.add_argument("--method", default="gl_ProxGD_primal")
+    ap.add_argument("--mu", type=float, default=None, help="mu0 (default: gen_data's)")
     a = ap.parse_args()
 
     import glx
@@ -45,6 +46,8 @@ def main():
         os.environ[k] = v
     m, n, l = (int(v) for v in a.shape.split(","))
     A, b, u, x0, mu = numpy_ref.gen_data(m, n, l, 2024)
+    if a.mu is not None:
+        mu = a.mu
     dt = np.float64 if a.dtype == "f64" else np.float32
     r0, r1 = shard_rows(m, world, rank)
     opts = {"alpha0": a.alpha_scale * numpy_ref.step_size_for(m, n)}
