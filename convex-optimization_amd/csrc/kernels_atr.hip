@@ -16,7 +16,9 @@ namespace glx {
 // A^T R on MFMA: a wave owns 64 columns of A (= 64 rows of G) x NT 16-col tiles of G.
 //   WL = 0: a block = one 64-column panel, its 4 waves split the block's rows (LDS-reduced);
 //   WL = 1: a block = four adjacent panels (256 columns) sharing one row range, so the four
-//           waves read the same R fragments (L1 hits) and write their slabs directly.
+//           waves read the same R fragments (L1 hits) and write their slabs directly;
+//   WL = 2: as WL 0 with eight waves (512 threads, two waves per SIMD): the block's rows split
+//           eight ways, waves 4..7 folded into 0..3 through LDS first (round 4).
 // blockIdx.y = row split. Needs n % 64 == 0 (n % 256 for WL = 1), m % 4 == 0.
 // Gp[split][n][16*NT].
 // ------------------------------------------------------------------------------------------
@@ -65,15 +67,17 @@ __device__ inline int64_t atr_panel(const T* __restrict__ A, const T* __restrict
   typedef MF<T> M;
   typedef typename M::acc_t C;
   constexpr int L = 16 * NT;
-  __shared__ C red[WL == 0 ? 4 : 1][WL == 0 ? 4 * NT : 1][64];   // [wave][e * NT + nt][lane]
+  constexpr bool RW = WL != 1;   // the block's waves split the rows of one panel
+  constexpr int NWV = WL == 2 ? 8 : 4;
+  __shared__ C red[RW ? 4 : 1][RW ? 4 * NT : 1][64];   // [wave][e * NT + nt][lane]
 
   const int lane = threadIdx.x & 63;
   const int wave = threadIdx.x >> 6;
   const int i = lane & 15, q = lane >> 4;
-  const int64_t col0 = WL == 0 ? pbx * 64 : pbx * 256 + wave * 64;
+  const int64_t col0 = RW ? pbx * 64 : pbx * 256 + wave * 64;
   const int64_t steps = m / 4;
-  const int64_t W = WL == 0 ? (int64_t)S * 4 : (int64_t)S;
-  const int64_t w = WL == 0 ? pby * 4 + wave : pby;
+  const int64_t W = RW ? (int64_t)S * NWV : (int64_t)S;
+  const int64_t w = RW ? pby * NWV + wave : pby;
   const int64_t sb = steps * w / W, se = steps * (w + 1) / W;
 
   const T* ap = A + (sb * 4 + q) * n + col0 + atr_col<T>(i, 0);
@@ -107,7 +111,7 @@ __device__ inline int64_t atr_panel(const T* __restrict__ A, const T* __restrict
   int64_t keep = 0;
   if constexpr (NTL) {
     const int64_t kb = (int64_t)keep_mib << 20;
-    keep = kb / ((int64_t)(WL == 0 ? W * (n / 64) : W * (n / 256)) * 4 * (WL == 0 ? 64 : 256) * (int64_t)sizeof(T));
+    keep = kb / ((int64_t)(RW ? W * (n / 64) : W * (n / 256)) * 4 * (RW ? 64 : 256) * (int64_t)sizeof(T));
   }
   const int64_t kt = nst - keep;
   auto mma_step = [&](int p) {
@@ -119,15 +123,22 @@ __device__ inline int64_t atr_panel(const T* __restrict__ A, const T* __restrict
   if (nst > 0) {
 #pragma unroll
     for (int p = 0; p < PF; ++p) ld(p, p);
-    int64_t s0 = 0;
-    for (; s0 + PF <= nst && (keep == 0 || s0 + 2 * PF <= kt); s0 += PF) {
+    // Trip bounds as wave-uniform 32-bit scalars (readfirstlane): round 3's fused condition
+    // `s0 + PF <= nst && (keep == 0 || s0 + 2 PF <= kt)` compiled into an exec-masked loop with
+    // an s_nop per MFMA group, and k_atr_prox ran 180 us against round 2's 168 us on one box
+    // (profiles/r4_diag/). Loop 1 runs while s0 + PF <= min(nst, kt - PF).
+    const int nsti = __builtin_amdgcn_readfirstlane((int)nst);
+    const int lim1 = __builtin_amdgcn_readfirstlane(
+        keep == 0 ? (int)nst : (int)(kt - PF < nst ? kt - PF : nst));
+    int s0 = 0;
+    for (; s0 + PF <= lim1; s0 += PF) {
 #pragma unroll
       for (int p = 0; p < PF; ++p) {
         mma_step(p);
         ld(p, s0 + p + PF);
       }
     }
-    for (; s0 + PF <= nst; s0 += PF) {   // the kept tail (only with keep > 0)
+    for (; s0 + PF <= nsti; s0 += PF) {   // the kept tail (only with keep > 0)
 #pragma unroll
       for (int p = 0; p < PF; ++p) {
         mma_step(p);
@@ -139,20 +150,40 @@ __device__ inline int64_t atr_panel(const T* __restrict__ A, const T* __restrict
       if (s0 + p < nst) mma_step(p);
   }
 
-  if (WL == 0) {
-#pragma unroll
-    for (int e = 0; e < 4; ++e)
-#pragma unroll
-      for (int nt = 0; nt < NT; ++nt) red[wave][e * NT + nt][lane] = acc[e][nt];
-    __syncthreads();
-#pragma unroll
-    for (int nt = 0; nt < NT; ++nt) {
-      C v = red[0][wave * NT + nt][lane];
-#pragma unroll
-      for (int s = 1; s < 4; ++s) v += red[s][wave * NT + nt][lane];
+  if constexpr (WL == 2) {   // waves 4..7 into 0..3: acc(w) + acc(w + 4)
+    if (wave >= 4) {
 #pragma unroll
       for (int e = 0; e < 4; ++e)
-        if (e == wave) acc[e][nt] = v;   // static register index; e == wave selects one
+#pragma unroll
+        for (int nt = 0; nt < NT; ++nt) red[wave - 4][e * NT + nt][lane] = acc[e][nt];
+    }
+    __syncthreads();
+    if (wave < 4) {
+#pragma unroll
+      for (int e = 0; e < 4; ++e)
+#pragma unroll
+        for (int nt = 0; nt < NT; ++nt) acc[e][nt] += red[wave][e * NT + nt][lane];
+    }
+    __syncthreads();
+  }
+  if (RW) {
+    if (wave < 4) {
+#pragma unroll
+      for (int e = 0; e < 4; ++e)
+#pragma unroll
+        for (int nt = 0; nt < NT; ++nt) red[wave][e * NT + nt][lane] = acc[e][nt];
+    }
+    __syncthreads();
+    if (wave < 4) {   // (WL 2: waves 4..7 hold no rows from here on)
+#pragma unroll
+      for (int nt = 0; nt < NT; ++nt) {
+        C v = red[0][wave * NT + nt][lane];
+#pragma unroll
+        for (int s = 1; s < 4; ++s) v += red[s][wave * NT + nt][lane];
+#pragma unroll
+        for (int e = 0; e < 4; ++e)
+          if (e == wave) acc[e][nt] = v;   // static register index; e == wave selects one
+      }
     }
   }
   return col0;
@@ -225,7 +256,7 @@ __device__ inline bool atr_split_combine(typename MF<T>::acc_t (&acc)[4][NT], T*
 }
 
 template <typename T, int NT, int PF, int WL, bool NTL>
-__global__ __launch_bounds__(256) void k_atr_mfma(const T* __restrict__ A, const T* __restrict__ R,
+__global__ __launch_bounds__(WL == 2 ? 512 : 256) void k_atr_mfma(const T* __restrict__ A, const T* __restrict__ R,
                                                   T* __restrict__ Gp, int64_t m, int64_t n, int S,
                                                   int keep_mib) {
   typedef MF<T> M;
@@ -238,7 +269,7 @@ __global__ __launch_bounds__(256) void k_atr_mfma(const T* __restrict__ A, const
   T* gout = Gp + (int64_t)blockIdx.y * n * L;
 #pragma unroll
   for (int e = 0; e < 4; ++e) {
-    if (WL == 0 && e != wave) continue;   // WL 0: wave w owns the rows e == w
+    if (WL != 1 && e != wave) continue;   // WL 0 / 2: wave w < 4 owns the rows e == w
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       const int64_t grow = col0 + atr_col<T>(M::row(lane, r), e);
@@ -253,8 +284,8 @@ __global__ __launch_bounds__(256) void k_atr_mfma(const T* __restrict__ A, const
 // columns i and 16 + i of 4 rows, exactly the 16-lanes-per-row layout of k_prox_pgd — every
 // wave writes its rows of G and runs the trial on them (prox_pgd_row, the same arithmetic as
 // k_prox_pgd) with x = the thresholded iterate; the six trial sums are reduced over the grid.
-template <typename T, int NT, int PF, bool NTL, bool SPLIT>
-__global__ __launch_bounds__(256, sizeof(T) == 8 ? 2 : 1) void k_atr_prox(const T* __restrict__ A, const T* __restrict__ R,
+template <typename T, int NT, int PF, bool NTL, bool SPLIT, int WL>
+__global__ __launch_bounds__(WL == 2 ? 512 : 256, (WL == 0 && sizeof(T) == 8) ? 2 : 1) void k_atr_prox(const T* __restrict__ A, const T* __restrict__ R,
                                                   T* __restrict__ G, int64_t m, int64_t n,
                                                   const T* __restrict__ x, T* __restrict__ p,
                                                   T* __restrict__ pthr, T* __restrict__ z,
@@ -274,7 +305,8 @@ __global__ __launch_bounds__(256, sizeof(T) == 8 ? 2 : 1) void k_atr_prox(const 
   // the extra workgroup (n / 64 * S + 1 in all); with K splits only the panel owners and the
   // publisher reduce (nparts)
   const int nparts = SPLIT ? (int)(n / 64) + (pub.host ? 1 : 0) : -1;
-  if (publisher_first<6, 0x8u>(pub, red, nparts)) return;
+  constexpr int NW = WL == 2 ? 8 : 4;
+  if (publisher_first<6, 0x8u, NW>(pub, red, nparts)) return;
   typedef MF<T> M;
   constexpr int L = 16 * NT;
   const int lane = threadIdx.x & 63;
@@ -283,7 +315,7 @@ __global__ __launch_bounds__(256, sizeof(T) == 8 ? 2 : 1) void k_atr_prox(const 
   typename M::acc_t acc[4][NT];
   const int64_t bid = (int64_t)blockIdx.x - (pub.host ? 1 : 0);
   const int64_t panel = SPLIT ? bid / S : bid, split = SPLIT ? bid % S : 0;
-  const int64_t col0 = atr_panel<T, NT, PF, 0, NTL>(A, R, m, n, SPLIT ? S : 1, acc, panel, split, keep_mib);
+  const int64_t col0 = atr_panel<T, NT, PF, WL, NTL>(A, R, m, n, SPLIT ? S : 1, acc, panel, split, keep_mib);
   double accr[6] = {0.0, 0.0, 0.0, -__builtin_inf(), 0.0, 0.0};
   int slot = work_slot(pub);
   if constexpr (SPLIT) {   // a separate instantiation: the S = 1 kernel keeps 2 blocks per CU
@@ -322,14 +354,14 @@ __global__ __launch_bounds__(256, sizeof(T) == 8 ? 2 : 1) void k_atr_prox(const 
       }
     }
   }
-  grid_reduce<6, 0x8u>(accr, red, slot, nparts);
+  grid_reduce<6, 0x8u, NW>(accr, red, slot, nparts);
 }
 
 // FISTA's backtracking trial fused into A^T R the same way (WL 0, one K split): each wave runs
 // fista_row (the arithmetic of k_fista_trial) on its 16 gradient rows, with y the extrapolated
 // point and xk the current iterate; writes G, xc, v_next, y_next and reduces the four sums.
-template <typename T, int NT, int PF, bool NTL, bool SPLIT>
-__global__ __launch_bounds__(256, sizeof(T) == 8 ? 2 : 1) void k_atr_fista(const T* __restrict__ A, const T* __restrict__ R,
+template <typename T, int NT, int PF, bool NTL, bool SPLIT, int WL>
+__global__ __launch_bounds__(WL == 2 ? 512 : 256, (WL == 0 && sizeof(T) == 8) ? 2 : 1) void k_atr_fista(const T* __restrict__ A, const T* __restrict__ R,
                                                    T* __restrict__ G, int64_t m, int64_t n,
                                                    const T* __restrict__ y, const T* __restrict__ xk,
                                                    T* __restrict__ xc, T* __restrict__ vnext,
@@ -345,7 +377,8 @@ __global__ __launch_bounds__(256, sizeof(T) == 8 ? 2 : 1) void k_atr_fista(const
     return;
   }
   const int nparts = SPLIT ? (int)(n / 64) + (pub.host ? 1 : 0) : -1;   // see k_atr_prox
-  if (publisher_first<4, 0x8u>(pub, red, nparts)) return;
+  constexpr int NW = WL == 2 ? 8 : 4;
+  if (publisher_first<4, 0x8u, NW>(pub, red, nparts)) return;
   typedef MF<T> M;
   constexpr int L = 16 * NT;
   const int lane = threadIdx.x & 63;
@@ -354,7 +387,7 @@ __global__ __launch_bounds__(256, sizeof(T) == 8 ? 2 : 1) void k_atr_fista(const
   typename M::acc_t acc[4][NT];
   const int64_t bid = (int64_t)blockIdx.x - (pub.host ? 1 : 0);
   const int64_t panel = SPLIT ? bid / S : bid, split = SPLIT ? bid % S : 0;
-  const int64_t col0 = atr_panel<T, NT, PF, 0, NTL>(A, R, m, n, SPLIT ? S : 1, acc, panel, split, keep_mib);
+  const int64_t col0 = atr_panel<T, NT, PF, WL, NTL>(A, R, m, n, SPLIT ? S : 1, acc, panel, split, keep_mib);
   double accr[4] = {0.0, 0.0, 0.0, -__builtin_inf()};
   int slot = work_slot(pub);
   if constexpr (SPLIT) {   // fixed reduction slots, see atr_split_combine
@@ -398,7 +431,7 @@ __global__ __launch_bounds__(256, sizeof(T) == 8 ? 2 : 1) void k_atr_fista(const
       }
     }
   }
-  grid_reduce<4, 0x8u>(accr, red, slot, nparts);
+  grid_reduce<4, 0x8u, NW>(accr, red, slot, nparts);
 }
 
 // A^T R on VALU: a thread owns E consecutive columns of A over a row range; R[row][c0..c0+LB)
@@ -471,9 +504,9 @@ static void atr_valu_lb(const GemmPlan& p, const T* A, const T* R, T* Gp, hipStr
 
 template <typename T, int NT, int PF, int WL, bool NTL>
 static void atr_mfma_go(const GemmPlan& p, const T* A, const T* R, T* Gp, hipStream_t st) {
-  const dim3 grid((unsigned)(p.n / (WL ? 256 : 64)), (unsigned)p.atr_S);
+  const dim3 grid((unsigned)(p.n / (WL == 1 ? 256 : 64)), (unsigned)p.atr_S);
   static const size_t pad = lds_pad(k_atr_mfma<T, NT, PF, WL, NTL>, "GLX_ATR_LDS_PAD");
-  glx_launch((k_atr_mfma<T, NT, PF, WL, NTL>), grid, dim3(256), pad, st, A, R, Gp, p.m, p.n, p.atr_S,
+  glx_launch((k_atr_mfma<T, NT, PF, WL, NTL>), grid, dim3(WL == 2 ? 512 : 256), pad, st, A, R, Gp, p.m, p.n, p.atr_S,
              p.atr_keep_mib);
 }
 
@@ -490,6 +523,9 @@ static void atr_mfma_nt(const GemmPlan& p, const T* A, const T* R, T* Gp, hipStr
     case 106: atr_mfma_go<T, NT, 6, 0, true>(p, A, R, Gp, st); break;
     case 108: atr_mfma_go<T, NT, 8, 0, true>(p, A, R, Gp, st); break;
     case 114: atr_mfma_go<T, NT, 4, 1, true>(p, A, R, Gp, st); break;
+    case 28: atr_mfma_go<T, NT, 8, 2, false>(p, A, R, Gp, st); break;
+    case 124: atr_mfma_go<T, NT, 4, 2, true>(p, A, R, Gp, st); break;
+    case 128: atr_mfma_go<T, NT, 8, 2, true>(p, A, R, Gp, st); break;
     default: atr_mfma_go<T, NT, 2, 0, false>(p, A, R, Gp, st); break;
   }
 }
@@ -511,36 +547,40 @@ void launch_atr(const GemmPlan& p, const T* A, const T* R, T* Gp, hipStream_t st
 
 
 bool atr_prox_ok(const GemmPlan& p) {
-  return p.atr_kind == 1 && p.atr_wl == 0 && p.atr_S >= 1 && p.atr_S <= 8 &&
+  return p.atr_kind == 1 && (p.atr_wl == 0 || p.atr_wl == 2) && p.atr_S >= 1 && p.atr_S <= 8 &&
          (p.l == 16 || p.l == 32) && p.n % 64 == 0 &&
          p.n / 64 < kMaxBlocks &&   // reducing slots (one per panel) + the publisher
          (p.atr_S == 1 || env_int("GLX_ATR_FUSE_SPLIT", 1) != 0);
 }
 
-template <typename T, int NT, int PF, bool NTL>
+template <typename T, int NT, int PF, bool NTL, int WL>
 static void atr_prox_go(const GemmPlan& p, const T* A, const T* R, T* G, const T* x, T* pp,
                         T* pthr, T* z, double t, double mu, double thres, Red red, hipStream_t st,
                         Pub pub, T* Gp, unsigned* pcnt, unsigned* zf) {
   const dim3 grid((unsigned)(p.n / 64 * p.atr_S + (pub.host ? 1 : 0)));
+  const dim3 block(WL == 2 ? 512 : 256);
   if (p.atr_S > 1) {
-    glx_launch((k_atr_prox<T, NT, PF, NTL, true>), grid, dim3(256), 0, st, A, R, G, p.m,
+    glx_launch((k_atr_prox<T, NT, PF, NTL, true, WL>), grid, block, 0, st, A, R, G, p.m,
                        p.n, x, pp, pthr, z, t, t * mu, thres, red, pub, p.atr_S, Gp, pcnt, zf, p.atr_keep_mib);
     return;
   }
-  static const size_t pad = lds_pad(k_atr_prox<T, NT, PF, NTL, false>, "GLX_ATR_LDS_PAD");
-  glx_launch((k_atr_prox<T, NT, PF, NTL, false>), grid, dim3(256), pad, st, A, R, G, p.m,
+  static const size_t pad = lds_pad(k_atr_prox<T, NT, PF, NTL, false, WL>, "GLX_ATR_LDS_PAD");
+  glx_launch((k_atr_prox<T, NT, PF, NTL, false, WL>), grid, block, pad, st, A, R, G, p.m,
                      p.n, x, pp, pthr, z, t, t * mu, thres, red, pub, 1, Gp, pcnt, zf, p.atr_keep_mib);
 }
 template <typename T, int NT>
 static void atr_prox_nt(const GemmPlan& p, const T* A, const T* R, T* G, const T* x, T* pp,
                         T* pthr, T* z, double t, double mu, double thres, Red red, hipStream_t st,
                         Pub pub, T* Gp, unsigned* pcnt, unsigned* zf) {
-  switch (p.atr_ntl * 100 + p.atr_pf) {
-    case 4: atr_prox_go<T, NT, 4, false>(p, A, R, G, x, pp, pthr, z, t, mu, thres, red, st, pub, Gp, pcnt, zf); break;
-    case 6: atr_prox_go<T, NT, 6, false>(p, A, R, G, x, pp, pthr, z, t, mu, thres, red, st, pub, Gp, pcnt, zf); break;
-    case 104: atr_prox_go<T, NT, 4, true>(p, A, R, G, x, pp, pthr, z, t, mu, thres, red, st, pub, Gp, pcnt, zf); break;
-    case 108: atr_prox_go<T, NT, 8, true>(p, A, R, G, x, pp, pthr, z, t, mu, thres, red, st, pub, Gp, pcnt, zf); break;
-    default: atr_prox_go<T, NT, 8, false>(p, A, R, G, x, pp, pthr, z, t, mu, thres, red, st, pub, Gp, pcnt, zf); break;
+  switch (p.atr_ntl * 100 + p.atr_wl * 10 + p.atr_pf) {
+    case 4: atr_prox_go<T, NT, 4, false, 0>(p, A, R, G, x, pp, pthr, z, t, mu, thres, red, st, pub, Gp, pcnt, zf); break;
+    case 6: atr_prox_go<T, NT, 6, false, 0>(p, A, R, G, x, pp, pthr, z, t, mu, thres, red, st, pub, Gp, pcnt, zf); break;
+    case 104: atr_prox_go<T, NT, 4, true, 0>(p, A, R, G, x, pp, pthr, z, t, mu, thres, red, st, pub, Gp, pcnt, zf); break;
+    case 108: atr_prox_go<T, NT, 8, true, 0>(p, A, R, G, x, pp, pthr, z, t, mu, thres, red, st, pub, Gp, pcnt, zf); break;
+    case 124: atr_prox_go<T, NT, 4, true, 2>(p, A, R, G, x, pp, pthr, z, t, mu, thres, red, st, pub, Gp, pcnt, zf); break;
+    case 128: atr_prox_go<T, NT, 8, true, 2>(p, A, R, G, x, pp, pthr, z, t, mu, thres, red, st, pub, Gp, pcnt, zf); break;
+    case 28: atr_prox_go<T, NT, 8, false, 2>(p, A, R, G, x, pp, pthr, z, t, mu, thres, red, st, pub, Gp, pcnt, zf); break;
+    default: atr_prox_go<T, NT, 8, false, 0>(p, A, R, G, x, pp, pthr, z, t, mu, thres, red, st, pub, Gp, pcnt, zf); break;
   }
 }
 template <typename T>
@@ -553,20 +593,21 @@ void launch_atr_prox(const GemmPlan& p, const T* A, const T* R, T* G, const T* x
   else atr_prox_nt<T, 2>(p, A, R, G, x, pp, pthr, z, t, mu, thres, red, st, pub, Gp, pcnt, zf);
 }
 
-template <typename T, int NT, int PF, bool NTL>
+template <typename T, int NT, int PF, bool NTL, int WL>
 static void atr_fista_go(const GemmPlan& p, const T* A, const T* R, T* G, const T* y, const T* xk,
                          T* xc, T* vn, T* yn, double t, double mu, double thres, double theta,
                          double theta_next, Red red, hipStream_t st, Pub pub, T* Gp, unsigned* pcnt,
                          T* ec, unsigned* zf) {
   const dim3 grid((unsigned)(p.n / 64 * p.atr_S + (pub.host ? 1 : 0)));
+  const dim3 block(WL == 2 ? 512 : 256);
   if (p.atr_S > 1) {
-    glx_launch((k_atr_fista<T, NT, PF, NTL, true>), grid, dim3(256), 0, st, A, R, G, p.m,
+    glx_launch((k_atr_fista<T, NT, PF, NTL, true, WL>), grid, block, 0, st, A, R, G, p.m,
                        p.n, y, xk, xc, vn, yn, t, t * mu, thres, theta, 1.0 - theta_next,
                        theta_next, red, pub, p.atr_S, Gp, pcnt, ec, zf, p.atr_keep_mib);
     return;
   }
-  static const size_t pad = lds_pad(k_atr_fista<T, NT, PF, NTL, false>, "GLX_ATR_LDS_PAD");
-  glx_launch((k_atr_fista<T, NT, PF, NTL, false>), grid, dim3(256), pad, st, A, R, G, p.m,
+  static const size_t pad = lds_pad(k_atr_fista<T, NT, PF, NTL, false, WL>, "GLX_ATR_LDS_PAD");
+  glx_launch((k_atr_fista<T, NT, PF, NTL, false, WL>), grid, block, pad, st, A, R, G, p.m,
                      p.n, y, xk, xc, vn, yn, t, t * mu, thres, theta, 1.0 - theta_next, theta_next,
                      red, pub, 1, Gp, pcnt, ec, zf, p.atr_keep_mib);
 }
@@ -575,11 +616,14 @@ static void atr_fista_nt(const GemmPlan& p, const T* A, const T* R, T* G, const 
                          T* xc, T* vn, T* yn, double t, double mu, double thres, double theta,
                          double theta_next, Red red, hipStream_t st, Pub pub, T* Gp, unsigned* pcnt,
                          T* ec, unsigned* zf) {
-  switch (p.atr_ntl * 100 + p.atr_pf) {
-    case 4: atr_fista_go<T, NT, 4, false>(p, A, R, G, y, xk, xc, vn, yn, t, mu, thres, theta, theta_next, red, st, pub, Gp, pcnt, ec, zf); break;
-    case 104: atr_fista_go<T, NT, 4, true>(p, A, R, G, y, xk, xc, vn, yn, t, mu, thres, theta, theta_next, red, st, pub, Gp, pcnt, ec, zf); break;
-    case 108: atr_fista_go<T, NT, 8, true>(p, A, R, G, y, xk, xc, vn, yn, t, mu, thres, theta, theta_next, red, st, pub, Gp, pcnt, ec, zf); break;
-    default: atr_fista_go<T, NT, 8, false>(p, A, R, G, y, xk, xc, vn, yn, t, mu, thres, theta, theta_next, red, st, pub, Gp, pcnt, ec, zf); break;
+  switch (p.atr_ntl * 100 + p.atr_wl * 10 + p.atr_pf) {
+    case 4: atr_fista_go<T, NT, 4, false, 0>(p, A, R, G, y, xk, xc, vn, yn, t, mu, thres, theta, theta_next, red, st, pub, Gp, pcnt, ec, zf); break;
+    case 104: atr_fista_go<T, NT, 4, true, 0>(p, A, R, G, y, xk, xc, vn, yn, t, mu, thres, theta, theta_next, red, st, pub, Gp, pcnt, ec, zf); break;
+    case 108: atr_fista_go<T, NT, 8, true, 0>(p, A, R, G, y, xk, xc, vn, yn, t, mu, thres, theta, theta_next, red, st, pub, Gp, pcnt, ec, zf); break;
+    case 124: atr_fista_go<T, NT, 4, true, 2>(p, A, R, G, y, xk, xc, vn, yn, t, mu, thres, theta, theta_next, red, st, pub, Gp, pcnt, ec, zf); break;
+    case 128: atr_fista_go<T, NT, 8, true, 2>(p, A, R, G, y, xk, xc, vn, yn, t, mu, thres, theta, theta_next, red, st, pub, Gp, pcnt, ec, zf); break;
+    case 28: atr_fista_go<T, NT, 8, false, 2>(p, A, R, G, y, xk, xc, vn, yn, t, mu, thres, theta, theta_next, red, st, pub, Gp, pcnt, ec, zf); break;
+    default: atr_fista_go<T, NT, 8, false, 0>(p, A, R, G, y, xk, xc, vn, yn, t, mu, thres, theta, theta_next, red, st, pub, Gp, pcnt, ec, zf); break;
   }
 }
 template <typename T>

@@ -667,7 +667,8 @@ GemmPlan make_plan(int esize, int64_t m, int64_t n, int64_t l, int ax_variant) {
   const int ntl = atr_code >= 1000 ? 1 : 0;
   int wl = (atr_code / 10) % 10;
   const int pf = atr_code % 10;
-  if (wl && n % 256 != 0) wl = 0;   // four shared-row panels need n % 256: one panel per block
+  if (wl == 1 && n % 256 != 0) wl = 0;   // four shared-row panels need n % 256: one panel per block
+  if (wl > 2) wl = 0;
   const bool atr_mfma_ok = mfma_l && (n % 64 == 0) && (m % 4 == 0);
   if (ax_variant == 3 || atr_code == 3 || !atr_mfma_ok) {
     p.atr_kind = 3;
@@ -680,11 +681,11 @@ GemmPlan make_plan(int esize, int64_t m, int64_t n, int64_t l, int ax_variant) {
     p.atr_S = (int)clampi(cdiv(kTargetWaves / 4, blocks), 1, std::max<int64_t>(1, std::min<int64_t>(kMaxSplit, m / 16)));
   } else {
     p.atr_kind = 1;
-    p.atr_wl = wl ? 1 : 0;
+    p.atr_wl = wl;   // 0: 4 waves split a panel's rows, 1: 4 panels per block, 2: 8 waves
     p.atr_pf = (pf >= 2 && pf <= 8) ? pf : 2;   // in-place ring: lookahead PF - 1 steps
     p.atr_ntl = ntl;
     const int64_t steps = m / 4;
-    if (p.atr_wl == 0) {
+    if (p.atr_wl != 1) {
       const int64_t blocks = n / 64;
       // f64: one wave per SIMD is enough with the PF-8 ring (and S = 1 at n = 16384 lets the
       // ProxGD trial fuse into the kernel); f32 wants 4 per SIMD

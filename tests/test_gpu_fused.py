@@ -129,3 +129,28 @@ def test_fused_trial_k_splits(monkeypatch, method, S, dc):
     assert r_f["k"] == k_r
     f_g, f_r = np.asarray(r_f["f_hist"], dtype=float), np.asarray(out_r["f_hist"], dtype=float)
     assert np.max(np.abs(f_g - f_r) / np.abs(f_r)) < 1e-8
+
+
+# Round 4: the eight-wave panel (A^T R code 1028: WL 2, two waves per SIMD) in the fused
+# kernels, with one and two K splits: the iterate stays bit-identical to the unfused path on the
+# same tile, and within the north-star bar of the oracle.
+@pytest.mark.parametrize("method", METHODS)
+@pytest.mark.parametrize("S", [1, 2])
+def test_fused_trial_eight_wave_panel(monkeypatch, method, S):
+    from oracle import numpy_ref
+    from glx import _lib
+    monkeypatch.setenv("GLX_ATR_VARIANT", "1028")
+    monkeypatch.setenv("GLX_ATR_S", str(S))
+    d = _lib.plan_describe(_lib.GLX_F64, *SHAPE)
+    assert "WL2" in d and d.rstrip().endswith("S=%d" % S), d
+    A, b, x0, mu, alpha0 = _instance()
+    opts = {"alpha0": alpha0, "maxit": 25}
+    x_f, r_f = _run(monkeypatch, True, True, opts, method)
+    x_u, r_u = _run(monkeypatch, False, False, opts, method)
+    assert r_f["k"] == r_u["k"]
+    assert np.array_equal(x_f, x_u)
+    np.testing.assert_allclose(np.asarray(r_f["f_hist"]), np.asarray(r_u["f_hist"]), rtol=1e-13)
+    x_r, k_r, out_r = numpy_ref.SOLVERS[method](x0.copy(), A, b, mu, dict(opts))
+    assert r_f["k"] == k_r
+    f_g, f_r = np.asarray(r_f["f_hist"], dtype=float), np.asarray(out_r["f_hist"], dtype=float)
+    assert np.max(np.abs(f_g - f_r) / np.abs(f_r)) < 1e-8

@@ -175,3 +175,25 @@ def test_residual_batch_split_groups(monkeypatch, dtype, split):
         s = float((R.double() ** 2).sum())
         assert abs(float(sq[j].item()) - s) <= (1e-12 if dtype == "f64" else 1e-6) * s
         assert torch.equal(R, Rs2[j]) and torch.equal(sq[j], sq2[j])   # deterministic
+
+
+# A^T R tiles by code (NTL * 1000 + WL * 10 + PF; WL 2 = eight waves per panel, round 4),
+# each against the fp64 reference, with K splits where the planner gives them
+@pytest.mark.parametrize("dtype", ["f64", "f32"])
+@pytest.mark.parametrize("shape", [(256, 512, 32), (512, 1024, 16), (1000, 1024, 32), (4096, 8192, 16),
+                                   (8, 256, 32), (2052, 2048, 32)])
+@pytest.mark.parametrize("code", [8, 1008, 14, 1114, 28, 1024, 1028])
+def test_gradient_atr_codes(monkeypatch, shape, dtype, code):
+    monkeypatch.setenv("GLX_ATR_VARIANT", str(code))
+    k = _glx()
+    m, n, l = shape
+    dt = torch.float64 if dtype == "f64" else torch.float32
+    g = torch.Generator(device="cuda").manual_seed(m * 5 + n + l + code)
+    A = torch.randn(m, n, device="cuda", dtype=torch.float64, generator=g).to(dt)
+    R = torch.randn(m, l, device="cuda", dtype=torch.float64, generator=g).to(dt)
+    G = k.gradient(A, R)
+    torch.cuda.synchronize()
+    gref = A.double().T @ R.double()
+    gmag = A.double().abs().T @ R.double().abs()
+    tolg = 1e-13 if dtype == "f64" else 2e-6 * (m ** 0.5)
+    assert _rel_err(G, gref, gmag) < tolg

@@ -1,0 +1,63 @@
+"""Whole-solve parity at the north-star size ("what's missing" item 2).
+
+(m, n, l) = (8192, 16384, 32), fp64, the reference's ``gen_data`` instance (seed 97006855),
+``opts = {"alpha0": 1/(sqrt(m)+sqrt(n))^2}``, every other option at the reference's default:
+the HIP solver's whole continuation solve through the drop-in ``gl_<method>`` entry point
+against the reference's own run of the same call (``tests/golden/ns_<method>.npz``, made by
+``tests/golden/make_golden_ns.py`` importing ``/root/reference/code``). North-star bar:
+identical k, fval and every f_hist / f_hist_best entry within 1e-8 relative, and the returned
+iterate within 1e-6 of max|x|.
+"""
+import hashlib
+import json
+import os
+
+import numpy as np
+import pytest
+
+torch = pytest.importorskip("torch")
+
+pytestmark = pytest.mark.gpu
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+GOLD = os.path.join(HERE, "golden")
+
+
+def _sha(a):
+    return hashlib.sha256(np.ascontiguousarray(a).tobytes()).hexdigest()
+
+
+@pytest.fixture(scope="module")
+def instance():
+    from oracle import numpy_ref
+    meta = json.load(open(os.path.join(GOLD, "ns_gl_ProxGD_primal.json")))
+    m, n, l = meta["m"], meta["n"], meta["l"]
+    A, _, u, x0, mu = numpy_ref.gen_data(m, n, l, meta["seed"])
+    b = np.load(os.path.join(GOLD, "ns_instance_b.npz"))["b"]
+    assert _sha(A) == meta["sha256"]["A"] and _sha(x0) == meta["sha256"]["x0"]
+    assert _sha(u) == meta["sha256"]["u"] and _sha(b) == meta["sha256"]["b"]
+    At = torch.from_numpy(A).cuda()
+    del A
+    return At, torch.from_numpy(b).cuda(), x0, mu, meta["opts"]
+
+
+@pytest.mark.parametrize("method", ["gl_ProxGD_primal", "gl_FProxGD_primal"])
+def test_whole_solve_north_star_size(instance, method):
+    import importlib
+    At, bt, x0, mu, opts = instance
+    gold = np.load(os.path.join(GOLD, "ns_%s.npz" % method))
+    fn = getattr(importlib.import_module(method), method)
+    x, k, out = fn(torch.from_numpy(x0).cuda(), At, bt, mu, dict(opts))
+    torch.cuda.synchronize()
+    x = x.cpu().numpy() if hasattr(x, "cpu") else np.asarray(x)
+    assert k == int(gold["k"]), (k, int(gold["k"]))
+    fg = float(gold["fval"])
+    assert abs(float(out["fval"]) - fg) <= 1e-8 * abs(fg), (float(out["fval"]), fg)
+    for key in ("f_hist", "f_hist_best"):
+        got = np.asarray([float(v) for v in out[key]])
+        ref = gold[key]
+        assert got.shape == ref.shape
+        rel = np.max(np.abs(got - ref) / np.abs(ref))
+        assert rel <= 1e-8, (key, rel, int(np.argmax(np.abs(got - ref) / np.abs(ref))))
+    xr = gold["x"].astype(np.float64)
+    assert np.max(np.abs(x - xr)) <= 1e-6 * np.max(np.abs(xr))

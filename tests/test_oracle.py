@@ -93,3 +93,20 @@ def test_oracle_log_lines_match_reference():
             lg.removeHandler(h)
             lg.setLevel(old)
         assert lines == case["lines"], name
+
+
+def test_ns_golden_fixtures_consistent():
+    """The north-star whole-solve fixtures (tests/golden/make_golden_ns.py): f_hist has k
+    entries, f_hist_best is its running minimum, and the stored b is the instance's."""
+    import hashlib
+    import json
+    gdir = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+    b = np.load(os.path.join(gdir, "ns_instance_b.npz"))["b"]
+    for m in ("gl_ProxGD_primal", "gl_FProxGD_primal"):
+        meta = json.load(open(os.path.join(gdir, "ns_%s.json" % m)))
+        d = np.load(os.path.join(gdir, "ns_%s.npz" % m))
+        assert hashlib.sha256(b.tobytes()).hexdigest() == meta["sha256"]["b"]
+        assert int(d["k"]) == meta["k"] == len(d["f_hist"]) == len(d["f_hist_best"])
+        assert np.array_equal(d["f_hist_best"], np.minimum.accumulate(d["f_hist"]))
+        assert float(d["fval"]) == meta["fval"]
+        assert d["x"].shape == (meta["n"], meta["l"])
