@@ -20,8 +20,9 @@ load run fast, then throttles (A@X 290 -> 400+ us) and recovers over ~30 ms
 (profiles/r2_power_probe.jsonl); a 20-step run would otherwise time that transient, not the
 solver. The timed session restarts from x0, so the iterations timed are the same ones.
 
-Also reported, for the dominant kernel (the dense A@X pass; at NS one right-hand side, A p_thr of
-the split-candidate trial, on the LDS-DMA tile, ~40 % of the iteration):
+Also reported, for the dominant kernel (round 4: whichever of the two passes over A — the dense
+A@X pass or the fused A^T r + trial — has the longer average launch; at NS that is A^T r, ~43 %
+of the iteration, with A@X a few us behind):
   roofline — the kernel's bound is whichever of MFMA time (flops / dense MFMA peak) and HBM time
              (bytes / 8 TB/s) is larger for this (m, n, l, dtype) and right-hand-side count: HBM
              at NS (one right-hand side: l/4 flop/B in fp64, 109 us of MFMA against 135 us of HBM),
@@ -31,8 +32,10 @@ the split-candidate trial, on the LDS-DMA tile, ~40 % of the iteration):
              launch time from HIP events on every k-th dense A@X / A^T r launch of the timed
              region (--profile k, default min(16, steps/4)), attached to the kernel itself
              (hipExtLaunchKernel: the pair is stamped with that kernel's start and end on the
-             solver's stream); the split-candidate A e gather is timed by its own pair and
-             reported apart. `pair_frac` / `pair4_frac` are the same fraction for
+             solver's stream); `roofline.kernels` holds the same object for both passes (`ax`,
+             `atr`), `roofline.dominant` names the one the top-level fields describe; the
+             split-candidate A e gather is timed by its own pair and reported apart.
+             `pair_frac` / `pair4_frac` are the same fraction for
              the A@x + A^T r pair (the north-star target), `pair4_frac_incl_gather` adds the
              gather. `traffic` = HBM bytes per launch from rocprofv3 PMC (profiles/pmc_traffic.json,
              2*FETCH_SIZE + WRITE_SIZE per the gfx950 correction) when that file holds the same
@@ -118,33 +121,56 @@ def cpu_baseline(method, A, b, x0, mu, opts, budget_s=15.0):
                       "%.1f s; BLAS %s" % (method, k, maxit, dt, blas)}
 
 
+def _plan_parts(dtype, m, n, l):
+    from glx import _lib
+    return _lib.plan_describe(_lib.GLX_F64 if dtype == "f64" else _lib.GLX_F32, m, n, l).split("; ")
+
+
 def ax_kernel_name(dtype, m, n, l, nsrc):
     """The A@X tile libglx launched for this shape and right-hand-side count (its own planner)."""
-    from glx import _lib
-    desc = _lib.plan_describe(_lib.GLX_F64 if dtype == "f64" else _lib.GLX_F32, m, n, l)
+    parts = _plan_parts(dtype, m, n, l)
     key = "ax%d=" % max(1, min(3, int(round(nsrc))))
-    for part in desc.split("; "):
+    for part in parts:
         if part.startswith(key):
             return "A@X: " + part[len(key):]
-    return desc
+    return "; ".join(parts)
 
 
 PMC_FILE = "profiles/pmc_traffic.json"
 
 
-def pmc_traffic(cfg_key):
-    """(bytes per A@X launch, source) from the committed rocprofv3 PMC summary of a separate run
-    of this same configuration (FETCH_SIZE / WRITE_SIZE passes cannot share the timed run);
-    (None, None) when that file holds no entry for this configuration."""
+def pmc_traffic(cfg_key, which="ax"):
+    """(bytes per launch of the A@X pass (which="ax") or of the A^T r pass ("atr"), source) from
+    the committed rocprofv3 PMC summary of a separate run of this same configuration
+    (FETCH_SIZE / WRITE_SIZE passes cannot share the timed run); (None, None) when that file
+    holds no entry for this configuration."""
     try:
         with open(os.path.join(ROOT, PMC_FILE)) as fh:
             d = json.load(fh)
         e = d.get(cfg_key)
         if e is None:
             return None, None
-        return float(e["bytes_per_launch"]), "%s[%s] (%s)" % (PMC_FILE, cfg_key, e.get("source", "committed PMC run"))
+        v = e["bytes_per_launch"] if which == "ax" else e.get("detail", {}).get("atr", {}).get("bytes_per_launch")
+        if v is None:
+            return None, None
+        return float(v), "%s[%s].%s (%s)" % (PMC_FILE, cfg_key, "bytes_per_launch" if which == "ax" else "detail.atr",
+                                              e.get("source", "committed PMC run"))
     except Exception:
         return None, None
+
+
+def roof_of(flops, nbytes, avg_s, peak_tf):
+    """bound / achieved / peak / frac of one kernel from its algorithmic flops and bytes per
+    launch and its average launch time"""
+    mfma_bound = flops / (peak_tf * 1e12) >= nbytes / (HBM_PEAK_GBS * 1e9)
+    tf = flops / avg_s / 1e12 if avg_s else None
+    gbs = nbytes / avg_s / 1e9 if avg_s else None
+    ach, peak, unit = (tf, peak_tf, "TFLOP/s") if mfma_bound else (gbs, HBM_PEAK_GBS, "GB/s")
+    return {"bound": "mfma" if mfma_bound else "hbm", "achieved": ach, "peak": peak, "unit": unit,
+            "frac": (ach / peak) if ach else None, "avg_launch_us": avg_s * 1e6 if avg_s else None,
+            "flops_per_launch": flops, "bytes_per_launch": nbytes,
+            "hbm_GBs": gbs, "hbm_frac": gbs / HBM_PEAK_GBS if gbs else None,
+            "mfma_tflops": tf, "mfma_frac": tf / peak_tf if tf else None}
 
 
 def launch_ranks(args):
@@ -371,15 +397,35 @@ def main():
         pair4g_tf = (((4.0 * ml * n * l) + ga_flops) / (ax_avg_s + atr_avg_s + ga_avg_s) / 1e12
                      if (ax_n and atr_n) else None)
         traffic, traffic_src = pmc_traffic(cfg_key)
+        atr_traffic, atr_traffic_src = pmc_traffic(cfg_key, "atr")
         if mfma_bound:
             ach, peak, unit = ax_tf, peak_tf, "TFLOP/s"
         else:
             ach, peak, unit = ax_gbs, HBM_PEAK_GBS, "GB/s"
-        roof = {"bound": "mfma" if mfma_bound else "hbm", "achieved": ach, "peak": peak,
-                "unit": unit, "frac": (ach / peak) if ach else None,
-                "traffic": traffic, "traffic_source": traffic_src, "pmc_key": cfg_key,
-                "kernel": ("k_gemv_pair_fused: A@[x|thr(x)] and A^T r in ONE pass over A (l = 1)"
-                           if work["atr_calls"] == 0 else ax_kname),
+        fused = {"gl_ProxGD_primal": "k_atr_prox", "gl_FProxGD_primal": "k_atr_fista"}.get(args.method)
+        atr_plan = [p for p in _plan_parts(args.dtype, ml, n, l) if p.startswith("atr=")]
+        if args.dtype == "f32" and fused and world == 1 and l in (16, 32) and n % 64 == 0:
+            # solver.cpp session_plan: fp32 trial methods fuse the trial into the 2-split panel
+            atr_plan = ["atr=k_atr_mfma<WL0,PF8,NTL1> S=2 (session plan)"]
+        atr_kname = ("A^T r%s: %s" % (" + the fused trial (%s)" % fused if fused and world == 1 else "",
+                                      atr_plan[0][4:] if atr_plan else "?"))
+        kernels = {"ax": dict(roof_of(ax_flops, ax_bytes, ax_avg_s if ax_n else None, peak_tf),
+                              kernel=("k_gemv_pair_fused: A@[x|thr(x)] and A^T r in ONE pass over A (l = 1)"
+                                      if work["atr_calls"] == 0 else ax_kname),
+                              launches_timed=ax_n, traffic=traffic, traffic_source=traffic_src)}
+        if work["atr_calls"] > 0:
+            kernels["atr"] = dict(roof_of(atr_flops, atr_bytes, atr_avg_s if atr_n else None, peak_tf),
+                                  kernel=atr_kname, launches_timed=atr_n, traffic=atr_traffic,
+                                  traffic_source=atr_traffic_src)
+        # the dominant kernel: the longer of the two passes
+        dominant = "ax"
+        if "atr" in kernels and atr_n and ax_n and atr_avg_s > ax_avg_s:
+            dominant = "atr"
+        dk = kernels[dominant]
+        roof = {"bound": dk["bound"], "achieved": dk["achieved"], "peak": dk["peak"],
+                "unit": dk["unit"], "frac": dk["frac"], "dominant": dominant,
+                "traffic": dk["traffic"], "traffic_source": dk["traffic_source"], "pmc_key": cfg_key,
+                "kernel": dk["kernel"], "kernels": kernels,
                 "flops_per_launch": ax_flops,
                 "bytes_per_launch": ax_bytes, "avg_launch_us": ax_avg_s * 1e6, "launches_timed": ax_n,
                 "timed_every": args.profile,

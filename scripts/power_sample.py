@@ -24,7 +24,7 @@ def sampler(stop, out, period):
         try:
             r = subprocess.run(["amd-smi", "metric", "-g", "0", "--power", "--clock", "--json"],
                                capture_output=True, text=True, timeout=5)
-            rec = {"t": t, "rc": r.returncode, "out": r.stdout[-4000:], "err": r.stderr[-300:]}
+            rec = {"t": t, "rc": r.returncode, "out": r.stdout[:200000], "err": r.stderr[-300:]}
         except Exception as e:  # report, never fake
             rec = {"t": t, "error": repr(e)}
         out.write(json.dumps(rec) + "\n")
