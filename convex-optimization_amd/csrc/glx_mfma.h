@@ -147,3 +147,32 @@ static size_t lds_pad(K kernel, const char* env) {
 // kind 5 (X staged in LDS) code: 5 MT PF VPL WAVES. Kind-5 defaults fall back to the register
 
 }  // namespace glx
+// In-kernel clock probe (diagnostic builds only: scripts/clock_probe.sh compiles the library with
+// -DGLX_CLOCK_PROBE; the shipped library has no stamps). Thread 0 of every workgroup stamps the
+// shader clock (s_memtime) and the 100 MHz constant clock (s_memrealtime) at kernel entry (k 0),
+// main-loop start (1) and end (2), kernel end (3), and in A^T R the end of the block's LDS
+// reduction (4) and of the fused epilogue's row work (5), of the two passes over A, into a buffer of the code object (one per translation unit) that no
+// kernel reads; the last launch's stamps are read back by glx_probe_clock_ax / _atr
+// (kernels_axdma.hip, kernels_atr.hip). MI355X_MICROARCH.md "DVFS give-back" (6).
+#ifdef GLX_CLOCK_PROBE
+namespace glx {
+static __device__ unsigned long long g_clk[2048][12];   // [block][stamp pair k: 2k, 2k+1]
+}
+#define GLX_CLK(k)                                                                          \
+  do {                                                                                      \
+    if (threadIdx.x == 0 && blockIdx.x < 2048) {                                            \
+      glx::g_clk[blockIdx.x][2 * (k)] = __builtin_amdgcn_s_memtime();                       \
+      glx::g_clk[blockIdx.x][2 * (k) + 1] = __builtin_amdgcn_s_memrealtime();               \
+    }                                                                                       \
+  } while (0)
+#define GLX_CLK_READER(fn)                                                                  \
+  extern "C" int fn(unsigned long long* out) {                                              \
+    return hipMemcpyFromSymbol(out, HIP_SYMBOL(glx::g_clk), sizeof(glx::g_clk), 0,          \
+                               hipMemcpyDeviceToHost) == hipSuccess ? 0 : 1;                \
+  }
+#else
+#define GLX_CLK(k) do {} while (0)
+#define GLX_CLK_READER(fn)
+#endif
+
+

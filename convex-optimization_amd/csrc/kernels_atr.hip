@@ -120,6 +120,7 @@ __device__ inline int64_t atr_panel(const T* __restrict__ A, const T* __restrict
 #pragma unroll
       for (int nt = 0; nt < NT; ++nt) acc[e][nt] = M::mma(a[p][e], rb[p][nt], acc[e][nt]);
   };
+  GLX_CLK(1);
   if (nst > 0) {
 #pragma unroll
     for (int p = 0; p < PF; ++p) ld(p, p);
@@ -149,6 +150,7 @@ __device__ inline int64_t atr_panel(const T* __restrict__ A, const T* __restrict
     for (int p = 0; p < PF - 1; ++p)
       if (s0 + p < nst) mma_step(p);
   }
+  GLX_CLK(2);
 
   if constexpr (WL == 2) {   // waves 4..7 into 0..3: acc(w) + acc(w + 4)
     if (wave >= 4) {
@@ -297,6 +299,7 @@ __global__ __launch_bounds__(WL == 2 ? 512 : 256, (WL == 0 && sizeof(T) == 8) ? 
   // counter or ticket is touched. (Testing the flag after the main loop instead measured no
   // faster and would spend a whole pass per cancelled launch.) The decision record still goes
   // to the host: the cancelling decision's own.
+  GLX_CLK(0);
   if (red_skipped(red)) {
     if (pub.host != nullptr && blockIdx.x == 0 && threadIdx.x == 0)
       publish_packet(pub.s, pub.ns, pub.host, pub.host_seq, pub.seq);
@@ -316,6 +319,7 @@ __global__ __launch_bounds__(WL == 2 ? 512 : 256, (WL == 0 && sizeof(T) == 8) ? 
   const int64_t bid = (int64_t)blockIdx.x - (pub.host ? 1 : 0);
   const int64_t panel = SPLIT ? bid / S : bid, split = SPLIT ? bid % S : 0;
   const int64_t col0 = atr_panel<T, NT, PF, WL, NTL>(A, R, m, n, SPLIT ? S : 1, acc, panel, split, keep_mib);
+  GLX_CLK(4);
   double accr[6] = {0.0, 0.0, 0.0, -__builtin_inf(), 0.0, 0.0};
   int slot = work_slot(pub);
   if constexpr (SPLIT) {   // a separate instantiation: the S = 1 kernel keeps 2 blocks per CU
@@ -354,7 +358,9 @@ __global__ __launch_bounds__(WL == 2 ? 512 : 256, (WL == 0 && sizeof(T) == 8) ? 
       }
     }
   }
+  GLX_CLK(5);
   grid_reduce<6, 0x8u, NW>(accr, red, slot, nparts);
+  GLX_CLK(3);
 }
 
 // FISTA's backtracking trial fused into A^T R the same way (WL 0, one K split): each wave runs
@@ -656,3 +662,5 @@ template void launch_atr<float>(const GemmPlan&, const float*, const float*, flo
 
 
 }  // namespace glx
+
+GLX_CLK_READER(glx_probe_clock_atr)

@@ -99,6 +99,7 @@ __global__ __launch_bounds__(64 * WAVES) void k_ax_dma(const T* __restrict__ A,
   constexpr int kWaitVmLgkm0 = (WAITN & 15) | (7 << 4) | ((WAITN >> 4) << 14);
   __shared__ __attribute__((aligned(1024))) char lds[LDSB];
 
+  GLX_CLK(0);
   if (pub.host != nullptr && blockIdx.x == 0) {   // as k_ax_lds: workgroup 0 carries the packet
     if (threadIdx.x == 0)
       publish_packet(pub.s, pub.ns, pub.host, pub.host_seq, pub.seq, pub.s2, pub.off2, pub.n2,
@@ -271,6 +272,7 @@ __global__ __launch_bounds__(64 * WAVES) void k_ax_dma(const T* __restrict__ A,
               for (int nt = 0; nt < NT; ++nt)
                 acc[mt][src * NT + nt] = M::mma(a[mt][j][e], x[j][e][src][nt], acc[mt][src * NT + nt]);
     };
+    GLX_CLK(1);
 #pragma unroll
     for (int d = 0; d < D; ++d) issue(d, d);
     asm volatile("s_waitcnt vmcnt(%0)" ::"n"(WAITN) : "memory");
@@ -320,6 +322,7 @@ __global__ __launch_bounds__(64 * WAVES) void k_ax_dma(const T* __restrict__ A,
       }
     }
     if (c < nch) mma_ops(av[0], xv[0]);   // odd count: the last chunk is in set 0
+    GLX_CLK(2);
   } else {
 #pragma unroll
   for (int d = 0; d < D; ++d) issue(d, d);
@@ -352,6 +355,7 @@ __global__ __launch_bounds__(64 * WAVES) void k_ax_dma(const T* __restrict__ A,
         }
       }
   }
+  GLX_CLK(3);
 }
 
 template <typename T, int NT, int NSRC, int NS, int KC, int WAVES, bool NTL, bool HOIST = false,
@@ -413,3 +417,5 @@ template bool launch_ax_dma<float>(const GemmPlan&, int, int, int, const float*,
                                    float*, const int*, int, hipStream_t, Pub);
 
 }  // namespace glx
+
+GLX_CLK_READER(glx_probe_clock_ax)
