@@ -318,48 +318,65 @@ __global__ __launch_bounds__(WL == 2 ? 512 : 256, (WL == 0 && sizeof(T) == 8) ? 
   typename M::acc_t acc[4][NT];
   const int64_t bid = (int64_t)blockIdx.x - (pub.host ? 1 : 0);
   const int64_t panel = SPLIT ? bid / S : bid, split = SPLIT ? bid % S : 0;
+  // Round 4: the row results are stored after the trial sums have been handed to grid_reduce,
+  // whose vmcnt(0) drain then waits for six partials instead of wave 0's G / p / p_thr / z stores
+  // (the fused epilogue took 8-10 us of the kernel at NS and C2, profiles/r4_clk). Loading the
+  // iterate rows before the main loop instead of after it measured 4-5 us slower at NS (+18
+  // VGPRs live through the ring, profiles/r4_ab2).
   const int64_t col0 = atr_panel<T, NT, PF, WL, NTL>(A, R, m, n, SPLIT ? S : 1, acc, panel, split, keep_mib);
   GLX_CLK(4);
-  double accr[6] = {0.0, 0.0, 0.0, -__builtin_inf(), 0.0, 0.0};
-  int slot = work_slot(pub);
-  if constexpr (SPLIT) {   // a separate instantiation: the S = 1 kernel keeps 2 blocks per CU
-    if (!atr_split_combine<T, NT>(acc, Gp, n, S, panel, split, pcnt, &slot)) return;
-  }
-  const T t = (T)t_, tmu = (T)tmu_, thres = (T)thres_;
+  T xa[4][NT];
 #pragma unroll
   for (int e = 0; e < 4; ++e) {
     if (e != wave) continue;   // wave w owns the rows e == w (4 per lane group)
-    T xa[4][NT];
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       const int64_t row = col0 + atr_col<T>(M::row(lane, r), e);
 #pragma unroll
       for (int nt = 0; nt < NT; ++nt) xa[r][nt] = x[row * L + nt * 16 + i];
     }
+  }
+  double accr[6] = {0.0, 0.0, 0.0, -__builtin_inf(), 0.0, 0.0};
+  int slot = work_slot(pub);
+  if constexpr (SPLIT) {   // a separate instantiation: the S = 1 kernel keeps 2 blocks per CU
+    if (!atr_split_combine<T, NT>(acc, Gp, n, S, panel, split, pcnt, &slot)) return;
+  }
+  const T t = (T)t_, tmu = (T)tmu_, thres = (T)thres_;
+  T gs[4][NT], ps[4][NT], pts[4][NT], zs[4][NT];
+  unsigned rows_e[4] = {0u, 0u, 0u, 0u};
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    if (e != wave) continue;
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
-      const int64_t row = col0 + atr_col<T>(M::row(lane, r), e);
-      T gv[NT], pv[NT], pth[NT], zv[NT];
       bool ok[NT];
 #pragma unroll
       for (int nt = 0; nt < NT; ++nt) {
-        gv[nt] = acc[e][nt][r];
+        gs[r][nt] = acc[e][nt][r];
         ok[nt] = true;
-        G[row * L + nt * 16 + i] = gv[nt];
       }
-      const unsigned rowe =
-          prox_pgd_row<T, 16, NT>(xa[r], gv, ok, true, i, t, tmu, thres, pv, pth, zv, accr, zf != nullptr);
-      if (zf != nullptr && i == 0) zf[row] = rowe;
-#pragma unroll
-      for (int nt = 0; nt < NT; ++nt) {
-        p[row * L + nt * 16 + i] = pv[nt];
-        pthr[row * L + nt * 16 + i] = pth[nt];
-        z[row * L + nt * 16 + i] = zv[nt];
-      }
+      rows_e[r] = prox_pgd_row<T, 16, NT>(xa[r], gs[r], ok, true, i, t, tmu, thres, ps[r], pts[r], zs[r],
+                                          accr, zf != nullptr);
     }
   }
   GLX_CLK(5);
   grid_reduce<6, 0x8u, NW>(accr, red, slot, nparts);
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    if (e != wave) continue;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int64_t row = col0 + atr_col<T>(M::row(lane, r), e);
+      if (zf != nullptr && i == 0) zf[row] = rows_e[r];
+#pragma unroll
+      for (int nt = 0; nt < NT; ++nt) {
+        G[row * L + nt * 16 + i] = gs[r][nt];
+        p[row * L + nt * 16 + i] = ps[r][nt];
+        pthr[row * L + nt * 16 + i] = pts[r][nt];
+        z[row * L + nt * 16 + i] = zs[r][nt];
+      }
+    }
+  }
   GLX_CLK(3);
 }
 

@@ -138,8 +138,11 @@ __global__ __launch_bounds__(kGThreads) void k_e_lists(const unsigned* __restric
 // of one At row. out[r][c] = the sum (one slab: no K split).
 // NT: At read with the non-temporal policy (each of its rows is read at most once per trial;
 // GLX_GATHER_NT)
-template <typename T, int L, bool NT>
-__global__ __launch_bounds__(kGThreads) void k_at_gather(const T* __restrict__ At,
+// GW waves per workgroup (round 4, GLX_GATHER_WAVES): with 1-wave workgroups the grid has 4x as
+// many, so the dispatcher keeps refilling CUs as the short columns finish instead of every CU
+// holding four workgroups that all wait for the longest list of their columns.
+template <typename T, int L, bool NT, int GW>
+__global__ __launch_bounds__(64 * GW) void k_at_gather(const T* __restrict__ At,
                                                          const T* __restrict__ E,
                                                          const unsigned short* __restrict__ lists,
                                                          const unsigned* __restrict__ counts,
@@ -149,7 +152,7 @@ __global__ __launch_bounds__(kGThreads) void k_at_gather(const T* __restrict__ A
   const int rb = (int)blockIdx.x % gx, c = (int)blockIdx.x / gx;
   const int total = (int)counts[c];
   const unsigned short* lst = lists + (int64_t)c * n;
-  const int64_t r = (int64_t)rb * kGThreads + threadIdx.x;
+  const int64_t r = (int64_t)rb * (64 * GW) + threadIdx.x;
   const int64_t rr = r < m ? r : m - 1;
   constexpr int U = 8;
   T acc = T(0);
@@ -206,18 +209,33 @@ template <typename T>
 void launch_at_gather(const T* At, const T* E, int64_t m, int64_t n, int64_t l, T* P, void* lists_ws,
                       hipStream_t st, const int* skip) {
   if (!gather_ok(n, l)) throw Error{GLX_E_INVALID, "A e gather: needs l in {16, 32}, n < 65536"};
-  const int gx = (int)((m + kGThreads - 1) / kGThreads);
   const unsigned short* lists = static_cast<const unsigned short*>(lists_ws);
   static const bool nt = [] {
     const char* e = std::getenv("GLX_GATHER_NT");
     return !(e && std::strcmp(e, "0") == 0);
   }();
-  auto go = [&](auto kern) {
-    glx_launch(kern, dim3((unsigned)(gx * l)), dim3(kGThreads), 0, st, At, E, lists,
+  const int gw = [] {   // read per launch (tests switch it within one process)
+    const char* e = std::getenv("GLX_GATHER_WAVES");
+    const int v = e ? std::atoi(e) : 4;
+    return (v == 1 || v == 2) ? v : 4;
+  }();
+  auto go = [&](auto kern, int waves) {
+    const int gx = (int)((m + 64 * waves - 1) / (64 * waves));
+    glx_launch(kern, dim3((unsigned)(gx * l)), dim3(64 * waves), 0, st, At, E, lists,
                        list_counts(lists_ws, n), m, n, P, gx, skip);
   };
-  if (l == 32) nt ? go(k_at_gather<T, 32, true>) : go(k_at_gather<T, 32, false>);
-  else nt ? go(k_at_gather<T, 16, true>) : go(k_at_gather<T, 16, false>);
+  auto go_l = [&](auto kern4, auto kern2, auto kern1) {
+    if (gw == 1) go(kern1, 1);
+    else if (gw == 2) go(kern2, 2);
+    else go(kern4, 4);
+  };
+  if (l == 32) {
+    if (nt) go_l(k_at_gather<T, 32, true, 4>, k_at_gather<T, 32, true, 2>, k_at_gather<T, 32, true, 1>);
+    else go_l(k_at_gather<T, 32, false, 4>, k_at_gather<T, 32, false, 2>, k_at_gather<T, 32, false, 1>);
+  } else {
+    if (nt) go_l(k_at_gather<T, 16, true, 4>, k_at_gather<T, 16, true, 2>, k_at_gather<T, 16, true, 1>);
+    else go_l(k_at_gather<T, 16, false, 4>, k_at_gather<T, 16, false, 2>, k_at_gather<T, 16, false, 1>);
+  }
 }
 
 // workspace of the column lists: l * n indices + 256 B of counts

@@ -30,6 +30,7 @@ def main():
     ap.add_argument("--n", type=int, default=16384)
     ap.add_argument("--l", type=int, default=32)
     ap.add_argument("--method", default="gl_ProxGD_primal")
+    ap.add_argument("--raw", default=None, help="also save the per-workgroup stamps (.npz)")
     ap.add_argument("--idle-ms", type=float, default=0.0,
                     help="sleep this long, then run one more iteration (a launch after idle)")
     a = ap.parse_args()
@@ -63,6 +64,8 @@ def main():
         assert getattr(_lib.lib(), fn)(buf) == 0
         v[p] = np.frombuffer(buf, dtype=np.uint64).reshape(2048, 12).astype(np.float64)
     out = {"steps": a.steps, "iters_per_s": a.steps / dt, "idle_ms": a.idle_ms}
+    if a.raw:
+        np.savez_compressed(a.raw, stamps=v)
     for p, name in ((0, "ax_dma"), (1, "atr")):
         mt = v[p, :, 0::2]   # shader clock at stamps 0..3
         rt = v[p, :, 1::2]   # 100 MHz clock at stamps 0..3

@@ -271,3 +271,20 @@ def test_full_size_long_trajectory_vs_oracle(solver, alpha_scale):
     assert np.max(np.abs(x - xr)) <= 1e-6 * np.max(np.abs(xr))
     if alpha_scale > 1:
         assert out["glx"]["syncs"] > k   # more than one readback per iteration: trials were retried
+
+
+@pytest.mark.parametrize("name", ["mid_512x1024x16_f64_gl_ProxGD_primal", "mid_256x512x32_f64_gl_FProxGD_primal"])
+def test_split_candidate_gather_waves_bit_identical(name, monkeypatch):
+    """The A e gather's workgroup size (GLX_GATHER_WAVES 1 / 2 / 4, round 4) changes only which
+    workgroup computes an output row, not its summation order: results are bit-identical."""
+    monkeypatch.setenv("GLX_SPLIT_CAND", "1")
+    meta, gold = golden_case(name)
+    A, b, u, x0, mu = golden_inputs(meta)
+    runs = []
+    for w in ("4", "2", "1"):
+        monkeypatch.setenv("GLX_GATHER_WAVES", w)
+        x, k, out = _solve(meta, A, b, x0, mu)
+        runs.append((x, k, [float(v) for v in out["f_hist"]]))
+    for x, k, fh in runs[1:]:
+        assert k == runs[0][1] and fh == runs[0][2] and np.array_equal(x, runs[0][0])
+    assert runs[0][1] == int(gold["k"])
