@@ -181,6 +181,14 @@ static GemmPlan session_plan(const glx_problem& P, const glx_opts& O) {
     f.atr_ntl = 1;
     f.atr_pf = 8;   // round 3: the PF 8 ring (1008), see above
     f.atr_S = 2;
+    // Round 4: with at least one panel per CU, the eight-wave panel (WL 2: two waves per SIMD)
+    // with one K split, no slab combine: C3 FProxGD A^T R + trial 101.2-101.4 us against
+    // 107.4-107.6, 3815-3825 against 3741-3748 it/s over 200 steps (profiles/r4_c3atr/; with
+    // two K splits it measured 119 us, with the PF 4 ring 104 us)
+    if (P.n / 64 >= 256) {
+      f.atr_wl = 2;
+      f.atr_S = 1;
+    }
     if (atr_prox_ok(f)) return f;   // only where the trial actually fuses (GLX_ATR_FUSE_SPLIT)
   }
   return p;
