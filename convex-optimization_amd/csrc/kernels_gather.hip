@@ -23,6 +23,7 @@
 
 #include "glx.h"
 #include "glx_device.h"
+#include "glx_mfma.h"
 
 namespace glx {
 
@@ -175,6 +176,58 @@ __global__ __launch_bounds__(64 * GW) void k_at_gather(const T* __restrict__ At,
   if (r < m) P[r * L + c] = acc;
 }
 
+// The same with two output rows per thread (round 4, GLX_GATHER_VEC): each thread loads At[k][r],
+// At[k][r + 1] as one 16-B vector, so a wave-instruction reads 1 KiB of the At row instead of
+// 512 B (8-B loads read at 0.54-0.70x the 16-B rate, MI355X_MICROARCH.md visibility table).
+// Per output element the same ascending-k sum: results are bit-identical to k_at_gather.
+// Needs m even (fp64: 16-B alignment of every At row).
+template <typename T, int L, bool NT>
+__global__ __launch_bounds__(kGThreads) void k_at_gather2(const T* __restrict__ At,
+                                                          const T* __restrict__ E,
+                                                          const unsigned short* __restrict__ lists,
+                                                          const unsigned* __restrict__ counts,
+                                                          int64_t m, int64_t n, T* __restrict__ P,
+                                                          int gx, const int* __restrict__ skip) {
+  static_assert(sizeof(T) == 8, "fp64: two rows = one 16-B vector");
+  if (skip != nullptr && *skip != 0) return;
+  const int rb = (int)blockIdx.x % gx, c = (int)blockIdx.x / gx;
+  const int total = (int)counts[c];
+  const unsigned short* lst = lists + (int64_t)c * n;
+  const int64_t r = ((int64_t)rb * kGThreads + threadIdx.x) * 2;
+  const int64_t rr = r < m ? r : m - 2;
+  constexpr int U = 8;
+  T acc0 = T(0), acc1 = T(0);
+  int idx = 0;
+  for (; idx + U <= total; idx += U) {
+    d2_t a[U];
+    T ev[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int64_t k = lst[idx + u];
+      const d2_t* ap = reinterpret_cast<const d2_t*>(At + k * m + rr);
+      a[u] = NT ? __builtin_nontemporal_load(ap) : *ap;
+      ev[u] = E[k * L + c];
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      acc0 = acc0 + a[u][0] * ev[u];
+      acc1 = acc1 + a[u][1] * ev[u];
+    }
+  }
+  for (; idx < total; ++idx) {
+    const int64_t k = lst[idx];
+    const d2_t* ap = reinterpret_cast<const d2_t*>(At + k * m + rr);
+    const d2_t a = NT ? __builtin_nontemporal_load(ap) : *ap;
+    const T ev = E[k * L + c];
+    acc0 = acc0 + a[0] * ev;
+    acc1 = acc1 + a[1] * ev;
+  }
+  if (r < m) {
+    P[r * L + c] = acc0;
+    P[(r + 1) * L + c] = acc1;
+  }
+}
+
 // A e is written as ONE slab (no K split)
 int gather_split(int64_t m) {
   (void)m;
@@ -229,6 +282,22 @@ void launch_at_gather(const T* At, const T* E, int64_t m, int64_t n, int64_t l, 
     else if (gw == 2) go(kern2, 2);
     else go(kern4, 4);
   };
+  const bool vec = [] {
+    const char* e = std::getenv("GLX_GATHER_VEC");
+    return !(e && std::strcmp(e, "0") == 0);
+  }();
+  if constexpr (sizeof(T) == 8) {
+    if (vec && m % 2 == 0) {   // two rows per thread, 16-B loads
+      const int gx = (int)((m / 2 + kGThreads - 1) / kGThreads);
+      auto g2 = [&](auto kern) {
+        glx_launch(kern, dim3((unsigned)(gx * l)), dim3(kGThreads), 0, st, At, E, lists,
+                   list_counts(lists_ws, n), m, n, P, gx, skip);
+      };
+      if (l == 32) nt ? g2(k_at_gather2<T, 32, true>) : g2(k_at_gather2<T, 32, false>);
+      else nt ? g2(k_at_gather2<T, 16, true>) : g2(k_at_gather2<T, 16, false>);
+      return;
+    }
+  }
   if (l == 32) {
     if (nt) go_l(k_at_gather<T, 32, true, 4>, k_at_gather<T, 32, true, 2>, k_at_gather<T, 32, true, 1>);
     else go_l(k_at_gather<T, 32, false, 4>, k_at_gather<T, 32, false, 2>, k_at_gather<T, 32, false, 1>);

@@ -275,14 +275,16 @@ def test_full_size_long_trajectory_vs_oracle(solver, alpha_scale):
 
 @pytest.mark.parametrize("name", ["mid_512x1024x16_f64_gl_ProxGD_primal", "mid_256x512x32_f64_gl_FProxGD_primal"])
 def test_split_candidate_gather_waves_bit_identical(name, monkeypatch):
-    """The A e gather's workgroup size (GLX_GATHER_WAVES 1 / 2 / 4, round 4) changes only which
-    workgroup computes an output row, not its summation order: results are bit-identical."""
+    """The A e gather's workgroup size (GLX_GATHER_WAVES 1 / 2 / 4) and its two-rows-per-thread
+    form (GLX_GATHER_VEC, round 4) change only which thread computes an output row, not its
+    summation order: results are bit-identical."""
     monkeypatch.setenv("GLX_SPLIT_CAND", "1")
     meta, gold = golden_case(name)
     A, b, u, x0, mu = golden_inputs(meta)
     runs = []
-    for w in ("4", "2", "1"):
+    for w, vec in (("4", "0"), ("2", "0"), ("1", "0"), ("4", "1")):
         monkeypatch.setenv("GLX_GATHER_WAVES", w)
+        monkeypatch.setenv("GLX_GATHER_VEC", vec)   # (round 4) two rows per thread, 16-B loads
         x, k, out = _solve(meta, A, b, x0, mu)
         runs.append((x, k, [float(v) for v in out["f_hist"]]))
     for x, k, fh in runs[1:]:
