@@ -176,11 +176,12 @@ __global__ __launch_bounds__(64 * GW) void k_at_gather(const T* __restrict__ At,
   if (r < m) P[r * L + c] = acc;
 }
 
-// The same with two output rows per thread (round 4, GLX_GATHER_VEC): each thread loads At[k][r],
-// At[k][r + 1] as one 16-B vector, so a wave-instruction reads 1 KiB of the At row instead of
-// 512 B (8-B loads read at 0.54-0.70x the 16-B rate, MI355X_MICROARCH.md visibility table).
-// Per output element the same ascending-k sum: results are bit-identical to k_at_gather.
-// Needs m even (fp64: 16-B alignment of every At row).
+// The same with two output rows per thread (round 4, GLX_GATHER_VEC=1): each thread loads
+// At[k][r], At[k][r + 1] as one 16-B vector, so a wave-instruction reads 1 KiB of the At row
+// instead of 512 B (8-B loads read at 0.54-0.70x the 16-B rate, MI355X_MICROARCH.md visibility
+// table). Per output element the same ascending-k sum: bit-identical to k_at_gather. Measured
+// over whole NS solves: 56.6 us against 53.8 us for k_at_gather (half the waves in flight),
+// so it is not the default (profiles/r4_gvec/). Needs m even (16-B alignment of every At row).
 template <typename T, int L, bool NT>
 __global__ __launch_bounds__(kGThreads) void k_at_gather2(const T* __restrict__ At,
                                                           const T* __restrict__ E,
@@ -282,9 +283,9 @@ void launch_at_gather(const T* At, const T* E, int64_t m, int64_t n, int64_t l, 
     else if (gw == 2) go(kern2, 2);
     else go(kern4, 4);
   };
-  const bool vec = [] {
+  const bool vec = [] {   // measured slower over whole NS solves (56.6 vs 53.8 us): off
     const char* e = std::getenv("GLX_GATHER_VEC");
-    return !(e && std::strcmp(e, "0") == 0);
+    return e && std::strcmp(e, "1") == 0;
   }();
   if constexpr (sizeof(T) == 8) {
     if (vec && m % 2 == 0) {   // two rows per thread, 16-B loads

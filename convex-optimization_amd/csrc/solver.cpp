@@ -598,11 +598,21 @@ class Session : public SessionBase {
 
   hipEvent_t prof_stop_ = nullptr;   // the stop event of the open prof_begin
   int64_t prof_tag_ = 0;             // its batch segment (0: not in a device-controlled batch)
+  // Timing-only events (round 4): hipEventDisableSystemFence drops the system-scope release /
+  // acquire the runtime otherwise wraps around an event-stamped launch (an L2 writeback and
+  // invalidate, "the cost of cache writeback and invalidation, and the performance impact of
+  // those actions on the execution of following work", hip_runtime_api.h). The pair still
+  // brackets exactly that kernel; nothing reads the events but hipEventElapsedTime.
+  // GLX_EVENT_FENCE=1 restores plain events.
   hipEvent_t get_event() {
     if (ev_pool_.empty()) {   // grow in batches: never create events inside a timed loop's steady state
+      static const bool fence = [] {
+        const char* e = std::getenv("GLX_EVENT_FENCE");
+        return e && std::strcmp(e, "1") == 0;
+      }();
       for (int i = 0; i < 256; ++i) {
         hipEvent_t e;
-        GLX_HIP(hipEventCreate(&e));
+        GLX_HIP(hipEventCreateWithFlags(&e, fence ? hipEventDefault : hipEventDisableSystemFence));
         ev_pool_.push_back(e);
       }
     }
