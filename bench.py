@@ -280,10 +280,17 @@ def main():
     opts = {"alpha0": alpha0, "maxit": max(total + 1, 2500), "max_total_iters": total,
             "profile": args.profile, "ax_variant": args.variant, "exact_objective": args.exact}
     prewarm = None
+    # the timed session is created first (its workspace, A's transposed copy), so that its warmup
+    # follows the pre-warm session's last iteration without the GPU idling in between (round 4:
+    # after an idle gap the power management throttles the next few ms of fp64 MFMA load, and
+    # the 20-step window times exactly that, profiles/r4_evt/)
+    x = x0.clone()
+    s = glx.Session(args.method, x, A, b, mu, opts, comm=comm)
+    pw = None
     if args.prewarm_s > 0:
         prewarm = {"seconds": args.prewarm_s, "iters": 0,
                    "what": "throwaway session of the same solver on the same instance before the "
-                           "warmup; the timed session restarts from x0"}
+                           "warmup, run right before it; the timed session starts from x0"}
         xw = x0.clone()
         pw = glx.Session(args.method, xw, A, b, mu, dict(opts, profile=0, max_total_iters=0),
                          comm=comm)
@@ -293,12 +300,7 @@ def main():
             prewarm["iters"] += got
             if pw.finished or got == 0:
                 break
-        pw.close()
-        del pw, xw
-        torch.cuda.synchronize()
         prewarm["seconds"] = round(time.perf_counter() - t_pw, 3)
-    x = x0.clone()
-    s = glx.Session(args.method, x, A, b, mu, opts, comm=comm)
     s.run(args.warmup)
     for kind in (0, 1, 2):
         s.kernel_time(kind)
@@ -321,6 +323,9 @@ def main():
         elapsed = float(t.item())
         dist.barrier()
     c1 = s.counters()
+    if pw is not None:
+        pw.close()
+        del pw
     work = {k: c1[k] - c0[k] for k in c1}   # executed work of the timed region
     ax_n, ax_ms = s.kernel_time(0)
     atr_n, atr_ms = s.kernel_time(1)
