@@ -26,6 +26,7 @@ import torch  # noqa: E402
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--steps", type=int, default=200)
+    ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--m", type=int, default=8192)
     ap.add_argument("--n", type=int, default=16384)
     ap.add_argument("--l", type=int, default=32)
@@ -48,7 +49,7 @@ def main():
         pw.run(16)
     pw.close()
     s = glx.Session(a.method, x0.clone(), A, b, 1e-2, dict(opts))
-    s.run(20)
+    s.run(a.warmup)
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     s.run(a.steps)
