@@ -385,12 +385,6 @@ static bool dma_code(const GemmPlan& p, int code, int S, const T* A, const T* co
   switch (code) {
     case 92278: ax_dma_go<T, NT, NSRC, 2, 32, 8, true, true, true, 2>(p, S, A, X, P, gate, epoch, st, pub); return true;
     case 92268: ax_dma_go<T, NT, NSRC, 2, 32, 8, false, true, true, 2>(p, S, A, X, P, gate, epoch, st, pub); return true;
-    // round 4: one 16-row tile per wave (kind 8) for the batched right-hand sides, whose two-tile
-    // form spills (256 VGPRs + 64 spilled at NT 2, NSRC 2: 469 us at NS); 2 or 3 ring slots
-    case 82278: ax_dma_go<T, NT, NSRC, 2, 32, 8, true, true, true, 1>(p, S, A, X, P, gate, epoch, st, pub); return true;
-    case 82268: ax_dma_go<T, NT, NSRC, 2, 32, 8, false, true, true, 1>(p, S, A, X, P, gate, epoch, st, pub); return true;
-    case 83278: ax_dma_go<T, NT, NSRC, 3, 32, 8, true, true, true, 1>(p, S, A, X, P, gate, epoch, st, pub); return true;
-    case 83268: ax_dma_go<T, NT, NSRC, 3, 32, 8, false, true, true, 1>(p, S, A, X, P, gate, epoch, st, pub); return true;
     default: return false;
   }
 }

@@ -507,9 +507,7 @@ static int axb_default(int nsrc, int esize) {
 // the tiles the planner picks (lds_plan); the LDS-DMA sweep's other codes are in DESIGN.md
 static constexpr int kLdsCodes[] = {52224, 52324, 52228, 51328,
                                      // kind 9 (LDS-DMA, f64, two row tiles per wave): 9 NS KC/16 flags WAVES
-                                     92278, 92268,
-                                     // kind 8 (one row tile per wave), round 4: batched RHS
-                                     82278, 82268, 83278, 83268};
+                                     92278, 92268};
 static inline bool dma_kind(int c) { return c / 10000 == 8 || c / 10000 == 9; }
 static inline bool lds_kind(int c) { return c / 10000 == 5 || dma_kind(c); }
 static bool lds_code_ok(int c, int64_t n, int64_t l, int esize, int nsrc = 1) {
