@@ -249,6 +249,21 @@ size_t resgrad_ws_bytes(int64_t m, int64_t n);
 void resgrad_reset(void* ws, int64_t m, int64_t n, hipStream_t st);
 // returns false (nothing launched) when the runtime refuses the cooperative launch; *err != 0
 // after the launch: a hand-off wait timed out or the XCD grouping failed, R / G are invalid
+// ---- the trial's batch + the next gradient in one pass, l = 16 (kernels_rg2.hip, round 4) ----
+// P0 = A X0, P1 = A X1 (one m x 16 slab each), Gs[RG][n][16] with G = A^T (P1 - B) = the sum of the
+// RG slabs in order. resgrad2_shape_ok: fp64, l = 16, n = 256 P (P a power of two in 2..128),
+// m % (16 RG) == 0, m / RG >= 32 (RG = 256 / P). Plain launch of 256 workgroups that wait for each
+// other with bounded spins (*err = 1 on a timeout: outputs invalid); resgrad2_device_ok checks
+// that all of them can be resident. ws: resgrad2_ws_bytes, zeroed (resgrad2_reset) before
+// launch_count 1; launch_count grows by one per launch on the same workspace.
+bool resgrad2_shape_ok(int esize, int64_t m, int64_t n, int64_t l);
+bool resgrad2_device_ok();
+int resgrad2_groups(int64_t n);
+size_t resgrad2_ws_bytes(int64_t n);
+void resgrad2_reset(void* ws, int64_t n, hipStream_t st);
+void launch_resgrad2(const double* A, const double* X0, const double* X1, const double* B,
+                     double* P0, double* P1, double* Gs, void* ws, unsigned launch_count, int64_t m,
+                     int64_t n, int* err, hipStream_t st);
 bool launch_resgrad(const double* A, const double* X, const double* B, double* Sraw, double* Gs,
                     void* ws, unsigned launch_count, int64_t m, int64_t n, int* err, hipStream_t st);
 

@@ -16,12 +16,14 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cstdio>
 #include <cstdlib>
 #include <chrono>
 #include <cmath>
 #include <cstring>
 #include <memory>
 #include <string>
+#include <type_traits>
 #include <vector>
 
 #include "glx.h"
@@ -1862,6 +1864,7 @@ static int guarded(F&& f) {
 struct KernelWs {
   void* pp; void* gp; double* part; unsigned* ticket; double* scal;
   void* rg_ws; double* rg_s; double* rg_g; int* rg_err;   // fused residual-gradient pass
+  void* rg2_ws; double* rg2_g;                              // its l = 16 two-source form
 };
 static size_t kernel_ws(int es, const GemmPlan& p, void* base, KernelWs* out) {
   Carver c(base);
@@ -1884,7 +1887,14 @@ static size_t kernel_ws(int es, const GemmPlan& p, void* base, KernelWs* out) {
     rg_g = static_cast<double*>(c.take(sizeof(double) * p.n * p.l * resgrad_groups(p.n)));
     rg_err = static_cast<int*>(c.take(256));
   }
-  if (out) *out = KernelWs{pp, gp, part, ticket, scal, rg_ws, rg_s, rg_g, rg_err};
+  void* rg2_ws = nullptr;
+  double* rg2_g = nullptr;
+  if (resgrad2_shape_ok(es, p.m, p.n, p.l)) {
+    rg2_ws = c.take(resgrad2_ws_bytes(p.n));
+    rg2_g = static_cast<double*>(c.take(sizeof(double) * p.n * p.l * resgrad2_groups(p.n)));
+    if (!rg_err) rg_err = static_cast<int*>(c.take(256));
+  }
+  if (out) *out = KernelWs{pp, gp, part, ticket, scal, rg_ws, rg_s, rg_g, rg_err, rg2_ws, rg2_g};
   return c.off + 256;
 }
 
@@ -2167,6 +2177,53 @@ int glx_residual_gradient(int dtype, int64_t m, int64_t n, int64_t l, const void
       launch_atr<float>(p, (const float*)A, (const float*)R, gp, st);
       if (p.atr_S > 1) launch_sum_partials<float>(gp, p.atr_S, (float*)G, n * l, st);
     }
+    check_launch();
+  });
+}
+
+int glx_residual_gradient2(int dtype, int64_t m, int64_t n, int64_t l, const void* A, const void* X0,
+                           const void* X1, const void* B, void* R0, void* R1, void* G, void* ws,
+                           size_t wsb, int one_pass, int* one_pass_ran, void* stream) {
+  return guarded([&] {
+    hipStream_t st = static_cast<hipStream_t>(stream);
+    GemmPlan p;
+    KernelWs k = kernel_setup(dtype, m, n, l, ws, wsb, 0, st, &p);
+    const bool fused = one_pass != 0 && dtype == GLX_F64 && k.rg2_ws != nullptr && resgrad2_device_ok();
+    if (one_pass_ran) *one_pass_ran = fused ? 1 : 0;
+    if (fused) {
+      resgrad2_reset(k.rg2_ws, n, st);
+      GLX_HIP(hipMemsetAsync(k.rg_err, 0, sizeof(int), st));
+      double* pp = static_cast<double*>(k.pp);   // two slabs: A X0, A X1
+      launch_resgrad2((const double*)A, (const double*)X0, (const double*)X1, (const double*)B, pp,
+                      pp + m * l, k.rg2_g, k.rg2_ws, 1, m, n, k.rg_err, st);
+      check_launch();
+      double* rs[3] = {(double*)R0, (double*)R1, nullptr};
+      launch_finalize_residual<double>(pp, 1, (const double*)B, 2, rs, m * l, nullptr, 0, 1,
+                                       nullptr, 0, nullptr, nullptr, 0.0, nullptr,
+                                       Red{k.part, k.ticket, k.scal}, st);
+      launch_sum_partials<double>(k.rg2_g, resgrad2_groups(n), (double*)G, n * l, st);
+      check_launch();
+      int herr = 0;   // valid only if no hand-off wait timed out (the call is synchronous)
+      GLX_HIP(hipMemcpyAsync(&herr, k.rg_err, sizeof(int), hipMemcpyDeviceToHost, st));
+      GLX_HIP(hipStreamSynchronize(st));
+      if (std::getenv("GLX_RG_VERBOSE")) std::fprintf(stderr, "glx_residual_gradient2: one-pass err flag %d\n", herr);
+      if (herr == 0) return;
+      if (one_pass_ran) *one_pass_ran = 0;
+    }
+    auto two = [&](auto* Ap) {
+      typedef std::remove_const_t<std::remove_pointer_t<decltype(Ap)>> T;
+      const T* xs[3] = {(const T*)X0, (const T*)X1, nullptr};
+      T* rs[3] = {(T*)R0, (T*)R1, nullptr};
+      launch_ax<T>(p, 2, Ap, xs, (T*)k.pp, nullptr, 0, st);
+      launch_finalize_residual<T>((const T*)k.pp, ax_split(p, 2), (const T*)B, 2, rs, m * l, nullptr, 0,
+                                  1, nullptr, 0, nullptr, nullptr, 0.0, nullptr,
+                                  Red{k.part, k.ticket, k.scal}, st);
+      T* gp = p.atr_S > 1 ? (T*)k.gp : (T*)G;
+      launch_atr<T>(p, Ap, (const T*)R1, gp, st);
+      if (p.atr_S > 1) launch_sum_partials<T>(gp, p.atr_S, (T*)G, n * l, st);
+    };
+    if (dtype == GLX_F64) two((const double*)A);
+    else two((const float*)A);
     check_launch();
   });
 }

@@ -82,6 +82,9 @@ _SIGS = {
     "glx_residual_gradient": (c_int, [c_int, c_int64, c_int64, c_int64, c_void_p, c_void_p,
                                       c_void_p, c_void_p, c_void_p, c_void_p, c_size_t,
                                       c_int, POINTER(c_int), c_void_p]),
+    "glx_residual_gradient2": (c_int, [c_int, c_int64, c_int64, c_int64, c_void_p, c_void_p,
+                                       c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
+                                       c_void_p, c_size_t, c_int, POINTER(c_int), c_void_p]),
     "glx_prox": (c_int, [c_int, c_int64, c_int64, c_void_p, c_double, c_double, c_double,
                          c_void_p, c_void_p, c_void_p, c_size_t, c_void_p]),
     "glx_kernel_workspace_bytes": (c_int, [c_int, c_int64, c_int64, c_int64, POINTER(c_size_t)]),

@@ -96,6 +96,27 @@ def residual_gradient(A: torch.Tensor, X: torch.Tensor, B: torch.Tensor, one_pas
     return R, G, bool(fused.value)
 
 
+def residual_gradient2(A: torch.Tensor, X0: torch.Tensor, X1: torch.Tensor, B: torch.Tensor,
+                       one_pass: bool = True
+                       ) -> Tuple[torch.Tensor, torch.Tensor, torch.Tensor, bool]:
+    """The line-search trial's batch and the next gradient: R0 = A X0 - B, R1 = A X1 - B and
+    G = A^T R1, with one read of A (the l = 16 role-split kernel) where the shape and device
+    allow it, else A @ [X0 | X1] then A^T R1. Returns (R0, R1, G, one_pass_ran)."""
+    m, n = A.shape
+    l = X0.shape[1]
+    dt = _dt(A)
+    R0 = torch.empty((m, l), dtype=A.dtype, device=A.device)
+    R1 = torch.empty((m, l), dtype=A.dtype, device=A.device)
+    G = torch.empty((n, l), dtype=A.dtype, device=A.device)
+    ws = _ws(dt, m, n, l, A.device)
+    ran = ctypes.c_int(0)
+    check(lib().glx_residual_gradient2(dt, m, n, l, A.data_ptr(), X0.data_ptr(), X1.data_ptr(),
+                                       B.data_ptr(), R0.data_ptr(), R1.data_ptr(), G.data_ptr(),
+                                       ws.data_ptr(), ws.numel(), 1 if one_pass else 0,
+                                       ctypes.byref(ran), _stream(A.device)))
+    return R0, R1, G, bool(ran.value)
+
+
 def prox(W: torch.Tensor, t: float, mu: float, thres: float = 1e-3
          ) -> Tuple[torch.Tensor, torch.Tensor]:
     """Group prox with the reference's denominator quirk; returns (X, [sum ||x_i||, max|x|])."""

@@ -194,6 +194,17 @@ int glx_prox(int dtype, int64_t n, int64_t l, const void* W, double t, double mu
 int glx_residual_gradient(int dtype, int64_t m, int64_t n, int64_t l, const void* A, const void* X,
                           const void* B, void* R, void* G, void* workspace, size_t workspace_bytes,
                           int one_pass, int* one_pass_ran, void* stream);
+/* The line-search trial's batch and the next gradient (round 4, SURVEY §8f row 1 at l = 16):
+ * R0 = A X0 - B, R1 = A X1 - B (the reference's A @ z and A @ p_thr, gl_ProxGD_primal.py:89-92,
+ * :112) and G = A^T R1 (:129 at the candidate). one_pass = 1: one read of A by the role-split
+ * kernel (kernels_rg2.hip) where the shape allows it (fp64, l = 16, n = 256 P with P a power of
+ * two in 2..128, m a multiple of 16 * 256 / P, >= 256 CUs); a timed-out hand-off wait inside it
+ * (error flag read back: the one-pass call is synchronous) or another shape runs A @ [X0 | X1],
+ * then A^T R1. *one_pass_ran (may be NULL) = 1 when the outputs come from the one-pass kernel. */
+int glx_residual_gradient2(int dtype, int64_t m, int64_t n, int64_t l, const void* A, const void* X0,
+                           const void* X1, const void* B, void* R0, void* R1, void* G,
+                           void* workspace, size_t workspace_bytes, int one_pass,
+                           int* one_pass_ran, void* stream);
 /* Workspace bytes for the single-kernel entry points above. */
 int glx_kernel_workspace_bytes(int dtype, int64_t m, int64_t n, int64_t l, size_t* bytes);
 /* One-line description of the kernels (tile, split) the planner picks for this shape, for
