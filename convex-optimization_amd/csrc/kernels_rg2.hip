@@ -53,6 +53,10 @@ constexpr int kRLA = 32;                // phase-A columns: z | p_thr
 constexpr int kRLB = 16;                // phase-B columns (l)
 constexpr int kRBlk = 16 * kRLA;        // 512 values of a block's partial
 constexpr int kRSlot = 3;               // LDS partial ring (A-waves may run 3 blocks ahead)
+#ifndef GLX_RG2_AB
+#define GLX_RG2_AB 4
+#endif
+constexpr int kRAB = GLX_RG2_AB;        // A-wave tile buffers (kRAB - 1 blocks of A in flight)
 // B-wave lags (template D1, D2): iteration j publishes block j's partial, runs hop 1 of block
 // j - D1 and hop 2 + phase B of block j - D2. Granule rings per row group (memory): a workgroup Y
 // publishes block j only after its hop 2 of j - 1 - D2, which needed r of that block, which needed
@@ -64,10 +68,16 @@ __host__ __device__ constexpr int rg_ring(int d2) { return d2 + 1; }
 constexpr int kRMaxPg = pg_ring(3, 6), kRMaxRg = rg_ring(6);
 constexpr int kRGrid = 256;
 
+// XL (XCD-local hand-off, as kernels_fused.hip's put_value): every reader of a row group's
+// granules runs on the writer's XCD, so a plain store (the vector L1 is write-through: the line
+// lands in that XCD's L2) is enough for the readers' sc1 loads; otherwise sc1 (write-through)
+// stores, visible on every XCD.
+template <bool XL>
 __device__ inline void put_gran(u64* g, unsigned tag, double v) {
   const u64 u = (u64)__double_as_longlong(v);
-  __hip_atomic_store(g, ((u64)tag << 32) | (u & 0xffffffffull), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  __hip_atomic_store(g + 1, ((u64)tag << 32) | (u >> 32), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  constexpr int scope = XL ? __HIP_MEMORY_SCOPE_WORKGROUP : __HIP_MEMORY_SCOPE_AGENT;
+  __hip_atomic_store(g, ((u64)tag << 32) | (u & 0xffffffffull), __ATOMIC_RELAXED, scope);
+  __hip_atomic_store(g + 1, ((u64)tag << 32) | (u >> 32), __ATOMIC_RELAXED, scope);
 }
 struct Gr { u64 w0, w1; };
 __device__ inline Gr get_gran(const u64* g) {
@@ -92,12 +102,12 @@ __device__ inline void lds_add(unsigned* p) {
 }
 }  // namespace
 
-template <int D1, int D2>
+template <int D1, int D2, bool XL>
 __global__ __launch_bounds__(kRThreads, 1) void k_resgrad2(
     const double* __restrict__ A, const double* __restrict__ X0, const double* __restrict__ X1,
     const double* __restrict__ B, double* __restrict__ P0, double* __restrict__ P1,
-    double* __restrict__ Gs, u64* Pg, u64* Rg, unsigned epoch0, int64_t m, int64_t n, int RG,
-    int NB, int* err, unsigned spin_max) {
+    double* __restrict__ Gs, u64* Pg, u64* Rg, unsigned* xslot, unsigned epoch0, int64_t m,
+    int64_t n, int RG, int NB, int* err, unsigned spin_max) {
   __shared__ __attribute__((aligned(16))) double xs[4][kRCols * kRLA];          // 64 KiB
   __shared__ __attribute__((aligned(16))) double part[kRSlot][4][kRBlk];        // 48 KiB
   __shared__ __attribute__((aligned(16))) double rsh[2][16 * kRLB];             // 4 KiB
@@ -109,7 +119,26 @@ __global__ __launch_bounds__(kRThreads, 1) void k_resgrad2(
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int i = lane & 15, q = lane >> 4;
   const int P = (int)(n / kRPanel);
-  const int rg = (int)blockIdx.x % RG, pnl = (int)blockIdx.x / RG;
+  // XL: the row group is this workgroup's XCD (HW_REG_XCC_ID; RG = 8) and the panel its arrival
+  // order there (xslot, zeroed before the launch); a workgroup beyond P on one XCD flags err = 2
+  // and leaves, the others of its XCD then time out (bad: every later wait returns at once) and
+  // the host recomputes with two passes.
+  __shared__ int xl_id[2];
+  if (XL) {
+    if (tid == 0) {
+      const int xcc = (int)(__builtin_amdgcn_s_getreg((3 << 11) | 20) & 7);   // HW_REG_XCC_ID[3:0]
+      xl_id[0] = xcc;
+      xl_id[1] = (int)__hip_atomic_fetch_add(xslot + xcc * 32, 1u, __ATOMIC_RELAXED,
+                                             __HIP_MEMORY_SCOPE_AGENT);
+    }
+    __syncthreads();
+  }
+  const int rg = XL ? xl_id[0] : (int)blockIdx.x % RG;
+  const int pnl = XL ? xl_id[1] : (int)blockIdx.x / RG;
+  if (XL && (pnl >= P || rg >= RG)) {
+    if (tid == 0) __hip_atomic_store(err, 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    return;
+  }
   const int64_t rbase = (int64_t)rg * (m / RG);
   const int wc = wave & 3;                                   // column slot of the wave
   const int64_t col0 = (int64_t)pnl * kRPanel + (int64_t)wc * kRCols;
@@ -139,7 +168,7 @@ __global__ __launch_bounds__(kRThreads, 1) void k_resgrad2(
     unsigned spins = 0;
     while (!__all(lds_get(ctr) >= want)) {
       __builtin_amdgcn_s_sleep(1);
-      if (++spins > spin_max) {
+      if (++spins > spin_max || bad) {
         fail();
         return;
       }
@@ -149,7 +178,9 @@ __global__ __launch_bounds__(kRThreads, 1) void k_resgrad2(
   if (wave < 4) {
     // ------------------------------------------------------------------ A-wave: phase A
     const double* xw = &xs[wc][0];
-    double a[2][4][4];   // two tile buffers: [chunk][e], row rbase + 16 b + i, cols col0 + 16 ch + 4 q + e
+    // AB tile buffers, AB - 1 blocks in flight (round 4: with one block ahead the A-waves waited
+    // a whole HBM latency per block); [chunk][e], row rbase + 16 b + i, cols col0 + 16 ch + 4 q + e
+    double a[kRAB][4][4];
     auto load_tile = [&](double (&t)[4][4], int b) {
       b = b < NB ? b : NB - 1;
       const double* ap = A + (rbase + 16 * (int64_t)b + i) * n + col0 + 4 * q;
@@ -187,13 +218,15 @@ __global__ __launch_bounds__(kRThreads, 1) void k_resgrad2(
       }
       lds_add(&cnt_part[s]);
     };
-    load_tile(a[0], 0);
-    for (int b = 0; b < NB; b += 2) {
-      load_tile(a[1], b + 1);
-      phase_a(a[0], b);
-      if (b + 1 >= NB) break;
-      load_tile(a[0], b + 2);
-      phase_a(a[1], b + 1);
+#pragma unroll
+    for (int d = 0; d < kRAB - 1; ++d) load_tile(a[d], d);
+    for (int b = 0; b < NB; b += kRAB) {
+#pragma unroll
+      for (int h = 0; h < kRAB; ++h) {
+        if (b + h >= NB) break;
+        load_tile(a[(h + kRAB - 1) % kRAB], b + h + kRAB - 1);
+        phase_a(a[h], b + h);
+      }
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the clamped re-loads, before exit
     return;
@@ -225,26 +258,30 @@ __global__ __launch_bounds__(kRThreads, 1) void k_resgrad2(
     while (!__all(gr_ok(x, tag))) {
       __builtin_amdgcn_s_sleep(1);
       if (!gr_ok(x, tag)) x = get_gran(g);
-      if (++spins > spin_max) {
+      if (++spins > spin_max || bad) {
         if (!gr_ok(x, tag)) fail();
         break;
       }
     }
     return gr_val(x);
   };
-  // phase B tile of block b: lane (i, q) holds A[row 4 s + q][col0 + 16 ct + i]
-  double at[4][4];
-  auto load_at = [&](int b) {
+  // phase B tile of block b: lane (i, q) holds A[row 4 s + q][col0 + 16 ct + i]; two tiles,
+  // loaded two blocks ahead (their latency overlaps two iterations of hop waits)
+  double at[2][4][4];
+  auto load_at = [&](double (&t)[4][4], int b) {
+    b = b < NB ? b : NB - 1;
     const double* ap = A + (rbase + 16 * (int64_t)b + q) * n + col0 + i;
 #pragma unroll
     for (int s = 0; s < 4; ++s)
 #pragma unroll
-      for (int ct = 0; ct < 4; ++ct) at[s][ct] = ap[(int64_t)4 * s * n + 16 * ct];
+      for (int ct = 0; ct < 4; ++ct) t[s][ct] = ap[(int64_t)4 * s * n + 16 * ct];
   };
 
-  // phase B's tile is loaded one iteration ahead (its latency overlaps the hop waits)
-  load_at(0);
-  for (int j = 0; j < NB + D2; ++j) {
+  load_at(at[0], 0);
+  load_at(at[1], 1);
+  // one B iteration; tb = the tile buffer of block j - D2 (constant after inlining: the loop
+  // below runs two iterations per trip)
+  auto iter = [&](int j, double (&tb)[4][4]) {
     const int b1 = j - D1, b2 = j - D2;
     // issue this iteration's remote reads first (vmcnt retires in order)
     Gr h1[2];
@@ -265,7 +302,7 @@ __global__ __launch_bounds__(kRThreads, 1) void k_resgrad2(
       for (int h = 0; h < 2; ++h) {
         const int v = bl + 256 * h;
         const double sv = ((part[s][0][v] + part[s][1][v]) + part[s][2][v]) + part[s][3][v];
-        put_gran(pg_at(j, pnl, v), tag_of(j), sv);
+        put_gran<XL>(pg_at(j, pnl, v), tag_of(j), sv);
       }
       lds_add(&cnt_free[s]);
     }
@@ -280,12 +317,12 @@ __global__ __launch_bounds__(kRThreads, 1) void k_resgrad2(
           P0[row * kRLB + vcol] = sum;
         } else {
           P1[row * kRLB + (vcol - 16)] = sum;
-          put_gran(rg_at(b1, vrow * kRLB + (vcol - 16)), tag_of(b1), sum - bv);
+          put_gran<XL>(rg_at(b1, vrow * kRLB + (vcol - 16)), tag_of(b1), sum - bv);
         }
       }
     }
     // 3. block b2, hop 2 + phase B
-    if (do2) {
+    if (do2 && b2 < NB) {
       const int rs = b2 & 1;
       if (b2 >= 2) spin_wait(&cnt_rfree[rs], 4u * (unsigned)(b2 / 2));
       rsh[rs][bl] = sweep(rg_at(b2, bl), tag_of(b2), h2);
@@ -295,11 +332,16 @@ __global__ __launch_bounds__(kRThreads, 1) void k_resgrad2(
       for (int s = 0; s < 4; ++s) {
         const double rr = rsh[rs][(4 * s + q) * kRLB + i];
 #pragma unroll
-        for (int ct = 0; ct < 4; ++ct) gacc[ct] = MF<double>::mma(at[s][ct], rr, gacc[ct]);
+        for (int ct = 0; ct < 4; ++ct) gacc[ct] = MF<double>::mma(tb[s][ct], rr, gacc[ct]);
       }
       lds_add(&cnt_rfree[rs]);
-      if (b2 + 1 < NB) load_at(b2 + 1);
+      if (b2 + 2 < NB) load_at(tb, b2 + 2);
     }
+  };
+  constexpr int p0 = D2 & 1;   // tile buffer of block j - D2 for even j
+  for (int j = 0; j < NB + D2; j += 2) {
+    iter(j, at[p0]);
+    if (j + 1 < NB + D2) iter(j + 1, at[p0 ^ 1]);
   }
   double* gout = Gs + (int64_t)rg * n * kRLB;
 #pragma unroll
@@ -315,7 +357,7 @@ __global__ __launch_bounds__(kRThreads, 1) void k_resgrad2(
 // shape / device checks and launch
 // ---------------------------------------------------------------------------------------------
 struct Rg2Layout {
-  size_t pg, rg, total;
+  size_t pg, rg, xs, total;
 };
 static Rg2Layout rg2_layout(int64_t n) {
   const int64_t P = n / kRPanel, RG = kRGrid / P;
@@ -323,7 +365,8 @@ static Rg2Layout rg2_layout(int64_t n) {
   Rg2Layout L;
   L.pg = 0;
   L.rg = up(sizeof(u64) * 2 * (size_t)RG * kRMaxPg * P * kRBlk);
-  L.total = L.rg + up(sizeof(u64) * 2 * (size_t)RG * kRMaxRg * 16 * kRLB) + 256;
+  L.xs = L.rg + up(sizeof(u64) * 2 * (size_t)RG * kRMaxRg * 16 * kRLB);
+  L.total = L.xs + 8 * 32 * sizeof(unsigned) + 256;
   return L;
 }
 
@@ -344,7 +387,7 @@ bool resgrad2_device_ok() {
     ok = 0;
     if (hipGetDevice(&dev) == hipSuccess &&
         hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess &&
-        hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, reinterpret_cast<const void*>(k_resgrad2<2, 4>),
+        hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, reinterpret_cast<const void*>(k_resgrad2<2, 4, true>),
                                                      kRThreads, 0) == hipSuccess)
       ok = (cus >= kRGrid && occ >= 1) ? 1 : 0;
   }
@@ -366,6 +409,7 @@ void launch_resgrad2(const double* A, const double* X0, const double* X1, const 
   char* w = static_cast<char*>(ws);
   u64* pg = reinterpret_cast<u64*>(w + L.pg);
   u64* rgp = reinterpret_cast<u64*>(w + L.rg);
+  unsigned* xs = reinterpret_cast<unsigned*>(w + L.xs);
   const unsigned ep = (unsigned)((launch_count - 1) * (unsigned)(NB + 8));
   static const unsigned spin_max = [] {
     const char* v = std::getenv("GLX_RG_SPIN");
@@ -378,16 +422,28 @@ void launch_resgrad2(const double* A, const double* X0, const double* X1, const 
     const int x = v && *v ? std::atoi(v) : 24;
     return (x == 12 || x == 23 || x == 24 || x == 36) ? x : 24;
   }();
+  // XCD-local hand-off where the row groups are the 8 XCDs (GLX_RG_XCD=0: the agent-scope form)
+  static const bool xcd = [] {
+    const char* v = std::getenv("GLX_RG_XCD");
+    return !(v && v[0] == '0');
+  }();
+  const bool xl = xcd && RG == 8;
   auto go = [&](auto kern) {
     glx_launch(kern, dim3((unsigned)(RG * P)), dim3(kRThreads), 0, st, A, X0, X1, B, P0, P1, Gs, pg, rgp,
-               ep, m, n, (int)RG, (int)NB, err, spin_max);
+               xs, ep, m, n, (int)RG, (int)NB, err, spin_max);
   };
-  switch (lag) {
-    case 12: go(k_resgrad2<1, 2>); break;
-    case 23: go(k_resgrad2<2, 3>); break;
-    case 36: go(k_resgrad2<3, 6>); break;
-    default: go(k_resgrad2<2, 4>); break;
-  }
+  auto lags = [&](auto k12, auto k23, auto k24, auto k36) {
+    switch (lag) {
+      case 12: go(k12); break;
+      case 23: go(k23); break;
+      case 36: go(k36); break;
+      default: go(k24); break;
+    }
+  };
+  if (xl)
+    lags(k_resgrad2<1, 2, true>, k_resgrad2<2, 3, true>, k_resgrad2<2, 4, true>, k_resgrad2<3, 6, true>);
+  else
+    lags(k_resgrad2<1, 2, false>, k_resgrad2<2, 3, false>, k_resgrad2<2, 4, false>, k_resgrad2<3, 6, false>);
 }
 
 }  // namespace glx

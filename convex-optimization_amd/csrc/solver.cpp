@@ -153,8 +153,12 @@ static void validate(const glx_problem* P, const glx_opts* O) {
 // 3543 / 6756 / 9748 vs 3623 / 6884 / 11162. GLX_SPLIT_CAND=1 forces it at any size (tests).
 static constexpr double kSplitMinBytes = 768.0 * 1024 * 1024;
 static int split_mode(const glx_problem& P, const glx_opts& O) {
-  if (O.exact_objective != 0 || P.dtype != GLX_F64) return 0;
+  if (O.exact_objective != 0) return 0;
   if (P.method != GLX_PROXGD && P.method != GLX_FPROXGD) return 0;
+  if (P.dtype != GLX_F64) {   // fp32 FProxGD: experiment (GLX_SPLIT_F32=1)
+    const char* f = std::getenv("GLX_SPLIT_F32");
+    if (!(f && std::strcmp(f, "1") == 0 && P.method == GLX_FPROXGD)) return 0;
+  }
   if (O.split_cand == 2) return 0;
   const char* sc = O.split_cand == 0 ? std::getenv("GLX_SPLIT_CAND") : nullptr;
   if (sc && std::strcmp(sc, "0") == 0) return 0;
