@@ -190,7 +190,7 @@ void launch_ax(const GemmPlan& p, int nsrc, const T* A, const T* const* X, T* P,
 template <typename T>
 bool launch_ax_dma(const GemmPlan& p, int code, int nsrc, int S, const T* A, const T* const* X, T* P,
                    const int* gate, int epoch, hipStream_t st, Pub pub);
-int dma_lds_need(int code, int64_t l, int nsrc);
+int dma_lds_need(int code, int64_t l, int nsrc, int esize);
 int dma_waves(int code);   // waves per workgroup of a kind-8/9 code (last digit; 1 = 16)
 int dma_mt(int code);      // 16-row tiles per wave (kind 9: 2)
 // Infinity-Cache hand-off between the passes (tuning experiment; MiB of A fetched with the

@@ -1,5 +1,5 @@
 // kernels_axdma.hip — A @ X (reference: gl_ProxGD_primal.py:25,61,129 `A @ x`) with A and X
-// staged in LDS by LDS-DMA, f64 (kind 8 of the A @ X planner, kernels_gemm.hip).
+// staged in LDS by LDS-DMA, f64 and f32 (kinds 8/9 of the A @ X planner, kernels_gemm.hip).
 #include "glx_mfma.h"
 
 namespace glx {
@@ -23,12 +23,16 @@ namespace glx {
 //
 // LDS images (one __shared__ array; the DMA destination is lane-linear, so swizzles go on the
 // SOURCE address, cdna_hip_programming.md §5.4 rule 21):
-//   A: wave's [16][KC/2] 16-B slots, slot s of row i stored at s ^ sw(i). Lane (i, q) reads
-//      slots s = q + 4j (j < KC/8), i.e. k = 2s + e — conflict-free ds_read_b128 for every
-//      4 x 16-lane group (MI355X_MICROARCH.md §LDS), checked by scripts/lds_banks.py.
-//   X: per source KC rows of l values as 128-B units (k * NT + half); unit u stored at
-//      u ^ ((k >> 1) & 1), so the two 16-lane halves of a ds_read_b64 group (lane groups
-//      q = 0/1 and 2/3 read rows k = 2(q + 4j) + e) fall on different bank halves.
+//   A: wave's [16][SLR] 16-B slots (SLR = KC / EV, EV = 16 / sizeof(T) values per slot), slot s
+//      of row i stored at s ^ sw(i). Lane (i, q) reads slots s = q + 4j (j < SLR / 4), i.e.
+//      k = EV s + e — conflict-free ds_read_b128 for every 4 x 16-lane group
+//      (MI355X_MICROARCH.md §LDS), checked by scripts/lds_banks.py. f32 with KC = 64 has the
+//      same byte image as f64 with KC = 32 (256-B row pieces).
+//   X: per source KC rows of l values as 16-value units of UB = 16 sizeof(T) bytes (k * NT +
+//      half); unit u stored at u ^ ((k / EV) & (EV - 1)). f64 (ds_read_b64): the two 16-lane
+//      halves of a group (lane groups q = 0/1 and 2/3 read rows k = 2(q + 4j) + e) fall on
+//      different bank halves; f32 (ds_read_b32, all 64 lanes at once): the four lane groups'
+//      64-B units (rows k = 4(q + 4j) + e) land on the four different 16-bank quarters.
 // MFMA operand maps as in kind 5 (k permuted inside a chunk, X read with the same permutation).
 // Past the end of a block's K range the ring re-issues the last chunk (an L2 hit, discarded),
 // so every wave's DMA count per chunk is the same constant the counted vmcnt needs.
@@ -44,10 +48,11 @@ __device__ inline void glds16(const void* src, void* lds_base) {
 
 // LDS bytes of a kind-8 tile: NS slots of WAVES 16-row A chunks + the X chunk of every source
 // (+ 1 KiB dummy when the X pieces do not divide evenly among the waves)
-template <int NT, int NSRC, int NS, int KC, int WAVES, int MT = 1>
+template <typename T, int NT, int NSRC, int NS, int KC, int WAVES, int MT = 1>
 constexpr int dma_lds_bytes() {
-  return NS * (WAVES * 16 * MT * KC * 8 + NSRC * KC * 16 * NT * 8) +
-         ((NSRC * KC * 16 * NT * 8 / 1024) % WAVES ? 1024 : 0);
+  constexpr int es = (int)sizeof(T);
+  return NS * (WAVES * 16 * MT * KC * es + NSRC * KC * 16 * NT * es) +
+         ((NSRC * KC * 16 * NT * es / 1024) % WAVES ? 1024 : 0);
 }
 
 // Infinity-Cache hand-off (GemmPlan::ax_keep_mib, a kernel argument; the solver's default is
@@ -55,8 +60,9 @@ constexpr int dma_lds_bytes() {
 // block's walk are fetched with the default policy instead, about that many MiB of A over the
 // grid, so they stay in the 256 MiB Infinity Cache for the next pass (A^T R).
 
-template <int KC>
-__device__ inline int dma_sw(int i) { return KC >= 32 ? (i & 15) : ((i >> 1) & 7); }
+// A slot swizzle of row i for SLR 16-B slots per row piece
+template <int SLR>
+__device__ inline int dma_sw(int i) { return SLR >= 16 ? (i & 15) : ((i >> 1) & 7); }
 
 template <typename T, int NT, int NSRC, int NS, int KC, int WAVES, bool NTL, bool HOIST, bool PIPE,
           int MT>
@@ -68,12 +74,17 @@ __global__ __launch_bounds__(64 * WAVES) void k_ax_dma(const T* __restrict__ A,
                                                       int64_t chunks, int S, int gx, int xmap,
                                                       const int* __restrict__ gate, int epoch,
                                                       Pub pub, int keep_mib) {
-  static_assert(sizeof(T) == 8, "f64 tile");
   typedef MF<T> M;
   typedef typename M::acc_t C;
+  typedef typename M::vec_t V;                      // one 16-B slot of A
+  constexpr int ES = (int)sizeof(T);
+  constexpr int EV = 16 / ES;                       // values per 16-B slot (2 f64, 4 f32)
+  constexpr int UB = 16 * ES;                       // bytes of one 16-value X unit
+  constexpr int LPU = UB / 16;                      // DMA lanes per X unit
+  constexpr int UPI = 1024 / UB;                    // X units per DMA wave-instruction
   constexpr int L = 16 * NT;
   constexpr int NC = NT * NSRC;
-  constexpr int SLR = KC / 2;                       // 16-B slots per row of an A chunk
+  constexpr int SLR = KC / EV;                      // 16-B slots per row of an A chunk
   constexpr int AW = 16 * MT * KC * (int)sizeof(T); // one wave's A chunk (MT 16-row tiles)
   constexpr int NIA = AW / 1024;                    // its LDS-DMA instructions
   constexpr int XS = KC * L * (int)sizeof(T);       // one source's X chunk
@@ -85,7 +96,7 @@ __global__ __launch_bounds__(64 * WAVES) void k_ax_dma(const T* __restrict__ A,
   constexpr int LDSB = NS * SLOT + (XDUP ? 1024 : 0);
   constexpr int NI = NIA + NIX;                     // DMA instructions per wave and chunk
   constexpr int D = NS - 1;                         // chunks in flight beyond the computed one
-  constexpr int JN = KC / 8;                        // ds_read_b128 of A per lane and chunk
+  constexpr int JN = SLR / 4;                       // ds_read_b128 of A per lane and chunk
   constexpr int WAITN = (D - 1) * NI;
   static_assert(KC == 16 || KC == 32 || KC == 64, "chunk of 16, 32 or 64 columns");
   static_assert(XS % 1024 == 0 && AW % 1024 == 0, "whole 1-KiB pieces");
@@ -125,21 +136,21 @@ __global__ __launch_bounds__(64 * WAVES) void k_ax_dma(const T* __restrict__ A,
     const int ls = 64 * t + lane, ri = ls / SLR, p = ls % SLR;
     int64_t r = row0 + ri;
     r = r < m ? r : m - 1;
-    asrc[t] = A + r * n + cb * KC + 2 * (p ^ dma_sw<KC>(ri & 15));
+    asrc[t] = A + r * n + cb * KC + EV * (p ^ dma_sw<SLR>(ri & 15));
   }
-  // X pieces: instruction tx = wave + WAVES r of the block covers 128-B units 8 tx .. 8 tx + 7
+  // X pieces: instruction tx = wave + WAVES r of the block covers the UPI units UPI tx ..
   const T* xsrc[NIX];
   int xdst[NIX];
 #pragma unroll
   for (int r = 0; r < NIX; ++r) {
     const int tx = wave + WAVES * r;
     const int txc = tx % NXT;                        // surplus: a real piece into the dummy
-    const int pu = 8 * txc + (lane >> 3);
+    const int pu = UPI * txc + lane / LPU;
     const int src = pu / (KC * NT), u = pu % (KC * NT);
     const int k = u / NT;
-    const int us = u ^ ((k >> 1) & 1);
+    const int us = u ^ ((k / EV) & (EV - 1));
     const T* xb = src == 0 ? X0 : (src == 1 ? X1 : X2);
-    xsrc[r] = xb + (cb * KC + us / NT) * L + (us % NT) * 16 + (lane & 7) * 2;
+    xsrc[r] = xb + (cb * KC + us / NT) * L + (us % NT) * 16 + (lane % LPU) * EV;
     xdst[r] = tx < NXT ? WAVES * AW + tx * 1024 : -1;
   }
   const int64_t rot = ax_rot(xmap, bx, gx, nch);
@@ -172,40 +183,42 @@ __global__ __launch_bounds__(64 * WAVES) void k_ax_dma(const T* __restrict__ A,
 #pragma unroll
     for (int c = 0; c < NC; ++c) acc[mt][c] = C{};
 
-  // lane (i, q): A slots q + 4j of row i; X units of rows k = 2(q + 4j) + e, (k >> 1) & 1 = q & 1
+  // lane (i, q): A slots q + 4j of row i; X units of rows k = EV (q + 4j) + e, whose swizzle
+  // (k / EV) & (EV - 1) = q & (EV - 1)
   const int aoff = wave * AW + i * (SLR * 16);
   int asl[MT][JN];
 #pragma unroll
   for (int mt = 0; mt < MT; ++mt)
 #pragma unroll
-    for (int j = 0; j < JN; ++j) asl[mt][j] = aoff + mt * 16 * SLR * 16 + 16 * ((q + 4 * j) ^ dma_sw<KC>(i));
-  const int xoff = WAVES * AW + 8 * i;
+    for (int j = 0; j < JN; ++j) asl[mt][j] = aoff + mt * 16 * SLR * 16 + 16 * ((q + 4 * j) ^ dma_sw<SLR>(i));
+  const int xoff = WAVES * AW + ES * i;
+  const int xq = q & (EV - 1);
   auto compute = [&](int slot) {
     const char* sb = lds + slot * SLOT;
-    d2_t av[JN];
+    V av[JN];
 #pragma unroll
-    for (int j = 0; j < JN; ++j) av[j] = *reinterpret_cast<const d2_t*>(sb + asl[0][j]);
+    for (int j = 0; j < JN; ++j) av[j] = *reinterpret_cast<const V*>(sb + asl[0][j]);
     if constexpr (HOIST) {
       // every LDS read of the chunk first, in MFMA order, then the MFMAs: the compiler's counted
       // lgkmcnt waits then retire them progressively instead of a wait per small read group
-      T xv[JN][2][NSRC][NT];
+      T xv[JN][EV][NSRC][NT];
 #pragma unroll
       for (int j = 0; j < JN; ++j)
 #pragma unroll
-        for (int e = 0; e < 2; ++e)
+        for (int e = 0; e < EV; ++e)
 #pragma unroll
           for (int src = 0; src < NSRC; ++src)
 #pragma unroll
             for (int nt = 0; nt < NT; ++nt) {
-              const int k = 2 * (q + 4 * j) + e;
-              const int unit = (k * NT + nt) ^ (q & 1);
-              xv[j][e][src][nt] = *reinterpret_cast<const T*>(sb + xoff + src * XS + unit * 128);
+              const int k = EV * (q + 4 * j) + e;
+              const int unit = (k * NT + nt) ^ xq;
+              xv[j][e][src][nt] = *reinterpret_cast<const T*>(sb + xoff + src * XS + unit * UB);
             }
       __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
       for (int j = 0; j < JN; ++j)
 #pragma unroll
-        for (int e = 0; e < 2; ++e)
+        for (int e = 0; e < EV; ++e)
 #pragma unroll
           for (int src = 0; src < NSRC; ++src)
 #pragma unroll
@@ -216,14 +229,14 @@ __global__ __launch_bounds__(64 * WAVES) void k_ax_dma(const T* __restrict__ A,
 #pragma unroll
     for (int j = 0; j < JN; ++j)
 #pragma unroll
-      for (int e = 0; e < 2; ++e) {
-        const int k = 2 * (q + 4 * j) + e;
+      for (int e = 0; e < EV; ++e) {
+        const int k = EV * (q + 4 * j) + e;
 #pragma unroll
         for (int src = 0; src < NSRC; ++src)
 #pragma unroll
           for (int nt = 0; nt < NT; ++nt) {
-            const int unit = (k * NT + nt) ^ (q & 1);
-            const T xv = *reinterpret_cast<const T*>(sb + xoff + src * XS + unit * 128);
+            const int unit = (k * NT + nt) ^ xq;
+            const T xv = *reinterpret_cast<const T*>(sb + xoff + src * XS + unit * UB);
             acc[0][src * NT + nt] = M::mma(av[j][e], xv, acc[0][src * NT + nt]);
           }
       }
@@ -238,32 +251,32 @@ __global__ __launch_bounds__(64 * WAVES) void k_ax_dma(const T* __restrict__ A,
     // takes chunk c + 1 + D.
     // (fp64 MFMA on live data holds the clock near 2.05-2.2 GHz, where A@X's 2 m n l flops
     // need ~125 us of MFMA pipe against ~158 us of streaming: scripts/axdma_ablate.hip.)
-    d2_t av[2][MT][JN];
-    T xv[2][JN][2][NSRC][NT];
-    auto read_ops = [&](int slot, d2_t (&a)[MT][JN], T (&x)[JN][2][NSRC][NT]) {
+    V av[2][MT][JN];
+    T xv[2][JN][EV][NSRC][NT];
+    auto read_ops = [&](int slot, V (&a)[MT][JN], T (&x)[JN][EV][NSRC][NT]) {
       const char* sb = lds + slot * SLOT;
 #pragma unroll
       for (int mt = 0; mt < MT; ++mt)
 #pragma unroll
-        for (int j = 0; j < JN; ++j) a[mt][j] = *reinterpret_cast<const d2_t*>(sb + asl[mt][j]);
+        for (int j = 0; j < JN; ++j) a[mt][j] = *reinterpret_cast<const V*>(sb + asl[mt][j]);
 #pragma unroll
       for (int j = 0; j < JN; ++j)
 #pragma unroll
-        for (int e = 0; e < 2; ++e)
+        for (int e = 0; e < EV; ++e)
 #pragma unroll
           for (int src = 0; src < NSRC; ++src)
 #pragma unroll
             for (int nt = 0; nt < NT; ++nt) {
-              const int k = 2 * (q + 4 * j) + e;
-              const int unit = (k * NT + nt) ^ (q & 1);
-              x[j][e][src][nt] = *reinterpret_cast<const T*>(sb + xoff + src * XS + unit * 128);
+              const int k = EV * (q + 4 * j) + e;
+              const int unit = (k * NT + nt) ^ xq;
+              x[j][e][src][nt] = *reinterpret_cast<const T*>(sb + xoff + src * XS + unit * UB);
             }
     };
-    auto mma_ops = [&](const d2_t (&a)[MT][JN], const T (&x)[JN][2][NSRC][NT]) {
+    auto mma_ops = [&](const V (&a)[MT][JN], const T (&x)[JN][EV][NSRC][NT]) {
 #pragma unroll
       for (int j = 0; j < JN; ++j)
 #pragma unroll
-        for (int e = 0; e < 2; ++e)
+        for (int e = 0; e < EV; ++e)
 #pragma unroll
           for (int mt = 0; mt < MT; ++mt)
 #pragma unroll
@@ -304,8 +317,8 @@ __global__ __launch_bounds__(64 * WAVES) void k_ax_dma(const T* __restrict__ A,
           // spread the NI DMAs over the first MFMAs (one after each), then the operand reads two
           // per MFMA, so the issue costs hide under the MFMA pipe instead of delaying it
           mma_ops(av[h], xv[h]);
-          constexpr int NMF = MT * JN * 2 * NSRC * NT;      // MFMAs per chunk and wave
-          constexpr int NRD = MT * JN + JN * 2 * NSRC * NT; // operand reads per chunk and wave
+          constexpr int NMF = MT * JN * EV * NSRC * NT;      // MFMAs per chunk and wave
+          constexpr int NRD = MT * JN + JN * EV * NSRC * NT; // operand reads per chunk and wave
 #pragma unroll
           for (int g = 0; g < NI; ++g) {
             __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);   // 1 MFMA
@@ -362,8 +375,8 @@ template <typename T, int NT, int NSRC, int NS, int KC, int WAVES, bool NTL, boo
           bool PIPE = false, int MT = 1>
 static void ax_dma_go(const GemmPlan& p, int S, const T* A, const T* const* X, T* P,
                       const int* gate, int epoch, hipStream_t st, Pub pub) {
-  if constexpr (sizeof(T) != 8 || dma_lds_bytes<NT, NSRC, NS, KC, WAVES, MT>() > 160 * 1024) {
-    throw Error{GLX_E_INVALID, "A@X: this LDS-DMA tile does not fit (f64 only, 160 KiB of LDS)"};
+  if constexpr (dma_lds_bytes<T, NT, NSRC, NS, KC, WAVES, MT>() > 160 * 1024) {
+    throw Error{GLX_E_INVALID, "A@X: this LDS-DMA tile does not fit (160 KiB of LDS)"};
   } else {
     const int gx = (int)cdiv(p.m, 16 * MT * WAVES);
     const int xmap = ax_xmap_flags(p, S);
@@ -385,6 +398,13 @@ static bool dma_code(const GemmPlan& p, int code, int S, const T* A, const T* co
   switch (code) {
     case 92278: ax_dma_go<T, NT, NSRC, 2, 32, 8, true, true, true, 2>(p, S, A, X, P, gate, epoch, st, pub); return true;
     case 92268: ax_dma_go<T, NT, NSRC, 2, 32, 8, false, true, true, 2>(p, S, A, X, P, gate, epoch, st, pub); return true;
+    // f32 (round 4): 64-column chunks, the same 256-B row pieces and LDS image as 92278 in f64
+    case 92478:
+      if constexpr (sizeof(T) == 4 && NSRC == 1) {
+        ax_dma_go<T, NT, NSRC, 2, 64, 8, true, true, true, 2>(p, S, A, X, P, gate, epoch, st, pub);
+        return true;
+      }
+      return false;
     default: return false;
   }
 }
@@ -393,10 +413,10 @@ int dma_waves(int code) { return code % 10 == 1 ? 16 : code % 10; }
 
 int dma_mt(int code) { return code / 10000 == 9 ? 2 : 1; }
 
-int dma_lds_need(int code, int64_t l, int nsrc) {
+int dma_lds_need(int code, int64_t l, int nsrc, int esize) {
   const int ns = (code / 1000) % 10, kc = 16 * ((code / 100) % 10), waves = dma_waves(code);
-  const int xb = nsrc * kc * (int)l * 8;
-  return ns * (waves * 16 * dma_mt(code) * kc * 8 + xb) + ((xb / 1024) % waves ? 1024 : 0);
+  const int xb = nsrc * kc * (int)l * esize;
+  return ns * (waves * 16 * dma_mt(code) * kc * esize + xb) + ((xb / 1024) % waves ? 1024 : 0);
 }
 
 template <typename T>

@@ -489,6 +489,7 @@ __global__ __launch_bounds__(256) void k_ax_valu(const T* __restrict__ A, const 
 static constexpr int kAxDefault = 52228;       // f64 single RHS: LDS, MT 2, PF 2, VPL 2, 8 waves
 static constexpr int kAxFallback = 21820;      // f64: VPL 2, direct loads, MT 8, PF 2
 static constexpr int kAxDefault32 = 21410;     // f32: VPL 2, direct loads, MT 4, PF 1
+static constexpr int kAxDma32 = 92478;         // f32 one RHS, A beyond the Infinity Cache (LDS-DMA)
 // A^T R code: NTL*1000 + WL*10 + PF (WL 1 = four panels of a block share rows, PF = ring depth)
 static constexpr int kAtrDefault = 108;        // f64: WL 0, PF 8 (A that stays in the MALL)
 static constexpr int kAtrDefaultBig = 1008;    // f64: non-temporal A, WL 0, PF 8
@@ -506,8 +507,9 @@ static int axb_default(int nsrc, int esize) {
 
 // the tiles the planner picks (lds_plan); the LDS-DMA sweep's other codes are in DESIGN.md
 static constexpr int kLdsCodes[] = {52224, 52324, 52228, 51328,
-                                     // kind 9 (LDS-DMA, f64, two row tiles per wave): 9 NS KC/16 flags WAVES
-                                     92278, 92268};
+                                     // kind 9 (LDS-DMA, two row tiles per wave): 9 NS KC/16 flags WAVES;
+                                     // 92278 / 92268 f64, 92478 f32 (one source)
+                                     92278, 92268, 92478};
 static inline bool dma_kind(int c) { return c / 10000 == 8 || c / 10000 == 9; }
 static inline bool lds_kind(int c) { return c / 10000 == 5 || dma_kind(c); }
 static bool lds_code_ok(int c, int64_t n, int64_t l, int esize, int nsrc = 1) {
@@ -515,8 +517,8 @@ static bool lds_code_ok(int c, int64_t n, int64_t l, int esize, int nsrc = 1) {
   for (int k : kLdsCodes) known |= (k == c);
   if (!known) return false;
   if (dma_kind(c))
-    return esize == 8 && (l == 16 || l == 32) && n % (16 * ((c / 100) % 10)) == 0 &&
-           dma_lds_need(c, l, nsrc) <= 160 * 1024;
+    return (c == kAxDma32 ? (esize == 4 && nsrc == 1) : esize == 8) && (l == 16 || l == 32) &&
+           n % (16 * ((c / 100) % 10)) == 0 && dma_lds_need(c, l, nsrc, esize) <= 160 * 1024;
   const int E = 16 / esize, vpl = (c / 10) % 10;
   return (l == 16 || l == 32) && n % (4 * E * vpl) == 0;
 }
@@ -614,6 +616,16 @@ GemmPlan make_plan(int esize, int64_t m, int64_t n, int64_t l, int ax_variant) {
     const int64_t waves = cdiv(m, 4);                    // RW = 4 rows per wave
     const int64_t kunits = n / (64 * (p.ax_vec ? E : 1)); // 64-lane strides per row
     p.ax_S = (int)clampi(cdiv(kTargetWaves, waves), 1, std::max<int64_t>(1, std::min<int64_t>(kMaxSplit, kunits / 4)));
+  } else if (esize == 4 && ax_variant == 0 && (double)m * (double)n * esize > kAtrNtBytes &&
+             lds_code_ok(kAxDma32, n, l, esize, 1) && env_int("GLX_AX_DMA", 1) != 0 &&
+             env_int("GLX_AX_DMA32", 0) != 0) {
+    // Round 4: f32 with one right-hand side and A beyond the Infinity Cache (C3's split-candidate
+    // dense pass A xc) on the LDS-DMA tile, as 92278 does for f64
+    p.ax_code = kAxDma32;
+    p.ax_kind = 5;
+    p.ax_S = lds_split(esize, m, n, kAxDma32);
+    p.ax_mt = 2;
+    p.ax_pf = 0;
   } else if (lds_code_ok(ax_variant ? ax_variant : (esize == 8 ? kAxDefault : kAxDefault32), n, l, esize)) {
     int code = ax_variant ? ax_variant : (esize == 8 ? kAxDefault : kAxDefault32);
     if (ax_variant) p.ax_S = lds_split(esize, m, n, code);

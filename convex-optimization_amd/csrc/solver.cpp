@@ -194,6 +194,8 @@ static GemmPlan session_plan(const glx_problem& P, const glx_opts& O) {
     if (P.n / 64 >= 256) {
       f.atr_wl = 2;
       f.atr_S = 1;
+      const char* pf16 = std::getenv("GLX_ATR_PF16");   // round 4 experiment: 16-step ring
+      if (pf16 && std::strcmp(pf16, "1") == 0) f.atr_pf = 16;
     }
     if (atr_prox_ok(f)) return f;   // only where the trial actually fuses (GLX_ATR_FUSE_SPLIT)
   }
@@ -423,6 +425,9 @@ class Session : public SessionBase {
     if (hs_) (void)hipHostFree(hs_);
     if (dc_ring_) (void)hipHostFree(dc_ring_);
     if (rb_event_) (void)hipEventDestroy(rb_event_);
+    if (ov_fork_) (void)hipEventDestroy(ov_fork_);
+    if (ov_join_) (void)hipEventDestroy(ov_join_);
+    if (side_) (void)hipStreamDestroy(side_);
     for (auto& v : ev_)
       for (auto& p : v) { (void)hipEventDestroy(p.a); (void)hipEventDestroy(p.b); }
     for (hipEvent_t e : ev_pool_) (void)hipEventDestroy(e);
@@ -698,6 +703,25 @@ class Session : public SessionBase {
   // pb: the dense launch carries that scalar packet.
   void cand_ax(const T* const* xs, Pub pb = Pub{}) {
     const T* xd[3] = {xs[1], nullptr, nullptr};
+    if (overlap_ok()) {   // round 4 experiment: lists + gather beside the dense pass
+      GLX_HIP(hipEventRecord(ov_fork_, st_));
+      GLX_HIP(hipStreamWaitEvent(side_, ov_fork_, 0));
+      launch_e_lists(zf_, n_, l_, glists_, side_, nullptr);
+      check_launch();
+      hipEvent_t e2 = prof_begin(2);
+      launch_at_gather<T>(At_, xs[0], m_, n_, l_, Pp_, glists_, side_, nullptr);
+      check_launch();
+      prof_end(2, e2);
+      GLX_HIP(hipEventRecord(ov_join_, side_));
+      hipEvent_t e0 = prof_begin(0);
+      launch_ax<T>(plan_, 1, A_, xd, Pp_ + (size_t)gsplit_ * ml_, dc_gate_, 0, st_, pb);
+      check_launch();
+      prof_end(0, e0);
+      GLX_HIP(hipStreamWaitEvent(st_, ov_join_, 0));   // the finalize reads the gather's slab
+      ++ax_calls_;
+      ax_cols_ += 1;
+      return;
+    }
     launch_e_lists(zf_, n_, l_, glists_, st_, dc_gate_);
     check_launch();
     hipEvent_t e0 = prof_begin(0);
@@ -1801,6 +1825,24 @@ class Session : public SessionBase {
   unsigned seq_ = 0;
   bool attach_ok_ = true;
   hipEvent_t rb_event_ = nullptr;
+  // Round 4 experiment (GLX_GATHER_OVERLAP=1): the split-candidate column lists and A e gather on
+  // a second stream, concurrent with the dense pass A p_thr (the LDS-DMA tile leaves VGPR room
+  // for gather waves on every SIMD and uses no LDS the gather needs); host control, one GPU
+  hipStream_t side_ = nullptr;
+  hipEvent_t ov_fork_ = nullptr, ov_join_ = nullptr;
+  int overlap_ = -1;
+  bool overlap_ok() {
+    if (overlap_ < 0) {
+      const char* e = std::getenv("GLX_GATHER_OVERLAP");
+      overlap_ = (e && std::strcmp(e, "1") == 0 && comm_ == nullptr) ? 1 : 0;
+      if (overlap_) {
+        GLX_HIP(hipStreamCreateWithFlags(&side_, hipStreamNonBlocking));
+        GLX_HIP(hipEventCreateWithFlags(&ov_fork_, hipEventDisableTiming));
+        GLX_HIP(hipEventCreateWithFlags(&ov_join_, hipEventDisableTiming));
+      }
+    }
+    return overlap_ == 1 && dc_gate_ == nullptr;
+  }
   int epoch_ = 0;
   // buffer roles
   int ix_ = 0, iv_ = 1, iy_ = 2, ic_ = 3, ivn_ = 4, iyn_ = 5;   // FISTA

@@ -34,7 +34,7 @@ SHAPES = [
 @pytest.mark.parametrize("dtype", ["f64", "f32"])
 @pytest.mark.parametrize("shape", SHAPES)
 @pytest.mark.parametrize("variant", [0, 2, 3, 1820, 21820, 21410, 52224, 52228, 51328, 52324, 92278,
-                                     92268])
+                                     92268, 92478])
 def test_residual_and_gradient(shape, dtype, variant):
     k = _glx()
     m, n, l = shape
@@ -60,6 +60,24 @@ def test_residual_and_gradient(shape, dtype, variant):
     gmag = Ad.double().abs().T @ R.double().abs()
     tolg = 1e-13 if dtype == "f64" else 2e-6 * (m ** 0.5)
     assert _rel_err(G, gref, gmag) < tolg
+
+
+@pytest.mark.parametrize("l", [16, 32])
+def test_f32_dma_tile_default_plan(l, monkeypatch):
+    """Round 4: f32 with one right-hand side and A beyond the Infinity Cache takes the LDS-DMA tile
+    (92478, 64-column chunks) by default — C3's shape (the split-candidate dense pass A xc)."""
+    monkeypatch.setenv("GLX_AX_DMA32", "1")
+    k = _glx()
+    m, n = 8192, 16384
+    g = torch.Generator(device="cuda").manual_seed(l)
+    A = torch.randn(m, n, device="cuda", dtype=torch.float32, generator=g)
+    X = torch.randn(n, l, device="cuda", dtype=torch.float32, generator=g)
+    B = torch.randn(m, l, device="cuda", dtype=torch.float32, generator=g)
+    R, _ = k.residual(A, X, B)
+    torch.cuda.synchronize()
+    ref = A.double() @ X.double() - B.double()
+    mag = A.double().abs() @ X.double().abs() + B.double().abs()
+    assert _rel_err(R, ref, mag) < 2e-6 * (n ** 0.5)
 
 
 BATCH_CODES = [0, 1420, 52224, 52324, 52228, 51328, 92278, 92268]
