@@ -358,10 +358,13 @@ def main():
         # only in the rows the hard threshold touched) gathered from the flagged rows of a
         # transposed copy of A (m values each); its algorithmic work is 2 m l flops per such row.
         nsrc = work["ax_sources"] / max(1, work["ax_calls"])
-        # the solver's split-candidate rule (solver.cpp split_mode): fp64, not exact, A of this
-        # rank >= 768 MiB unless GLX_SPLIT_CAND=1 forces it; l in {16, 32} and n < 65536 (gather)
+        # the solver's split-candidate rule (solver.cpp split_mode): fp64 (fp32: FProxGD only,
+        # round 4), not exact, m n * 8 B of this rank >= 768 MiB unless GLX_SPLIT_CAND=1 forces
+        # it; l in {16, 32} and n < 65536 (gather)
         split_env = os.environ.get("GLX_SPLIT_CAND", "")
-        split_on = (args.dtype == "f64" and not args.exact and split_env != "0" and
+        dtype_ok = args.dtype == "f64" or (args.method == "gl_FProxGD_primal" and
+                                           os.environ.get("GLX_SPLIT_F32", "") != "0")
+        split_on = (dtype_ok and not args.exact and split_env != "0" and
                     (ml * n * 8 >= 768 * 2 ** 20 or split_env == "1"))
         gather_fits = l in (16, 32) and n <= 65535
         st = res["stats"]
@@ -410,8 +413,10 @@ def main():
         fused = {"gl_ProxGD_primal": "k_atr_prox", "gl_FProxGD_primal": "k_atr_fista"}.get(args.method)
         atr_plan = [p for p in _plan_parts(args.dtype, ml, n, l) if p.startswith("atr=")]
         if args.dtype == "f32" and fused and world == 1 and l in (16, 32) and n % 64 == 0:
-            # solver.cpp session_plan: fp32 trial methods fuse the trial into the 2-split panel
-            atr_plan = ["atr=k_atr_mfma<WL0,PF8,NTL1> S=2 (session plan)"]
+            # solver.cpp session_plan: fp32 trial methods fuse the trial into the panel form, the
+            # eight-wave panel with one K split where n / 64 >= 256 (round 4), else 2 K splits
+            atr_plan = ["atr=k_atr_mfma<WL2,PF8,NTL1> S=1 (session plan)" if n // 64 >= 256 else
+                        "atr=k_atr_mfma<WL0,PF8,NTL1> S=2 (session plan)"]
         atr_kname = ("A^T r%s: %s" % (" + the fused trial (%s)" % fused if fused and world == 1 else "",
                                       atr_plan[0][4:] if atr_plan else "?"))
         kernels = {"ax": dict(roof_of(ax_flops, ax_bytes, ax_avg_s if ax_n else None, peak_tf),

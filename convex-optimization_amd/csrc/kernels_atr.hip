@@ -603,12 +603,6 @@ static void atr_prox_nt(const GemmPlan& p, const T* A, const T* R, T* G, const T
     case 124: atr_prox_go<T, NT, 4, true, 2>(p, A, R, G, x, pp, pthr, z, t, mu, thres, red, st, pub, Gp, pcnt, zf); break;
     case 128: atr_prox_go<T, NT, 8, true, 2>(p, A, R, G, x, pp, pthr, z, t, mu, thres, red, st, pub, Gp, pcnt, zf); break;
     case 28: atr_prox_go<T, NT, 8, false, 2>(p, A, R, G, x, pp, pthr, z, t, mu, thres, red, st, pub, Gp, pcnt, zf); break;
-    case 136:   // f32, eight-wave panel with a 16-step ring (round 4 experiment, GLX_ATR_PF16)
-      if constexpr (sizeof(T) == 4) {
-        atr_prox_go<T, NT, 16, true, 2>(p, A, R, G, x, pp, pthr, z, t, mu, thres, red, st, pub, Gp, pcnt, zf);
-        break;
-      }
-      throw Error{GLX_E_INVALID, "A^T R: the 16-step ring is f32 only"};
     default: atr_prox_go<T, NT, 8, false, 0>(p, A, R, G, x, pp, pthr, z, t, mu, thres, red, st, pub, Gp, pcnt, zf); break;
   }
 }
@@ -652,12 +646,6 @@ static void atr_fista_nt(const GemmPlan& p, const T* A, const T* R, T* G, const 
     case 124: atr_fista_go<T, NT, 4, true, 2>(p, A, R, G, y, xk, xc, vn, yn, t, mu, thres, theta, theta_next, red, st, pub, Gp, pcnt, ec, zf); break;
     case 128: atr_fista_go<T, NT, 8, true, 2>(p, A, R, G, y, xk, xc, vn, yn, t, mu, thres, theta, theta_next, red, st, pub, Gp, pcnt, ec, zf); break;
     case 28: atr_fista_go<T, NT, 8, false, 2>(p, A, R, G, y, xk, xc, vn, yn, t, mu, thres, theta, theta_next, red, st, pub, Gp, pcnt, ec, zf); break;
-    case 136:   // f32, eight-wave panel with a 16-step ring (round 4 experiment, GLX_ATR_PF16)
-      if constexpr (sizeof(T) == 4) {
-        atr_fista_go<T, NT, 16, true, 2>(p, A, R, G, y, xk, xc, vn, yn, t, mu, thres, theta, theta_next, red, st, pub, Gp, pcnt, ec, zf);
-        break;
-      }
-      throw Error{GLX_E_INVALID, "A^T R: the 16-step ring is f32 only"};
     default: atr_fista_go<T, NT, 8, false, 0>(p, A, R, G, y, xk, xc, vn, yn, t, mu, thres, theta, theta_next, red, st, pub, Gp, pcnt, ec, zf); break;
   }
 }

@@ -618,9 +618,10 @@ GemmPlan make_plan(int esize, int64_t m, int64_t n, int64_t l, int ax_variant) {
     p.ax_S = (int)clampi(cdiv(kTargetWaves, waves), 1, std::max<int64_t>(1, std::min<int64_t>(kMaxSplit, kunits / 4)));
   } else if (esize == 4 && ax_variant == 0 && (double)m * (double)n * esize > kAtrNtBytes &&
              lds_code_ok(kAxDma32, n, l, esize, 1) && env_int("GLX_AX_DMA", 1) != 0 &&
-             env_int("GLX_AX_DMA32", 0) != 0) {
+             env_int("GLX_AX_DMA32", 1) != 0) {
     // Round 4: f32 with one right-hand side and A beyond the Infinity Cache (C3's split-candidate
-    // dense pass A xc) on the LDS-DMA tile, as 92278 does for f64
+    // dense pass A xc) on the LDS-DMA tile, as 92278 does for f64: 85-88 us = 6.1-6.3 TB/s
+    // against 115 us for the direct-load tile 21410 (profiles/r4_exp3/). GLX_AX_DMA32=0: off.
     p.ax_code = kAxDma32;
     p.ax_kind = 5;
     p.ax_S = lds_split(esize, m, n, kAxDma32);

@@ -90,15 +90,21 @@ __device__ inline bool gr_ok(const Gr& x, unsigned tag) {
 __device__ inline double gr_val(const Gr& x) {
   return __longlong_as_double((long long)((x.w1 << 32) | (x.w0 & 0xffffffffull)));
 }
-// LDS counters shared by the roles
-// (acquire / release at workgroup scope: the compiler keeps the data accesses on their side of
-// the counter access; on LDS that costs an lgkmcnt wait)
+// LDS counters shared by the roles. Every counter guards LDS data only (the partial ring, r of
+// a block), and one wave's LDS operations execute in issue order, so relaxed atomics with
+// compiler-only fences suffice: acquire / release at workgroup scope also made the compiler
+// drain vmcnt (s_waitcnt vmcnt(0)) at every counter access, i.e. wait for the A-waves' tile
+// prefetch and the B-waves' granule and tile loads each block (round 4: 146-158 us at C2
+// whatever the lags or the prefetch depth).
 __device__ inline unsigned lds_get(const unsigned* p) {
-  return __hip_atomic_load(p, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
+  const unsigned v = __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+  __atomic_signal_fence(__ATOMIC_SEQ_CST);   // later LDS reads stay behind the counter read
+  return v;
 }
-// one add per wave (lane 0; the release waits for all of the wave's earlier LDS accesses)
+// one add per wave (lane 0), behind the wave's earlier LDS accesses (issue order)
 __device__ inline void lds_add(unsigned* p) {
-  if ((threadIdx.x & 63) == 0) __hip_atomic_fetch_add(p, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+  __atomic_signal_fence(__ATOMIC_SEQ_CST);
+  if ((threadIdx.x & 63) == 0) __hip_atomic_fetch_add(p, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
 }
 }  // namespace
 
@@ -218,12 +224,19 @@ __global__ __launch_bounds__(kRThreads, 1) void k_resgrad2(
       }
       lds_add(&cnt_part[s]);
     };
+    // in block order (the scheduler would otherwise issue block 0's loads last, and the loop
+    // head's wait would cover all of them on every trip)
 #pragma unroll
-    for (int d = 0; d < kRAB - 1; ++d) load_tile(a[d], d);
+    for (int d = 0; d < kRAB - 1; ++d) {
+      load_tile(a[d], d);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    // NB % kRAB == 0 (resgrad2_shape_ok): no early exit inside the trip, so the compiler's
+    // waitcnt state at the loop head keeps kRAB - 1 tiles in flight (an exit edge made it drain
+    // vmcnt to 0 at the top of every trip)
     for (int b = 0; b < NB; b += kRAB) {
 #pragma unroll
       for (int h = 0; h < kRAB; ++h) {
-        if (b + h >= NB) break;
         load_tile(a[(h + kRAB - 1) % kRAB], b + h + kRAB - 1);
         phase_a(a[h], b + h);
       }
@@ -279,21 +292,28 @@ __global__ __launch_bounds__(kRThreads, 1) void k_resgrad2(
 
   load_at(at[0], 0);
   load_at(at[1], 1);
-  // one B iteration; tb = the tile buffer of block j - D2 (constant after inlining: the loop
-  // below runs two iterations per trip)
-  auto iter = [&](int j, double (&tb)[4][4]) {
-    const int b1 = j - D1, b2 = j - D2;
-    // issue this iteration's remote reads first (vmcnt retires in order)
+  // The remote reads of iteration j (hop-1 granules of block j - D1, b, the r granule of block
+  // j - D2) are issued at the end of iteration j - 1, BEFORE that iteration's phase-B tile
+  // prefetch: loads retire in order, so waiting for them then leaves the tile loads in flight.
+  struct Pre {
     Gr h1[2];
-    double bv = 0.0;
-    const bool do1 = b1 >= 0 && b1 < NB, do2 = b2 >= 0;
-    if (do1) {
-      h1[0] = get_gran(pg_at(b1, k0, v1));
-      h1[1] = get_gran(pg_at(b1, k0 + 1, v1));
-      if (k0 == 0 && vcol >= 16) bv = B[(rbase + 16 * b1 + vrow) * kRLB + (vcol - 16)];
-    }
+    double bv;
     Gr h2;
-    if (do2) h2 = get_gran(rg_at(b2, bl));
+  };
+  auto issue = [&](int j, Pre& p) {
+    const int b1 = j - D1, b2 = j - D2;
+    if (b1 >= 0 && b1 < NB) {
+      p.h1[0] = get_gran(pg_at(b1, k0, v1));
+      p.h1[1] = get_gran(pg_at(b1, k0 + 1, v1));
+      p.bv = (k0 == 0 && vcol >= 16) ? B[(rbase + 16 * b1 + vrow) * kRLB + (vcol - 16)] : 0.0;
+    }
+    if (b2 >= 0 && b2 < NB) p.h2 = get_gran(rg_at(b2, bl));
+  };
+  // one B iteration; tb = the tile buffer of block j - D2 (constant after inlining: the loop
+  // below runs two iterations per trip); cur: this iteration's remote reads, nxt: the next one's
+  auto iter = [&](int j, double (&tb)[4][4], Pre& cur, Pre& nxt) {
+    const int b1 = j - D1, b2 = j - D2;
+    const bool do1 = b1 >= 0 && b1 < NB, do2 = b2 >= 0 && b2 < NB;
     // 1. block j: the four A-wave partials (fixed order), handed out as granules
     if (j < NB) {
       const int s = j % kRSlot;
@@ -308,8 +328,8 @@ __global__ __launch_bounds__(kRThreads, 1) void k_resgrad2(
     }
     // 2. block b1, hop 1: slice sums in a fixed butterfly order; S to the output slabs, r out
     if (do1) {
-      double sum = sweep(pg_at(b1, k0, v1), tag_of(b1), h1[0]) +
-                   sweep(pg_at(b1, k0 + 1, v1), tag_of(b1), h1[1]);
+      double sum = sweep(pg_at(b1, k0, v1), tag_of(b1), cur.h1[0]) +
+                   sweep(pg_at(b1, k0 + 1, v1), tag_of(b1), cur.h1[1]);
       for (int off = 1; off < P / 2; off <<= 1) sum = sum + __shfl_xor(sum, off);
       if (k0 == 0) {
         const int64_t row = rbase + 16 * b1 + vrow;
@@ -317,15 +337,15 @@ __global__ __launch_bounds__(kRThreads, 1) void k_resgrad2(
           P0[row * kRLB + vcol] = sum;
         } else {
           P1[row * kRLB + (vcol - 16)] = sum;
-          put_gran<XL>(rg_at(b1, vrow * kRLB + (vcol - 16)), tag_of(b1), sum - bv);
+          put_gran<XL>(rg_at(b1, vrow * kRLB + (vcol - 16)), tag_of(b1), sum - cur.bv);
         }
       }
     }
     // 3. block b2, hop 2 + phase B
-    if (do2 && b2 < NB) {
+    if (do2) {
       const int rs = b2 & 1;
       if (b2 >= 2) spin_wait(&cnt_rfree[rs], 4u * (unsigned)(b2 / 2));
-      rsh[rs][bl] = sweep(rg_at(b2, bl), tag_of(b2), h2);
+      rsh[rs][bl] = sweep(rg_at(b2, bl), tag_of(b2), cur.h2);
       lds_add(&cnt_r[rs]);
       spin_wait(&cnt_r[rs], 4u * (unsigned)(b2 / 2 + 1));
 #pragma unroll
@@ -335,13 +355,17 @@ __global__ __launch_bounds__(kRThreads, 1) void k_resgrad2(
         for (int ct = 0; ct < 4; ++ct) gacc[ct] = MF<double>::mma(tb[s][ct], rr, gacc[ct]);
       }
       lds_add(&cnt_rfree[rs]);
-      if (b2 + 2 < NB) load_at(tb, b2 + 2);
     }
+    issue(j + 1, nxt);
+    __builtin_amdgcn_sched_barrier(0);   // (the scheduler would hoist the tile loads above them)
+    if (do2 && b2 + 2 < NB) load_at(tb, b2 + 2);
   };
   constexpr int p0 = D2 & 1;   // tile buffer of block j - D2 for even j
+  Pre pa, pb;
+  issue(0, pa);
   for (int j = 0; j < NB + D2; j += 2) {
-    iter(j, at[p0]);
-    if (j + 1 < NB + D2) iter(j + 1, at[p0 ^ 1]);
+    iter(j, at[p0], pa, pb);
+    if (j + 1 < NB + D2) iter(j + 1, at[p0 ^ 1], pb, pa);
   }
   double* gout = Gs + (int64_t)rg * n * kRLB;
 #pragma unroll
@@ -375,7 +399,7 @@ bool resgrad2_shape_ok(int esize, int64_t m, int64_t n, int64_t l) {
   const int64_t P = n / kRPanel;
   if (P < 2 || P > 128 || (P & (P - 1)) != 0) return false;
   const int64_t RG = kRGrid / P;
-  return m % (RG * 16) == 0 && m / RG >= 32;
+  return m % (RG * 16 * kRAB) == 0 && m / RG >= 32;   // NB = m / RG / 16, a multiple of kRAB
 }
 
 int resgrad2_groups(int64_t n) { return (int)(kRGrid / (n / kRPanel)); }

@@ -141,9 +141,14 @@ static void validate(const glx_problem* P, const glx_opts* O) {
 // methods, shapes the gather does not cover, or GLX_SPLIT_CAND=0 / glx_opts.split_cand = 0: the
 // dense [z | p_thr] batch of round 1); 1 = A e from the transposed copy of A (kernels_gather.hip;
 // costs an extra m x n copy of A in the workspace, glx_session_workspace_bytes).
-// fp64 only: in fp32 the regrouped sum (A p_thr - b) + A e moves f by ~1e-6 relative on short
-// unconverged runs (measured 1.5e-6 on mid_384x640x16 against the 1e-6 fp32 bar), and no fp32
-// ProxGD configuration is on the benchmark path.
+// ProxGD: fp64 only. In fp32 its regrouped sum (A p_thr - b) + A e IS the recorded objective
+// and moves f by ~1e-6 relative on short unconverged runs (measured 1.5e-6 on mid_384x640x16
+// against the 1e-6 fp32 bar); no fp32 ProxGD configuration is on the benchmark path.
+// FProxGD in fp32 (round 4, C3): the objective is A xc computed directly; only A y_next is
+// regrouped. Against the fp32 reference / oracle it measured fval 2e-8..2e-7 and f_hist up to
+// 1.4e-5 (bars 1e-6 / 2e-5; the dense batch: 3e-8..2e-7, 3.1e-6), profiles/r4_exp3/margins.jsonl;
+// with its dense pass on the f32 LDS-DMA tile C3 runs 4406-4475 against 3738-3781 it/s over
+// 200 steps. GLX_SPLIT_F32=0 keeps the dense batch. (The size gate counts elements as fp64.)
 // FProxGD with line search takes the gather form too (iter_fista: A y_next by linearity from
 // A xc, A e_c and the kept A thr(x_k)); GLX_SPLIT_FISTA=0 keeps its dense [xc | y_next] batch.
 // Only for A of at least kSplitMinBytes (this rank's rows): the column lists and the gather
@@ -155,9 +160,9 @@ static constexpr double kSplitMinBytes = 768.0 * 1024 * 1024;
 static int split_mode(const glx_problem& P, const glx_opts& O) {
   if (O.exact_objective != 0) return 0;
   if (P.method != GLX_PROXGD && P.method != GLX_FPROXGD) return 0;
-  if (P.dtype != GLX_F64) {   // fp32 FProxGD: experiment (GLX_SPLIT_F32=1)
+  if (P.dtype != GLX_F64) {   // fp32: FProxGD only (above); GLX_SPLIT_F32=0: off
     const char* f = std::getenv("GLX_SPLIT_F32");
-    if (!(f && std::strcmp(f, "1") == 0 && P.method == GLX_FPROXGD)) return 0;
+    if (P.method != GLX_FPROXGD || (f && std::strcmp(f, "0") == 0)) return 0;
   }
   if (O.split_cand == 2) return 0;
   const char* sc = O.split_cand == 0 ? std::getenv("GLX_SPLIT_CAND") : nullptr;
@@ -194,8 +199,6 @@ static GemmPlan session_plan(const glx_problem& P, const glx_opts& O) {
     if (P.n / 64 >= 256) {
       f.atr_wl = 2;
       f.atr_S = 1;
-      const char* pf16 = std::getenv("GLX_ATR_PF16");   // round 4 experiment: 16-step ring
-      if (pf16 && std::strcmp(pf16, "1") == 0) f.atr_pf = 16;
     }
     if (atr_prox_ok(f)) return f;   // only where the trial actually fuses (GLX_ATR_FUSE_SPLIT)
   }
@@ -425,9 +428,6 @@ class Session : public SessionBase {
     if (hs_) (void)hipHostFree(hs_);
     if (dc_ring_) (void)hipHostFree(dc_ring_);
     if (rb_event_) (void)hipEventDestroy(rb_event_);
-    if (ov_fork_) (void)hipEventDestroy(ov_fork_);
-    if (ov_join_) (void)hipEventDestroy(ov_join_);
-    if (side_) (void)hipStreamDestroy(side_);
     for (auto& v : ev_)
       for (auto& p : v) { (void)hipEventDestroy(p.a); (void)hipEventDestroy(p.b); }
     for (hipEvent_t e : ev_pool_) (void)hipEventDestroy(e);
@@ -703,25 +703,6 @@ class Session : public SessionBase {
   // pb: the dense launch carries that scalar packet.
   void cand_ax(const T* const* xs, Pub pb = Pub{}) {
     const T* xd[3] = {xs[1], nullptr, nullptr};
-    if (overlap_ok()) {   // round 4 experiment: lists + gather beside the dense pass
-      GLX_HIP(hipEventRecord(ov_fork_, st_));
-      GLX_HIP(hipStreamWaitEvent(side_, ov_fork_, 0));
-      launch_e_lists(zf_, n_, l_, glists_, side_, nullptr);
-      check_launch();
-      hipEvent_t e2 = prof_begin(2);
-      launch_at_gather<T>(At_, xs[0], m_, n_, l_, Pp_, glists_, side_, nullptr);
-      check_launch();
-      prof_end(2, e2);
-      GLX_HIP(hipEventRecord(ov_join_, side_));
-      hipEvent_t e0 = prof_begin(0);
-      launch_ax<T>(plan_, 1, A_, xd, Pp_ + (size_t)gsplit_ * ml_, dc_gate_, 0, st_, pb);
-      check_launch();
-      prof_end(0, e0);
-      GLX_HIP(hipStreamWaitEvent(st_, ov_join_, 0));   // the finalize reads the gather's slab
-      ++ax_calls_;
-      ax_cols_ += 1;
-      return;
-    }
     launch_e_lists(zf_, n_, l_, glists_, st_, dc_gate_);
     check_launch();
     hipEvent_t e0 = prof_begin(0);
@@ -1825,24 +1806,6 @@ class Session : public SessionBase {
   unsigned seq_ = 0;
   bool attach_ok_ = true;
   hipEvent_t rb_event_ = nullptr;
-  // Round 4 experiment (GLX_GATHER_OVERLAP=1): the split-candidate column lists and A e gather on
-  // a second stream, concurrent with the dense pass A p_thr (the LDS-DMA tile leaves VGPR room
-  // for gather waves on every SIMD and uses no LDS the gather needs); host control, one GPU
-  hipStream_t side_ = nullptr;
-  hipEvent_t ov_fork_ = nullptr, ov_join_ = nullptr;
-  int overlap_ = -1;
-  bool overlap_ok() {
-    if (overlap_ < 0) {
-      const char* e = std::getenv("GLX_GATHER_OVERLAP");
-      overlap_ = (e && std::strcmp(e, "1") == 0 && comm_ == nullptr) ? 1 : 0;
-      if (overlap_) {
-        GLX_HIP(hipStreamCreateWithFlags(&side_, hipStreamNonBlocking));
-        GLX_HIP(hipEventCreateWithFlags(&ov_fork_, hipEventDisableTiming));
-        GLX_HIP(hipEventCreateWithFlags(&ov_join_, hipEventDisableTiming));
-      }
-    }
-    return overlap_ == 1 && dc_gate_ == nullptr;
-  }
   int epoch_ = 0;
   // buffer roles
   int ix_ = 0, iv_ = 1, iy_ = 2, ic_ = 3, ivn_ = 4, iyn_ = 5;   // FISTA

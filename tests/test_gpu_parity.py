@@ -109,6 +109,25 @@ def test_split_candidate_forced_golden(name, monkeypatch):
     assert np.max(np.abs(x - xg)) <= 1e-6 * max(1.0, np.max(np.abs(xg)))
 
 
+F32_SPLIT_CASES = sorted(c for c, meta in golden_index().items()
+                         if meta["dtype"] == "f32" and meta["solver"] == "gl_FProxGD_primal"
+                         and meta["l"] in (16, 32))
+
+
+@pytest.mark.parametrize("name", F32_SPLIT_CASES)
+def test_split_candidate_forced_golden_f32_fista(name, monkeypatch):
+    """Round 4: fp32 FProxGD takes the split-candidate batch (A y_next by linearity) by default
+    where A is large (C3); forced here on the fp32 golden cases, against the fp32 bars (measured
+    fval 5e-8..9e-8, f_hist up to 1.4e-5: profiles/r4_exp3/margins.jsonl)."""
+    monkeypatch.setenv("GLX_SPLIT_CAND", "1")
+    meta, gold = golden_case(name)
+    A, b, u, x0, mu = golden_inputs(meta)
+    x, k, out = _solve(meta, A, b, x0, mu)
+    assert _rel(out["fval"], gold["fval"]) < FP32_FVAL_BAR
+    if k == int(gold["k"]):
+        assert _rel(np.asarray([float(v) for v in out["f_hist"]]), gold["f_hist"]) < FP32_FHIST_BAR
+
+
 @pytest.mark.parametrize("name", ["default_gl_ProxGD_primal", "seed114514_gl_ProxGD_primal",
                                   "mid_512x1024x16_f64_gl_ProxGD_primal"])
 def test_proxgd_exact_objective_mode(name):
