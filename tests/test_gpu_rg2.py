@@ -23,8 +23,9 @@ def _rel(got, ref, mag):
 
 
 # (m, n): P = n / 256 panels (a power of two, 2..128), RG = 256 / P row groups, m a multiple of
-# 16 RG with >= 2 blocks per group. (4096, 8192) is SURVEY's C2.
-SHAPES = [(4096, 8192), (1024, 2048), (4096, 512), (2048, 32768), (8192, 4096), (512, 16384)]
+# 64 RG (NB = m / RG / 16 blocks per group, a multiple of the A-waves' 4 tile buffers).
+# (4096, 8192) is SURVEY's C2 (RG = 8: the XCD-local hand-off).
+SHAPES = [(4096, 8192), (4096, 2048), (16384, 512), (2048, 32768), (8192, 4096), (512, 16384)]
 
 
 def _inputs(m, n, seed):
@@ -73,7 +74,8 @@ def test_rg2_residuals_match_two_pass_bits():
 
 def test_rg2_unsupported_shapes_run_two_passes():
     from glx import kernels
-    for m, n in [(1000, 8192), (4096, 8448), (4096, 6144)]:   # ragged m, n % 256, P = 24
+    # ragged m, n % 256, P = 24, NB = 2
+    for m, n in [(1000, 8192), (4096, 8448), (4096, 6144), (1024, 2048)]:
         A, X0, X1, B = _inputs(m, n, m + n)
         R0, R1, G, ran = kernels.residual_gradient2(A, X0, X1, B, one_pass=True)
         assert not ran
