@@ -163,4 +163,8 @@ def test_device_control_world2_repeated_mu(tmp_path, method):
     o = dict(opts, alpha0=numpy_ref.step_size_for(m, n))
     _, k, out = numpy_ref.SOLVERS[method](x0, A, b, 0.0, o)
     assert dev[0]["k"] == k
-    assert abs(dev[0]["fval"] - float(out["fval"])) <= 1e-8 * abs(float(out["fval"]))
+    # mu0 = 0 with m < n drives the objective to the rounding floor (~1e-25 here, from ~1e3):
+    # relative agreement is meaningless there, so the bar has an absolute floor of 1e-12 of the
+    # first objective
+    f0 = abs(float(out["f_hist"][0]))
+    assert abs(dev[0]["fval"] - float(out["fval"])) <= 1e-8 * abs(float(out["fval"])) + 1e-12 * f0
