@@ -632,7 +632,22 @@ static void dispatch_row(int64_t l, F&& f) {
   else if (l <= 8) f(std::integral_constant<int, 8>{}, std::integral_constant<int, 1>{});
   else dispatch_epl<16>(l, [&](auto epl) { f(std::integral_constant<int, 16>{}, epl); });
 }
-static inline unsigned row_grid(int64_t n, int lpr) { return grid_for(n, 256 / lpr); }
+// Work workgroups of the row kernels, at most kRowBlocks (GLX_ROW_BLOCKS overrides): at n = 16384
+// two 16-row trips per workgroup instead of one halve the grid reduction's fan-in. Round 4, the
+// 8-GPU shard model (1024 rows, communicator path, where the trial kernel runs every iteration;
+// two interleaved rounds, profiles/r4_exp8/, profiles/r4_exp9/): k_prox_pgd 14.4 -> 12.4 us,
+// ProxGD 10853-10898 -> 11109-11149 it/s, FProxGD 10621-10671 -> 10783-10817; caps 768 / 384 /
+// 256 / 128 measured between or below; NS level (its trial is fused into A^T R).
+constexpr unsigned kRowBlocks = 512;
+static inline unsigned row_grid(int64_t n, int lpr) {
+  static const unsigned cap = [] {
+    const char* e = std::getenv("GLX_ROW_BLOCKS");
+    const int v = e ? std::atoi(e) : 0;
+    return v > 0 ? (unsigned)v : kRowBlocks;
+  }();
+  const unsigned g = grid_for(n, 256 / lpr);
+  return g < cap ? g : cap;
+}
 // + one publisher workgroup when the launch carries the scalar packet (the grid reduction's
 // partials hold at most kMaxBlocks workgroups). The work workgroups are capped at kMaxBlocks - 1
 // with or without the packet, so the rows each workgroup sums, and with them the rounding of the
