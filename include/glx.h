@@ -198,7 +198,8 @@ int glx_residual_gradient(int dtype, int64_t m, int64_t n, int64_t l, const void
  * R0 = A X0 - B, R1 = A X1 - B (the reference's A @ z and A @ p_thr, gl_ProxGD_primal.py:89-92,
  * :112) and G = A^T R1 (:129 at the candidate). one_pass = 1: one read of A by the role-split
  * kernel (kernels_rg2.hip) where the shape allows it (fp64, l = 16, n = 256 P with P a power of
- * two in 2..128, m a multiple of 16 * 256 / P, >= 256 CUs); a timed-out hand-off wait inside it
+ * two in 2..128, m a multiple of 64 * 256 / P, >= 256 CUs; slower than two passes on MI355X,
+ * DESIGN.md (f), so the solver does not use it); a timed-out hand-off wait inside it
  * (error flag read back: the one-pass call is synchronous) or another shape runs A @ [X0 | X1],
  * then A^T R1. *one_pass_ran (may be NULL) = 1 when the outputs come from the one-pass kernel. */
 int glx_residual_gradient2(int dtype, int64_t m, int64_t n, int64_t l, const void* A, const void* X0,
