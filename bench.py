@@ -358,12 +358,12 @@ def main():
         # only in the rows the hard threshold touched) gathered from the flagged rows of a
         # transposed copy of A (m values each); its algorithmic work is 2 m l flops per such row.
         nsrc = work["ax_sources"] / max(1, work["ax_calls"])
-        # the solver's split-candidate rule (solver.cpp split_mode): fp64 (fp32: FProxGD only,
-        # round 4), not exact, m n * 8 B of this rank >= 768 MiB unless GLX_SPLIT_CAND=1 forces
+        # the solver's split-candidate rule (solver.cpp split_mode): fp64 (fp32: FProxGD with
+        # GLX_SPLIT_F32=1, round 4), not exact, m n * 8 B of this rank >= 768 MiB unless GLX_SPLIT_CAND=1 forces
         # it; l in {16, 32} and n < 65536 (gather)
         split_env = os.environ.get("GLX_SPLIT_CAND", "")
         dtype_ok = args.dtype == "f64" or (args.method == "gl_FProxGD_primal" and
-                                           os.environ.get("GLX_SPLIT_F32", "") != "0")
+                                           os.environ.get("GLX_SPLIT_F32", "") == "1")
         split_on = (dtype_ok and not args.exact and split_env != "0" and
                     (ml * n * 8 >= 768 * 2 ** 20 or split_env == "1"))
         gather_fits = l in (16, 32) and n <= 65535

@@ -144,11 +144,13 @@ static void validate(const glx_problem* P, const glx_opts* O) {
 // ProxGD: fp64 only. In fp32 its regrouped sum (A p_thr - b) + A e IS the recorded objective
 // and moves f by ~1e-6 relative on short unconverged runs (measured 1.5e-6 on mid_384x640x16
 // against the 1e-6 fp32 bar); no fp32 ProxGD configuration is on the benchmark path.
-// FProxGD in fp32 (round 4, C3): the objective is A xc computed directly; only A y_next is
-// regrouped. Against the fp32 reference / oracle it measured fval 2e-8..2e-7 and f_hist up to
-// 1.4e-5 (bars 1e-6 / 2e-5; the dense batch: 3e-8..2e-7, 3.1e-6), profiles/r4_exp3/margins.jsonl;
-// with its dense pass on the f32 LDS-DMA tile C3 runs 4406-4475 against 3738-3781 it/s over
-// 200 steps. GLX_SPLIT_F32=0 keeps the dense batch. (The size gate counts elements as fp64.)
+// FProxGD in fp32 (round 4, C3; opt-in, GLX_SPLIT_F32=1): the objective is A xc computed
+// directly; only A y_next is regrouped. On short runs against the fp32 reference / oracle it
+// measured fval 2e-8..2e-7 and f_hist up to 1.4e-5 (bars 1e-6 / 2e-5; profiles/r4_exp3/), and
+// with its dense pass on the f32 LDS-DMA tile C3 runs 4406-4475 against 3738-3781 it/s over 200
+// steps; but over C3's whole solve against the reference's fp32 run it ends 3.4e-5 from the
+// reference's objective, the dense batch 3.4e-7 (profiles/r4_c3gold/), so the dense batch stays
+// the default. (The size gate counts elements as fp64.)
 // FProxGD with line search takes the gather form too (iter_fista: A y_next by linearity from
 // A xc, A e_c and the kept A thr(x_k)); GLX_SPLIT_FISTA=0 keeps its dense [xc | y_next] batch.
 // Only for A of at least kSplitMinBytes (this rank's rows): the column lists and the gather
@@ -160,9 +162,9 @@ static constexpr double kSplitMinBytes = 768.0 * 1024 * 1024;
 static int split_mode(const glx_problem& P, const glx_opts& O) {
   if (O.exact_objective != 0) return 0;
   if (P.method != GLX_PROXGD && P.method != GLX_FPROXGD) return 0;
-  if (P.dtype != GLX_F64) {   // fp32: FProxGD only (above); GLX_SPLIT_F32=0: off
+  if (P.dtype != GLX_F64) {   // fp32: FProxGD only and opt-in (GLX_SPLIT_F32=1, above)
     const char* f = std::getenv("GLX_SPLIT_F32");
-    if (P.method != GLX_FPROXGD || (f && std::strcmp(f, "0") == 0)) return 0;
+    if (P.method != GLX_FPROXGD || !(f && std::strcmp(f, "1") == 0)) return 0;
   }
   if (O.split_cand == 2) return 0;
   const char* sc = O.split_cand == 0 ? std::getenv("GLX_SPLIT_CAND") : nullptr;

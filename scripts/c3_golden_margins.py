@@ -1,6 +1,7 @@
 """Margins of the HIP fp32 FProxGD whole solve at C3 against the reference's run
 (tests/golden/c3_gl_FProxGD_primal.npz): k, fval and f_hist relative differences, for the
-default (split-candidate) and the dense batch (GLX_SPLIT_F32=0). One JSON line per mode."""
+default (the dense batch) and the opt-in split-candidate batch (GLX_SPLIT_F32=1). One JSON line
+per mode."""
 import json
 import os
 import subprocess
@@ -30,7 +31,7 @@ print(json.dumps({"mode": os.environ.get("MODE"), "k": int(k), "k_ref": int(gold
                   "fhist_rel_max": float(rel.max()), "fhist_rel_last": float(rel[-1]),
                   "x_err_over_max": float(np.max(np.abs(xx - xr)) / np.max(np.abs(xr)))}), flush=True)
 ''' % {"root": ROOT}
-for mode, env in (("split", {}), ("dense", {"GLX_SPLIT_F32": "0"})):
+for mode, env in (("split", {"GLX_SPLIT_F32": "1"}), ("dense", {})):
     e = dict(os.environ, MODE=mode, **env)
     r = subprocess.run([sys.executable, "-c", CODE], env=e, capture_output=True, text=True, timeout=600)
     sys.stdout.write(r.stdout)
