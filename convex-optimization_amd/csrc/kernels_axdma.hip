@@ -398,14 +398,6 @@ static bool dma_code(const GemmPlan& p, int code, int S, const T* A, const T* co
   switch (code) {
     case 92278: ax_dma_go<T, NT, NSRC, 2, 32, 8, true, true, true, 2>(p, S, A, X, P, gate, epoch, st, pub); return true;
     case 92268: ax_dma_go<T, NT, NSRC, 2, 32, 8, false, true, true, 2>(p, S, A, X, P, gate, epoch, st, pub); return true;
-    // f32 two-source batch (round 4 experiment, GLX_AXB_VARIANT=82478): one 16-row tile per
-    // wave, 64-column chunks
-    case 82478:
-      if constexpr (sizeof(T) == 4) {
-        ax_dma_go<T, NT, NSRC, 2, 64, 8, true, true, true, 1>(p, S, A, X, P, gate, epoch, st, pub);
-        return true;
-      }
-      return false;
     // f32 (round 4): 64-column chunks, the same 256-B row pieces and LDS image as 92278 in f64
     case 92478:
       if constexpr (sizeof(T) == 4 && NSRC == 1) {

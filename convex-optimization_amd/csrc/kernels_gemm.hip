@@ -509,7 +509,7 @@ static int axb_default(int nsrc, int esize) {
 static constexpr int kLdsCodes[] = {52224, 52324, 52228, 51328,
                                      // kind 9 (LDS-DMA, two row tiles per wave): 9 NS KC/16 flags WAVES;
                                      // 92278 / 92268 f64, 92478 f32 (one source)
-                                     92278, 92268, 92478, 82478};
+                                     92278, 92268, 92478};
 static inline bool dma_kind(int c) { return c / 10000 == 8 || c / 10000 == 9; }
 static inline bool lds_kind(int c) { return c / 10000 == 5 || dma_kind(c); }
 static bool lds_code_ok(int c, int64_t n, int64_t l, int esize, int nsrc = 1) {
@@ -517,8 +517,7 @@ static bool lds_code_ok(int c, int64_t n, int64_t l, int esize, int nsrc = 1) {
   for (int k : kLdsCodes) known |= (k == c);
   if (!known) return false;
   if (dma_kind(c))
-    return (c == kAxDma32 ? (esize == 4 && nsrc == 1) : (c == 82478 ? esize == 4 : esize == 8)) &&
-           (l == 16 || l == 32) &&
+    return (c == kAxDma32 ? (esize == 4 && nsrc == 1) : esize == 8) && (l == 16 || l == 32) &&
            n % (16 * ((c / 100) % 10)) == 0 && dma_lds_need(c, l, nsrc, esize) <= 160 * 1024;
   const int E = 16 / esize, vpl = (c / 10) % 10;
   return (l == 16 || l == 32) && n % (4 * E * vpl) == 0;
