@@ -31,7 +31,13 @@ print(json.dumps({"mode": os.environ.get("MODE"), "k": int(k), "k_ref": int(gold
                   "fhist_rel_max": float(rel.max()), "fhist_rel_last": float(rel[-1]),
                   "x_err_over_max": float(np.max(np.abs(xx - xr)) / np.max(np.abs(xr)))}), flush=True)
 ''' % {"root": ROOT}
-for mode, env in (("split", {"GLX_SPLIT_F32": "1"}), ("dense", {})):
+MODES = [("split", {"GLX_SPLIT_F32": "1"}), ("dense", {})]
+if "--variants" in sys.argv:   # other summation orders of the same two forms (noise draws)
+    MODES = [("dense_S4", {"GLX_AXB_S": "4"}), ("dense_S16", {"GLX_AXB_S": "16"}),
+             ("dense_52224", {"GLX_AXB_VARIANT": "52224"}),
+             ("split_21410", {"GLX_SPLIT_F32": "1", "GLX_AX_DMA32": "0"}),
+             ("split_S4", {"GLX_SPLIT_F32": "1", "GLX_AX_S": "4"})]
+for mode, env in MODES:
     e = dict(os.environ, MODE=mode, **env)
     r = subprocess.run([sys.executable, "-c", CODE], env=e, capture_output=True, text=True, timeout=600)
     sys.stdout.write(r.stdout)
