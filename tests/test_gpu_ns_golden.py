@@ -106,3 +106,41 @@ def test_whole_solve_c3_fp32():
         xr = gold["x"].astype(np.float64)
         xx = x.cpu().numpy().astype(np.float64) if hasattr(x, "cpu") else np.asarray(x, np.float64)
         assert np.max(np.abs(xx - xr)) <= 5e-2 * np.max(np.abs(xr))
+
+
+
+@pytest.mark.parametrize("tag,method", [("c2", "gl_ProxGD_primal"), ("c4", "gl_SGD_primal")])
+def test_whole_solve_baseline_configs(tag, method):
+    """BASELINE configs C2 (gl_ProxGD_primal fp64, (4096, 8192, 16)) and C4 (gl_SGD_primal fp64,
+    l = 1, (65536, 8192)): the whole solve against the reference's own run of the same call
+    (tests/golden/make_golden_<tag>.py). North-star fp64 bar: identical k, fval and every
+    f_hist / f_hist_best entry within 1e-8 relative, the iterate within 1e-6 of max|x|."""
+    import importlib
+    # generated at the end of round 4 and not yet run on a GPU box: kept under golden/pending/
+    # and exercised only with GLX_GOLDEN_PENDING=1 until they have been validated
+    gdir = os.path.join(GOLD, "pending") if os.environ.get("GLX_GOLDEN_PENDING") == "1" else GOLD
+    meta_path = os.path.join(gdir, "%s_%s.json" % (tag, method))
+    if not os.path.exists(meta_path):
+        pytest.skip("%s fixture not in %s" % (tag, gdir))
+    meta = json.load(open(meta_path))
+    from oracle import numpy_ref
+    A, _, u, x0, mu = numpy_ref.gen_data(meta["m"], meta["n"], meta["l"], meta["seed"])
+    gold = np.load(os.path.join(gdir, "%s_%s.npz" % (tag, method)))
+    b = gold["b"]
+    assert _sha(A) == meta["sha256"]["A"] and _sha(x0) == meta["sha256"]["x0"]
+    assert _sha(u) == meta["sha256"]["u"] and _sha(b) == meta["sha256"]["b"]
+    fn = getattr(importlib.import_module(method), method)
+    At = torch.from_numpy(A).cuda()
+    del A
+    x, k, out = fn(torch.from_numpy(x0).cuda(), At, torch.from_numpy(b).cuda(), mu, dict(meta["opts"]))
+    torch.cuda.synchronize()
+    x = x.cpu().numpy()
+    assert k == int(gold["k"]), (k, int(gold["k"]))
+    fg = float(gold["fval"])
+    assert abs(float(out["fval"]) - fg) <= 1e-8 * abs(fg), (float(out["fval"]), fg)
+    for key in ("f_hist", "f_hist_best"):
+        got = np.asarray([float(v) for v in out[key]])
+        rel = np.max(np.abs(got - gold[key]) / np.abs(gold[key]))
+        assert rel <= 1e-8, (key, rel)
+    xr = gold["x"].astype(np.float64)
+    assert np.max(np.abs(x - xr)) <= 1e-6 * np.max(np.abs(xr))
