@@ -116,9 +116,7 @@ def test_whole_solve_baseline_configs(tag, method):
     (tests/golden/make_golden_<tag>.py). North-star fp64 bar: identical k, fval and every
     f_hist / f_hist_best entry within 1e-8 relative, the iterate within 1e-6 of max|x|."""
     import importlib
-    # generated at the end of round 4 and not yet run on a GPU box: kept under golden/pending/
-    # and exercised only with GLX_GOLDEN_PENDING=1 until they have been validated
-    gdir = os.path.join(GOLD, "pending") if os.environ.get("GLX_GOLDEN_PENDING") == "1" else GOLD
+    gdir = GOLD
     meta_path = os.path.join(gdir, "%s_%s.json" % (tag, method))
     if not os.path.exists(meta_path):
         pytest.skip("%s fixture not in %s" % (tag, gdir))
