@@ -70,9 +70,10 @@ def log(*a):
 
 
 def make_instance(m, n, l, r0, r1, dtype, device, seed=97006855):
-    """Synthetic instance (the gen_data recipe of main.py:37-51 at scale): A ~ N(0,1), a 10 %
-    row-sparse ground truth u, b = A u, x0 ~ N(0,1). Generated on the device in 256-row blocks
-    with per-block seeds, so every rank builds exactly its rows of the same global A."""
+    """Large shapes (A beyond HOST_GEN_BYTES, e.g. C5's 131072 rows): A ~ N(0,1), a 10 % row-sparse
+    ground truth u, b = A u, x0 ~ N(0,1), drawn with torch's Philox generator on the device per
+    256-row block with per-block seeds, so every rank builds exactly its rows of the same global
+    A. NOT the main.py:37-51 stream (the `data` label says so); no reference run exists for it."""
     g = torch.Generator(device=device)
     g.manual_seed(seed)
     k = round(0.1 * n)
@@ -92,9 +93,101 @@ def make_instance(m, n, l, r0, r1, dtype, device, seed=97006855):
     return A.contiguous(), b.contiguous(), x0.to(dtype).contiguous()
 
 
+# The reference's own whole solves of the BASELINE configs (tests/golden/make_golden_*.py ran
+# /root/reference/code on gen_data's instance in the build container): (method, dtype, m, n, l) ->
+# (fixture stem, where b comes from). b = A u is taken from the fixture, because the host BLAS's
+# A @ u is not portable bit for bit; A and x0 are re-drawn and sha256-checked against the fixture.
+GOLDEN = {
+    ("gl_ProxGD_primal", "f64", 8192, 16384, 32): ("ns_gl_ProxGD_primal", "ns_instance_b"),
+    ("gl_FProxGD_primal", "f64", 8192, 16384, 32): ("ns_gl_FProxGD_primal", "ns_instance_b"),
+    ("gl_FProxGD_primal", "f32", 8192, 16384, 32): ("c3_gl_FProxGD_primal", "ns_instance_b"),
+    ("gl_ProxGD_primal", "f64", 4096, 8192, 16): ("c2_gl_ProxGD_primal", "c2_gl_ProxGD_primal"),
+    ("gl_SGD_primal", "f64", 65536, 8192, 1): ("c4_gl_SGD_primal", "c4_gl_SGD_primal"),
+}
+GOLDEN_DIR = os.path.join(ROOT, "tests", "golden")
+HOST_GEN_BYTES = 4.5 * 2 ** 30   # gen_data on the host up to this much fp64 A (C4: 4 GiB)
+
+
+def _sha(a):
+    import hashlib
+    return hashlib.sha256(np.ascontiguousarray(a).tobytes()).hexdigest()
+
+
+def reference_instance(method, dt, m, n, l, r0, r1, dtype, device, seed=97006855):
+    """The instance main.py:37-51 draws (gen_data: one MT19937(seed) stream, A, permutation, rows of
+    u, x0 in that order; glx.driver.gen_data), generalised to (m, n, l); every rank draws the whole
+    A on the host and keeps its rows [r0, r1). Where a reference whole solve of this exact call is
+    committed (GOLDEN), b is that run's own A u and the line's whole_solve is checked against it.
+    Returns (A, b, x0, info)."""
+    from glx.driver import gen_data
+    if m * n * 8 > HOST_GEN_BYTES:
+        A, b, x0 = make_instance(m, n, l, r0, r1, dtype, device, seed)
+        return A, b, x0, {"data": "synthetic, torch Philox on the device per 256-row block (A beyond "
+                                  "%.1f GiB: main.py's MT19937 stream not drawn on the host); no "
+                                  "reference run of this instance" % (HOST_GEN_BYTES / 2 ** 30),
+                          "golden": None}
+    _, _, _, _, An, bn, _, xn, _, _, _ = gen_data(seed, m, n, l)
+    info = {"data": "synthetic: main.py:37-51 gen_data (MT19937 seed %d: A, permutation, u rows, x0) "
+                    "at (m,n,l)=(%d,%d,%d), drawn on the host%s" % (seed, m, n, l,
+                                                                    "" if dt == "f64" else ", cast to fp32"),
+            "golden": None}
+    key = GOLDEN.get((method, dt, m, n, l))
+    if key is not None:
+        stem, bsrc = key
+        meta_p = os.path.join(GOLDEN_DIR, stem + ".json")
+        if os.path.exists(meta_p):
+            meta = json.load(open(meta_p))
+            bref = np.load(os.path.join(GOLDEN_DIR, bsrc + ".npz"))["b"]
+            if dt == "f64":
+                ok = _sha(An) == meta["sha256"]["A"] and _sha(xn) == meta["sha256"]["x0"] and \
+                    _sha(bref) == meta["sha256"]["b"]
+            else:
+                ok = _sha(An.astype(np.float32)) == meta["sha256"]["A32"] and \
+                    _sha(xn.astype(np.float32)) == meta["sha256"]["x032"] and \
+                    _sha(bref.astype(np.float32)) == meta["sha256"]["b32"]
+            if ok:
+                bn = bref
+                info["golden"] = {"stem": stem, "meta": meta}
+                info["data"] += ("; b = the reference run's own A u (tests/golden/%s.npz), A / x0 / b "
+                                 "sha256 = tests/golden/%s.json" % (bsrc, stem))
+            else:
+                info["data"] += "; instance sha256 differs from tests/golden/%s.json: no reference check" % stem
+    npdt = np.float64 if dt == "f64" else np.float32
+    A = torch.from_numpy(np.ascontiguousarray(An[r0:r1], dtype=npdt)).to(device)
+    b = torch.from_numpy(np.ascontiguousarray(bn[r0:r1], dtype=npdt)).to(device)
+    x0 = torch.from_numpy(np.ascontiguousarray(xn, dtype=npdt)).to(device)
+    return A, b, x0, info
+
+
+def vs_reference(info, k, fval, f_hist, dt):
+    """The whole solve against the committed reference run of the same call (GOLDEN): the
+    north-star bar in fp64 (k identical, fval and every f_hist entry within 1e-8 relative), the
+    fp32 bar on fval (1e-6) in fp32."""
+    g = info.get("golden")
+    if g is None:
+        return None
+    gold = np.load(os.path.join(GOLDEN_DIR, g["stem"] + ".npz"))
+    kg, fg = int(gold["k"]), float(gold["fval"])
+    fh = np.asarray(f_hist, dtype=np.float64)
+    fh_rel = (float(np.max(np.abs(fh - gold["f_hist"]) / np.abs(gold["f_hist"])))
+              if fh.shape == gold["f_hist"].shape else None)
+    frel = abs(fval - fg) / abs(fg)
+    if dt == "f64":
+        ok = k == kg and frel <= 1e-8 and fh_rel is not None and fh_rel <= 1e-8
+        bar = "k identical, fval and every f_hist entry within 1e-8 relative (north star, fp64)"
+    else:
+        ok = frel <= 1e-6 and abs(k - kg) <= max(1, int(0.005 * kg))
+        bar = "fval within 1e-6 relative, k within 0.5 % (fp32)"
+    return {"reference": "tests/golden/%s.npz (the reference's own run of this call)" % g["stem"],
+            "k_ref": kg, "k": int(k), "fval_ref": fg, "fval_rel_diff": frel,
+            "f_hist_max_rel_diff": fh_rel, "bar": bar, "within_bar": bool(ok)}
+
+
 def cpu_baseline(method, A, b, x0, mu, opts, budget_s=15.0):
     """Time the NumPy oracle (test infrastructure) on the host on a bounded sample: the same
-    instance, a fixed number of iterations per continuation phase."""
+    instance, a fixed number of iterations per continuation phase. The GPU solver then runs the
+    same sample (same opts and maxit) and its f_hist is compared with the oracle's entry by entry
+    (`gpu_same_sample`): parity evidence of the measured path inside the bench run itself."""
     from oracle import numpy_ref
     try:
         from threadpoolctl import threadpool_info
@@ -114,26 +207,21 @@ def cpu_baseline(method, A, b, x0, mu, opts, budget_s=15.0):
     maxit = int(max(1, min(200, budget_s / (3 * per_iter))))
     o = dict(opts, maxit=maxit)
     t0 = time.perf_counter()
-    _, k, _ = fn(xn, An, bn, mu, o)
+    _, k, outc = fn(xn, An, bn, mu, o)
     dt = time.perf_counter() - t0
+    import glx
+    _, kg, outg = glx.solve(method, x0.clone(), A, b, mu, dict(o))
+    fc = np.asarray([float(v) for v in outc["f_hist"]])
+    fg = np.asarray([float(v) for v in outg["f_hist"]])
+    same = {"k_cpu": int(k), "k_gpu": int(kg),
+            "f_hist_max_rel_diff": (float(np.max(np.abs(fg - fc) / np.abs(fc)))
+                                    if fg.shape == fc.shape else None),
+            "fval_rel_diff": abs(float(outg["fval"]) - float(outc["fval"])) / abs(float(outc["fval"])),
+            "what": "glx.solve on the same sample (maxit=%d per phase) against the oracle's run" % maxit}
     return {"value": k / dt, "unit": "iters/s", "cores": threads, "kind": "port",
             "sample": "oracle/numpy_ref.%s on the same instance, %d iterations (maxit=%d per phase), "
-                      "%.1f s; BLAS %s" % (method, k, maxit, dt, blas)}
-
-
-def _plan_parts(dtype, m, n, l):
-    from glx import _lib
-    return _lib.plan_describe(_lib.GLX_F64 if dtype == "f64" else _lib.GLX_F32, m, n, l).split("; ")
-
-
-def ax_kernel_name(dtype, m, n, l, nsrc):
-    """The A@X tile libglx launched for this shape and right-hand-side count (its own planner)."""
-    parts = _plan_parts(dtype, m, n, l)
-    key = "ax%d=" % max(1, min(3, int(round(nsrc))))
-    for part in parts:
-        if part.startswith(key):
-            return "A@X: " + part[len(key):]
-    return "; ".join(parts)
+                      "%.1f s; BLAS %s" % (method, k, maxit, dt, blas),
+            "gpu_same_sample": same}
 
 
 PMC_FILE = "profiles/pmc_traffic.json"
@@ -270,12 +358,15 @@ def main():
     dtype = torch.float64 if args.dtype == "f64" else torch.float32
     r0, r1 = shard_rows(m, world, rank)
     t_gen = time.perf_counter()
-    A, b, x0 = make_instance(m, n, l, r0, r1, dtype, device)
+    A, b, x0, inst = reference_instance(args.method, args.dtype, m, n, l, r0, r1, dtype, device)
     torch.cuda.synchronize()
-    log("rank %d: instance rows [%d,%d) x %d x %d %s generated in %.1fs" %
-        (rank, r0, r1, n, l, args.dtype, time.perf_counter() - t_gen))
+    log("rank %d: instance rows [%d,%d) x %d x %d %s generated in %.1fs (%s)" %
+        (rank, r0, r1, n, l, args.dtype, time.perf_counter() - t_gen,
+         "reference run %s" % inst["golden"]["stem"] if inst["golden"] else "no reference run"))
     mu = 1e-2
     alpha0 = float(1.0 / (math.sqrt(m) + math.sqrt(n)) ** 2)
+    if inst["golden"] is not None:   # the reference run's own alpha0 (the same expression)
+        alpha0 = float(inst["golden"]["meta"]["opts"]["alpha0"])
     total = args.warmup + args.steps
     opts = {"alpha0": alpha0, "maxit": max(total + 1, 2500), "max_total_iters": total,
             "profile": args.profile, "ax_variant": args.variant, "exact_objective": args.exact}
@@ -301,6 +392,11 @@ def main():
             if pw.finished or got == 0:
                 break
         prewarm["seconds"] = round(time.perf_counter() - t_pw, 3)
+        # closed before the timed warmup: only one session's workspace (with
+        # its transposed copy of A) is live while timing; closing costs host time only
+        pw.close()
+        pw = None
+    plan = s.describe()
     s.run(args.warmup)
     for kind in (0, 1, 2):
         s.kernel_time(kind)
@@ -323,9 +419,6 @@ def main():
         elapsed = float(t.item())
         dist.barrier()
     c1 = s.counters()
-    if pw is not None:
-        pw.close()
-        del pw
     work = {k: c1[k] - c0[k] for k in c1}   # executed work of the timed region
     ax_n, ax_ms = s.kernel_time(0)
     atr_n, atr_ms = s.kernel_time(1)
@@ -345,6 +438,8 @@ def main():
         torch.cuda.synchronize()
         whole = {"k": int(kw), "tt_s": float(outw["tt"]), "iters_per_s": float(kw) / float(outw["tt"]),
                  "fval": float(outw["fval"]),
+                 "vs_reference": vs_reference(inst, int(kw), float(outw["fval"]), outw["f_hist"],
+                                              args.dtype),
                  "what": "the whole continuation solve from x0 to the solver's stop rule (default "
                          "maxit), same instance and opts, timed by the solver (tt); not `value`"}
 
@@ -358,28 +453,22 @@ def main():
         # only in the rows the hard threshold touched) gathered from the flagged rows of a
         # transposed copy of A (m values each); its algorithmic work is 2 m l flops per such row.
         nsrc = work["ax_sources"] / max(1, work["ax_calls"])
-        # the solver's split-candidate rule (solver.cpp split_mode): fp64 (fp32: FProxGD with
-        # GLX_SPLIT_F32=1, round 4), not exact, m n * 8 B of this rank >= 768 MiB unless GLX_SPLIT_CAND=1 forces
-        # it; l in {16, 32} and n < 65536 (gather)
-        split_env = os.environ.get("GLX_SPLIT_CAND", "")
-        dtype_ok = args.dtype == "f64" or (args.method == "gl_FProxGD_primal" and
-                                           os.environ.get("GLX_SPLIT_F32", "") == "1")
-        split_on = (dtype_ok and not args.exact and split_env != "0" and
-                    (ml * n * 8 >= 768 * 2 ** 20 or split_env == "1"))
-        gather_fits = l in (16, 32) and n <= 65535
+        # the split-candidate form the session runs (glx_session_describe: dense / the row form
+        # k_at_rows / the column-list gather)
+        parts = plan.split("; ")
+        split_desc = next((q[6:] for q in parts if q.startswith("split=")), "dense")
+        split_cand = split_desc != "dense"
         st = res["stats"]
-        if args.method == "gl_ProxGD_primal":
-            split_cand = split_on and gather_fits
-            sparse_rows = st[1] / max(1.0, st[2]) if split_cand else 0.0
+        if args.method == "gl_ProxGD_primal" and split_cand:
+            sparse_rows = st[1] / max(1.0, st[2])   # rows of e flagged per trial
             gather_rows = sparse_rows
-        elif args.method == "gl_FProxGD_primal":
-            split_cand = (split_on and gather_fits and
-                          os.environ.get("GLX_SPLIT_FISTA", "") != "0")
-            # nnz(e_c) per gathered batch; bytes averaged over all trial batches (some are dense)
-            sparse_rows = st[5] / max(1.0, st[3]) if split_cand else 0.0
-            gather_rows = st[5] / max(1.0, st[3] + st[4]) if split_cand else 0.0
+        elif args.method == "gl_FProxGD_primal" and split_cand:
+            # flagged rows (row form; VALU gather: nonzeros) of e_c per gathered batch; bytes
+            # averaged over all trial batches (some are dense)
+            sparse_rows = st[5] / max(1.0, st[3])
+            gather_rows = st[5] / max(1.0, st[3] + st[4])
         else:
-            split_cand, sparse_rows, gather_rows = False, 0.0, 0.0
+            sparse_rows, gather_rows = 0.0, 0.0
         # the dense A@X pass and the split-candidate gather are separate kernels, timed apart
         ax_bytes = es * (ml * n + (ml + n) * l * nsrc)
         ga_bytes = es * (n * l + ml * gather_rows) if split_cand else 0.0
@@ -388,15 +477,12 @@ def main():
         ga_flops = 2.0 * ml * l * sparse_rows
         atr_flops = 2.0 * ml * n * l
         ga_avg_s = (ga_ms / ga_n) / 1e3 if ga_n else 0.0
-        ach = ax_bytes / ax_avg_s / 1e9 if ax_n else None
-        ax_kname = ax_kernel_name(args.dtype, ml, n, l, nsrc)
+        key = "ax%d=" % max(1, min(3, int(round(nsrc))))
+        ax_kname = "A@X: " + next((q[len(key):] for q in parts if q.startswith(key)), "?")
         # PMC entries are keyed by configuration AND the A@X tile the planner picks, so a
         # measurement of another kernel is never reported as this one's traffic
         cfg_key = "%s_%s_%dx%dx%d_g%d|%s" % (args.method, args.dtype, m, n, l, world, ax_kname)
         peak_tf = MFMA_PEAK_TFS[args.dtype]
-        mfma_bound = ax_flops / (peak_tf * 1e12) >= ax_bytes / (HBM_PEAK_GBS * 1e9)
-        ax_tf = ax_flops / ax_avg_s / 1e12 if ax_n else None
-        ax_gbs = ax_bytes / ax_avg_s / 1e9 if ax_n else None
         pair_tf = ((ax_flops + atr_flops) / (ax_avg_s + atr_avg_s) / 1e12) if (ax_n and atr_n) else None
         # SURVEY §8d's literal pair: one A@x (l right-hand sides) + one A^T r = 4 m n l flops over
         # the same two launches (the batched second right-hand side is not counted)
@@ -406,19 +492,8 @@ def main():
                      if (ax_n and atr_n) else None)
         traffic, traffic_src = pmc_traffic(cfg_key)
         atr_traffic, atr_traffic_src = pmc_traffic(cfg_key, "atr")
-        if mfma_bound:
-            ach, peak, unit = ax_tf, peak_tf, "TFLOP/s"
-        else:
-            ach, peak, unit = ax_gbs, HBM_PEAK_GBS, "GB/s"
-        fused = {"gl_ProxGD_primal": "k_atr_prox", "gl_FProxGD_primal": "k_atr_fista"}.get(args.method)
-        atr_plan = [p for p in _plan_parts(args.dtype, ml, n, l) if p.startswith("atr=")]
-        if args.dtype == "f32" and fused and world == 1 and l in (16, 32) and n % 64 == 0:
-            # solver.cpp session_plan: fp32 trial methods fuse the trial into the panel form, the
-            # eight-wave panel with one K split where n / 64 >= 256 (round 4), else 2 K splits
-            atr_plan = ["atr=k_atr_mfma<WL2,PF8,NTL1> S=1 (session plan)" if n // 64 >= 256 else
-                        "atr=k_atr_mfma<WL0,PF8,NTL1> S=2 (session plan)"]
-        atr_kname = ("A^T r%s: %s" % (" + the fused trial (%s)" % fused if fused and world == 1 else "",
-                                      atr_plan[0][4:] if atr_plan else "?"))
+        # the A^T r panel and trial the session itself launches (glx_session_describe)
+        atr_kname = "A^T r: " + next((q[4:] for q in parts if q.startswith("atr=")), "?")
         kernels = {"ax": dict(roof_of(ax_flops, ax_bytes, ax_avg_s if ax_n else None, peak_tf),
                               kernel=("k_gemv_pair_fused: A@[x|thr(x)] and A^T r in ONE pass over A (l = 1)"
                                       if work["atr_calls"] == 0 else ax_kname),
@@ -432,20 +507,22 @@ def main():
         if "atr" in kernels and atr_n and ax_n and atr_avg_s > ax_avg_s:
             dominant = "atr"
         dk = kernels[dominant]
+        # every top-level per-kernel field describes the dominant kernel;
+        # the other pass's are under kernels
         roof = {"bound": dk["bound"], "achieved": dk["achieved"], "peak": dk["peak"],
                 "unit": dk["unit"], "frac": dk["frac"], "dominant": dominant,
                 "traffic": dk["traffic"], "traffic_source": dk["traffic_source"], "pmc_key": cfg_key,
                 "kernel": dk["kernel"], "kernels": kernels,
-                "flops_per_launch": ax_flops,
-                "bytes_per_launch": ax_bytes, "avg_launch_us": ax_avg_s * 1e6, "launches_timed": ax_n,
+                "flops_per_launch": dk["flops_per_launch"],
+                "bytes_per_launch": dk["bytes_per_launch"], "avg_launch_us": dk["avg_launch_us"],
+                "launches_timed": dk["launches_timed"],
+                "hbm_GBs": dk["hbm_GBs"], "hbm_frac": dk["hbm_frac"],
+                "mfma_tflops": dk["mfma_tflops"], "mfma_frac": dk["mfma_frac"],
+                "session_plan": plan,
                 "timed_every": args.profile,
                 "rhs_per_launch": nsrc,
-                "split_candidate": "gather" if split_cand else False,
-                "sparse_rows_per_launch": sparse_rows, "hbm_GBs": ax_gbs, "hbm_frac": ax_gbs / HBM_PEAK_GBS if ax_n else None,
-                "mfma_tflops": ax_tf, "mfma_frac": ax_tf / peak_tf if ax_n else None,
-                "atr_avg_launch_us": atr_avg_s * 1e6,
-                "atr_GBs": atr_bytes / atr_avg_s / 1e9 if atr_n else None,
-                "atr_mfma_frac": (atr_flops / atr_avg_s / 1e12) / peak_tf if atr_n else None,
+                "split_candidate": split_desc if split_cand else False,
+                "sparse_rows_per_launch": sparse_rows,
                 "pair_tflops": pair_tf, "pair_frac": pair_tf / peak_tf if pair_tf else None,
                 "pair_definition": "pair_frac: algorithmic MFMA flops of the dense A@X launch "
                                    "(2 m n l per dense right-hand side) + A^T r (2 m n l), over "
@@ -468,8 +545,7 @@ def main():
             "steps": steps, "warmup": args.warmup, "ms_per_step": 1e3 * elapsed / steps,
             "higher_is_better": True, "scaling": "strong", "vs_baseline": None,
             "dtype": args.dtype,
-            "data": "synthetic: Gaussian A, 10% row-sparse ground truth u, b = A u (main.py:37-51 "
-                    "recipe, generated on device per 256-row block)",
+            "data": inst["data"],
             "config": {"workload": "%s %s (m,n,l)=(%d,%d,%d), mu0=1e-2, alpha0=1/(sqrt(m)+sqrt(n))^2"
                                    % (args.method, args.dtype, m, n, l, ),
                        "method": args.method, "m": m, "n": n, "l": l,

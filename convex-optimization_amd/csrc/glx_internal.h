@@ -221,7 +221,16 @@ void launch_atr_fista(const GemmPlan& p, const T* A, const T* R, T* G, const T* 
 // gather_ok: the shape supports it (l in {16, 32}, n < 65536); gather_split: K splits of the
 // flagged-row list for m output rows (slabs P[S][m][l]).
 bool gather_ok(int64_t n, int64_t l);
-int gather_split(int64_t m);
+// round 5: the MFMA row form (k_at_rows): the shapes it takes, the solver's default (GLX_GATHER=valu:
+// the column-list gather, ONE slab), and its K splits for this shape (1 where it does not apply)
+bool gather_rows_ok(int64_t m, int64_t n);
+bool gather_rows_env();
+int gather_split(int64_t m, int64_t n);
+// P[s][r][c] = sum over the flagged rows k (zf[k] != 0) of K range s, ascending:
+// At[k][r] E[k][c], s < gather_split(m, n); counts[s] (gather_counts) = the flagged rows of range s
+template <typename T>
+void launch_at_rows(const T* At, const T* E, const unsigned* zf, int64_t m, int64_t n, int64_t l,
+                    T* P, void* lists_ws, hipStream_t st, const int* skip = nullptr);
 // At (n x m) = A^T
 template <typename T>
 void launch_transpose(const T* A, T* At, int64_t m, int64_t n, hipStream_t st);

@@ -107,6 +107,33 @@ static inline int ax_xmap_flags(const GemmPlan& p, int S) {
   return ((p.ax_xmap & 1) && ax_xmap_ok(S) ? 1 : 0) | (p.ax_xmap & 2);
 }
 
+// A lane (i, q) of a row step feeds the four MFMAs e = 0..3 with row q of A at panel columns
+// atr_col(i, e); MFMA e's output row i is then G row col0 + atr_col(i, e). f64: columns
+// {2i, 2i+1} and {32 + 2i, 33 + 2i}, so each of the two 16-B loads of a wave-instruction covers
+// 256 contiguous bytes of each of its four rows (the streaming probe, scripts/stream_probe.hip:
+// 6.1 TB/s for the 4i..4i+3 form, whose loads leave every other 16 B of a 512-B span to the
+// next instruction, against 6.3-7.1 TB/s for contiguous 256/512-B pieces). f32: one 16-B load
+// already covers columns 4i..4i+3.
+template <typename T>
+__device__ inline int atr_col(int i, int e) {
+  if constexpr (sizeof(T) == 8) return (e >> 1) * 32 + 2 * i + (e & 1);
+  else return 4 * i + e;
+}
+template <typename T, bool NTL> struct Load4;
+template <bool NTL> struct Load4<double, NTL> {
+  __device__ static inline void go(const double* p, double (&a)[4]) {   // p = row + col0 + 2i
+    const d2_t v0 = load_vec<double, NTL>(p);
+    const d2_t v1 = load_vec<double, NTL>(p + 32);
+    a[0] = v0[0]; a[1] = v0[1]; a[2] = v1[0]; a[3] = v1[1];
+  }
+};
+template <bool NTL> struct Load4<float, NTL> {
+  __device__ static inline void go(const float* p, float (&a)[4]) {
+    const f4_t v = load_vec<float, NTL>(p);
+    a[0] = v[0]; a[1] = v[1]; a[2] = v[2]; a[3] = v[3];
+  }
+};
+
 __device__ inline double wave_sum(double v) {
 #pragma unroll
   for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off);

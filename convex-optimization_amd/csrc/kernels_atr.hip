@@ -22,33 +22,6 @@ namespace glx {
 // blockIdx.y = row split. Needs n % 64 == 0 (n % 256 for WL = 1), m % 4 == 0.
 // Gp[split][n][16*NT].
 // ------------------------------------------------------------------------------------------
-// A lane (i, q) of a row step feeds the four MFMAs e = 0..3 with row q of A at panel columns
-// atr_col(i, e); MFMA e's output row i is then G row col0 + atr_col(i, e). f64: columns
-// {2i, 2i+1} and {32 + 2i, 33 + 2i}, so each of the two 16-B loads of a wave-instruction covers
-// 256 contiguous bytes of each of its four rows (the streaming probe, scripts/stream_probe.hip:
-// 6.1 TB/s for the 4i..4i+3 form, whose loads leave every other 16 B of a 512-B span to the
-// next instruction, against 6.3-7.1 TB/s for contiguous 256/512-B pieces). f32: one 16-B load
-// already covers columns 4i..4i+3.
-template <typename T>
-__device__ inline int atr_col(int i, int e) {
-  if constexpr (sizeof(T) == 8) return (e >> 1) * 32 + 2 * i + (e & 1);
-  else return 4 * i + e;
-}
-template <typename T, bool NTL> struct Load4;
-template <bool NTL> struct Load4<double, NTL> {
-  __device__ static inline void go(const double* p, double (&a)[4]) {   // p = row + col0 + 2i
-    const d2_t v0 = load_vec<double, NTL>(p);
-    const d2_t v1 = load_vec<double, NTL>(p + 32);
-    a[0] = v0[0]; a[1] = v0[1]; a[2] = v1[0]; a[3] = v1[1];
-  }
-};
-template <bool NTL> struct Load4<float, NTL> {
-  __device__ static inline void go(const float* p, float (&a)[4]) {
-    const f4_t v = load_vec<float, NTL>(p);
-    a[0] = v[0]; a[1] = v[1]; a[2] = v[2]; a[3] = v[3];
-  }
-};
-
 // One 64-column panel of A^T R over this wave's (WL 1: this block's) row range; returns the
 // panel's first column. acc[e][nt] holds rows col0 + atr_col(M::row(lane, r), e). For WL 0 the
 // block's four waves split the rows (K) and are summed through LDS in the fixed order

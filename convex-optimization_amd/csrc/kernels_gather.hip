@@ -229,10 +229,197 @@ __global__ __launch_bounds__(kGThreads) void k_at_gather2(const T* __restrict__ 
   }
 }
 
-// A e is written as ONE slab (no K split)
-int gather_split(int64_t m) {
-  (void)m;
-  return 1;
+// ------------------------------------------------------------------------------------------
+// Round 5: A e as the A^T R panel over the flagged rows of e (k_at_rows, the default).
+//
+//   P[s][r][c] = sum over the flagged rows k of K range s (ascending):  At[k][r] * e[k][c]
+//
+// i.e. Y = At_F^T e_F, the gradient contraction's shape (kernels_atr.hip atr_panel) with its K
+// index (rows of A there, rows of At here) drawn from the list F of rows whose column mask zf[k]
+// (written by the trial kernels) is nonzero. The VALU gather above reads one At row per NONZERO
+// of e and one 512-B piece per wave-instruction at ~4.5 TB/s; this form reads each flagged row
+// once, whatever its nonzero count, in the 512-B pieces of the A^T R panel (4 rows x 2 x 256 B per
+// wave-instruction pair, non-temporal), and multiplies all l columns on MFMA: FProxGD's e_c
+// (flagged rows ~0.4 n late in a solve) is dense enough that the zero products cost nothing
+// beside the bytes, and ProxGD's e (~1.1 nonzeros per flagged row) pays 2 m l flops per row at
+// l / 4 flop/B, still HBM-bound. No column lists: every workgroup compacts the flags of its own
+// K range into an ascending list in LDS (a block scan over n / S0 masks, L2 hits), so k_e_lists
+// goes too.
+// Grid: (m / 64 panels) x S0 K splits; block = 4 waves splitting the K range's list (WL 0 of
+// atr_panel), reduced through LDS in the fixed order ((w0 + w1) + w2) + w3. Slab s of P holds K
+// range s; the finalize sums the S0 slabs in order: deterministic. counts[s] = the flagged rows
+// of range s (panel 0's workgroup): FProxGD's budget input (nnz of e_c counted in rows).
+// Needs m % 64 == 0 (whole panels, 16-B aligned At rows) and a K range of at most kRowsListMax
+// rows (S0 >= n / kRowsListMax); else the VALU gather runs.
+constexpr int kRowsListMax = 16384;   // u16 row indices (n <= 65535), 32 KiB of LDS
+
+template <typename T, int NT, int PF, bool NTL>
+__global__ __launch_bounds__(256, 2) void k_at_rows(const T* __restrict__ At, const T* __restrict__ E,
+                                                    const unsigned* __restrict__ zf, int64_t m,
+                                                    int64_t n, int S0, T* __restrict__ P,
+                                                    unsigned* __restrict__ counts,
+                                                    const int* __restrict__ skip) {
+  if (skip != nullptr && *skip != 0) return;
+  typedef MF<T> M;
+  typedef typename M::acc_t C;
+  constexpr int L = 16 * NT;
+  constexpr int kRedBytes = 4 * 4 * NT * 64 * (int)sizeof(C);
+  constexpr int kLdsBytes = kRedBytes > 2 * (kRowsListMax + 8) ? kRedBytes : 2 * (kRowsListMax + 8);
+  // the list lives through the main loop, the wave partials after it: one buffer
+  __shared__ __attribute__((aligned(16))) unsigned char lds[kLdsBytes];
+  __shared__ unsigned wsum[4];
+  unsigned short* lst = reinterpret_cast<unsigned short*>(lds);
+  C(*red)[4 * NT][64] = reinterpret_cast<C(*)[4 * NT][64]>(lds);
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63, wave = tid >> 6;
+  const int i = lane & 15, q = lane >> 4;
+  const int64_t gp = m / 64;
+  const int64_t panel = (int64_t)blockIdx.x % gp, split = (int64_t)blockIdx.x / gp;
+  const int64_t col0 = panel * 64;
+  // K range of this split in whole 64-row chunks (16-B aligned mask loads)
+  const int64_t nch = (n + 63) / 64;
+  const int64_t k0 = 64 * (nch * split / S0);
+  const int64_t k1e = 64 * (nch * (split + 1) / S0);
+  const int64_t k1 = k1e < n ? k1e : n;
+
+  // ---- compaction: thread t owns the masks [k0 + t per, k0 + (t + 1) per), per % 4 == 0
+  const int64_t len = k1 - k0;
+  const int64_t per = (((len + 255) / 256) + 3) & ~int64_t(3);   // <= 64 (len <= 16384)
+  const int64_t f0 = k0 + tid * per;
+  uint64_t bits = 0;   // bit j: row f0 + j flagged
+  for (int64_t j = 0; j < per; j += 4) {
+    const int64_t k = f0 + j;
+    if (k < k1) {
+      const uint4 v = *reinterpret_cast<const uint4*>(zf + k);
+      const unsigned w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+      for (int u = 0; u < 4; ++u)
+        if (k + u < k1 && w[u] != 0u) bits |= uint64_t(1) << (j + u);
+    }
+  }
+  const unsigned cnt = (unsigned)__builtin_popcountll(bits);
+  unsigned inc = cnt;
+#pragma unroll
+  for (int off = 1; off < 64; off <<= 1) {
+    const unsigned v = __shfl_up(inc, off);
+    if (lane >= off) inc += v;
+  }
+  if (lane == 63) wsum[wave] = inc;
+  __syncthreads();
+  unsigned pos = inc - cnt, R = 0;
+#pragma unroll
+  for (int w = 0; w < 4; ++w) {
+    if (w < wave) pos += wsum[w];
+    R += wsum[w];
+  }
+  while (bits != 0) {
+    const int j = __builtin_ctzll(bits);
+    bits &= bits - 1;
+    lst[pos++] = (unsigned short)(f0 + j);
+  }
+  __syncthreads();
+  // pad the last row step: positions R .. R + 3 repeat a valid row, their e is taken as 0
+  if (tid < 4) lst[R + tid] = (unsigned short)(R > 0 ? lst[R - 1] : k0);
+  if (panel == 0 && tid == 0) counts[split] = R;
+  __syncthreads();
+
+  // ---- the A^T R panel over the list (atr_panel, WL 0): wave w takes row steps [sb, se)
+  const int Ri = __builtin_amdgcn_readfirstlane((int)R);
+  const int steps = (Ri + 3) / 4;
+  const int sb = steps * wave / 4, se = steps * (wave + 1) / 4;
+  const int nst = __builtin_amdgcn_readfirstlane(se - sb);
+  C acc[4][NT];
+#pragma unroll
+  for (int e = 0; e < 4; ++e)
+#pragma unroll
+    for (int nt = 0; nt < NT; ++nt) acc[e][nt] = C{};
+  T a[PF][4], rb[PF][NT];
+  // ring slot p's next row: its index is read from the LDS list one ring cycle ahead of the
+  // global loads that use it, so no LDS wait sits in front of a load issue
+  int kx[PF];
+  bool lv[PF];
+  auto fetch = [&](int p, int off) {
+    off = off < nst ? off : nst - 1;   // past the end: the last step again (never consumed)
+    const int pos = (sb + off) * 4 + q;
+    kx[p] = lst[pos];
+    lv[p] = pos < Ri;
+  };
+  auto ld = [&](int p) {
+    const int64_t k = kx[p];
+    Load4<T, NTL>::go(At + k * m + col0 + atr_col<T>(i, 0), a[p]);
+#pragma unroll
+    for (int nt = 0; nt < NT; ++nt) {
+      const T ev = E[k * L + nt * 16 + i];
+      rb[p][nt] = lv[p] ? ev : T(0);
+    }
+  };
+  auto mma_step = [&](int p) {
+#pragma unroll
+    for (int e = 0; e < 4; ++e)
+#pragma unroll
+      for (int nt = 0; nt < NT; ++nt) acc[e][nt] = M::mma(a[p][e], rb[p][nt], acc[e][nt]);
+  };
+  if (nst > 0) {
+#pragma unroll
+    for (int p = 0; p < PF; ++p) {
+      fetch(p, p);
+      ld(p);
+      fetch(p, p + PF);
+    }
+    int s0 = 0;
+    for (; s0 + PF <= nst; s0 += PF) {
+#pragma unroll
+      for (int p = 0; p < PF; ++p) {
+        mma_step(p);
+        ld(p);
+        fetch(p, s0 + p + 2 * PF);
+      }
+    }
+#pragma unroll
+    for (int p = 0; p < PF - 1; ++p)
+      if (s0 + p < nst) mma_step(p);
+  }
+  __syncthreads();   // the list is dead: its LDS takes the wave partials
+#pragma unroll
+  for (int e = 0; e < 4; ++e)
+#pragma unroll
+    for (int nt = 0; nt < NT; ++nt) red[wave][e * NT + nt][lane] = acc[e][nt];
+  __syncthreads();
+  T* out = P + split * m * L;
+#pragma unroll
+  for (int nt = 0; nt < NT; ++nt) {
+    C v = red[0][wave * NT + nt][lane];
+#pragma unroll
+    for (int s = 1; s < 4; ++s) v += red[s][wave * NT + nt][lane];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int64_t row = col0 + atr_col<T>(M::row(lane, r), wave);
+      out[row * L + nt * 16 + i] = v[r];
+    }
+  }
+}
+
+static int env_rows_s() {
+  const char* e = std::getenv("GLX_ATROWS_S");
+  return e ? std::atoi(e) : 0;
+}
+// the shapes the MFMA row form (k_at_rows) takes: whole 64-row panels of At
+bool gather_rows_ok(int64_t m, int64_t n) { return m % 64 == 0 && m > 0 && n <= 65535; }
+// the solver's choice: the row form unless GLX_GATHER=valu (the round-2 column-list gather)
+bool gather_rows_env() {
+  const char* e = std::getenv("GLX_GATHER");
+  return !(e && std::strcmp(e, "valu") == 0);
+}
+// K splits of the row form: about two workgroups per CU (512 on 256 CUs), each K range within
+// the LDS list; GLX_ATROWS_S overrides (clamped to that bound)
+int gather_split(int64_t m, int64_t n) {
+  if (!gather_rows_ok(m, n)) return 1;   // the VALU gather: ONE slab
+  const int64_t gp = m / 64;
+  const int64_t need = (n + kRowsListMax - 1) / kRowsListMax;
+  int64_t s = env_rows_s() > 0 ? env_rows_s() : (512 + gp - 1) / gp;
+  s = s < 1 ? 1 : (s > 16 ? 16 : s);
+  return (int)(s < need ? need : s);
 }
 
 bool gather_ok(int64_t n, int64_t l) { return (l == 16 || l == 32) && n <= 65535; }
@@ -308,9 +495,36 @@ void launch_at_gather(const T* At, const T* E, int64_t m, int64_t n, int64_t l, 
   }
 }
 
+// A e over the flagged rows (k_at_rows): S0 = gather_split(m, n) slabs at P, the flagged rows of
+// each K range into the counts area of lists_ws (gather_counts)
+template <typename T>
+void launch_at_rows(const T* At, const T* E, const unsigned* zf, int64_t m, int64_t n, int64_t l,
+                    T* P, void* lists_ws, hipStream_t st, const int* skip) {
+  if (!gather_ok(n, l) || !gather_rows_ok(m, n))
+    throw Error{GLX_E_INVALID, "A e row form: needs l in {16, 32}, m % 64 == 0, n < 65536"};
+  const int S0 = gather_split(m, n);
+  const dim3 grid((unsigned)(m / 64 * S0));
+  unsigned* cnt = list_counts(lists_ws, n);
+  static const bool nt = [] {
+    const char* e = std::getenv("GLX_GATHER_NT");
+    return !(e && std::strcmp(e, "0") == 0);
+  }();
+  if (l == 32) {
+    if (nt) glx_launch(k_at_rows<T, 2, 8, true>, grid, dim3(256), 0, st, At, E, zf, m, n, S0, P, cnt, skip);
+    else glx_launch(k_at_rows<T, 2, 8, false>, grid, dim3(256), 0, st, At, E, zf, m, n, S0, P, cnt, skip);
+  } else {
+    if (nt) glx_launch(k_at_rows<T, 1, 8, true>, grid, dim3(256), 0, st, At, E, zf, m, n, S0, P, cnt, skip);
+    else glx_launch(k_at_rows<T, 1, 8, false>, grid, dim3(256), 0, st, At, E, zf, m, n, S0, P, cnt, skip);
+  }
+}
+
 // workspace of the column lists: l * n indices + 256 B of counts
 size_t gather_lists_bytes(int64_t n) { return (((size_t)32 * n * 2 + 255) & ~size_t(255)) + 256; }
 
+template void launch_at_rows<double>(const double*, const double*, const unsigned*, int64_t, int64_t,
+                                     int64_t, double*, void*, hipStream_t, const int*);
+template void launch_at_rows<float>(const float*, const float*, const unsigned*, int64_t, int64_t,
+                                    int64_t, float*, void*, hipStream_t, const int*);
 template void launch_transpose<double>(const double*, double*, int64_t, int64_t, hipStream_t);
 template void launch_transpose<float>(const float*, float*, int64_t, int64_t, hipStream_t);
 template void launch_at_gather<double>(const double*, const double*, int64_t, int64_t, int64_t, double*,

@@ -215,6 +215,8 @@ class SessionBase {
   virtual void kernel_time(int kind, int64_t* launches, double* ms) = 0;
   virtual void counters(int64_t out[4]) const = 0;
   virtual void trace(double* sp_after, int64_t cap, int64_t* n, int64_t phase_info[6]) const = 0;
+  virtual std::string describe() const = 0;
+  virtual int64_t split_trace(double* out, int64_t cap) const = 0;
 };
 
 template <typename T>
@@ -241,7 +243,7 @@ class Session : public SessionBase {
     }
     // A@X slabs of up to 3 batched sources; split-candidate gather: the A e slabs + A p_thr's
     const int64_t pslabs = std::max<int64_t>((int64_t)ax_split_max(plan) * 3,
-                                             smode == 1 ? gather_split(P.m) + ax_split(plan, 1) : 0);
+                                             smode == 1 ? gather_split(P.m, P.n) + ax_split(plan, 1) : 0);
     T* pp = static_cast<T*>(c.take(sizeof(T) * ml * pslabs));
     T* at = smode == 1 ? static_cast<T*>(c.take(sizeof(T) * P.m * P.n)) : nullptr;   // A^T
     void* glists = smode == 1 ? c.take(gather_lists_bytes(P.n)) : nullptr;
@@ -388,11 +390,12 @@ class Session : public SessionBase {
     // nonzero only where the hard threshold zeroed p (see iter_proxgd, split_mode)
     emode_ = smode_ != 0 && P.method == GLX_PROXGD;
     fsplit_ = smode_ == 1 && P.method == GLX_FPROXGD;
-    {
+    rows_form_ = gather_rows_env() && gather_rows_ok(m_, n_);
+    gsplit_ = rows_form_ ? gather_split(m_, n_) : 1;
+    {   // the VALU gather's budget counts nonzeros of e_c, the row form's flagged rows (round 5)
       const char* nb = std::getenv("GLX_SPLIT_NNZ");
-      nnz_budget_ = (nb ? std::atof(nb) : 0.35) * (double)n_;
+      nnz_budget_ = (nb ? std::atof(nb) : (rows_form_ ? kRowsBudget : 0.35)) * (double)n_;
     }
-    gsplit_ = gather_split(m_);
     if (smode_ == 1) {
       launch_transpose<T>(static_cast<const T*>(P.A), At_, m_, n_, st_);   // once
     }
@@ -528,6 +531,28 @@ class Session : public SessionBase {
     if (n) *n = sp_after ? cnt : (int64_t)trace_sp_.size();
     if (phase_info)
       for (int p = 0; p < 3; ++p) { phase_info[p] = phase_start_[p]; phase_info[3 + p] = phase_break_[p]; }
+  }
+
+  // per trial batch of the split-candidate form: ProxGD the rows of e (rows the threshold
+  // changed, accepted trials), FProxGD nnz(e_c) of a gathered batch (row form: flagged rows) or -1
+  // for a dense batch; returns the count, copies up to cap
+  int64_t split_trace(double* out, int64_t cap) const override {
+    const int64_t cnt = std::min<int64_t>(cap, (int64_t)split_hist_.size());
+    if (out && cnt > 0) std::memcpy(out, split_hist_.data(), sizeof(double) * cnt);
+    return (int64_t)split_hist_.size();
+  }
+
+  // the kernels this session actually launches (bench.py re-derived the plan)
+  std::string describe() const override {
+    std::string s = describe_plan(plan_);
+    if (comm_ == nullptr && fused_ok_) s += " +trial (k_atr_prox)";
+    if (comm_ == nullptr && fused_fista_ok_) s += " +trial (k_atr_fista)";
+    s += "; split=";
+    if (smode_ == 0) s += "dense";
+    else if (rows_form_) s += "rows k_at_rows S0=" + std::to_string(gsplit_);
+    else s += "gather k_e_lists+k_at_gather";
+    s += "; dc_window=" + std::to_string(dc_window_);
+    return s;
   }
 
   void counters(int64_t out[4]) const override {
@@ -703,16 +728,21 @@ class Session : public SessionBase {
   // and the cross-stream wait left the queue idle, see kernels_gather.hip). The dense pass and the
   // gather are timed apart (kinds 0 and 2), so each event pair brackets one kernel of the trace.
   // pb: the dense launch carries that scalar packet.
+  // Round 5 (rows_form_): A e is the A^T R panel over the flagged rows of At (k_at_rows: gsplit_
+  // slabs, each workgroup compacts its K range's row flags itself), so no column lists.
   void cand_ax(const T* const* xs, Pub pb = Pub{}) {
     const T* xd[3] = {xs[1], nullptr, nullptr};
-    launch_e_lists(zf_, n_, l_, glists_, st_, dc_gate_);
-    check_launch();
+    if (!rows_form_) {
+      launch_e_lists(zf_, n_, l_, glists_, st_, dc_gate_);
+      check_launch();
+    }
     hipEvent_t e0 = prof_begin(0);
     launch_ax<T>(plan_, 1, A_, xd, Pp_ + (size_t)gsplit_ * ml_, dc_gate_, 0, st_, pb);
     check_launch();
     prof_end(0, e0);
     hipEvent_t e2 = prof_begin(2);
-    launch_at_gather<T>(At_, xs[0], m_, n_, l_, Pp_, glists_, st_, dc_gate_);
+    if (rows_form_) launch_at_rows<T>(At_, xs[0], zf_, m_, n_, l_, Pp_, glists_, st_, dc_gate_);
+    else launch_at_gather<T>(At_, xs[0], m_, n_, l_, Pp_, glists_, st_, dc_gate_);
     check_launch();
     prof_end(2, e2);
     ++ax_calls_;
@@ -1041,6 +1071,7 @@ class Session : public SessionBase {
     stats_[0] += hs_[S_TR + 4];
     stats_[1] += hs_[S_TR + 5];
     stats_[2] += 1;
+    split_hist_.push_back(hs_[S_TR + 5]);
     irg_ = rpt;
     gx_ = 0.5 * hs_[S_RT + 1];
     // exact: A p from the batch; split-candidate: A p - b = (A p_thr - b) + A e; dense z
@@ -1439,6 +1470,7 @@ class Session : public SessionBase {
     tk_ = t;
     kslot_ = (accepted && fs_batch) ? (kslot_ + 1) % 3 : -1;
     if (fsplit_ && ls) {
+      split_hist_.push_back(fs_batch ? hs_[S_RT + 2] : -1.0);
       if (fs_batch) {
         stats_[3] += 1;
         stats_[5] += hs_[S_RT + 2];
@@ -1497,7 +1529,7 @@ class Session : public SessionBase {
       cand_ax(xs);
       launch_finalize_fista<T>(Pp_ + (size_t)gsplit_ * ml_, ax_split(plan_, 1), Pp_, gsplit_, B_,
                                R_[ryn], SXO_[q.ks], SXO_[(q.ks + 1) % 3], ml_, 1.0 - thn, thn, th,
-                               X_[q.ic], nl_, scal_ + S_TR + 3, gather_counts(glists_, n_), (int)l_,
+                               X_[q.ic], nl_, scal_ + S_TR + 3, gather_counts(glists_, n_), gcount_n(),
                                defer ? red_to(defer) : red(S_RT), st_, comm_ ? Ctl{} : c);
       check_launch();
       q.ks = (q.ks + 1) % 3;
@@ -1627,6 +1659,9 @@ class Session : public SessionBase {
   // kFistaDenseRun batches are the dense [xc | y_next] pair, then A thr(x_k) is restored and
   // the gather form tried again.
   static constexpr int kFistaDenseRun = 128;
+  // the row form reads one At row per flagged row: its cost passes the dense second source's
+  // (~0.7 of a pass at NS) near 0.65 n flagged rows
+  static constexpr double kRowsBudget = 0.6;
   void fista_split_prologue() {
     T* scratch = X_[ff1_];   // free between iterations (the speculation's spare)
     launch_threshold<T>(X_[ix_], scratch, nl_, O_.thres, flag_, ++epoch_, st_);
@@ -1644,7 +1679,7 @@ class Session : public SessionBase {
     cand_ax(xs);
     launch_finalize_fista<T>(Pp_ + (size_t)gsplit_ * ml_, ax_split(plan_, 1), Pp_, gsplit_, B_, ry,
                              SXO_[kslot_], SXO_[(kslot_ + 1) % 3], ml_, 1.0 - theta_next,
-                             theta_next, theta, cx, nl_, cmax, gather_counts(glists_, n_), (int)l_,
+                             theta_next, theta, cx, nl_, cmax, gather_counts(glists_, n_), gcount_n(),
                              defer ? Red{part_, ticket_, defer} : red(slot), st_);
     check_launch();
     if (defer) return;
@@ -1771,6 +1806,10 @@ class Session : public SessionBase {
   T* At_ = nullptr;            // A^T (split-candidate gather form)
   void* glists_ = nullptr;     // the gather's per-column index lists of e
   int smode_ = 0, gsplit_ = 1;
+  bool rows_form_ = false;     // A e by k_at_rows (round 5), else the VALU column-list gather
+  // entries of the gather counts the FISTA finalize sums: flagged rows per K range (row form) or
+  // nonzeros per column (VALU gather)
+  int gcount_n() const { return rows_form_ ? gsplit_ : (int)l_; }
   bool emode_ = false;         // split-candidate ProxGD: trials write e = p - p_thr, not z
   unsigned* ezf() const { return emode_ ? zf_ : nullptr; }
   // split-candidate FProxGD (iter_fista): trials also write e_c = xc - thr(xc) to E_ and its
@@ -1840,6 +1879,7 @@ class Session : public SessionBase {
   // later iterations queued (device-controlled batches)
   int64_t ax_calls_ = 0, ax_cols_ = 0, atr_calls_ = 0, syncs_ = 0, record_waits_ = 0;
   double stats_[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  std::vector<double> split_hist_;
   struct EvSample { hipEvent_t a, b; int64_t tag; };
   std::vector<EvSample> ev_[3];
   int64_t prof_n_[3] = {0, 0, 0};
@@ -1876,6 +1916,7 @@ struct KernelWs {
   void* pp; void* gp; double* part; unsigned* ticket; double* scal;
   void* rg_ws; double* rg_s; double* rg_g; int* rg_err;   // fused residual-gradient pass
   void* rg2_ws; double* rg2_g;                              // its l = 16 two-source form
+  void* fr_slabs; void* fr_lists;                           // glx_flagged_rows_product
 };
 static size_t kernel_ws(int es, const GemmPlan& p, void* base, KernelWs* out) {
   Carver c(base);
@@ -1905,7 +1946,15 @@ static size_t kernel_ws(int es, const GemmPlan& p, void* base, KernelWs* out) {
     rg2_g = static_cast<double*>(c.take(sizeof(double) * p.n * p.l * resgrad2_groups(p.n)));
     if (!rg_err) rg_err = static_cast<int*>(c.take(256));
   }
-  if (out) *out = KernelWs{pp, gp, part, ticket, scal, rg_ws, rg_s, rg_g, rg_err, rg2_ws, rg2_g};
+  // the flagged-row product (A e of the split-candidate trial): its slabs and lists / counts
+  void* fr_slabs = nullptr;
+  void* fr_lists = nullptr;
+  if (gather_ok(p.n, p.l)) {
+    fr_slabs = c.take((size_t)es * p.m * p.l * std::max(1, gather_split(p.m, p.n)));
+    fr_lists = c.take(gather_lists_bytes(p.n));
+  }
+  if (out)
+    *out = KernelWs{pp, gp, part, ticket, scal, rg_ws, rg_s, rg_g, rg_err, rg2_ws, rg2_g, fr_slabs, fr_lists};
   return c.off + 256;
 }
 
@@ -2011,6 +2060,21 @@ int glx_session_trace(glx_session* s, double* sparsity_after, int64_t cap, int64
   return guarded([&] {
     if (!s || !s->impl) throw Error{GLX_E_INVALID, "null session"};
     s->impl->trace(sparsity_after, cap, n, phase_info);
+  });
+}
+
+int glx_session_split_trace(glx_session* s, double* out, int64_t cap, int64_t* n) {
+  return guarded([&] {
+    if (!s || !s->impl) throw Error{GLX_E_INVALID, "null session"};
+    const int64_t k = s->impl->split_trace(out, cap);
+    if (n) *n = k;
+  });
+}
+
+int glx_session_describe(glx_session* s, char* out, size_t cap) {
+  return guarded([&] {
+    if (!s || !s->impl || !out || cap == 0) throw Error{GLX_E_INVALID, "null session/out"};
+    std::snprintf(out, cap, "%s", s->impl->describe().c_str());
   });
 }
 
@@ -2132,6 +2196,35 @@ int glx_gradient(int dtype, int64_t m, int64_t n, int64_t l, const void* A, cons
       launch_atr<float>(p, (const float*)A, (const float*)R, gp, st);
       if (p.atr_S > 1) launch_sum_partials<float>(gp, p.atr_S, (float*)G, n * l, st);
     }
+    check_launch();
+  });
+}
+
+int glx_flagged_rows_product(int dtype, int64_t m, int64_t n, int64_t l, const void* At,
+                             const void* E, const uint32_t* row_masks, void* Y, int form,
+                             void* ws, size_t wsb, void* stream) {
+  return guarded([&] {
+    hipStream_t st = static_cast<hipStream_t>(stream);
+    GemmPlan p;
+    KernelWs k = kernel_setup(dtype, m, n, l, ws, wsb, 0, st, &p);
+    if (!gather_ok(n, l) || k.fr_slabs == nullptr) throw Error{GLX_E_INVALID, "needs l in {16, 32}, n < 65536"};
+    if (form != 0 && form != 1) throw Error{GLX_E_INVALID, "form must be 0 (MFMA rows) or 1 (VALU gather)"};
+    if (form == 0 && !gather_rows_ok(m, n)) throw Error{GLX_E_INVALID, "the row form needs m % 64 == 0"};
+    const int S0 = form == 0 ? gather_split(m, n) : 1;
+    auto go = [&](auto* tag) {
+      typedef std::remove_pointer_t<decltype(tag)> T;
+      T* slabs = static_cast<T*>(k.fr_slabs);
+      if (form == 0) {
+        launch_at_rows<T>(static_cast<const T*>(At), static_cast<const T*>(E), row_masks, m, n, l, slabs,
+                          k.fr_lists, st);
+      } else {
+        launch_e_lists(row_masks, n, l, k.fr_lists, st);
+        launch_at_gather<T>(static_cast<const T*>(At), static_cast<const T*>(E), m, n, l, slabs, k.fr_lists, st);
+      }
+      launch_sum_partials<T>(slabs, S0, static_cast<T*>(Y), m * l, st);
+    };
+    if (dtype == GLX_F64) go(static_cast<double*>(nullptr));
+    else go(static_cast<float*>(nullptr));
     check_launch();
   });
 }

@@ -69,6 +69,8 @@ _SIGS = {
     "glx_session_counters": (c_int, [c_void_p, POINTER(c_int64)]),
     "glx_session_trace": (c_int, [c_void_p, POINTER(c_double), c_int64, POINTER(c_int64),
                                   POINTER(c_int64)]),
+    "glx_session_describe": (c_int, [c_void_p, c_char_p, c_size_t]),
+    "glx_session_split_trace": (c_int, [c_void_p, POINTER(c_double), c_int64, POINTER(c_int64)]),
     "glx_session_destroy": (None, [c_void_p]),
     "glx_solve": (c_int, [POINTER(GlxProblem), POINTER(GlxOpts), c_void_p, c_size_t,
                           POINTER(GlxResult), c_void_p]),
@@ -87,6 +89,8 @@ _SIGS = {
                                        c_void_p, c_size_t, c_int, POINTER(c_int), c_void_p]),
     "glx_prox": (c_int, [c_int, c_int64, c_int64, c_void_p, c_double, c_double, c_double,
                          c_void_p, c_void_p, c_void_p, c_size_t, c_void_p]),
+    "glx_flagged_rows_product": (c_int, [c_int, c_int64, c_int64, c_int64, c_void_p, c_void_p,
+                                         c_void_p, c_void_p, c_int, c_void_p, c_size_t, c_void_p]),
     "glx_kernel_workspace_bytes": (c_int, [c_int, c_int64, c_int64, c_int64, POINTER(c_size_t)]),
     "glx_plan_describe": (c_int, [c_int, c_int64, c_int64, c_int64, c_char_p, c_size_t]),
     "glx_comm_unique_id": (c_int, [POINTER(c_uint8)]),

@@ -117,6 +117,23 @@ def residual_gradient2(A: torch.Tensor, X0: torch.Tensor, X1: torch.Tensor, B: t
     return R0, R1, G, bool(ran.value)
 
 
+def flagged_rows_product(At: torch.Tensor, E: torch.Tensor, row_masks: torch.Tensor,
+                         form: int = 0) -> torch.Tensor:
+    """Y = sum over the rows k with row_masks[k] != 0 of At[k]^T E[k] (m x l): the split-candidate
+    trial's A e from the transposed copy At = A^T (n x m). form 0: the MFMA row form (the
+    solver's default, m % 64 == 0), 1: the VALU column-list gather (bit c of row_masks[k] must be
+    E[k][c] != 0). row_masks: int32 device tensor of n (+ padding) column masks."""
+    n, m = At.shape
+    l = E.shape[1]
+    dt = _dt(At)
+    Y = torch.empty((m, l), dtype=At.dtype, device=At.device)
+    ws = _ws(dt, m, n, l, At.device)
+    check(lib().glx_flagged_rows_product(dt, m, n, l, At.data_ptr(), E.data_ptr(),
+                                         row_masks.data_ptr(), Y.data_ptr(), int(form),
+                                         ws.data_ptr(), ws.numel(), _stream(At.device)))
+    return Y
+
+
 def prox(W: torch.Tensor, t: float, mu: float, thres: float = 1e-3
          ) -> Tuple[torch.Tensor, torch.Tensor]:
     """Group prox with the reference's denominator quirk; returns (X, [sum ||x_i||, max|x|])."""

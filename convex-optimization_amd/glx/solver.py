@@ -186,6 +186,25 @@ class Session:
         check(lib().glx_session_counters(self.h, out))
         return {"ax_calls": out[0], "ax_sources": out[1], "atr_calls": out[2], "syncs": out[3]}
 
+    def describe(self) -> str:
+        """The kernels this session launches (glx_session_describe): A@X tiles per right-hand
+        side count, A^T r panel (+ the fused trial), the split-candidate form, the device-control
+        window."""
+        buf = ctypes.create_string_buffer(1024)
+        check(lib().glx_session_describe(self.h, buf, len(buf)))
+        return buf.value.decode()
+
+    def split_trace(self) -> np.ndarray:
+        """Per trial batch: ProxGD's flagged rows of e, FProxGD's nnz(e_c) of a gathered batch
+        (row form: flagged rows) or -1 for a dense batch (glx_session_split_trace)."""
+        n = ctypes.c_int64(0)
+        check(lib().glx_session_split_trace(self.h, None, 0, ctypes.byref(n)))
+        out = np.zeros(int(n.value), dtype=np.float64)
+        if n.value:
+            check(lib().glx_session_split_trace(self.h, out.ctypes.data_as(ctypes.POINTER(ctypes.c_double)),
+                                                int(n.value), ctypes.byref(n)))
+        return out
+
     def trace(self) -> Tuple[np.ndarray, List[int], List[int]]:
         """(sparsity after each iteration's update, phase start k's, phases ended by the stop rule)
         — see glx_session_trace; valid after finish()."""

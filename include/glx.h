@@ -158,6 +158,14 @@ int  glx_session_counters(glx_session* s, int64_t out[4]);
  * nothing, :118-125). */
 int  glx_session_trace(glx_session* s, double* sparsity_after, int64_t cap, int64_t* n,
                        int64_t phase_info[6]);
+/* One-line description of the kernels this session launches (the planner's tiles and splits
+ * after the session's own choices: the fused trial, the split-candidate form, the device-control
+ * window), NUL-terminated, truncated to cap. */
+int  glx_session_describe(glx_session* s, char* out, size_t cap);
+/* The split-candidate trials' sparsity, one value per trial batch so far (diagnostic): ProxGD the
+ * rows of e = p - p_thr (accepted trials), FProxGD nnz(e_c) of a gathered batch (flagged rows in
+ * the row form) or -1 for a dense batch. *n = the count; up to cap values copied to out. */
+int  glx_session_split_trace(glx_session* s, double* out, int64_t cap, int64_t* n);
 void glx_session_destroy(glx_session* s);
 
 /* One-shot solve: create + run to completion + finish + destroy. */
@@ -206,6 +214,16 @@ int glx_residual_gradient2(int dtype, int64_t m, int64_t n, int64_t l, const voi
                            const void* X1, const void* B, void* R0, void* R1, void* G,
                            void* workspace, size_t workspace_bytes, int one_pass,
                            int* one_pass_ran, void* stream);
+/* The thresholded part of the split-candidate line-search trial (round 5, SURVEY §8a row a9:
+ * A e with e = p - p_thr nonzero only in the rows the hard threshold touched,
+ * gl_ProxGD_primal.py:91,112,127; FProxGD's A e_c, gl_FProxGD_primal.py:92-97,136):
+ *   Y (m x l) = sum over the rows k with row_masks[k] != 0 of At[k,:]^T E[k,:],  At = A^T (n x m).
+ * row_masks[k] (device uint32, n + 3 readable) = the column mask of row k of E (bit c = E[k][c] != 0,
+ * as the trial kernels write it). form 0: the MFMA row form (k_at_rows, the solver's default; m % 64
+ * == 0); form 1: the VALU column-list gather of rounds 2-4 (needs the exact column masks). */
+int glx_flagged_rows_product(int dtype, int64_t m, int64_t n, int64_t l, const void* At,
+                             const void* E, const uint32_t* row_masks, void* Y, int form,
+                             void* workspace, size_t workspace_bytes, void* stream);
 /* Workspace bytes for the single-kernel entry points above. */
 int glx_kernel_workspace_bytes(int dtype, int64_t m, int64_t n, int64_t l, size_t* bytes);
 /* One-line description of the kernels (tile, split) the planner picks for this shape, for
