@@ -209,6 +209,105 @@ __device__ inline T slab_sum(const T* __restrict__ g, int S, int64_t stride, int
 
 template <typename T> __device__ inline T tabs(T v) { return v < T(0) ? -v : v; }
 
+// Device-side control of a ProxGD (mode 0) / FProxGD (mode 1) line-search iteration (struct Ctl,
+// solver.cpp dc_run / fista_dc_run): the Armijo test of gl_ProxGD_primal.py:89-92 (FProxGD's
+// backtracking test, gl_FProxGD_primal.py:92-97) with t = the trial's step, then — on acceptance — the
+// next record's objective and sparsity (:132-133 via the split-candidate/dense residual sums) and
+// the stop rule of :118-125. The expressions are the host's (solver.cpp iter_proxgd, stop_rule)
+// term for term, so with -ffp-contract=off the decision is the host's bit for bit; the host
+// re-derives it from the record and checks it. out = the four residual sums of this finalize.
+// pre = tr[0..5], state[0..3], loaded when the kernel starts (they were final before it began),
+// so the last block's decision costs no dependent global loads at the end of the kernel
+__device__ inline void ctl_decide(const Ctl& c, const double* out, const double (&pre)[10]) {
+  double* st = c.state;
+  const double* tr = pre;
+  double rec[kCtlRec];
+  for (int k = 0; k < 4; ++k) rec[k] = out[k];
+  for (int k = 0; k < 6; ++k) rec[4 + k] = tr[k];
+  bool acc;
+  if (c.mode == 1) {   // FProxGD (solver.cpp fista_trials): g(xc) <= g(y) + <g, xc - y> + |xc - y|^2/(2t)
+    const double gy = 0.5 * pre[6], gxc = 0.5 * out[0];
+    acc = gxc <= gy + tr[0] + tr[1] / (2 * c.t);
+  } else {             // ProxGD (iter_proxgd): g(z) <= g(x) - t <g, G_t> + t/2 |G_t|^2
+    const double gz = 0.5 * out[0];
+    acc = gz <= pre[6] - c.t * tr[0] + 0.5 * c.t * tr[1];
+  }
+  int code = 2;
+  if (acc) {
+    double f;
+    if (c.mode == 1) {
+      f = 0.5 * out[0] + c.mu0 * tr[2];
+    } else {
+      const double sqx = (c.emode || tr[4] != 0) ? out[0] : out[1];
+      f = 0.5 * sqx + c.mu0 * tr[2];
+    }
+    const double s = out[3] / c.nl;
+    const double fl = pre[7], sl = pre[8];
+    bool ok = fabs(f - fl) / fabs(fl) < c.ftol;
+    if (ok && c.use_sp) ok = fabs(s - sl) / fabs(sl) < c.ftol;
+    const double stable = ok ? pre[9] + 1.0 : 0.0;
+    st[0] = c.mode == 1 ? out[1] : 0.5 * out[1];
+    st[1] = f;
+    st[2] = s;
+    st[3] = stable;
+    code = stable > (double)c.stable_thr ? 1 : 0;
+    if (code == 0 && c.nnz_budget >= 0.0 && out[2] > c.nnz_budget) code = 3;
+  }
+  *c.abort = code == 0 ? 0 : (code == 2 ? -1 : c.pass);
+  rec[10] = (double)code;
+  for (int k = 0; k <= 10; ++k) c.rec[k] = rec[k];
+}
+
+// ------------------------------------------------------------------------------------------
+// Split-candidate column bitmaps (round 5). Behind the n per-row column masks zf[k] of e (bit c =
+// e[k][c] != 0) the trial kernels also write, per column c, a bitmap of the rows whose mask has
+// bit c: u16 word g of column c = rows 16 g .. 16 g + 15 (bit j = row 16 g + j), at
+// zf_bitmaps(zf, n)[c * zf_npad(n) / 16 + g]; read as u64, word w of column c covers the 64 rows
+// of panel w. The A e gather builds its ascending per-column row lists from them in LDS
+// (kernels_gather.hip k_at_gather_bm) instead of a k_e_lists launch over all n masks. Every
+// trial rewrites every word of every column < l (the words of rows >= n are 0), so nothing needs
+// clearing between trials.
+// ------------------------------------------------------------------------------------------
+__host__ __device__ inline int64_t zf_npad(int64_t n) { return (n + 63) / 64 * 64; }
+__device__ inline unsigned short* zf_bitmaps(unsigned* zf, int64_t n) {
+  return reinterpret_cast<unsigned short*>(zf + zf_npad(n));
+}
+// A 64-row panel [col0, col0 + 64) of masks, held one per row in the LDS array msk (all of the
+// workgroup's waves wrote theirs and passed a barrier): wave 0 transposes it with one ballot per
+// column and lane c < l stores column c's u64 word. Called by the whole workgroup.
+__device__ inline void zf_store_panel(const unsigned* msk, unsigned* zf, int64_t n, int l,
+                                      int64_t col0) {
+  if ((threadIdx.x >> 6) != 0) return;
+  const int lane = threadIdx.x & 63;
+  const unsigned v = msk[lane];
+  uint64_t mine = 0;
+#pragma unroll
+  for (int c = 0; c < 32; ++c) {
+    const uint64_t b = __ballot((v >> c) & 1u);
+    if (lane == c) mine = b;
+  }
+  if (lane < l) {
+    uint64_t* w = reinterpret_cast<uint64_t*>(zf_bitmaps(zf, n) + (int64_t)lane * (zf_npad(n) / 16));
+    w[col0 / 64] = mine;
+  }
+}
+// The row kernels' form (16 lanes per row, so a 256-thread workgroup holds the 16 rows of one
+// 16-row group per trip): the lane sub == 0 of each row puts its mask in msk[16], a barrier, then
+// thread c < l stores column c's u16 word of the group starting at row0; a second barrier frees
+// msk for the next trip. Called by the whole workgroup (the trip count is uniform).
+__device__ inline void zf_store_group16(unsigned* msk, unsigned rowe, bool rv, int sub, unsigned* zf,
+                                        int64_t n, int l, int64_t row0) {
+  if (sub == 0) msk[threadIdx.x >> 4] = rv ? rowe : 0u;
+  __syncthreads();
+  if ((int)threadIdx.x < l && row0 < zf_npad(n)) {
+    unsigned b = 0;
+#pragma unroll
+    for (int j = 0; j < 16; ++j) b |= ((msk[j] >> threadIdx.x) & 1u) << j;
+    zf_bitmaps(zf, n)[(int64_t)threadIdx.x * (zf_npad(n) / 16) + row0 / 16] = (unsigned short)b;
+  }
+  __syncthreads();
+}
+
 // ------------------------------------------------------------------------------------------
 // row helpers
 // ------------------------------------------------------------------------------------------

@@ -135,6 +135,26 @@ struct Pub {
   int off3 = 0, n3 = 0;
 };
 
+// Round 5: the split-candidate trial's residual finalize folded into the dense pass A p_thr
+// (launch_ax_fin, the LDS-DMA tile): the K-split workgroups store their slabs (agent scope) and
+// arrive on their row block's counter; the last arriver sums the S slabs in slab order, forms
+// r1 = A p_thr - b (stored to R1: the next gradient residual) and r0 = r1 + A e (the A e slabs P0,
+// computed BEFORE the pass), and every workgroup joins one grid reduction of
+// [sum r0^2, sum r1^2, 0, count(|cx| > 1e-6 *cmax)] (its share of cx) into red; the final block
+// runs the device-side decision when ctl.rec != NULL. Replaces k_finalize_residual's chain mode.
+struct AxFin {
+  const void* B = nullptr;
+  void* R1 = nullptr;
+  const void* P0 = nullptr;
+  int S0 = 0;
+  const void* cx = nullptr;
+  int64_t cn = 0;
+  const double* cmax = nullptr;
+  unsigned* cnt = nullptr;   // one arrival counter per row block (zero; the last arriver resets it)
+  Red red{};
+  Ctl ctl{};
+};
+
 // Launch plan of the two dense products for one (dtype, m, n, l).
 struct GemmPlan {
   int esize;        // 4 or 8
@@ -191,6 +211,14 @@ template <typename T>
 bool launch_ax_dma(const GemmPlan& p, int code, int nsrc, int S, const T* A, const T* const* X, T* P,
                    const int* gate, int epoch, hipStream_t st, Pub pub);
 int dma_lds_need(int code, int64_t l, int nsrc, int esize);
+// the dense single-source pass with the folded finalize (AxFin): false when this plan's tile or
+// shape does not take it (the caller then runs launch_ax + launch_finalize_residual); needs
+// fin.cnt to hold ax_fin_counters(p) words
+template <typename T>
+bool launch_ax_fin(const GemmPlan& p, const T* A, const T* X, T* P, const int* gate, int epoch,
+                   hipStream_t st, const AxFin& fin);
+int ax_fin_counters(const GemmPlan& p);
+bool ax_fin_ok(const GemmPlan& p, int esize);
 int dma_waves(int code);   // waves per workgroup of a kind-8/9 code (last digit; 1 = 16)
 int dma_mt(int code);      // 16-row tiles per wave (kind 9: 2)
 // Infinity-Cache hand-off between the passes (tuning experiment; MiB of A fetched with the
@@ -224,8 +252,16 @@ bool gather_ok(int64_t n, int64_t l);
 // round 5: the MFMA row form (k_at_rows): the shapes it takes, the solver's default (GLX_GATHER=valu:
 // the column-list gather, ONE slab), and its K splits for this shape (1 where it does not apply)
 bool gather_rows_ok(int64_t m, int64_t n);
-bool gather_rows_env();
+int gather_form();   // GLX_GATHER: 0 bitmaps (default), 1 MFMA rows, 2 k_e_lists + k_at_gather
 int gather_split(int64_t m, int64_t n);
+// zf: the per-row column masks of e and, behind them, the per-column row bitmaps (glx_device.h)
+size_t zf_bytes(int64_t n);
+// A e from the column bitmaps behind zf (ONE slab at P; the column list lengths to gather_counts)
+template <typename T>
+void launch_at_gather_bm(const T* At, const T* E, unsigned* zf, int64_t m, int64_t n, int64_t l, T* P,
+                         void* lists_ws, hipStream_t st, const int* skip = nullptr);
+// the column bitmaps behind zf from its row masks (where no trial kernel wrote them)
+void launch_zf_bitmaps(unsigned* zf, int64_t n, int64_t l, hipStream_t st);
 // P[s][r][c] = sum over the flagged rows k (zf[k] != 0) of K range s, ascending:
 // At[k][r] E[k][c], s < gather_split(m, n); counts[s] (gather_counts) = the flagged rows of range s
 template <typename T>

@@ -334,13 +334,17 @@ __global__ __launch_bounds__(WL == 2 ? 512 : 256, (WL == 0 && sizeof(T) == 8) ? 
   }
   GLX_CLK(5);
   grid_reduce<6, 0x8u, NW>(accr, red, slot, nparts);
+  __shared__ unsigned msk[64];   // the panel's row masks of e (column bitmaps, zf_store_panel)
 #pragma unroll
   for (int e = 0; e < 4; ++e) {
     if (e != wave) continue;
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       const int64_t row = col0 + atr_col<T>(M::row(lane, r), e);
-      if (zf != nullptr && i == 0) zf[row] = rows_e[r];
+      if (zf != nullptr && i == 0) {
+        zf[row] = rows_e[r];
+        msk[row - col0] = rows_e[r];
+      }
 #pragma unroll
       for (int nt = 0; nt < NT; ++nt) {
         G[row * L + nt * 16 + i] = gs[r][nt];
@@ -349,6 +353,10 @@ __global__ __launch_bounds__(WL == 2 ? 512 : 256, (WL == 0 && sizeof(T) == 8) ? 
         z[row * L + nt * 16 + i] = zs[r][nt];
       }
     }
+  }
+  if (zf != nullptr) {
+    __syncthreads();
+    zf_store_panel(msk, zf, n, L, col0);
   }
   GLX_CLK(3);
 }
@@ -390,6 +398,7 @@ __global__ __launch_bounds__(WL == 2 ? 512 : 256, (WL == 0 && sizeof(T) == 8) ? 
     if (!atr_split_combine<T, NT>(acc, Gp, n, S, panel, split, pcnt, &slot)) return;
   }
   const T t = (T)t_, tmu = (T)tmu_, thres = (T)thres_, theta = (T)theta_, a1 = (T)a1_, b1 = (T)b1_;
+  __shared__ unsigned msk[64];   // the panel's row masks of e_c (column bitmaps, zf_store_panel)
 #pragma unroll
   for (int e = 0; e < 4; ++e) {
     if (e != wave) continue;   // wave w owns the rows e == w
@@ -417,7 +426,10 @@ __global__ __launch_bounds__(WL == 2 ? 512 : 256, (WL == 0 && sizeof(T) == 8) ? 
       const unsigned rowe = fista_row<T, 16, NT, true>(ya[r], gv, xa[r], ok, true, i, t, tmu, thres, theta,
                                                    a1, b1, T(0), T(0), xcv, vnv, ynv, accr,
                                                    ec != nullptr ? ecv : nullptr);
-      if (zf != nullptr && i == 0) zf[row] = rowe;
+      if (zf != nullptr && i == 0) {
+        zf[row] = rowe;
+        msk[row - col0] = rowe;
+      }
 #pragma unroll
       for (int nt = 0; nt < NT; ++nt) {
         xc[row * L + nt * 16 + i] = xcv[nt];
@@ -428,6 +440,10 @@ __global__ __launch_bounds__(WL == 2 ? 512 : 256, (WL == 0 && sizeof(T) == 8) ? 
     }
   }
   grid_reduce<4, 0x8u, NW>(accr, red, slot, nparts);
+  if (zf != nullptr) {   // (grid_reduce's barriers ordered the msk stores above)
+    __syncthreads();
+    zf_store_panel(msk, zf, n, L, col0);
+  }
 }
 
 // A^T R on VALU: a thread owns E consecutive columns of A over a row range; R[row][c0..c0+LB)

@@ -73,55 +73,6 @@ __device__ inline T group_slab_sum(const T* __restrict__ P, int S, int64_t ml, i
   return v;
 }
 
-// Device-side control of a ProxGD (mode 0) / FProxGD (mode 1) line-search iteration (struct Ctl,
-// solver.cpp dc_run / fista_dc_run): the Armijo test of gl_ProxGD_primal.py:89-92 (FProxGD's
-// backtracking test, gl_FProxGD_primal.py:92-97) with t = the trial's step, then — on acceptance — the
-// next record's objective and sparsity (:132-133 via the split-candidate/dense residual sums) and
-// the stop rule of :118-125. The expressions are the host's (solver.cpp iter_proxgd, stop_rule)
-// term for term, so with -ffp-contract=off the decision is the host's bit for bit; the host
-// re-derives it from the record and checks it. out = the four residual sums of this finalize.
-// pre = tr[0..5], state[0..3], loaded when the kernel starts (they were final before it began),
-// so the last block's decision costs no dependent global loads at the end of the kernel
-__device__ inline void ctl_decide(const Ctl& c, const double* out, const double (&pre)[10]) {
-  double* st = c.state;
-  const double* tr = pre;
-  double rec[kCtlRec];
-  for (int k = 0; k < 4; ++k) rec[k] = out[k];
-  for (int k = 0; k < 6; ++k) rec[4 + k] = tr[k];
-  bool acc;
-  if (c.mode == 1) {   // FProxGD (solver.cpp fista_trials): g(xc) <= g(y) + <g, xc - y> + |xc - y|^2/(2t)
-    const double gy = 0.5 * pre[6], gxc = 0.5 * out[0];
-    acc = gxc <= gy + tr[0] + tr[1] / (2 * c.t);
-  } else {             // ProxGD (iter_proxgd): g(z) <= g(x) - t <g, G_t> + t/2 |G_t|^2
-    const double gz = 0.5 * out[0];
-    acc = gz <= pre[6] - c.t * tr[0] + 0.5 * c.t * tr[1];
-  }
-  int code = 2;
-  if (acc) {
-    double f;
-    if (c.mode == 1) {
-      f = 0.5 * out[0] + c.mu0 * tr[2];
-    } else {
-      const double sqx = (c.emode || tr[4] != 0) ? out[0] : out[1];
-      f = 0.5 * sqx + c.mu0 * tr[2];
-    }
-    const double s = out[3] / c.nl;
-    const double fl = pre[7], sl = pre[8];
-    bool ok = fabs(f - fl) / fabs(fl) < c.ftol;
-    if (ok && c.use_sp) ok = fabs(s - sl) / fabs(sl) < c.ftol;
-    const double stable = ok ? pre[9] + 1.0 : 0.0;
-    st[0] = c.mode == 1 ? out[1] : 0.5 * out[1];
-    st[1] = f;
-    st[2] = s;
-    st[3] = stable;
-    code = stable > (double)c.stable_thr ? 1 : 0;
-    if (code == 0 && c.nnz_budget >= 0.0 && out[2] > c.nnz_budget) code = 3;
-  }
-  *c.abort = code == 0 ? 0 : (code == 2 ? -1 : c.pass);
-  rec[10] = (double)code;
-  for (int k = 0; k <= 10; ++k) c.rec[k] = rec[k];
-}
-
 // Device-controlled ProxGD with a communicator (solver.cpp dc_queue): the trial's residual sums
 // are final only after the gradient all-reduce that carries them (a gradient set's tail), so the
 // decision runs as its own one-thread launch right behind that all-reduce. Skipped once an earlier
@@ -325,6 +276,10 @@ __global__ __launch_bounds__(256) void k_prox_pgd(const T* __restrict__ x, const
   const unsigned rowe = prox_pgd_row<T, LPR, EPL>(xv, gv, ok, rv, sub, t, tmu, thres, pv, pth, zv, acc,
                                               zf != nullptr);
   if (zf != nullptr && rv && sub == 0) zf[row] = rowe;
+  if constexpr (LPR == 16) {   // the split-candidate shapes (l in {16, 32}): the column bitmaps
+    __shared__ unsigned msk[16];
+    if (zf != nullptr) zf_store_group16(msk, rowe, rv, sub, zf, n, (int)l, row - (threadIdx.x >> 4));
+  }
 #pragma unroll
   for (int e = 0; e < EPL; ++e) {
     const int64_t j = sub + (int64_t)e * LPR;
@@ -383,6 +338,10 @@ __global__ __launch_bounds__(256) void k_fista_trial(
                                                   b1, dd, delta, xcv, vnv, ynv, acc,
                                                   ec != nullptr ? ecv : nullptr);
   if (zf != nullptr && rv && sub == 0) zf[row] = rowe;
+  if constexpr (LPR == 16) {   // the split-candidate shapes (l in {16, 32}): the column bitmaps
+    __shared__ unsigned msk[16];
+    if (zf != nullptr) zf_store_group16(msk, rowe, rv, sub, zf, n, (int)l, row - (threadIdx.x >> 4));
+  }
 #pragma unroll
   for (int e = 0; e < EPL; ++e) {
     const int64_t j = sub + (int64_t)e * LPR;

@@ -229,6 +229,99 @@ __global__ __launch_bounds__(kGThreads) void k_at_gather2(const T* __restrict__ 
   }
 }
 
+// Round 5: the same gather without k_e_lists (k_at_gather_bm, the default). The trial kernels
+// also write per-column row bitmaps of e (glx_device.h zf_store_panel / zf_store_group16), and
+// each workgroup (row block rb, column c) builds column c's ascending row list itself, in LDS:
+// thread t takes the u64 bitmap words t, t + 256, ... of a 256-word segment (16 384 rows), a
+// popcount, one block scan, the set bits written in order; then the same walk as k_at_gather
+// with the indices read from LDS. Same list, same order, same arithmetic: bit-identical to
+// k_e_lists + k_at_gather, one launch and ~8 us fewer per trial (the lists kernel's 32
+// workgroups ran alone on the chip). counts[c] (rb == 0) = the list length (FProxGD's budget).
+template <typename T, int L, bool NT>
+__global__ __launch_bounds__(kGThreads) void k_at_gather_bm(const T* __restrict__ At,
+                                                            const T* __restrict__ E,
+                                                            unsigned* __restrict__ zf, int64_t m,
+                                                            int64_t n, T* __restrict__ P,
+                                                            unsigned* __restrict__ counts, int gx,
+                                                            const int* __restrict__ skip) {
+  if (skip != nullptr && *skip != 0) return;
+  __shared__ unsigned short lst[64 * kGThreads];   // one segment: 256 words x 64 rows
+  __shared__ unsigned wsum[kGW];
+  const int tid = threadIdx.x;
+  const int lane = tid & 63, wave = tid >> 6;
+  const int rb = (int)blockIdx.x % gx, c = (int)blockIdx.x / gx;
+  const int64_t nw = zf_npad(n) / 64;
+  const uint64_t* words = reinterpret_cast<const uint64_t*>(zf_bitmaps(zf, n) + (int64_t)c * (zf_npad(n) / 16));
+  const int64_t r = (int64_t)rb * kGThreads + tid;
+  const int64_t rr = r < m ? r : m - 1;
+  constexpr int U = 8;
+  T acc = T(0);
+  unsigned all = 0;
+  for (int64_t w0 = 0; w0 < nw; w0 += kGThreads) {
+    const int64_t w = w0 + tid;
+    uint64_t bits = w < nw ? words[w] : uint64_t(0);
+    const unsigned cnt = (unsigned)__builtin_popcountll(bits);
+    unsigned inc = cnt;
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+      const unsigned v = __shfl_up(inc, off);
+      if (lane >= off) inc += v;
+    }
+    if (lane == 63) wsum[wave] = inc;
+    __syncthreads();
+    unsigned pos = inc - cnt, total = 0;
+#pragma unroll
+    for (int q = 0; q < kGW; ++q) {
+      if (q < wave) pos += wsum[q];
+      total += wsum[q];
+    }
+    while (bits != 0) {
+      const int j = __builtin_ctzll(bits);
+      bits &= bits - 1;
+      lst[pos++] = (unsigned short)((w - w0) * 64 + j);   // row - 64 w0
+    }
+    __syncthreads();
+    const int tot = (int)total;
+    const int64_t kb = w0 * 64;
+    int idx = 0;
+    for (; idx + U <= tot; idx += U) {
+      T a[U], ev[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int64_t k = kb + lst[idx + u];
+        a[u] = NT ? __builtin_nontemporal_load(At + k * m + rr) : At[k * m + rr];
+        ev[u] = E[k * L + c];
+      }
+#pragma unroll
+      for (int u = 0; u < U; ++u) acc = acc + a[u] * ev[u];
+    }
+    for (; idx < tot; ++idx) {
+      const int64_t k = kb + lst[idx];
+      acc = acc + (NT ? __builtin_nontemporal_load(At + k * m + rr) : At[k * m + rr]) * E[k * L + c];
+    }
+    all += total;
+    __syncthreads();   // lst and wsum are rewritten by the next segment
+  }
+  if (r < m) P[r * L + c] = acc;
+  if (rb == 0 && tid == 0) counts[c] = all;
+}
+
+// zf's column bitmaps from its n row masks (glx_flagged_rows_product's bitmap form, where no
+// trial kernel wrote them): thread (c, word g) ORs bit c of the 16 masks of rows 16 g .. 16 g + 15
+__global__ void k_zf_bitmaps(unsigned* __restrict__ zf, int64_t n, int l) {
+  const int64_t ng = zf_npad(n) / 16;
+  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= ng * l) return;
+  const int c = (int)(t / ng);
+  const int64_t g = t % ng;
+  unsigned b = 0;
+  for (int j = 0; j < 16; ++j) {
+    const int64_t k = 16 * g + j;
+    if (k < n) b |= ((zf[k] >> c) & 1u) << j;
+  }
+  zf_bitmaps(zf, n)[(int64_t)c * ng + g] = (unsigned short)b;
+}
+
 // ------------------------------------------------------------------------------------------
 // Round 5: A e as the A^T R panel over the flagged rows of e (k_at_rows, the default).
 //
@@ -406,10 +499,13 @@ static int env_rows_s() {
 }
 // the shapes the MFMA row form (k_at_rows) takes: whole 64-row panels of At
 bool gather_rows_ok(int64_t m, int64_t n) { return m % 64 == 0 && m > 0 && n <= 65535; }
-// the solver's choice: the row form unless GLX_GATHER=valu (the round-2 column-list gather)
-bool gather_rows_env() {
+// the solver's A e form (GLX_GATHER): 0 = the bitmap gather (k_at_gather_bm, default), 1 = the
+// MFMA row form ("rows", where gather_rows_ok), 2 = k_e_lists + k_at_gather ("lists", rounds 2-4)
+int gather_form() {
   const char* e = std::getenv("GLX_GATHER");
-  return !(e && std::strcmp(e, "valu") == 0);
+  if (e && std::strcmp(e, "rows") == 0) return 1;
+  if (e && (std::strcmp(e, "lists") == 0 || std::strcmp(e, "valu") == 0)) return 2;
+  return 0;
 }
 // K splits of the row form: about two workgroups per CU (512 on 256 CUs), each K range within
 // the LDS list; GLX_ATROWS_S overrides (clamped to that bound)
@@ -495,6 +591,33 @@ void launch_at_gather(const T* At, const T* E, int64_t m, int64_t n, int64_t l, 
   }
 }
 
+// A e by the column bitmaps the trial kernels wrote behind zf (k_at_gather_bm): ONE slab at P,
+// the column list lengths into the counts area of lists_ws (gather_counts)
+template <typename T>
+void launch_at_gather_bm(const T* At, const T* E, unsigned* zf, int64_t m, int64_t n, int64_t l, T* P,
+                         void* lists_ws, hipStream_t st, const int* skip) {
+  if (!gather_ok(n, l)) throw Error{GLX_E_INVALID, "A e gather: needs l in {16, 32}, n < 65536"};
+  static const bool nt = [] {
+    const char* e = std::getenv("GLX_GATHER_NT");
+    return !(e && std::strcmp(e, "0") == 0);
+  }();
+  const int gx = (int)((m + kGThreads - 1) / kGThreads);
+  unsigned* cnt = list_counts(lists_ws, n);
+  if (l == 32) {
+    if (nt) glx_launch(k_at_gather_bm<T, 32, true>, dim3((unsigned)(gx * l)), dim3(kGThreads), 0, st, At, E, zf, m, n, P, cnt, gx, skip);
+    else glx_launch(k_at_gather_bm<T, 32, false>, dim3((unsigned)(gx * l)), dim3(kGThreads), 0, st, At, E, zf, m, n, P, cnt, gx, skip);
+  } else {
+    if (nt) glx_launch(k_at_gather_bm<T, 16, true>, dim3((unsigned)(gx * l)), dim3(kGThreads), 0, st, At, E, zf, m, n, P, cnt, gx, skip);
+    else glx_launch(k_at_gather_bm<T, 16, false>, dim3((unsigned)(gx * l)), dim3(kGThreads), 0, st, At, E, zf, m, n, P, cnt, gx, skip);
+  }
+}
+void launch_zf_bitmaps(unsigned* zf, int64_t n, int64_t l, hipStream_t st) {
+  const int64_t t = zf_npad(n) / 16 * l;
+  hipLaunchKernelGGL(k_zf_bitmaps, dim3((unsigned)((t + 255) / 256)), dim3(256), 0, st, zf, n, (int)l);
+}
+// bytes of zf: the row masks (zf_npad(n) words) and the column bitmaps behind them
+size_t zf_bytes(int64_t n) { return (((size_t)zf_npad(n) * 8) + 255) & ~size_t(255); }
+
 // A e over the flagged rows (k_at_rows): S0 = gather_split(m, n) slabs at P, the flagged rows of
 // each K range into the counts area of lists_ws (gather_counts)
 template <typename T>
@@ -525,6 +648,10 @@ template void launch_at_rows<double>(const double*, const double*, const unsigne
                                      int64_t, double*, void*, hipStream_t, const int*);
 template void launch_at_rows<float>(const float*, const float*, const unsigned*, int64_t, int64_t,
                                     int64_t, float*, void*, hipStream_t, const int*);
+template void launch_at_gather_bm<double>(const double*, const double*, unsigned*, int64_t, int64_t,
+                                          int64_t, double*, void*, hipStream_t, const int*);
+template void launch_at_gather_bm<float>(const float*, const float*, unsigned*, int64_t, int64_t,
+                                         int64_t, float*, void*, hipStream_t, const int*);
 template void launch_transpose<double>(const double*, double*, int64_t, int64_t, hipStream_t);
 template void launch_transpose<float>(const float*, float*, int64_t, int64_t, hipStream_t);
 template void launch_at_gather<double>(const double*, const double*, int64_t, int64_t, int64_t, double*,

@@ -258,12 +258,14 @@ class Session : public SessionBase {
     unsigned* ticket = static_cast<unsigned*>(c.take(kTicketBytes));
     // per-panel arrival counters of the fused A^T R with K splits (atr_split_combine)
     unsigned* pcnt = static_cast<unsigned*>(c.take(sizeof(unsigned) * (P.n / 64 + 64)));
+    // row-block arrival counters of the dense pass with the folded finalize (launch_ax_fin)
+    unsigned* fcnt = static_cast<unsigned*>(c.take(sizeof(unsigned) * (ax_fin_counters(plan) + 64)));
     int* flag = static_cast<int*>(c.take(256));
     // device-controlled batches: Ctl::state (4 doubles) and the abort word; decision records
     double* dcs = static_cast<double*>(c.take(256));
     double* dcr = static_cast<double*>(c.take(sizeof(double) * kCtlRec * kCtlMaxBatch));
     // split-candidate mode: per-row column masks of e = p - p_thr (z's buffer; bit c = e[k][c] != 0)
-    unsigned* zf = static_cast<unsigned*>(c.take((size_t)((P.n * 4 + 255) / 256) * 256));
+    unsigned* zf = static_cast<unsigned*>(c.take(zf_bytes(P.n)));   // + the column bitmaps
     double* fh = static_cast<double*>(c.take(sizeof(double) * (fh_cap + 1)));
     double* sp100 = static_cast<double*>(c.take(sizeof(double) * (fh_cap / 100 + 2)));
     const int gb = gemv_blocks_for(P);
@@ -276,6 +278,7 @@ class Session : public SessionBase {
       s->G_ = g[0]; s->Gp_ = gp[0]; s->Pp_ = pp; s->At_ = at; s->glists_ = glists;
       s->scal_ = scal; s->part_ = part; s->ticket_ = ticket; s->flag_ = flag; s->fh_dev_ = fh;
       s->pcnt_ = pcnt;
+      s->fcnt_ = fcnt;
       s->dc_state_ = dcs;
       s->dc_abort_ = reinterpret_cast<int*>(dcs + 8);
       s->dc_rec_ = dcr;
@@ -390,7 +393,9 @@ class Session : public SessionBase {
     // nonzero only where the hard threshold zeroed p (see iter_proxgd, split_mode)
     emode_ = smode_ != 0 && P.method == GLX_PROXGD;
     fsplit_ = smode_ == 1 && P.method == GLX_FPROXGD;
-    rows_form_ = gather_rows_env() && gather_rows_ok(m_, n_);
+    gform_ = gather_form();
+    if (gform_ == 1 && !gather_rows_ok(m_, n_)) gform_ = 0;
+    rows_form_ = gform_ == 1;
     gsplit_ = rows_form_ ? gather_split(m_, n_) : 1;
     {   // the VALU gather's budget counts nonzeros of e_c, the row form's flagged rows (round 5)
       const char* nb = std::getenv("GLX_SPLIT_NNZ");
@@ -400,6 +405,10 @@ class Session : public SessionBase {
       launch_transpose<T>(static_cast<const T*>(P.A), At_, m_, n_, st_);   // once
     }
     fused_fista_ok_ = fuse_any && P.method == GLX_FPROXGD;
+    // Round 5: the split-candidate ProxGD trial's finalize folded into its dense pass (one GPU;
+    // with a communicator the sums ride the gradient all-reduce; GLX_AX_FIN=0: the separate
+    // k_finalize_residual)
+    fin_ok_ = emode_ && comm_ == nullptr && ax_fin_ok(plan_, (int)sizeof(T)) && !env_is("GLX_AX_FIN", "0");
     // device-controlled batches (dc_run / fista_dc_run): ProxGD / FProxGD with line search on
     // the fused speculative path; GLX_DC_BATCH = iterations in flight (0: the host decides every
     // iteration). With a communicator fp64 only (the trial sums ride the gradient all-reduce).
@@ -414,6 +423,7 @@ class Session : public SessionBase {
     }
     GLX_HIP(hipMemsetAsync(ticket_, 0, kTicketBytes, st_));
     GLX_HIP(hipMemsetAsync(pcnt_, 0, sizeof(unsigned) * (P.n / 64 + 64), st_));
+    GLX_HIP(hipMemsetAsync(fcnt_, 0, sizeof(unsigned) * (ax_fin_counters(plan_) + 64), st_));
     GLX_HIP(hipMemsetAsync(flag_, 0, 256, st_));
     GLX_HIP(hipMemsetAsync(scal_, 0, sizeof(double) * NSCAL_DEV, st_));
     mus_[0] = 100 * P.mu0;
@@ -550,7 +560,9 @@ class Session : public SessionBase {
     s += "; split=";
     if (smode_ == 0) s += "dense";
     else if (rows_form_) s += "rows k_at_rows S0=" + std::to_string(gsplit_);
-    else s += "gather k_e_lists+k_at_gather";
+    else if (gform_ == 2) s += "gather k_e_lists+k_at_gather";
+    else s += "gather k_at_gather_bm";
+    if (fin_ok_) s += " + finalize folded into A p_thr";
     s += "; dc_window=" + std::to_string(dc_window_);
     return s;
   }
@@ -685,6 +697,11 @@ class Session : public SessionBase {
                  unsigned* pub_seq = nullptr, double* defer = nullptr, bool skip_ax = false,
                  bool snap_trial = false, bool chain = false) {
     const bool gat = chain && smode_ == 1;
+    if (gat && fin_ok_ && !skip_ax && defer == nullptr && !snap_trial && fh == nullptr) {
+      cand_ax_fin(xs, rs[1], cx, cmax, red(slot));
+      if (pub_seq != nullptr) *pub_seq = post_readback();
+      return;
+    }
     if (!skip_ax) {
       if (gat) cand_ax(xs);
       else spec_ax(nsrc, xs);
@@ -732,7 +749,7 @@ class Session : public SessionBase {
   // slabs, each workgroup compacts its K range's row flags itself), so no column lists.
   void cand_ax(const T* const* xs, Pub pb = Pub{}) {
     const T* xd[3] = {xs[1], nullptr, nullptr};
-    if (!rows_form_) {
+    if (gform_ == 2) {
       launch_e_lists(zf_, n_, l_, glists_, st_, dc_gate_);
       check_launch();
     }
@@ -741,10 +758,45 @@ class Session : public SessionBase {
     check_launch();
     prof_end(0, e0);
     hipEvent_t e2 = prof_begin(2);
-    if (rows_form_) launch_at_rows<T>(At_, xs[0], zf_, m_, n_, l_, Pp_, glists_, st_, dc_gate_);
-    else launch_at_gather<T>(At_, xs[0], m_, n_, l_, Pp_, glists_, st_, dc_gate_);
+    if (gform_ == 1) launch_at_rows<T>(At_, xs[0], zf_, m_, n_, l_, Pp_, glists_, st_, dc_gate_);
+    else if (gform_ == 2) launch_at_gather<T>(At_, xs[0], m_, n_, l_, Pp_, glists_, st_, dc_gate_);
+    else launch_at_gather_bm<T>(At_, xs[0], zf_, m_, n_, l_, Pp_, glists_, st_, dc_gate_);
     check_launch();
     prof_end(2, e2);
+    ++ax_calls_;
+    ax_cols_ += 1;
+  }
+  // The same trial with the finalize folded into the dense pass (fin_ok_, launch_ax_fin): A e first
+  // (its slabs at Pp_), then A p_thr, whose row blocks' last K-split arrivals form r1 = A p_thr - b
+  // (into r1), r0 = r1 + A e and the sums (red: [|r0|^2, |r1|^2, 0, count(|cx| > 1e-6 *cmax)];
+  // dc_ctl_: the device-side decision in the final workgroup).
+  void cand_ax_fin(const T* const* xs, T* r1, const T* cx, const double* cmax, Red rd) {
+    if (gform_ == 2) {
+      launch_e_lists(zf_, n_, l_, glists_, st_, dc_gate_);
+      check_launch();
+    }
+    hipEvent_t e2 = prof_begin(2);
+    if (gform_ == 1) launch_at_rows<T>(At_, xs[0], zf_, m_, n_, l_, Pp_, glists_, st_, dc_gate_);
+    else if (gform_ == 2) launch_at_gather<T>(At_, xs[0], m_, n_, l_, Pp_, glists_, st_, dc_gate_);
+    else launch_at_gather_bm<T>(At_, xs[0], zf_, m_, n_, l_, Pp_, glists_, st_, dc_gate_);
+    check_launch();
+    prof_end(2, e2);
+    AxFin f;
+    f.B = B_;
+    f.R1 = r1;
+    f.P0 = Pp_;
+    f.S0 = gsplit_;
+    f.cx = cx;
+    f.cn = cx ? nl_ : 0;
+    f.cmax = cmax;
+    f.cnt = fcnt_;
+    f.red = rd;
+    f.ctl = dc_ctl_;
+    hipEvent_t e0 = prof_begin(0);
+    if (!launch_ax_fin<T>(plan_, A_, xs[1], Pp_ + (size_t)gsplit_ * ml_, dc_gate_, 0, st_, f))
+      throw Error{GLX_E_STATE, "folded finalize: the plan does not take it"};
+    check_launch();
+    prof_end(0, e0);
     ++ax_calls_;
     ax_cols_ += 1;
   }
@@ -1802,11 +1854,14 @@ class Session : public SessionBase {
   unsigned *hseq_ = nullptr, *hseq_dev_ = nullptr;
   unsigned* ticket_ = nullptr;
   unsigned* pcnt_ = nullptr;   // per-panel counters (fused A^T R with K splits)
+  unsigned* fcnt_ = nullptr;   // per-row-block counters (the dense pass's folded finalize)
+  bool fin_ok_ = false;        // the split-candidate ProxGD finalize folded into the dense pass
   unsigned* zf_ = nullptr;     // per-row column masks of e (split-candidate mode)
   T* At_ = nullptr;            // A^T (split-candidate gather form)
   void* glists_ = nullptr;     // the gather's per-column index lists of e
   int smode_ = 0, gsplit_ = 1;
-  bool rows_form_ = false;     // A e by k_at_rows (round 5), else the VALU column-list gather
+  int gform_ = 0;              // A e: 0 bitmap gather, 1 k_at_rows, 2 lists + gather (gather_form)
+  bool rows_form_ = false;     // gform_ == 1: A e by k_at_rows (round 5), gsplit_ slabs
   // entries of the gather counts the FISTA finalize sums: flagged rows per K range (row form) or
   // nonzeros per column (VALU gather)
   int gcount_n() const { return rows_form_ ? gsplit_ : (int)l_; }
@@ -1916,7 +1971,7 @@ struct KernelWs {
   void* pp; void* gp; double* part; unsigned* ticket; double* scal;
   void* rg_ws; double* rg_s; double* rg_g; int* rg_err;   // fused residual-gradient pass
   void* rg2_ws; double* rg2_g;                              // its l = 16 two-source form
-  void* fr_slabs; void* fr_lists;                           // glx_flagged_rows_product
+  void* fr_slabs; void* fr_lists; void* fr_zf;              // glx_flagged_rows_product
 };
 static size_t kernel_ws(int es, const GemmPlan& p, void* base, KernelWs* out) {
   Carver c(base);
@@ -1949,12 +2004,15 @@ static size_t kernel_ws(int es, const GemmPlan& p, void* base, KernelWs* out) {
   // the flagged-row product (A e of the split-candidate trial): its slabs and lists / counts
   void* fr_slabs = nullptr;
   void* fr_lists = nullptr;
+  void* fr_zf = nullptr;
   if (gather_ok(p.n, p.l)) {
     fr_slabs = c.take((size_t)es * p.m * p.l * std::max(1, gather_split(p.m, p.n)));
     fr_lists = c.take(gather_lists_bytes(p.n));
+    fr_zf = c.take(zf_bytes(p.n));
   }
   if (out)
-    *out = KernelWs{pp, gp, part, ticket, scal, rg_ws, rg_s, rg_g, rg_err, rg2_ws, rg2_g, fr_slabs, fr_lists};
+    *out = KernelWs{pp, gp, part, ticket, scal, rg_ws, rg_s, rg_g, rg_err, rg2_ws, rg2_g, fr_slabs, fr_lists,
+                    fr_zf};
   return c.off + 256;
 }
 
@@ -2208,7 +2266,7 @@ int glx_flagged_rows_product(int dtype, int64_t m, int64_t n, int64_t l, const v
     GemmPlan p;
     KernelWs k = kernel_setup(dtype, m, n, l, ws, wsb, 0, st, &p);
     if (!gather_ok(n, l) || k.fr_slabs == nullptr) throw Error{GLX_E_INVALID, "needs l in {16, 32}, n < 65536"};
-    if (form != 0 && form != 1) throw Error{GLX_E_INVALID, "form must be 0 (MFMA rows) or 1 (VALU gather)"};
+    if (form < 0 || form > 2) throw Error{GLX_E_INVALID, "form must be 0 (MFMA rows), 1 (lists), 2 (bitmaps)"};
     if (form == 0 && !gather_rows_ok(m, n)) throw Error{GLX_E_INVALID, "the row form needs m % 64 == 0"};
     const int S0 = form == 0 ? gather_split(m, n) : 1;
     auto go = [&](auto* tag) {
@@ -2217,9 +2275,15 @@ int glx_flagged_rows_product(int dtype, int64_t m, int64_t n, int64_t l, const v
       if (form == 0) {
         launch_at_rows<T>(static_cast<const T*>(At), static_cast<const T*>(E), row_masks, m, n, l, slabs,
                           k.fr_lists, st);
-      } else {
+      } else if (form == 1) {
         launch_e_lists(row_masks, n, l, k.fr_lists, st);
         launch_at_gather<T>(static_cast<const T*>(At), static_cast<const T*>(E), m, n, l, slabs, k.fr_lists, st);
+      } else {   // the masks copied into a zf-shaped buffer, its bitmaps built, then the gather
+        unsigned* zf = static_cast<unsigned*>(k.fr_zf);
+        GLX_HIP(hipMemcpyAsync(zf, row_masks, sizeof(unsigned) * n, hipMemcpyDeviceToDevice, st));
+        launch_zf_bitmaps(zf, n, l, st);
+        launch_at_gather_bm<T>(static_cast<const T*>(At), static_cast<const T*>(E), zf, m, n, l, slabs,
+                               k.fr_lists, st);
       }
       launch_sum_partials<T>(slabs, S0, static_cast<T*>(Y), m * l, st);
     };

@@ -120,9 +120,10 @@ def residual_gradient2(A: torch.Tensor, X0: torch.Tensor, X1: torch.Tensor, B: t
 def flagged_rows_product(At: torch.Tensor, E: torch.Tensor, row_masks: torch.Tensor,
                          form: int = 0) -> torch.Tensor:
     """Y = sum over the rows k with row_masks[k] != 0 of At[k]^T E[k] (m x l): the split-candidate
-    trial's A e from the transposed copy At = A^T (n x m). form 0: the MFMA row form (the
-    solver's default, m % 64 == 0), 1: the VALU column-list gather (bit c of row_masks[k] must be
-    E[k][c] != 0). row_masks: int32 device tensor of n (+ padding) column masks."""
+    trial's A e from the transposed copy At = A^T (n x m). form 0: the MFMA row form
+    (m % 64 == 0), 1: the VALU column-list gather of rounds 2-4, 2: the bitmap gather (the
+    solver's default; 1 and 2 need bit c of row_masks[k] == (E[k][c] != 0)). row_masks: int32
+    device tensor of n (+ padding) column masks."""
     n, m = At.shape
     l = E.shape[1]
     dt = _dt(At)

@@ -220,7 +220,8 @@ int glx_residual_gradient2(int dtype, int64_t m, int64_t n, int64_t l, const voi
  *   Y (m x l) = sum over the rows k with row_masks[k] != 0 of At[k,:]^T E[k,:],  At = A^T (n x m).
  * row_masks[k] (device uint32, n + 3 readable) = the column mask of row k of E (bit c = E[k][c] != 0,
  * as the trial kernels write it). form 0: the MFMA row form (k_at_rows, the solver's default; m % 64
- * == 0); form 1: the VALU column-list gather of rounds 2-4 (needs the exact column masks). */
+ * == 0); form 1: the VALU column-list gather of rounds 2-4; form 2: the bitmap gather (the solver's
+ * default since round 5, bit-identical to form 1). Forms 1, 2 need the exact column masks. */
 int glx_flagged_rows_product(int dtype, int64_t m, int64_t n, int64_t l, const void* At,
                              const void* E, const uint32_t* row_masks, void* Y, int form,
                              void* workspace, size_t workspace_bytes, void* stream);

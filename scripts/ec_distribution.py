@@ -26,9 +26,10 @@ def main():
     mu = 1e-2
     opts = {"alpha0": 1.0 / (m ** 0.5 + n ** 0.5) ** 2, "profile": 4}
     from glx.solver import Session
-    cases = [("gl_FProxGD_primal", "rows", "10"), ("gl_FProxGD_primal", "valu", "10"),
-             ("gl_FProxGD_primal", "rows", None), ("gl_ProxGD_primal", "rows", None),
-             ("gl_ProxGD_primal", "valu", None)]
+    cases = [("gl_FProxGD_primal", "rows", "10"), ("gl_FProxGD_primal", "bm", "10"),
+             ("gl_FProxGD_primal", "rows", None), ("gl_FProxGD_primal", "bm", None),
+             ("gl_ProxGD_primal", "rows", None), ("gl_ProxGD_primal", "bm", None),
+             ("gl_ProxGD_primal", "lists", None)]
     for method, form, budget in cases:
         os.environ["GLX_GATHER"] = form
         if budget is None:

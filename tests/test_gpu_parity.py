@@ -311,3 +311,27 @@ def test_split_candidate_gather_waves_bit_identical(name, monkeypatch):
     for x, k, fh in runs[1:]:
         assert k == runs[0][1] and fh == runs[0][2] and np.array_equal(x, runs[0][0])
     assert runs[0][1] == int(gold["k"])
+
+
+def test_folded_finalize_matches_separate_kernel(monkeypatch):
+    """Round 5: at the north-star size the split-candidate ProxGD trial's residual finalize runs
+    inside the dense pass A p_thr (launch_ax_fin: the row blocks' last K-split arrivals sum the
+    slabs; GLX_AX_FIN=0 restores k_finalize_residual). The next gradient residual is summed in the
+    same slab order, so the iterates are bit-identical; the recorded objective's squared sums are
+    reduced in another order (ulp level). 60 iterations per phase, both phase boundaries."""
+    from oracle import numpy_ref
+    m, n, l = 8192, 16384, 32
+    A, b, u, x0, mu = numpy_ref.gen_data(m, n, l, 97006855)
+    opts = {"alpha0": numpy_ref.step_size_for(m, n), "maxit": 60}
+    import importlib
+    fn = getattr(importlib.import_module("gl_ProxGD_primal"), "gl_ProxGD_primal")
+    At, bt = torch.from_numpy(A).cuda(), torch.from_numpy(b).cuda()
+    runs = []
+    for fin in ("0", "1"):
+        monkeypatch.setenv("GLX_AX_FIN", fin)
+        x, k, out = fn(torch.from_numpy(x0).cuda(), At, bt, mu, dict(opts))
+        runs.append((x.cpu().numpy(), k, np.asarray([float(v) for v in out["f_hist"]])))
+    (x0_, k0, f0), (x1, k1, f1) = runs
+    assert k0 == k1 == 180
+    assert np.array_equal(x0_, x1)
+    assert np.max(np.abs(f1 - f0) / np.abs(f0)) < 1e-13

@@ -4,9 +4,10 @@ Reference: the line-search candidate's objective g(p) = 1/2 ||A p - b||^2 (gl_Pr
 :112) with p = p_thr + e, e = p - p_thr nonzero only where the hard threshold (:127) zeroed an
 entry; FProxGD's A y_next from A e_c (gl_FProxGD_primal.py:92-97, :136). libglx computes A e from a
 transposed copy At = A^T over the flagged rows only. Checked here through the C ABI
-(glx_flagged_rows_product) against an fp64 torch reference of the same product, in both forms (the
-MFMA row form, the solver's default, and the VALU column-list gather of rounds 2-4), on aligned,
-large and empty flag sets, and bit-reproducible run to run.
+(glx_flagged_rows_product) against an fp64 torch reference of the same product, in its three forms
+(the MFMA row form, the VALU column-list gather of rounds 2-4, and the round-5 bitmap gather that
+builds the same lists in LDS: bit-identical to the list form), on aligned, large, ragged and
+empty flag sets, and bit-reproducible run to run.
 """
 import numpy as np
 import pytest
@@ -57,11 +58,15 @@ def test_flagged_rows_product_vs_torch(m, n, l, frac, dense, dtype):
     from glx import kernels
     At, E, masks, ref, scale = _case(m, n, l, frac, dtype, seed=m + n + l, dense_rows=dense)
     tol = 1e-13 if dtype == torch.float64 else 2e-6
-    for form in (0, 1):
-        Y = kernels.flagged_rows_product(At, E, masks, form=form).double().cpu()
+    Ys = {}
+    for form in (0, 1, 2):
+        Ys[form] = kernels.flagged_rows_product(At, E, masks, form=form)
+        Y = Ys[form].double().cpu()
         err = (Y - ref).abs().max().item()
         bound = tol * max(1.0, scale.max().item())
         assert err <= bound, (form, err, bound)
+    # the bitmap gather walks the same ascending lists as k_e_lists + k_at_gather: bit-identical
+    assert torch.equal(Ys[1], Ys[2])
 
 
 def test_row_form_ignores_unflagged_rows():
@@ -86,5 +91,6 @@ def test_row_form_needs_whole_panels():
     At, E, masks, ref, _ = _case(100, 256, 16, 0.3, torch.float64, seed=3)
     with pytest.raises(GlxError):
         kernels.flagged_rows_product(At, E, masks, form=0)
-    Y = kernels.flagged_rows_product(At, E, masks, form=1).cpu()   # the gather takes any m
-    assert (Y - ref).abs().max().item() <= 1e-12
+    for form in (1, 2):   # the gathers take any m
+        Y = kernels.flagged_rows_product(At, E, masks, form=form).cpu()
+        assert (Y - ref).abs().max().item() <= 1e-12
