@@ -252,7 +252,7 @@ bool gather_ok(int64_t n, int64_t l);
 // round 5: the MFMA row form (k_at_rows): the shapes it takes, the solver's default (GLX_GATHER=valu:
 // the column-list gather, ONE slab), and its K splits for this shape (1 where it does not apply)
 bool gather_rows_ok(int64_t m, int64_t n);
-int gather_form();   // GLX_GATHER: 0 bitmaps (default), 1 MFMA rows, 2 k_e_lists + k_at_gather
+int gather_form();   // GLX_GATHER: 0 bitmaps, 1 MFMA rows, 2 k_e_lists + k_at_gather, -1 unset
 int gather_split(int64_t m, int64_t n);
 // zf: the per-row column masks of e and, behind them, the per-column row bitmaps (glx_device.h)
 size_t zf_bytes(int64_t n);

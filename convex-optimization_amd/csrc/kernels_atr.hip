@@ -210,20 +210,37 @@ __device__ inline bool atr_split_combine(typename MF<T>::acc_t (&acc)[4][NT], T*
   __syncthreads();
   if (!last) return false;
   *slot = (int)panel;
+  // Round 5: every slab load of the wave's 4 x NT elements issued before the first add (S <= 8,
+  // atr_prox_ok), one round trip instead of S - 1 dependent ones per element; same slab order
+  constexpr int KS = NT == 1 ? 8 : 4;   // slabs per load batch (register budget)
 #pragma unroll
   for (int e = 0; e < 4; ++e) {
     if (e != wave) continue;
+    for (int k0 = 0; k0 < S; k0 += KS) {
+      T sv[4][NT][KS];
 #pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const int64_t row = col0 + atr_col<T>(M::row(lane, r), e);
+      for (int r = 0; r < 4; ++r) {
+        const int64_t row = col0 + atr_col<T>(M::row(lane, r), e);
 #pragma unroll
-      for (int nt = 0; nt < NT; ++nt) {
-        const T* g = Gp + row * L + nt * 16 + i;
-        T v = __hip_atomic_load(g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        for (int k = 1; k < S; ++k)
-          v = v + __hip_atomic_load(g + (int64_t)k * nl, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        acc[e][nt][r] = v;
+        for (int nt = 0; nt < NT; ++nt) {
+          const T* g = Gp + row * L + nt * 16 + i;
+#pragma unroll
+          for (int k = 0; k < KS; ++k)
+            sv[r][nt][k] = k0 + k < S ? __hip_atomic_load(g + (int64_t)(k0 + k) * nl, __ATOMIC_RELAXED,
+                                                          __HIP_MEMORY_SCOPE_AGENT)
+                                      : T(0);
+        }
       }
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+#pragma unroll
+        for (int nt = 0; nt < NT; ++nt) {
+          T v = k0 == 0 ? sv[r][nt][0] : acc[e][nt][r] + sv[r][nt][0];
+#pragma unroll
+          for (int k = 1; k < KS; ++k)
+            if (k0 + k < S) v = v + sv[r][nt][k];
+          acc[e][nt][r] = v;
+        }
     }
   }
   if (threadIdx.x == 0) __hip_atomic_store(pcnt + panel, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);

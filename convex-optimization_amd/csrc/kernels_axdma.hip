@@ -91,15 +91,38 @@ __device__ inline void ax_fin_epilogue(const AxFin& fin, const T* __restrict__ P
       const T* __restrict__ B = static_cast<const T*>(fin.B);
       const T* __restrict__ P0 = static_cast<const T*>(fin.P0);
       T* __restrict__ R1 = static_cast<T*>(fin.R1);
-      for (int64_t idx = e0 + threadIdx.x; idx < e1; idx += nthr) {
-        T a = __hip_atomic_load(P + idx, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        for (int k = 1; k < S; ++k)
-          a = a + __hip_atomic_load(P + (int64_t)k * ml + idx, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        const T r1 = a - B[idx];
-        const T r0 = r1 + slab_sum(P0, fin.S0, ml, idx);
-        R1[idx] = r1;
-        v[0] += (double)(r0 * r0);
-        v[1] += (double)(r1 * r1);
+      // all loads of a batch of EB elements per thread issued before the first is used (the S
+      // slabs with agent-scope loads, S <= kFinSlabs): a few round trips per row block instead of
+      // one per slab and element
+      constexpr int EB = 4, KS = 8;
+      for (int64_t base = e0 + threadIdx.x; base < e1; base += (int64_t)nthr * EB) {
+        T a[EB][KS], bv[EB], e[EB];
+#pragma unroll
+        for (int u = 0; u < EB; ++u) {
+          const int64_t idx = base + (int64_t)u * nthr;
+          const int64_t ic = idx < e1 ? idx : e1 - 1;
+#pragma unroll
+          for (int k = 0; k < KS; ++k)
+            a[u][k] = k < S ? __hip_atomic_load(P + (int64_t)k * ml + ic, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                            : T(0);
+          bv[u] = B[ic];
+          e[u] = slab_sum(P0, fin.S0, ml, ic);
+        }
+#pragma unroll
+        for (int u = 0; u < EB; ++u) {
+          const int64_t idx = base + (int64_t)u * nthr;
+          T sum = a[u][0];
+#pragma unroll
+          for (int k = 1; k < KS; ++k)
+            if (k < S) sum = sum + a[u][k];
+          const T r1 = sum - bv[u];
+          const T r0 = r1 + e[u];
+          if (idx < e1) {
+            R1[idx] = r1;
+            v[0] += (double)(r0 * r0);
+            v[1] += (double)(r1 * r1);
+          }
+        }
       }
       if (threadIdx.x == 0) __hip_atomic_store(fin.cnt + rb, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
@@ -502,7 +525,7 @@ int ax_fin_counters(const GemmPlan& p) { return (int)cdiv(p.m, 16 * 2 * 8); }
 bool ax_fin_ok(const GemmPlan& p, int esize) {
   const int S = p.axb_S[1];
   return esize == 8 && p.ax_kind != 3 && p.axb_code[1] == 92278 && (p.l == 16 || p.l == 32) &&
-         S >= 1 && p.n / 32 >= S && ax_grid(ax_xmap_flags(p, S), (int)cdiv(p.m, 256), S) <= kMaxBlocks;
+         S >= 1 && S <= 8 && p.n / 32 >= S && ax_grid(ax_xmap_flags(p, S), (int)cdiv(p.m, 256), S) <= kMaxBlocks;
 }
 
 template <typename T>

@@ -499,13 +499,15 @@ static int env_rows_s() {
 }
 // the shapes the MFMA row form (k_at_rows) takes: whole 64-row panels of At
 bool gather_rows_ok(int64_t m, int64_t n) { return m % 64 == 0 && m > 0 && n <= 65535; }
-// the solver's A e form (GLX_GATHER): 0 = the bitmap gather (k_at_gather_bm, default), 1 = the
-// MFMA row form ("rows", where gather_rows_ok), 2 = k_e_lists + k_at_gather ("lists", rounds 2-4)
+// the A e form GLX_GATHER asks for: 0 = the bitmap gather ("bm", k_at_gather_bm), 1 = the MFMA
+// row form ("rows", where gather_rows_ok), 2 = k_e_lists + k_at_gather ("lists", rounds 2-4),
+// -1 = unset (the solver's per-method default)
 int gather_form() {
   const char* e = std::getenv("GLX_GATHER");
   if (e && std::strcmp(e, "rows") == 0) return 1;
   if (e && (std::strcmp(e, "lists") == 0 || std::strcmp(e, "valu") == 0)) return 2;
-  return 0;
+  if (e && std::strcmp(e, "bm") == 0) return 0;
+  return -1;
 }
 // K splits of the row form: about two workgroups per CU (512 on 256 CUs), each K range within
 // the LDS list; GLX_ATROWS_S overrides (clamped to that bound)

@@ -393,7 +393,14 @@ class Session : public SessionBase {
     // nonzero only where the hard threshold zeroed p (see iter_proxgd, split_mode)
     emode_ = smode_ != 0 && P.method == GLX_PROXGD;
     fsplit_ = smode_ == 1 && P.method == GLX_FPROXGD;
+    // A e form (round 5, scripts/ec_distribution.py over whole NS solves, profiles/r5_c/): ProxGD's
+    // e has ~1.1 nonzeros per flagged row (27 % of the rows), so the VALU bitmap gather does 1/30
+    // of the row form's MFMA work (whole solve 2206 against 2128 it/s for the row form, 2185 for
+    // the round-4 lists); FProxGD's e_c reaches 96 % of the rows with ~7.5 nonzeros each late in
+    // a solve, where the row form reads every flagged At row once (whole solves 2131-2143 against
+    // 2114-2121 bitmap, 2122-2124 lists).
     gform_ = gather_form();
+    if (gform_ < 0) gform_ = P.method == GLX_FPROXGD ? 1 : 0;
     if (gform_ == 1 && !gather_rows_ok(m_, n_)) gform_ = 0;
     rows_form_ = gform_ == 1;
     gsplit_ = rows_form_ ? gather_split(m_, n_) : 1;
