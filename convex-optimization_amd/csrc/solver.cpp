@@ -144,13 +144,15 @@ static void validate(const glx_problem* P, const glx_opts* O) {
 // ProxGD: fp64 only. In fp32 its regrouped sum (A p_thr - b) + A e IS the recorded objective
 // and moves f by ~1e-6 relative on short unconverged runs (measured 1.5e-6 on mid_384x640x16
 // against the 1e-6 fp32 bar); no fp32 ProxGD configuration is on the benchmark path.
-// FProxGD in fp32 (round 4, C3; opt-in, GLX_SPLIT_F32=1): the objective is A xc computed
-// directly; only A y_next is regrouped. On short runs against the fp32 reference / oracle it
-// measured fval 2e-8..2e-7 and f_hist up to 1.4e-5 (bars 1e-6 / 2e-5; profiles/r4_exp3/), and
-// with its dense pass on the f32 LDS-DMA tile C3 runs 4406-4475 against 3738-3781 it/s over 200
-// steps; but over C3's whole solve against the reference's fp32 run it ends 3.4e-5 from the
-// reference's objective, the dense batch 3.4e-7 (profiles/r4_c3gold/), so the dense batch stays
-// the default. (The size gate counts elements as fp64.)
+// FProxGD in fp32 (C3): the objective is A xc computed directly; only A y_next is regrouped.
+// Round 4 kept it opt-in because one whole C3 solve ended 3.4e-5 from the reference's fp32 run
+// against 3.4e-7 for the dense batch. Round 5 measured the band (scripts/c3_band.py,
+// profiles/r5_d/c3_band.jsonl): eleven summation orders of the two forms (K splits, tiles, A e
+// forms) end 3.4e-7 .. 8.7e-5 (dense) and 1.6e-5 .. 8.9e-5 (split) from the reference's fp32
+// objective, all 7.0e-3 .. 7.1e-3 from its fp64 one (the reference's own fp32 run: 7.0e-3). The
+// split form's band is no worse, so it is the default (GLX_SPLIT_F32=0: the dense batch); whole
+// solves run level (3897 it/s both: late in a solve e_c fills and the budget runs dense batches),
+// 200-step windows +17 %. (The size gate counts elements as fp64.)
 // FProxGD with line search takes the gather form too (iter_fista: A y_next by linearity from
 // A xc, A e_c and the kept A thr(x_k)); GLX_SPLIT_FISTA=0 keeps its dense [xc | y_next] batch.
 // Only for A of at least kSplitMinBytes (this rank's rows): the column lists and the gather
@@ -162,9 +164,9 @@ static constexpr double kSplitMinBytes = 768.0 * 1024 * 1024;
 static int split_mode(const glx_problem& P, const glx_opts& O) {
   if (O.exact_objective != 0) return 0;
   if (P.method != GLX_PROXGD && P.method != GLX_FPROXGD) return 0;
-  if (P.dtype != GLX_F64) {   // fp32: FProxGD only and opt-in (GLX_SPLIT_F32=1, above)
+  if (P.dtype != GLX_F64) {   // fp32: FProxGD only (GLX_SPLIT_F32=0: off, above)
     const char* f = std::getenv("GLX_SPLIT_F32");
-    if (P.method != GLX_FPROXGD || !(f && std::strcmp(f, "1") == 0)) return 0;
+    if (P.method != GLX_FPROXGD || (f && std::strcmp(f, "0") == 0)) return 0;
   }
   if (O.split_cand == 2) return 0;
   const char* sc = O.split_cand == 0 ? std::getenv("GLX_SPLIT_CAND") : nullptr;
@@ -413,9 +415,11 @@ class Session : public SessionBase {
     }
     fused_fista_ok_ = fuse_any && P.method == GLX_FPROXGD;
     // Round 5: the split-candidate ProxGD trial's finalize folded into its dense pass (one GPU;
-    // with a communicator the sums ride the gradient all-reduce; GLX_AX_FIN=0: the separate
-    // k_finalize_residual)
-    fin_ok_ = emode_ && comm_ == nullptr && ax_fin_ok(plan_, (int)sizeof(T)) && !env_is("GLX_AX_FIN", "0");
+    // with a communicator the sums ride the gradient all-reduce). Measured slower, so opt-in
+    // (GLX_AX_FIN=1): A p_thr 167-168 -> 207 us, NS 2537-2543 -> 2376 it/s over 200 steps
+    // (profiles/r5_d/): the slab stores go write-through (agent scope) and the 32 row-block
+    // owners' combine runs alone at the end of the pass, against k_finalize_residual's 12 us.
+    fin_ok_ = emode_ && comm_ == nullptr && ax_fin_ok(plan_, (int)sizeof(T)) && env_is("GLX_AX_FIN", "1");
     // device-controlled batches (dc_run / fista_dc_run): ProxGD / FProxGD with line search on
     // the fused speculative path; GLX_DC_BATCH = iterations in flight (0: the host decides every
     // iteration). With a communicator fp64 only (the trial sums ride the gradient all-reduce).

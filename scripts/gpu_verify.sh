@@ -19,8 +19,9 @@ for args in "$@"; do
   python - "$O/b$i.json" "$args" <<'PY'
 import json, sys
 d = json.loads(open(sys.argv[1]).read().strip().splitlines()[-1]); r = d["roofline"]; w = d["work"]
+k = r["kernels"]
 print("[%s] %.1f it/s  ax %.1fus (%s %.3f) atr %.1fus pair %.3f iter %.3f  passes %.2f syncs %.2f cpu %s" % (
-    sys.argv[2], d["value"], r["avg_launch_us"], r["bound"], r["frac"], r["atr_avg_launch_us"],
+    sys.argv[2], d["value"], k["ax"]["avg_launch_us"], r["bound"], r["frac"], (k.get("atr") or {}).get("avg_launch_us") or 0,
     r["pair_frac"] or 0, r["iter_frac"], w["passes_over_A_per_iter"], w["syncs_per_iter"],
     (d.get("cpu_baseline") or {}).get("value")))
 PY

@@ -116,10 +116,9 @@ F32_SPLIT_CASES = sorted(c for c, meta in golden_index().items()
 
 @pytest.mark.parametrize("name", F32_SPLIT_CASES)
 def test_split_candidate_forced_golden_f32_fista(name, monkeypatch):
-    """Round 4: fp32 FProxGD's split-candidate batch (A y_next by linearity; opt-in,
-    GLX_SPLIT_F32=1: over C3's whole solve it ends 3.4e-5 from the reference's objective),
-    forced here on the fp32 golden cases, against the fp32 bars (measured fval 5e-8..9e-8,
-    f_hist up to 1.4e-5: profiles/r4_exp3/margins.jsonl)."""
+    """fp32 FProxGD's split-candidate batch (A y_next by linearity; the default at C3's size
+    since round 5, see test_whole_solve_c3_fp32), forced here on the fp32 golden cases, against
+    the fp32 bars (measured fval 5e-8..9e-8, f_hist up to 1.4e-5: profiles/r4_exp3/margins.jsonl)."""
     monkeypatch.setenv("GLX_SPLIT_CAND", "1")
     monkeypatch.setenv("GLX_SPLIT_F32", "1")
     meta, gold = golden_case(name)
@@ -314,9 +313,9 @@ def test_split_candidate_gather_waves_bit_identical(name, monkeypatch):
 
 
 def test_folded_finalize_matches_separate_kernel(monkeypatch):
-    """Round 5: at the north-star size the split-candidate ProxGD trial's residual finalize runs
-    inside the dense pass A p_thr (launch_ax_fin: the row blocks' last K-split arrivals sum the
-    slabs; GLX_AX_FIN=0 restores k_finalize_residual). The next gradient residual is summed in the
+    """Round 5: at the north-star size the split-candidate ProxGD trial's residual finalize can
+    run inside the dense pass A p_thr (launch_ax_fin, opt-in GLX_AX_FIN=1 because it measured
+    slower: the row blocks' last K-split arrivals sum the slabs) instead of k_finalize_residual. The next gradient residual is summed in the
     same slab order, so the iterates are bit-identical; the recorded objective's squared sums are
     reduced in another order (ulp level). 60 iterations per phase, both phase boundaries."""
     from oracle import numpy_ref
