@@ -18,6 +18,7 @@
 // a trial at NS, round 2: its flops were ~97 % zeros.)
 #include <hip/hip_runtime.h>
 
+#include <cstdio>
 #include <cstdlib>
 #include <cstring>
 
@@ -237,15 +238,18 @@ __global__ __launch_bounds__(kGThreads) void k_at_gather2(const T* __restrict__ 
 // with the indices read from LDS. Same list, same order, same arithmetic: bit-identical to
 // k_e_lists + k_at_gather, one launch and ~8 us fewer per trial (the lists kernel's 32
 // workgroups ran alone on the chip). counts[c] (rb == 0) = the list length (FProxGD's budget).
-template <typename T, int L, bool NT>
+// U: At loads in flight per thread; SEGW: bitmap words per segment (64 SEGW rows, its list in
+// 128 SEGW bytes of LDS; 128: twice the workgroups per CU). Neither changes the summation order.
+template <typename T, int L, bool NT, int U, int SEGW>
 __global__ __launch_bounds__(kGThreads) void k_at_gather_bm(const T* __restrict__ At,
                                                             const T* __restrict__ E,
                                                             unsigned* __restrict__ zf, int64_t m,
                                                             int64_t n, T* __restrict__ P,
                                                             unsigned* __restrict__ counts, int gx,
                                                             const int* __restrict__ skip) {
+  static_assert(SEGW <= kGThreads, "one bitmap word per thread and segment");
   if (skip != nullptr && *skip != 0) return;
-  __shared__ unsigned short lst[64 * kGThreads];   // one segment: 256 words x 64 rows
+  __shared__ unsigned short lst[64 * SEGW];   // one segment: SEGW words x 64 rows
   __shared__ unsigned wsum[kGW];
   const int tid = threadIdx.x;
   const int lane = tid & 63, wave = tid >> 6;
@@ -254,12 +258,11 @@ __global__ __launch_bounds__(kGThreads) void k_at_gather_bm(const T* __restrict_
   const uint64_t* words = reinterpret_cast<const uint64_t*>(zf_bitmaps(zf, n) + (int64_t)c * (zf_npad(n) / 16));
   const int64_t r = (int64_t)rb * kGThreads + tid;
   const int64_t rr = r < m ? r : m - 1;
-  constexpr int U = 8;
   T acc = T(0);
   unsigned all = 0;
-  for (int64_t w0 = 0; w0 < nw; w0 += kGThreads) {
+  for (int64_t w0 = 0; w0 < nw; w0 += SEGW) {
     const int64_t w = w0 + tid;
-    uint64_t bits = w < nw ? words[w] : uint64_t(0);
+    uint64_t bits = (tid < SEGW && w < nw) ? words[w] : uint64_t(0);
     const unsigned cnt = (unsigned)__builtin_popcountll(bits);
     unsigned inc = cnt;
 #pragma unroll
@@ -594,7 +597,18 @@ void launch_at_gather(const T* At, const T* E, int64_t m, int64_t n, int64_t l, 
 }
 
 // A e by the column bitmaps the trial kernels wrote behind zf (k_at_gather_bm): ONE slab at P,
-// the column list lengths into the counts area of lists_ws (gather_counts)
+// the column list lengths into the counts area of lists_ws (gather_counts). GLX_GATHER_BM =
+// "U,SEGW" selects the loads in flight and the segment (8,256 default; 16 / 128 the variants).
+template <typename T, int L, bool NT>
+static void at_gather_bm_go(int code, dim3 g, hipStream_t st, const T* At, const T* E, unsigned* zf,
+                            int64_t m, int64_t n, T* P, unsigned* cnt, int gx, const int* skip) {
+  switch (code) {
+    case 16256: glx_launch(k_at_gather_bm<T, L, NT, 16, 256>, g, dim3(kGThreads), 0, st, At, E, zf, m, n, P, cnt, gx, skip); break;
+    case 8128: glx_launch(k_at_gather_bm<T, L, NT, 8, 128>, g, dim3(kGThreads), 0, st, At, E, zf, m, n, P, cnt, gx, skip); break;
+    case 16128: glx_launch(k_at_gather_bm<T, L, NT, 16, 128>, g, dim3(kGThreads), 0, st, At, E, zf, m, n, P, cnt, gx, skip); break;
+    default: glx_launch(k_at_gather_bm<T, L, NT, 8, 256>, g, dim3(kGThreads), 0, st, At, E, zf, m, n, P, cnt, gx, skip); break;
+  }
+}
 template <typename T>
 void launch_at_gather_bm(const T* At, const T* E, unsigned* zf, int64_t m, int64_t n, int64_t l, T* P,
                          void* lists_ws, hipStream_t st, const int* skip) {
@@ -603,14 +617,21 @@ void launch_at_gather_bm(const T* At, const T* E, unsigned* zf, int64_t m, int64
     const char* e = std::getenv("GLX_GATHER_NT");
     return !(e && std::strcmp(e, "0") == 0);
   }();
+  const int code = [] {   // read per launch (tests switch it within one process)
+    const char* e = std::getenv("GLX_GATHER_BM");
+    int u = 8, w = 256;
+    if (e) std::sscanf(e, "%d,%d", &u, &w);
+    return (u == 16 ? 16 : 8) * 1000 + (w == 128 ? 128 : 256);
+  }();
   const int gx = (int)((m + kGThreads - 1) / kGThreads);
+  const dim3 g((unsigned)(gx * l));
   unsigned* cnt = list_counts(lists_ws, n);
   if (l == 32) {
-    if (nt) glx_launch(k_at_gather_bm<T, 32, true>, dim3((unsigned)(gx * l)), dim3(kGThreads), 0, st, At, E, zf, m, n, P, cnt, gx, skip);
-    else glx_launch(k_at_gather_bm<T, 32, false>, dim3((unsigned)(gx * l)), dim3(kGThreads), 0, st, At, E, zf, m, n, P, cnt, gx, skip);
+    if (nt) at_gather_bm_go<T, 32, true>(code, g, st, At, E, zf, m, n, P, cnt, gx, skip);
+    else at_gather_bm_go<T, 32, false>(code, g, st, At, E, zf, m, n, P, cnt, gx, skip);
   } else {
-    if (nt) glx_launch(k_at_gather_bm<T, 16, true>, dim3((unsigned)(gx * l)), dim3(kGThreads), 0, st, At, E, zf, m, n, P, cnt, gx, skip);
-    else glx_launch(k_at_gather_bm<T, 16, false>, dim3((unsigned)(gx * l)), dim3(kGThreads), 0, st, At, E, zf, m, n, P, cnt, gx, skip);
+    if (nt) at_gather_bm_go<T, 16, true>(code, g, st, At, E, zf, m, n, P, cnt, gx, skip);
+    else at_gather_bm_go<T, 16, false>(code, g, st, At, E, zf, m, n, P, cnt, gx, skip);
   }
 }
 void launch_zf_bitmaps(unsigned* zf, int64_t n, int64_t l, hipStream_t st) {
