@@ -160,6 +160,14 @@ static void validate(const glx_problem* P, const glx_opts* O) {
 // batch (profiles/r2_splitgate/): NS (1 GiB) 2295 vs 2080 it/s, (4096,16384,32) 3894 vs 3832,
 // but C2 (4096,8192,16) 7329 vs 8948 and the comm-path shards of 4096 / 2048 / 1024 rows
 // 3543 / 6756 / 9748 vs 3623 / 6884 / 11162. GLX_SPLIT_CAND=1 forces it at any size (tests).
+// Round 5 (the bitmap gather: no lists kernel, ~5 us fixed): ProxGD at l = 32 takes it from
+// 64 MiB of A on this rank. Measured against the dense batch (profiles/r5_e/, profiles/r5_f/;
+// 200-step windows / whole solves): (4096, 16384, 32) 4844 / 4894 vs 3987 / 4069 it/s; the
+// communicator-path shards of 1024 / 2048 / 4096 rows 12114 / 8016 / 4759 vs 11122 / 6931 / 3915
+// (whole solves at 1024 / 4096 rows 12082 / 4848 vs 11226 / 4015). C2 (l = 16, A in the Infinity
+// Cache, where At would evict it) stays dense: 8411 / 8205 vs 9127 / 9151; FProxGD's shards too
+// (whole solves 10480 / 3943 vs 10847 / 4000: e_c fills late in a solve).
+static constexpr double kSplitMinBytesL32 = 64.0 * 1024 * 1024;
 static constexpr double kSplitMinBytes = 768.0 * 1024 * 1024;
 static int split_mode(const glx_problem& P, const glx_opts& O) {
   if (O.exact_objective != 0) return 0;
@@ -172,7 +180,8 @@ static int split_mode(const glx_problem& P, const glx_opts& O) {
   const char* sc = O.split_cand == 0 ? std::getenv("GLX_SPLIT_CAND") : nullptr;
   if (sc && std::strcmp(sc, "0") == 0) return 0;
   const bool force = O.split_cand == 1 || (sc && std::strcmp(sc, "1") == 0);
-  if (!force && (double)P.m * (double)P.n * 8.0 < kSplitMinBytes) return 0;
+  const double gate = (P.method == GLX_PROXGD && P.l == 32) ? kSplitMinBytesL32 : kSplitMinBytes;
+  if (!force && (double)P.m * (double)P.n * 8.0 < gate) return 0;
   if (P.method == GLX_FPROXGD) {
     const char* sf = std::getenv("GLX_SPLIT_FISTA");
     if (sf && std::strcmp(sf, "0") == 0) return 0;

@@ -111,8 +111,8 @@ def test_workspace_planning_host_only():
             # split-candidate trials (m n * 8 B of 768 MiB or more; fp32: FProxGD only, round 5
             # default) keep a transposed copy of A (kernels_gather.hip); FProxGD's also e_c and
             # three A thr(x) residual-sized slots
-            split = (dt == 1 or meth == _lib.GLX_FPROXGD) and l in (16, 32) and \
-                m * n * 8 >= 768 * 2**20   # kSplitMinBytes
+            gate = (64 if meth == _lib.GLX_PROXGD and l == 32 else 768) * 2**20   # kSplitMinBytes*
+            split = (dt == 1 or meth == _lib.GLX_FPROXGD) and l in (16, 32) and m * n * 8 >= gate
             at = es * m * n if split else 0
             extra = es * (n * l + 3 * m * l) if (split and meth == _lib.GLX_FPROXGD) else 0
             assert nb.value >= es * (2 * n * l + 2 * m * l) + at + extra  # x-buffers + residuals at least
