@@ -297,7 +297,7 @@ void resgrad_reset(void* ws, int64_t m, int64_t n, hipStream_t st);
 // ---- the trial's batch + the next gradient in one pass, l = 16 (kernels_rg2.hip, round 4) ----
 // P0 = A X0, P1 = A X1 (one m x 16 slab each), Gs[RG][n][16] with G = A^T (P1 - B) = the sum of the
 // RG slabs in order. resgrad2_shape_ok: fp64, l = 16, n = 256 P (P a power of two in 2..128),
-// m % (16 RG) == 0, m / RG >= 32 (RG = 256 / P). Plain launch of 256 workgroups that wait for each
+// m % (16 kRAB RG) == 0 (kRAB = 4 A-tiles per hand-off: 64 * 256 / P), m / RG >= 32 (RG = 256 / P). Plain launch of 256 workgroups that wait for each
 // other with bounded spins (*err = 1 on a timeout: outputs invalid); resgrad2_device_ok checks
 // that all of them can be resident. ws: resgrad2_ws_bytes, zeroed (resgrad2_reset) before
 // launch_count 1; launch_count grows by one per launch on the same workspace.

@@ -428,17 +428,25 @@ int resgrad_groups(int64_t n) { return (int)(kFGrid / (n / kFPanel)); }
 
 // every workgroup of the launch must be resident at once: kFPerCU per CU on >= 256 CUs
 bool resgrad_device_ok() {
-  static int ok = -1;
-  if (ok < 0) {
-    int dev = 0, cus = 0, occ = 0;
-    ok = 0;
-    if (hipGetDevice(&dev) == hipSuccess &&
-        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess &&
+  // per device (one process-wide answer was taken from whichever device was
+  // current at the first call)
+  static int ok[64];
+  static bool init = false;
+  if (!init) {
+    for (int& v : ok) v = -1;
+    init = true;
+  }
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return false;
+  if (ok[dev] < 0) {
+    int cus = 0, occ = 0;
+    ok[dev] = 0;
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess &&
         hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, reinterpret_cast<const void*>(k_resgrad<true>),
                                                      kFThreads, 0) == hipSuccess)
-      ok = (cus * kFPerCU >= kFGrid && occ >= kFPerCU) ? 1 : 0;
+      ok[dev] = (cus * kFPerCU >= kFGrid && occ >= kFPerCU) ? 1 : 0;
   }
-  return ok == 1;
+  return ok[dev] == 1;
 }
 
 size_t resgrad_ws_bytes(int64_t m, int64_t n) { return rg_layout(m, n).total; }

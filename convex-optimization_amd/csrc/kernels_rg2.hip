@@ -405,17 +405,25 @@ bool resgrad2_shape_ok(int esize, int64_t m, int64_t n, int64_t l) {
 int resgrad2_groups(int64_t n) { return (int)(kRGrid / (n / kRPanel)); }
 
 bool resgrad2_device_ok() {
-  static int ok = -1;
-  if (ok < 0) {
-    int dev = 0, cus = 0, occ = 0;
-    ok = 0;
-    if (hipGetDevice(&dev) == hipSuccess &&
-        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess &&
+  // per device (one process-wide answer was taken from whichever device was
+  // current at the first call)
+  static int ok[64];
+  static bool init = false;
+  if (!init) {
+    for (int& v : ok) v = -1;
+    init = true;
+  }
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return false;
+  if (ok[dev] < 0) {
+    int cus = 0, occ = 0;
+    ok[dev] = 0;
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess &&
         hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, reinterpret_cast<const void*>(k_resgrad2<2, 4, true>),
                                                      kRThreads, 0) == hipSuccess)
-      ok = (cus >= kRGrid && occ >= 1) ? 1 : 0;
+      ok[dev] = (cus >= kRGrid && occ >= 1) ? 1 : 0;
   }
-  return ok == 1;
+  return ok[dev] == 1;
 }
 
 size_t resgrad2_ws_bytes(int64_t n) { return rg2_layout(n).total; }
