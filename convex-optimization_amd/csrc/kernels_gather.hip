@@ -240,7 +240,10 @@ __global__ __launch_bounds__(kGThreads) void k_at_gather2(const T* __restrict__ 
 // workgroups ran alone on the chip). counts[c] (rb == 0) = the list length (FProxGD's budget).
 // U: At loads in flight per thread; SEGW: bitmap words per segment (64 SEGW rows, its list in
 // 128 SEGW bytes of LDS; 128: twice the workgroups per CU). Neither changes the summation order.
-template <typename T, int L, bool NT, int U, int SEGW>
+// VEC: each thread owns E = 16 / sizeof(T) consecutive output rows and reads them with one 16-B
+// load per list entry (1 KiB per wave-instruction instead of 512 B; 8-B loads stream at ~0.54-0.70
+// of the 16-B rate, MI355X_MICROARCH.md), each row's sum in the same order (needs m % E == 0).
+template <typename T, int L, bool NT, int U, int SEGW, bool VEC = false>
 __global__ __launch_bounds__(kGThreads) void k_at_gather_bm(const T* __restrict__ At,
                                                             const T* __restrict__ E,
                                                             unsigned* __restrict__ zf, int64_t m,
@@ -256,9 +259,23 @@ __global__ __launch_bounds__(kGThreads) void k_at_gather_bm(const T* __restrict_
   const int rb = (int)blockIdx.x % gx, c = (int)blockIdx.x / gx;
   const int64_t nw = zf_npad(n) / 64;
   const uint64_t* words = reinterpret_cast<const uint64_t*>(zf_bitmaps(zf, n) + (int64_t)c * (zf_npad(n) / 16));
-  const int64_t r = (int64_t)rb * kGThreads + tid;
-  const int64_t rr = r < m ? r : m - 1;
-  T acc = T(0);
+  typedef typename MF<T>::vec_t V;
+  constexpr int RW = VEC ? MF<T>::E : 1;   // output rows per thread
+  const int64_t r = ((int64_t)rb * kGThreads + tid) * RW;
+  const int64_t rr = r < m ? r : m - RW;
+  T acc[RW];
+#pragma unroll
+  for (int j = 0; j < RW; ++j) acc[j] = T(0);
+  auto ldat = [&](int64_t k, T (&a)[RW]) {
+    if constexpr (VEC) {
+      const V* ap = reinterpret_cast<const V*>(At + k * m + rr);
+      const V v = NT ? __builtin_nontemporal_load(ap) : *ap;
+#pragma unroll
+      for (int j = 0; j < RW; ++j) a[j] = v[j];
+    } else {
+      a[0] = NT ? __builtin_nontemporal_load(At + k * m + rr) : At[k * m + rr];
+    }
+  };
   unsigned all = 0;
   for (int64_t w0 = 0; w0 < nw; w0 += SEGW) {
     const int64_t w = w0 + tid;
@@ -288,24 +305,32 @@ __global__ __launch_bounds__(kGThreads) void k_at_gather_bm(const T* __restrict_
     const int64_t kb = w0 * 64;
     int idx = 0;
     for (; idx + U <= tot; idx += U) {
-      T a[U], ev[U];
+      T a[U][RW], ev[U];
 #pragma unroll
       for (int u = 0; u < U; ++u) {
         const int64_t k = kb + lst[idx + u];
-        a[u] = NT ? __builtin_nontemporal_load(At + k * m + rr) : At[k * m + rr];
+        ldat(k, a[u]);
         ev[u] = E[k * L + c];
       }
 #pragma unroll
-      for (int u = 0; u < U; ++u) acc = acc + a[u] * ev[u];
+      for (int u = 0; u < U; ++u)
+#pragma unroll
+        for (int j = 0; j < RW; ++j) acc[j] = acc[j] + a[u][j] * ev[u];
     }
     for (; idx < tot; ++idx) {
       const int64_t k = kb + lst[idx];
-      acc = acc + (NT ? __builtin_nontemporal_load(At + k * m + rr) : At[k * m + rr]) * E[k * L + c];
+      T a[RW];
+      ldat(k, a);
+      const T ev = E[k * L + c];
+#pragma unroll
+      for (int j = 0; j < RW; ++j) acc[j] = acc[j] + a[j] * ev;
     }
     all += total;
     __syncthreads();   // lst and wsum are rewritten by the next segment
   }
-  if (r < m) P[r * L + c] = acc;
+#pragma unroll
+  for (int j = 0; j < RW; ++j)
+    if (r + j < m) P[(r + j) * L + c] = acc[j];
   if (rb == 0 && tid == 0) counts[c] = all;
 }
 
@@ -598,14 +623,22 @@ void launch_at_gather(const T* At, const T* E, int64_t m, int64_t n, int64_t l, 
 
 // A e by the column bitmaps the trial kernels wrote behind zf (k_at_gather_bm): ONE slab at P,
 // the column list lengths into the counts area of lists_ws (gather_counts). GLX_GATHER_BM =
-// "U,SEGW" selects the loads in flight and the segment (8,256 default; 16 / 128 the variants).
+// "U,SEGW,VEC" selects the loads in flight, the segment and the 16-B row form (8,256,0 default).
 template <typename T, int L, bool NT>
-static void at_gather_bm_go(int code, dim3 g, hipStream_t st, const T* At, const T* E, unsigned* zf,
-                            int64_t m, int64_t n, T* P, unsigned* cnt, int gx, const int* skip) {
-  switch (code) {
-    case 16256: glx_launch(k_at_gather_bm<T, L, NT, 16, 256>, g, dim3(kGThreads), 0, st, At, E, zf, m, n, P, cnt, gx, skip); break;
-    case 8128: glx_launch(k_at_gather_bm<T, L, NT, 8, 128>, g, dim3(kGThreads), 0, st, At, E, zf, m, n, P, cnt, gx, skip); break;
-    case 16128: glx_launch(k_at_gather_bm<T, L, NT, 16, 128>, g, dim3(kGThreads), 0, st, At, E, zf, m, n, P, cnt, gx, skip); break;
+static void at_gather_bm_go(int code, int64_t m, hipStream_t st, const T* At, const T* E, unsigned* zf,
+                            int64_t n, int64_t l, T* P, unsigned* cnt, const int* skip) {
+  const bool vec = (code % 10) == 1 && m % MF<T>::E == 0;
+  const int rpb = kGThreads * (vec ? MF<T>::E : 1);   // output rows per workgroup
+  const int gx = (int)((m + rpb - 1) / rpb);
+  const dim3 g((unsigned)(gx * l));
+  switch (vec ? code : code / 10 * 10) {
+    case 162560: glx_launch(k_at_gather_bm<T, L, NT, 16, 256>, g, dim3(kGThreads), 0, st, At, E, zf, m, n, P, cnt, gx, skip); break;
+    case 81280: glx_launch(k_at_gather_bm<T, L, NT, 8, 128>, g, dim3(kGThreads), 0, st, At, E, zf, m, n, P, cnt, gx, skip); break;
+    case 161280: glx_launch(k_at_gather_bm<T, L, NT, 16, 128>, g, dim3(kGThreads), 0, st, At, E, zf, m, n, P, cnt, gx, skip); break;
+    case 82561: glx_launch(k_at_gather_bm<T, L, NT, 8, 256, true>, g, dim3(kGThreads), 0, st, At, E, zf, m, n, P, cnt, gx, skip); break;
+    case 162561: glx_launch(k_at_gather_bm<T, L, NT, 16, 256, true>, g, dim3(kGThreads), 0, st, At, E, zf, m, n, P, cnt, gx, skip); break;
+    case 81281: glx_launch(k_at_gather_bm<T, L, NT, 8, 128, true>, g, dim3(kGThreads), 0, st, At, E, zf, m, n, P, cnt, gx, skip); break;
+    case 161281: glx_launch(k_at_gather_bm<T, L, NT, 16, 128, true>, g, dim3(kGThreads), 0, st, At, E, zf, m, n, P, cnt, gx, skip); break;
     default: glx_launch(k_at_gather_bm<T, L, NT, 8, 256>, g, dim3(kGThreads), 0, st, At, E, zf, m, n, P, cnt, gx, skip); break;
   }
 }
@@ -619,19 +652,17 @@ void launch_at_gather_bm(const T* At, const T* E, unsigned* zf, int64_t m, int64
   }();
   const int code = [] {   // read per launch (tests switch it within one process)
     const char* e = std::getenv("GLX_GATHER_BM");
-    int u = 8, w = 256;
-    if (e) std::sscanf(e, "%d,%d", &u, &w);
-    return (u == 16 ? 16 : 8) * 1000 + (w == 128 ? 128 : 256);
+    int u = 8, w = 256, v = 0;
+    if (e) std::sscanf(e, "%d,%d,%d", &u, &w, &v);
+    return ((u == 16 ? 16 : 8) * 1000 + (w == 128 ? 128 : 256)) * 10 + (v == 1 ? 1 : 0);
   }();
-  const int gx = (int)((m + kGThreads - 1) / kGThreads);
-  const dim3 g((unsigned)(gx * l));
   unsigned* cnt = list_counts(lists_ws, n);
   if (l == 32) {
-    if (nt) at_gather_bm_go<T, 32, true>(code, g, st, At, E, zf, m, n, P, cnt, gx, skip);
-    else at_gather_bm_go<T, 32, false>(code, g, st, At, E, zf, m, n, P, cnt, gx, skip);
+    if (nt) at_gather_bm_go<T, 32, true>(code, m, st, At, E, zf, n, l, P, cnt, skip);
+    else at_gather_bm_go<T, 32, false>(code, m, st, At, E, zf, n, l, P, cnt, skip);
   } else {
-    if (nt) at_gather_bm_go<T, 16, true>(code, g, st, At, E, zf, m, n, P, cnt, gx, skip);
-    else at_gather_bm_go<T, 16, false>(code, g, st, At, E, zf, m, n, P, cnt, gx, skip);
+    if (nt) at_gather_bm_go<T, 16, true>(code, m, st, At, E, zf, n, l, P, cnt, skip);
+    else at_gather_bm_go<T, 16, false>(code, m, st, At, E, zf, n, l, P, cnt, skip);
   }
 }
 void launch_zf_bitmaps(unsigned* zf, int64_t n, int64_t l, hipStream_t st) {

@@ -48,7 +48,7 @@ def main():
     for name in fetch:
         short = ("ax" if ("k_ax_" in name or "k_gemv_" in name) else
                  ("atr" if "k_atr_" in name else
-                  ("gather" if ("k_at_gather" in name or "k_e_lists" in name) else None)))
+                  ("gather" if ("k_at_gather" in name or "k_e_lists" in name or "k_at_rows" in name) else None)))
         if short is None:
             continue
         f = sum(fetch[name]) / len(fetch[name])

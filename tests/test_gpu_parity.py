@@ -295,16 +295,21 @@ def test_full_size_long_trajectory_vs_oracle(solver, alpha_scale):
 
 @pytest.mark.parametrize("name", ["mid_512x1024x16_f64_gl_ProxGD_primal", "mid_256x512x32_f64_gl_FProxGD_primal"])
 def test_split_candidate_gather_waves_bit_identical(name, monkeypatch):
-    """The A e gather's workgroup size (GLX_GATHER_WAVES 1 / 2 / 4) and its two-rows-per-thread
-    form (GLX_GATHER_VEC, round 4) change only which thread computes an output row, not its
-    summation order: results are bit-identical."""
+    """The A e gathers walk every column's ascending list in the same order whatever the form:
+    round 2's lists kernel + gather (GLX_GATHER=lists, with 1 / 2 / 4-wave workgroups and its
+    two-rows-per-thread variant) and round 5's bitmap gather (GLX_GATHER=bm, its loads-in-flight /
+    segment / 16-B variants) give bit-identical trajectories."""
     monkeypatch.setenv("GLX_SPLIT_CAND", "1")
     meta, gold = golden_case(name)
     A, b, u, x0, mu = golden_inputs(meta)
     runs = []
-    for w, vec in (("4", "0"), ("2", "0"), ("1", "0"), ("4", "1")):
+    for form, w, vec, bm in (("lists", "4", "0", ""), ("lists", "2", "0", ""), ("lists", "1", "0", ""),
+                             ("lists", "4", "1", ""), ("bm", "4", "0", "8,256,0"),
+                             ("bm", "4", "0", "16,128,0"), ("bm", "4", "0", "8,256,1")):
+        monkeypatch.setenv("GLX_GATHER", form)
         monkeypatch.setenv("GLX_GATHER_WAVES", w)
         monkeypatch.setenv("GLX_GATHER_VEC", vec)   # (round 4) two rows per thread, 16-B loads
+        monkeypatch.setenv("GLX_GATHER_BM", bm)
         x, k, out = _solve(meta, A, b, x0, mu)
         runs.append((x, k, [float(v) for v in out["f_hist"]]))
     for x, k, fh in runs[1:]:

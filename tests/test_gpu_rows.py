@@ -94,3 +94,17 @@ def test_row_form_needs_whole_panels():
     for form in (1, 2):   # the gathers take any m
         Y = kernels.flagged_rows_product(At, E, masks, form=form).cpu()
         assert (Y - ref).abs().max().item() <= 1e-12
+
+
+@pytest.mark.parametrize("variant", ["16,256,0", "8,128,0", "16,128,0", "8,256,1", "16,256,1", "8,128,1"])
+def test_bitmap_gather_variants_bit_identical(variant, monkeypatch):
+    """GLX_GATHER_BM = loads in flight, bitmap words per segment, 16-B row form: none changes a
+    row's summation order, so every variant equals the default bit for bit (fp64 and fp32)."""
+    from glx import kernels
+    for dtype in (torch.float64, torch.float32):
+        At, E, masks, ref, _ = _case(4096, 16384, 32, 0.2, dtype, seed=17)
+        monkeypatch.delenv("GLX_GATHER_BM", raising=False)
+        Y0 = kernels.flagged_rows_product(At, E, masks, form=2)
+        monkeypatch.setenv("GLX_GATHER_BM", variant)
+        Y1 = kernels.flagged_rows_product(At, E, masks, form=2)
+        assert torch.equal(Y0, Y1), (variant, dtype)
