@@ -272,14 +272,17 @@ __host__ __device__ inline int64_t zf_npad(int64_t n) { return (n + 63) / 64 * 6
 __device__ inline unsigned short* zf_bitmaps(unsigned* zf, int64_t n) {
   return reinterpret_cast<unsigned short*>(zf + zf_npad(n));
 }
-// A 64-row panel [col0, col0 + 64) of masks, held one per row in the LDS array msk (all of the
-// workgroup's waves wrote theirs and passed a barrier): wave 0 transposes it with one ballot per
-// column and lane c < l stores column c's u64 word. Called by the whole workgroup.
+// A PW-row panel [col0, col0 + PW) of masks (PW = 64, or 32 for the narrow A^T R panel), held
+// one per row in the LDS array msk (all of the workgroup's waves wrote theirs and passed a
+// barrier): wave 0 transposes it with one ballot per column and lane c < l stores column c's
+// u64 (u32) word. Called by the whole workgroup.
+template <int PW = 64>
 __device__ inline void zf_store_panel(const unsigned* msk, unsigned* zf, int64_t n, int l,
                                       int64_t col0) {
+  static_assert(PW == 64 || PW == 32, "64- or 32-row panels");
   if ((threadIdx.x >> 6) != 0) return;
   const int lane = threadIdx.x & 63;
-  const unsigned v = msk[lane];
+  const unsigned v = lane < PW ? msk[lane] : 0u;
   uint64_t mine = 0;
 #pragma unroll
   for (int c = 0; c < 32; ++c) {
@@ -287,8 +290,9 @@ __device__ inline void zf_store_panel(const unsigned* msk, unsigned* zf, int64_t
     if (lane == c) mine = b;
   }
   if (lane < l) {
-    uint64_t* w = reinterpret_cast<uint64_t*>(zf_bitmaps(zf, n) + (int64_t)lane * (zf_npad(n) / 16));
-    w[col0 / 64] = mine;
+    unsigned short* col = zf_bitmaps(zf, n) + (int64_t)lane * (zf_npad(n) / 16);
+    if constexpr (PW == 64) reinterpret_cast<uint64_t*>(col)[col0 / 64] = mine;
+    else reinterpret_cast<unsigned*>(col)[col0 / 32] = (unsigned)mine;
   }
 }
 // The row kernels' form (16 lanes per row, so a 256-thread workgroup holds the 16 rows of one

@@ -18,7 +18,9 @@ namespace glx {
 //   WL = 1: a block = four adjacent panels (256 columns) sharing one row range, so the four
 //           waves read the same R fragments (L1 hits) and write their slabs directly;
 //   WL = 2: as WL 0 with eight waves (512 threads, two waves per SIMD): the block's rows split
-//           eight ways, waves 4..7 folded into 0..3 through LDS first (round 4).
+//           eight ways, waves 4..7 folded into 0..3 through LDS first (round 4);
+//   WL = 3: as WL 0 with a 32-column panel (f64; round 5): twice the panels, so a shape with
+//           n / 64 < 256 (C2: 128) fills the chip without K splits and their slab combine.
 // blockIdx.y = row split. Needs n % 64 == 0 (n % 256 for WL = 1), m % 4 == 0.
 // Gp[split][n][16*NT].
 // ------------------------------------------------------------------------------------------
@@ -33,6 +35,10 @@ namespace glx {
 // pass reads are loaded with the default policy, so that about that many MiB of A stay in the
 // 256 MiB Infinity Cache for the next pass over A (A@X) to hit.
 
+// panel width (columns of A = rows of G) of a wave layout, and its MFMA output groups e
+template <int WL> constexpr int atr_pw() { return WL == 3 ? 32 : 64; }
+template <int WL> constexpr int atr_ne() { return atr_pw<WL>() / 16; }
+
 template <typename T, int NT, int PF, int WL, bool NTL>
 __device__ inline int64_t atr_panel(const T* __restrict__ A, const T* __restrict__ R, int64_t m,
                                     int64_t n, int S, typename MF<T>::acc_t (&acc)[4][NT],
@@ -42,12 +48,14 @@ __device__ inline int64_t atr_panel(const T* __restrict__ A, const T* __restrict
   constexpr int L = 16 * NT;
   constexpr bool RW = WL != 1;   // the block's waves split the rows of one panel
   constexpr int NWV = WL == 2 ? 8 : 4;
+  constexpr int PW = atr_pw<WL>(), NE = atr_ne<WL>();
+  static_assert(WL != 3 || sizeof(T) == 8, "the 32-column panel is f64 (one 16-B load per row)");
   __shared__ C red[RW ? 4 : 1][RW ? 4 * NT : 1][64];   // [wave][e * NT + nt][lane]
 
   const int lane = threadIdx.x & 63;
   const int wave = threadIdx.x >> 6;
   const int i = lane & 15, q = lane >> 4;
-  const int64_t col0 = RW ? pbx * 64 : pbx * 256 + wave * 64;
+  const int64_t col0 = RW ? pbx * PW : pbx * 256 + wave * 64;
   const int64_t steps = m / 4;
   const int64_t W = RW ? (int64_t)S * NWV : (int64_t)S;
   const int64_t w = RW ? pby * NWV + wave : pby;
@@ -67,15 +75,24 @@ __device__ inline int64_t atr_panel(const T* __restrict__ A, const T* __restrict
   // makes the compiler drain vmcnt to 0 there). Lookahead = PF - 1 steps.
   const int64_t nst = se - sb;
   T a[PF][4], rb[PF][NT];
+  auto lda = [&](const T* p, T (&dst)[4], auto ntl) {
+    if constexpr (NE == 2) {   // columns 2i, 2i + 1 (atr_col for e < 2): one 16-B load
+      const typename M::vec_t v = load_vec<T, decltype(ntl)::value>(p);
+      dst[0] = v[0];
+      dst[1] = v[1];
+    } else {
+      Load4<T, decltype(ntl)::value>::go(p, dst);
+    }
+  };
   auto ld = [&](int p, int64_t off) {
     off = off < nst ? off : nst - 1;
-    Load4<T, NTL>::go(ap + off * 4 * n, a[p]);
+    lda(ap + off * 4 * n, a[p], std::integral_constant<bool, NTL>{});
 #pragma unroll
     for (int nt = 0; nt < NT; ++nt) rb[p][nt] = rp[off * 4 * L + nt * 16];
   };
   auto ld_def = [&](int p, int64_t off) {   // default policy (the Infinity-Cache hand-off)
     off = off < nst ? off : nst - 1;
-    Load4<T, false>::go(ap + off * 4 * n, a[p]);
+    lda(ap + off * 4 * n, a[p], std::integral_constant<bool, false>{});
 #pragma unroll
     for (int nt = 0; nt < NT; ++nt) rb[p][nt] = rp[off * 4 * L + nt * 16];
   };
@@ -84,12 +101,12 @@ __device__ inline int64_t atr_panel(const T* __restrict__ A, const T* __restrict
   int64_t keep = 0;
   if constexpr (NTL) {
     const int64_t kb = (int64_t)keep_mib << 20;
-    keep = kb / ((int64_t)(RW ? W * (n / 64) : W * (n / 256)) * 4 * (RW ? 64 : 256) * (int64_t)sizeof(T));
+    keep = kb / ((int64_t)(RW ? W * (n / PW) : W * (n / 256)) * 4 * (RW ? PW : 256) * (int64_t)sizeof(T));
   }
   const int64_t kt = nst - keep;
   auto mma_step = [&](int p) {
 #pragma unroll
-    for (int e = 0; e < 4; ++e)
+    for (int e = 0; e < NE; ++e)
 #pragma unroll
       for (int nt = 0; nt < NT; ++nt) acc[e][nt] = M::mma(a[p][e], rb[p][nt], acc[e][nt]);
   };
@@ -144,19 +161,19 @@ __device__ inline int64_t atr_panel(const T* __restrict__ A, const T* __restrict
   if (RW) {
     if (wave < 4) {
 #pragma unroll
-      for (int e = 0; e < 4; ++e)
+      for (int e = 0; e < NE; ++e)
 #pragma unroll
         for (int nt = 0; nt < NT; ++nt) red[wave][e * NT + nt][lane] = acc[e][nt];
     }
     __syncthreads();
-    if (wave < 4) {   // (WL 2: waves 4..7 hold no rows from here on)
+    if (wave < NE) {   // (WL 2: waves 4..7 hold no rows from here on; WL 3: waves 2, 3)
 #pragma unroll
       for (int nt = 0; nt < NT; ++nt) {
         C v = red[0][wave * NT + nt][lane];
 #pragma unroll
         for (int s = 1; s < 4; ++s) v += red[s][wave * NT + nt][lane];
 #pragma unroll
-        for (int e = 0; e < 4; ++e)
+        for (int e = 0; e < NE; ++e)
           if (e == wave) acc[e][nt] = v;   // static register index; e == wave selects one
       }
     }
@@ -260,8 +277,8 @@ __global__ __launch_bounds__(WL == 2 ? 512 : 256) void k_atr_mfma(const T* __res
   const int64_t col0 = atr_panel<T, NT, PF, WL, NTL>(A, R, m, n, S, acc, blockIdx.x, blockIdx.y, keep_mib);
   T* gout = Gp + (int64_t)blockIdx.y * n * L;
 #pragma unroll
-  for (int e = 0; e < 4; ++e) {
-    if (WL != 1 && e != wave) continue;   // WL 0 / 2: wave w < 4 owns the rows e == w
+  for (int e = 0; e < atr_ne<WL>(); ++e) {
+    if (WL != 1 && e != wave) continue;   // WL 0 / 2 / 3: wave w < NE owns the rows e == w
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       const int64_t grow = col0 + atr_col<T>(M::row(lane, r), e);
@@ -277,7 +294,7 @@ __global__ __launch_bounds__(WL == 2 ? 512 : 256) void k_atr_mfma(const T* __res
 // wave writes its rows of G and runs the trial on them (prox_pgd_row, the same arithmetic as
 // k_prox_pgd) with x = the thresholded iterate; the six trial sums are reduced over the grid.
 template <typename T, int NT, int PF, bool NTL, bool SPLIT, int WL>
-__global__ __launch_bounds__(WL == 2 ? 512 : 256, (WL == 0 && sizeof(T) == 8) ? 2 : 1) void k_atr_prox(const T* __restrict__ A, const T* __restrict__ R,
+__global__ __launch_bounds__(WL == 2 ? 512 : 256, ((WL == 0 || WL == 3) && sizeof(T) == 8) ? 2 : 1) void k_atr_prox(const T* __restrict__ A, const T* __restrict__ R,
                                                   T* __restrict__ G, int64_t m, int64_t n,
                                                   const T* __restrict__ x, T* __restrict__ p,
                                                   T* __restrict__ pthr, T* __restrict__ z,
@@ -317,7 +334,7 @@ __global__ __launch_bounds__(WL == 2 ? 512 : 256, (WL == 0 && sizeof(T) == 8) ? 
   GLX_CLK(4);
   T xa[4][NT];
 #pragma unroll
-  for (int e = 0; e < 4; ++e) {
+  for (int e = 0; e < atr_ne<WL>(); ++e) {
     if (e != wave) continue;   // wave w owns the rows e == w (4 per lane group)
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
@@ -335,7 +352,7 @@ __global__ __launch_bounds__(WL == 2 ? 512 : 256, (WL == 0 && sizeof(T) == 8) ? 
   T gs[4][NT], ps[4][NT], pts[4][NT], zs[4][NT];
   unsigned rows_e[4] = {0u, 0u, 0u, 0u};
 #pragma unroll
-  for (int e = 0; e < 4; ++e) {
+  for (int e = 0; e < atr_ne<WL>(); ++e) {
     if (e != wave) continue;
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
@@ -353,7 +370,7 @@ __global__ __launch_bounds__(WL == 2 ? 512 : 256, (WL == 0 && sizeof(T) == 8) ? 
   grid_reduce<6, 0x8u, NW>(accr, red, slot, nparts);
   __shared__ unsigned msk[64];   // the panel's row masks of e (column bitmaps, zf_store_panel)
 #pragma unroll
-  for (int e = 0; e < 4; ++e) {
+  for (int e = 0; e < atr_ne<WL>(); ++e) {
     if (e != wave) continue;
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
@@ -373,7 +390,7 @@ __global__ __launch_bounds__(WL == 2 ? 512 : 256, (WL == 0 && sizeof(T) == 8) ? 
   }
   if (zf != nullptr) {
     __syncthreads();
-    zf_store_panel(msk, zf, n, L, col0);
+    zf_store_panel<atr_pw<WL>()>(msk, zf, n, L, col0);
   }
   GLX_CLK(3);
 }
@@ -382,7 +399,7 @@ __global__ __launch_bounds__(WL == 2 ? 512 : 256, (WL == 0 && sizeof(T) == 8) ? 
 // fista_row (the arithmetic of k_fista_trial) on its 16 gradient rows, with y the extrapolated
 // point and xk the current iterate; writes G, xc, v_next, y_next and reduces the four sums.
 template <typename T, int NT, int PF, bool NTL, bool SPLIT, int WL>
-__global__ __launch_bounds__(WL == 2 ? 512 : 256, (WL == 0 && sizeof(T) == 8) ? 2 : 1) void k_atr_fista(const T* __restrict__ A, const T* __restrict__ R,
+__global__ __launch_bounds__(WL == 2 ? 512 : 256, ((WL == 0 || WL == 3) && sizeof(T) == 8) ? 2 : 1) void k_atr_fista(const T* __restrict__ A, const T* __restrict__ R,
                                                    T* __restrict__ G, int64_t m, int64_t n,
                                                    const T* __restrict__ y, const T* __restrict__ xk,
                                                    T* __restrict__ xc, T* __restrict__ vnext,
@@ -417,7 +434,7 @@ __global__ __launch_bounds__(WL == 2 ? 512 : 256, (WL == 0 && sizeof(T) == 8) ? 
   const T t = (T)t_, tmu = (T)tmu_, thres = (T)thres_, theta = (T)theta_, a1 = (T)a1_, b1 = (T)b1_;
   __shared__ unsigned msk[64];   // the panel's row masks of e_c (column bitmaps, zf_store_panel)
 #pragma unroll
-  for (int e = 0; e < 4; ++e) {
+  for (int e = 0; e < atr_ne<WL>(); ++e) {
     if (e != wave) continue;   // wave w owns the rows e == w
     T ya[4][NT], xa[4][NT];
 #pragma unroll
@@ -459,7 +476,7 @@ __global__ __launch_bounds__(WL == 2 ? 512 : 256, (WL == 0 && sizeof(T) == 8) ? 
   grid_reduce<4, 0x8u, NW>(accr, red, slot, nparts);
   if (zf != nullptr) {   // (grid_reduce's barriers ordered the msk stores above)
     __syncthreads();
-    zf_store_panel(msk, zf, n, L, col0);
+    zf_store_panel<atr_pw<WL>()>(msk, zf, n, L, col0);
   }
 }
 
@@ -533,7 +550,7 @@ static void atr_valu_lb(const GemmPlan& p, const T* A, const T* R, T* Gp, hipStr
 
 template <typename T, int NT, int PF, int WL, bool NTL>
 static void atr_mfma_go(const GemmPlan& p, const T* A, const T* R, T* Gp, hipStream_t st) {
-  const dim3 grid((unsigned)(p.n / (WL == 1 ? 256 : 64)), (unsigned)p.atr_S);
+  const dim3 grid((unsigned)(p.n / (WL == 1 ? 256 : atr_pw<WL>())), (unsigned)p.atr_S);
   static const size_t pad = lds_pad(k_atr_mfma<T, NT, PF, WL, NTL>, "GLX_ATR_LDS_PAD");
   glx_launch((k_atr_mfma<T, NT, PF, WL, NTL>), grid, dim3(WL == 2 ? 512 : 256), pad, st, A, R, Gp, p.m, p.n, p.atr_S,
              p.atr_keep_mib);
@@ -555,6 +572,14 @@ static void atr_mfma_nt(const GemmPlan& p, const T* A, const T* R, T* Gp, hipStr
     case 28: atr_mfma_go<T, NT, 8, 2, false>(p, A, R, Gp, st); break;
     case 124: atr_mfma_go<T, NT, 4, 2, true>(p, A, R, Gp, st); break;
     case 128: atr_mfma_go<T, NT, 8, 2, true>(p, A, R, Gp, st); break;
+    case 38:
+    case 138:
+      if constexpr (sizeof(T) == 8) {
+        if (p.atr_ntl) atr_mfma_go<T, NT, 8, 3, true>(p, A, R, Gp, st);
+        else atr_mfma_go<T, NT, 8, 3, false>(p, A, R, Gp, st);
+        break;
+      }
+      throw Error{GLX_E_INVALID, "A^T R: the 32-column panel is f64"};
     default: atr_mfma_go<T, NT, 2, 0, false>(p, A, R, Gp, st); break;
   }
 }
@@ -576,6 +601,9 @@ void launch_atr(const GemmPlan& p, const T* A, const T* R, T* Gp, hipStream_t st
 
 
 bool atr_prox_ok(const GemmPlan& p) {
+  if (p.atr_wl == 3)   // the 32-column panel: f64, no K splits (session_plan)
+    return p.atr_kind == 1 && p.esize == 8 && p.atr_S == 1 && (p.l == 16 || p.l == 32) &&
+           p.n % 32 == 0 && p.n / 32 < kMaxBlocks;
   return p.atr_kind == 1 && (p.atr_wl == 0 || p.atr_wl == 2) && p.atr_S >= 1 && p.atr_S <= 8 &&
          (p.l == 16 || p.l == 32) && p.n % 64 == 0 &&
          p.n / 64 < kMaxBlocks &&   // reducing slots (one per panel) + the publisher
@@ -586,9 +614,9 @@ template <typename T, int NT, int PF, bool NTL, int WL>
 static void atr_prox_go(const GemmPlan& p, const T* A, const T* R, T* G, const T* x, T* pp,
                         T* pthr, T* z, double t, double mu, double thres, Red red, hipStream_t st,
                         Pub pub, T* Gp, unsigned* pcnt, unsigned* zf) {
-  const dim3 grid((unsigned)(p.n / 64 * p.atr_S + (pub.host ? 1 : 0)));
+  const dim3 grid((unsigned)(p.n / atr_pw<WL>() * p.atr_S + (pub.host ? 1 : 0)));
   const dim3 block(WL == 2 ? 512 : 256);
-  if (p.atr_S > 1) {
+  if (WL != 3 && p.atr_S > 1) {
     glx_launch((k_atr_prox<T, NT, PF, NTL, true, WL>), grid, block, 0, st, A, R, G, p.m,
                        p.n, x, pp, pthr, z, t, t * mu, thres, red, pub, p.atr_S, Gp, pcnt, zf, p.atr_keep_mib);
     return;
@@ -609,6 +637,14 @@ static void atr_prox_nt(const GemmPlan& p, const T* A, const T* R, T* G, const T
     case 124: atr_prox_go<T, NT, 4, true, 2>(p, A, R, G, x, pp, pthr, z, t, mu, thres, red, st, pub, Gp, pcnt, zf); break;
     case 128: atr_prox_go<T, NT, 8, true, 2>(p, A, R, G, x, pp, pthr, z, t, mu, thres, red, st, pub, Gp, pcnt, zf); break;
     case 28: atr_prox_go<T, NT, 8, false, 2>(p, A, R, G, x, pp, pthr, z, t, mu, thres, red, st, pub, Gp, pcnt, zf); break;
+    case 38:
+    case 138:
+      if constexpr (sizeof(T) == 8) {
+        if (p.atr_ntl) atr_prox_go<T, NT, 8, true, 3>(p, A, R, G, x, pp, pthr, z, t, mu, thres, red, st, pub, Gp, pcnt, zf);
+        else atr_prox_go<T, NT, 8, false, 3>(p, A, R, G, x, pp, pthr, z, t, mu, thres, red, st, pub, Gp, pcnt, zf);
+        break;
+      }
+      throw Error{GLX_E_INVALID, "A^T R: the 32-column panel is f64"};
     default: atr_prox_go<T, NT, 8, false, 0>(p, A, R, G, x, pp, pthr, z, t, mu, thres, red, st, pub, Gp, pcnt, zf); break;
   }
 }
@@ -627,9 +663,9 @@ static void atr_fista_go(const GemmPlan& p, const T* A, const T* R, T* G, const 
                          T* xc, T* vn, T* yn, double t, double mu, double thres, double theta,
                          double theta_next, Red red, hipStream_t st, Pub pub, T* Gp, unsigned* pcnt,
                          T* ec, unsigned* zf) {
-  const dim3 grid((unsigned)(p.n / 64 * p.atr_S + (pub.host ? 1 : 0)));
+  const dim3 grid((unsigned)(p.n / atr_pw<WL>() * p.atr_S + (pub.host ? 1 : 0)));
   const dim3 block(WL == 2 ? 512 : 256);
-  if (p.atr_S > 1) {
+  if (WL != 3 && p.atr_S > 1) {
     glx_launch((k_atr_fista<T, NT, PF, NTL, true, WL>), grid, block, 0, st, A, R, G, p.m,
                        p.n, y, xk, xc, vn, yn, t, t * mu, thres, theta, 1.0 - theta_next,
                        theta_next, red, pub, p.atr_S, Gp, pcnt, ec, zf, p.atr_keep_mib);
@@ -652,6 +688,14 @@ static void atr_fista_nt(const GemmPlan& p, const T* A, const T* R, T* G, const 
     case 124: atr_fista_go<T, NT, 4, true, 2>(p, A, R, G, y, xk, xc, vn, yn, t, mu, thres, theta, theta_next, red, st, pub, Gp, pcnt, ec, zf); break;
     case 128: atr_fista_go<T, NT, 8, true, 2>(p, A, R, G, y, xk, xc, vn, yn, t, mu, thres, theta, theta_next, red, st, pub, Gp, pcnt, ec, zf); break;
     case 28: atr_fista_go<T, NT, 8, false, 2>(p, A, R, G, y, xk, xc, vn, yn, t, mu, thres, theta, theta_next, red, st, pub, Gp, pcnt, ec, zf); break;
+    case 38:
+    case 138:
+      if constexpr (sizeof(T) == 8) {
+        if (p.atr_ntl) atr_fista_go<T, NT, 8, true, 3>(p, A, R, G, y, xk, xc, vn, yn, t, mu, thres, theta, theta_next, red, st, pub, Gp, pcnt, ec, zf);
+        else atr_fista_go<T, NT, 8, false, 3>(p, A, R, G, y, xk, xc, vn, yn, t, mu, thres, theta, theta_next, red, st, pub, Gp, pcnt, ec, zf);
+        break;
+      }
+      throw Error{GLX_E_INVALID, "A^T R: the 32-column panel is f64"};
     default: atr_fista_go<T, NT, 8, false, 0>(p, A, R, G, y, xk, xc, vn, yn, t, mu, thres, theta, theta_next, red, st, pub, Gp, pcnt, ec, zf); break;
   }
 }

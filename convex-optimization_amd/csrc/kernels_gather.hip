@@ -623,7 +623,9 @@ void launch_at_gather(const T* At, const T* E, int64_t m, int64_t n, int64_t l, 
 
 // A e by the column bitmaps the trial kernels wrote behind zf (k_at_gather_bm): ONE slab at P,
 // the column list lengths into the counts area of lists_ws (gather_counts). GLX_GATHER_BM =
-// "U,SEGW,VEC" selects the loads in flight, the segment and the 16-B row form (8,256,0 default).
+// "U,SEGW,VEC" selects the loads in flight, the segment and the 16-B row form (default 8,256,1:
+// NS 200-step windows 42.2-42.4 against 44.7 us for 8-B loads, whole solves 2456-2458 against
+// 2433-2436 it/s, profiles/r5_h/; 16 loads in flight or 128-word segments measured slower).
 template <typename T, int L, bool NT>
 static void at_gather_bm_go(int code, int64_t m, hipStream_t st, const T* At, const T* E, unsigned* zf,
                             int64_t n, int64_t l, T* P, unsigned* cnt, const int* skip) {
@@ -652,8 +654,8 @@ void launch_at_gather_bm(const T* At, const T* E, unsigned* zf, int64_t m, int64
   }();
   const int code = [] {   // read per launch (tests switch it within one process)
     const char* e = std::getenv("GLX_GATHER_BM");
-    int u = 8, w = 256, v = 0;
-    if (e) std::sscanf(e, "%d,%d,%d", &u, &w, &v);
+    int u = 8, w = 256, v = 1;   // round 5: the 16-B row form (42.2-42.4 vs 44.7 us at NS)
+    if (e && *e) std::sscanf(e, "%d,%d,%d", &u, &w, &v);
     return ((u == 16 ? 16 : 8) * 1000 + (w == 128 ? 128 : 256)) * 10 + (v == 1 ? 1 : 0);
   }();
   unsigned* cnt = list_counts(lists_ws, n);

@@ -215,6 +215,21 @@ static GemmPlan session_plan(const glx_problem& P, const glx_opts& O) {
     }
     if (atr_prox_ok(f)) return f;   // only where the trial actually fuses (GLX_ATR_FUSE_SPLIT)
   }
+  // Round 5: fp64 with fewer than 256 64-column panels (C2: 128, planned as 2 K splits) takes
+  // the 32-column panel without K splits (WL 3): 256+ workgroups and no slab combine in front of
+  // the fused trial. GLX_ATR_NARROW=0: off.
+  if (es == 8 && P.comm == nullptr && trial_method && p.atr_kind == 1 && (P.l == 16 || P.l == 32) &&
+      P.n % 32 == 0 && P.n / 64 < 256 && P.n / 32 >= 256 && !std::getenv("GLX_ATR_VARIANT") &&
+      !std::getenv("GLX_ATR_S") && !std::getenv("GLX_FUSED_TRIAL")) {
+    const char* nw = std::getenv("GLX_ATR_NARROW");
+    if (!(nw && std::strcmp(nw, "0") == 0)) {
+      GemmPlan f = p;
+      f.atr_wl = 3;
+      f.atr_pf = 8;
+      f.atr_S = 1;
+      if (atr_prox_ok(f)) return f;
+    }
+  }
   return p;
 }
 

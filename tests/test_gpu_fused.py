@@ -154,3 +154,40 @@ def test_fused_trial_eight_wave_panel(monkeypatch, method, S):
     assert r_f["k"] == k_r
     f_g, f_r = np.asarray(r_f["f_hist"], dtype=float), np.asarray(out_r["f_hist"], dtype=float)
     assert np.max(np.abs(f_g - f_r) / np.abs(f_r)) < 1e-8
+
+
+# Round 5: the 32-column A^T R panel (WL 3, f64, one K split) in the fused kernels: the iterate is
+# bit-identical to the unfused path on the same tile and within the north-star bar of the oracle.
+@pytest.mark.parametrize("method", METHODS)
+def test_fused_trial_narrow_panel(monkeypatch, method):
+    from oracle import numpy_ref
+    from glx import _lib
+    monkeypatch.setenv("GLX_ATR_VARIANT", "1038")
+    monkeypatch.setenv("GLX_ATR_S", "1")
+    d = _lib.plan_describe(_lib.GLX_F64, *SHAPE)
+    assert "WL3" in d and "S=1" in d, d
+    A, b, x0, mu, alpha0 = _instance()
+    opts = {"alpha0": alpha0, "maxit": 25}
+    x_f, r_f = _run(monkeypatch, True, True, opts, method)
+    x_u, r_u = _run(monkeypatch, False, False, opts, method)
+    assert r_f["k"] == r_u["k"]
+    assert np.array_equal(x_f, x_u)
+    np.testing.assert_allclose(np.asarray(r_f["f_hist"]), np.asarray(r_u["f_hist"]), rtol=1e-13)
+    x_r, k_r, out_r = numpy_ref.SOLVERS[method](x0.copy(), A, b, mu, dict(opts))
+    assert r_f["k"] == k_r
+    f_g, f_r = np.asarray(r_f["f_hist"], dtype=float), np.asarray(out_r["f_hist"], dtype=float)
+    assert np.max(np.abs(f_g - f_r) / np.abs(f_r)) < 1e-8
+
+
+def test_session_plan_takes_narrow_panel_at_c2():
+    """C2's shape (4096, 8192, 16): 128 64-column panels, so the session plans 256 32-column
+    panels without K splits for the fused trial (GLX_ATR_NARROW=0: the 2-split 64-column form)."""
+    import glx
+    m, n, l = 4096, 8192, 16
+    A = torch.zeros(m, n, dtype=torch.float64, device="cuda")
+    b = torch.zeros(m, l, dtype=torch.float64, device="cuda")
+    x = torch.zeros(n, l, dtype=torch.float64, device="cuda")
+    s = glx.Session("gl_ProxGD_primal", x, A, b, 1e-2, {"alpha0": 1e-5})
+    d = s.describe()
+    s.close()
+    assert "atr=k_atr_mfma<WL3,PF8" in d and "S=1" in d and "+trial (k_atr_prox)" in d, d
