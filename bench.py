@@ -161,8 +161,8 @@ def reference_instance(method, dt, m, n, l, r0, r1, dtype, device, seed=97006855
 
 def vs_reference(info, k, fval, f_hist, dt):
     """The whole solve against the committed reference run of the same call (GOLDEN): the
-    north-star bar in fp64 (k identical, fval and every f_hist entry within 1e-8 relative), the
-    fp32 bar on fval (1e-6) in fp32."""
+    north-star bar in fp64 (k identical, fval and every f_hist entry within 1e-8 relative); in
+    fp32 the measured-band bar of the C3 test (fval within 2.5e-4, k within 0.5 %)."""
     g = info.get("golden")
     if g is None:
         return None
@@ -175,9 +175,10 @@ def vs_reference(info, k, fval, f_hist, dt):
     if dt == "f64":
         ok = k == kg and frel <= 1e-8 and fh_rel is not None and fh_rel <= 1e-8
         bar = "k identical, fval and every f_hist entry within 1e-8 relative (north star, fp64)"
-    else:
-        ok = frel <= 1e-6 and abs(k - kg) <= max(1, int(0.005 * kg))
-        bar = "fval within 1e-6 relative, k within 0.5 % (fp32)"
+    else:   # C3 stops at maxit unconverged: its fp32 objective scatters with the summation order
+        ok = frel <= 2.5e-4 and abs(k - kg) <= max(1, int(0.005 * kg))
+        bar = ("fval within 2.5e-4 relative, k within 0.5 % (fp32: the band of eleven summation "
+               "orders is 3e-7..9e-5, tests/test_gpu_ns_golden.py::test_whole_solve_c3_fp32)")
     return {"reference": "tests/golden/%s.npz (the reference's own run of this call)" % g["stem"],
             "k_ref": kg, "k": int(k), "fval_ref": fg, "fval_rel_diff": frel,
             "f_hist_max_rel_diff": fh_rel, "bar": bar, "within_bar": bool(ok)}
