@@ -550,7 +550,10 @@ def main():
             "config": {"workload": "%s %s (m,n,l)=(%d,%d,%d), mu0=1e-2, alpha0=1/(sqrt(m)+sqrt(n))^2"
                                    % (args.method, args.dtype, m, n, l, ),
                        "method": args.method, "m": m, "n": n, "l": l,
-                       "parallelism": ("row-shard x%d (%s all-reduce of A^T r)" % (world, "RCCL" if args.comm == "rccl" else "host-staged gloo, ranks sharing one GPU"))
+                       "parallelism": ("row-shard x%d (%s; %s)" % (
+                                           world, "RCCL" if args.comm == "rccl" else "host-staged gloo, ranks sharing one GPU",
+                                           "reduce-scatter of A^T r, trial on n/%d rows, all-gather of p" % world
+                                           if "rows=sharded" in plan else "all-reduce of A^T r"))
                                        if world > 1 else "single GPU",
                        "exact_objective": args.exact, "ax_variant": args.variant},
             "roofline": roof,

@@ -1,12 +1,15 @@
 // comm.cpp — RCCL (over xGMI) for the multi-GPU path.
 //
 // The reference has no distribution. Row-sharding A and b across G ranks makes the per-rank
-// work A_g x - b_g and A_g^T r_g; the only exchange per gradient is one sum all-reduce of the
-// n x l gradient (4 MiB at the north-star size) plus 8-byte all-reduces of the squared
-// residual norms the objective and the line-search tests need. x and every row-wise step are
-// replicated, and RCCL hands every rank identical sums, so all ranks take identical branches.
+// work A_g x - b_g and A_g^T r_g. Two schedules (solver.cpp): the all-reduce schedule sums the
+// n x l gradient on every rank (4 MiB at the north-star size) and replicates the row-wise step;
+// the row-sharded schedule (round 5) reduce-scatters the gradient, runs the prox / trial on this
+// rank's n / G rows and all-gathers the new iterate's rows with every rank's partial sums, which
+// each rank then combines in rank order. Either way every rank holds identical values, so all
+// ranks take identical branches.
 #include <rccl/rccl.h>
 
+#include <algorithm>
 #include <cstring>
 #include <string>
 
@@ -29,14 +32,7 @@ struct glx_comm {
 };
 
 namespace glx {
-void comm_allreduce(glx_comm* c, void* buf, int64_t count, int dtype, hipStream_t st) {
-  if (c->host_fn == nullptr) {
-    const ncclDataType_t t = dtype == GLX_F64 ? ncclFloat64 : ncclFloat32;
-    const ncclResult_t r = ncclAllReduce(buf, buf, (size_t)count, t, ncclSum, c->comm, st);
-    if (r != ncclSuccess) throw Error{GLX_E_RCCL, std::string("ncclAllReduce: ") + ncclGetErrorString(r)};
-    return;
-  }
-  const size_t bytes = (size_t)count * (dtype == GLX_F64 ? 8 : 4);
+static void stage_reserve(glx_comm* c, size_t bytes) {
   if (bytes > c->stage_bytes) {
     if (c->stage) (void)hipHostFree(c->stage);
     c->stage = nullptr;
@@ -45,6 +41,19 @@ void comm_allreduce(glx_comm* c, void* buf, int64_t count, int dtype, hipStream_
       throw Error{GLX_E_HIP, "host comm: hipHostMalloc failed"};
     c->stage_bytes = bytes;
   }
+}
+static void rccl_check(ncclResult_t r, const char* what) {
+  if (r != ncclSuccess) throw Error{GLX_E_RCCL, std::string(what) + ": " + ncclGetErrorString(r)};
+}
+static ncclDataType_t rccl_type(int dtype) { return dtype == GLX_F64 ? ncclFloat64 : ncclFloat32; }
+
+void comm_allreduce(glx_comm* c, void* buf, int64_t count, int dtype, hipStream_t st) {
+  if (c->host_fn == nullptr) {
+    rccl_check(ncclAllReduce(buf, buf, (size_t)count, rccl_type(dtype), ncclSum, c->comm, st), "ncclAllReduce");
+    return;
+  }
+  const size_t bytes = (size_t)count * (dtype == GLX_F64 ? 8 : 4);
+  stage_reserve(c, bytes);
   if (hipMemcpyAsync(c->stage, buf, bytes, hipMemcpyDeviceToHost, st) != hipSuccess ||
       hipStreamSynchronize(st) != hipSuccess)
     throw Error{GLX_E_HIP, "host comm: device-to-host staging failed"};
@@ -54,6 +63,59 @@ void comm_allreduce(glx_comm* c, void* buf, int64_t count, int dtype, hipStream_
       hipStreamSynchronize(st) != hipSuccess)   // the staging buffer is reused by the next call
     throw Error{GLX_E_HIP, "host comm: host-to-device staging failed"};
 }
+
+// In place: buf holds nranks chunks of `count` elements; chunk `rank` receives the sum of every
+// rank's chunk `rank` (the others are left undefined). Host transport: a full all-reduce.
+void comm_reduce_scatter(glx_comm* c, void* buf, int64_t count, int dtype, hipStream_t st) {
+  if (c->host_fn == nullptr) {
+    const size_t es = dtype == GLX_F64 ? 8 : 4;
+    void* own = static_cast<char*>(buf) + (size_t)c->rank * (size_t)count * es;
+    rccl_check(ncclReduceScatter(buf, own, (size_t)count, rccl_type(dtype), ncclSum, c->comm, st),
+               "ncclReduceScatter");
+    return;
+  }
+  comm_allreduce(c, buf, count * c->nranks, dtype, st);
+}
+
+// In place: chunk `rank` of buf (count elements) is sent, every chunk is received. Host
+// transport: the other chunks are filled with -0.0 and summed, which is exact (x + (-0) = x for
+// every x, +0 and -0 included), so the gathered bits are the senders' bits.
+void comm_all_gather(glx_comm* c, void* buf, int64_t count, int dtype, hipStream_t st) {
+  const size_t es = dtype == GLX_F64 ? 8 : 4;
+  char* own = static_cast<char*>(buf) + (size_t)c->rank * (size_t)count * es;
+  if (c->host_fn == nullptr) {
+    rccl_check(ncclAllGather(own, buf, (size_t)count, rccl_type(dtype), c->comm, st), "ncclAllGather");
+    return;
+  }
+  const size_t chunk = (size_t)count * es, bytes = chunk * (size_t)c->nranks;
+  stage_reserve(c, bytes);
+  if (hipMemcpyAsync(static_cast<char*>(c->stage) + (size_t)c->rank * chunk, own, chunk,
+                     hipMemcpyDeviceToHost, st) != hipSuccess ||
+      hipStreamSynchronize(st) != hipSuccess)
+    throw Error{GLX_E_HIP, "host comm: device-to-host staging failed"};
+  for (int r = 0; r < c->nranks; ++r) {
+    if (r == c->rank) continue;
+    char* p = static_cast<char*>(c->stage) + (size_t)r * chunk;
+    if (dtype == GLX_F64) std::fill_n(reinterpret_cast<double*>(p), count, -0.0);
+    else std::fill_n(reinterpret_cast<float*>(p), count, -0.0f);
+  }
+  const int rc = c->host_fn(c->stage, count * c->nranks, dtype, c->host_user);
+  if (rc != 0) throw Error{GLX_E_RCCL, "host comm: all-gather callback returned " + std::to_string(rc)};
+  if (hipMemcpyAsync(buf, c->stage, bytes, hipMemcpyHostToDevice, st) != hipSuccess ||
+      hipStreamSynchronize(st) != hipSuccess)
+    throw Error{GLX_E_HIP, "host comm: host-to-device staging failed"};
+}
+
+// RCCL group: the collectives issued in between go out as one launch (no-op for the host
+// transport, whose calls complete one by one)
+void comm_group_begin(glx_comm* c) {
+  if (c->host_fn == nullptr) rccl_check(ncclGroupStart(), "ncclGroupStart");
+}
+void comm_group_end(glx_comm* c) {
+  if (c->host_fn == nullptr) rccl_check(ncclGroupEnd(), "ncclGroupEnd");
+}
+int comm_rank(const glx_comm* c) { return c->rank; }
+int comm_size(const glx_comm* c) { return c->nranks; }
 }  // namespace glx
 
 extern "C" {
@@ -108,6 +170,26 @@ int glx_comm_create_host(glx_comm** out, int nranks, int rank, glx_host_allreduc
 int glx_comm_allreduce(glx_comm* c, void* buf, int64_t count, int dtype, void* stream) {
   try {
     glx::comm_allreduce(c, buf, count, dtype, static_cast<hipStream_t>(stream));
+    return GLX_OK;
+  } catch (const glx::Error& e) {
+    glx::g_last_error = e.msg;
+    return e.code;
+  }
+}
+
+int glx_comm_reduce_scatter(glx_comm* c, void* buf, int64_t count, int dtype, void* stream) {
+  try {
+    glx::comm_reduce_scatter(c, buf, count, dtype, static_cast<hipStream_t>(stream));
+    return GLX_OK;
+  } catch (const glx::Error& e) {
+    glx::g_last_error = e.msg;
+    return e.code;
+  }
+}
+
+int glx_comm_all_gather(glx_comm* c, void* buf, int64_t count, int dtype, void* stream) {
+  try {
+    glx::comm_all_gather(c, buf, count, dtype, static_cast<hipStream_t>(stream));
     return GLX_OK;
   } catch (const glx::Error& e) {
     glx::g_last_error = e.msg;

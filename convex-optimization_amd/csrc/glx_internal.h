@@ -84,6 +84,9 @@ struct Red {
   // skip_pass
   const int* skip = nullptr;
   int skip_pass = 0;
+  // 1: every workgroup stores its NV block values at part[slot * NV + j] and returns (no tickets,
+  // no out): the row-sharded trial's partials ride the all-gather (ShardPub)
+  int parts_only = 0;
 };
 
 // Device-side line-search decision of a device-controlled ProxGD batch (solver.cpp dc_batch),
@@ -348,6 +351,34 @@ template <typename T>
 void launch_prox_pgd(const T* x, const T* g, int S, T* gout, T* p, T* pthr, T* z, int64_t n,
                      int64_t l, double t, double mu, double thres, Red red, hipStream_t st,
                      Pub pub = Pub{}, unsigned* zf = nullptr);
+// The row-sharded trial's all-gathered sums: blk holds nranks chunks of `chunk` doubles, [6, 10)
+// a finalize's sums (launch_finalize_residual's out), [kShardPartOff + 6 b, + 6) the trial's
+// (launch_prox_pgd's out) as the partials of its nbp workgroups (Red::parts_only). Combined in a
+// fixed order (sums; trial slot 3: max, NaN-propagating), identical on every rank: mask & 1 ->
+// tr[0, 6), mask & 2 -> rt[0, 4); with pub.host the scalar packet follows with these values.
+constexpr int kShardPartOff = 16;
+struct ShardPub {
+  const double* blk = nullptr;
+  int nranks = 1, chunk = 0, nbp = 0, mask = 0;
+  double* tr = nullptr;
+  double* rt = nullptr;
+  int tr_off = 0, rt_off = 0;   // their packet slots
+  Pub pub{};
+};
+void launch_shard_combine(const ShardPub& sp, hipStream_t st);
+// workgroups of launch_prox_pgd over n rows of l columns (without a packet)
+int prox_blocks(int64_t n, int64_t l);
+// Row-sharded schedule (round 5, solver.cpp iter_proxgd_shard): the replicated half of a ProxGD
+// trial, from the all-gathered p (n x l): pthr = p with |p| < thres zeroed; z = e = p - pthr
+// (emode) or z = xt - t (xt - p) / t (launch_prox_pgd's dense z, xt = the thresholded iterate);
+// zf != NULL: zf[i] = the column mask of row i of e and the column bitmaps behind the masks —
+// the same bits launch_prox_pgd writes.
+// z == NULL: not written. sp.blk != NULL: one more workgroup runs launch_shard_combine's work
+// beside the rows.
+template <typename T>
+void launch_trial_split(const T* p, const T* xt, T* pthr, T* z, unsigned* zf, int64_t n, int64_t l,
+                        double t, double thres, bool emode, const ShardPub& sp, hipStream_t st);
+
 // FISTA (prox = true) / FGD (prox = false: identity) trial fused with the next combine:
 // xc = prox(y - t g, t); vnext = thr(xk) + (xc - thr(xk))/theta;
 // ynext = (1 - theta_next) thr(xc) + theta_next vnext.

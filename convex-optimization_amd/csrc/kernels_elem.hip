@@ -293,6 +293,106 @@ __global__ __launch_bounds__(256) void k_prox_pgd(const T* __restrict__ x, const
   grid_reduce<6, 0x8u>(acc, red);
 }
 
+// The all-gathered sums of the row-sharded trial, combined by one 256-thread workgroup in a fixed
+// order (the same bits on every rank): the trial's nranks * nbp workgroup partials strided over
+// the threads in (rank, workgroup) order, then the butterfly and the waves in order; the
+// finalize's sums rank by rank. Writes tr / rt and, with sp.pub.host, the scalar packet with
+// these values in place (read from LDS, not back from memory).
+__device__ inline void shard_combine_block(const ShardPub& sp) {
+  __shared__ double wv[6][4];
+  __shared__ double fin[10];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  if (sp.mask & 1) {
+    double acc[6] = {0.0, 0.0, 0.0, -__builtin_inf(), 0.0, 0.0};
+    const int np = sp.nranks * sp.nbp;
+    for (int i = threadIdx.x; i < np; i += 256) {
+      const int r = i / sp.nbp, b = i - r * sp.nbp;
+      const double* q = sp.blk + (int64_t)r * sp.chunk + kShardPartOff + b * 6;
+#pragma unroll
+      for (int j = 0; j < 6; ++j) acc[j] = combine(j == 3 ? OP_MAX : OP_SUM, acc[j], q[j]);
+    }
+#pragma unroll
+    for (int j = 0; j < 6; ++j)
+#pragma unroll
+      for (int off = 32; off > 0; off >>= 1)
+        acc[j] = combine(j == 3 ? OP_MAX : OP_SUM, acc[j], __shfl_xor(acc[j], off));
+    if (lane == 0)
+#pragma unroll
+      for (int j = 0; j < 6; ++j) wv[j][wave] = acc[j];
+  }
+  __syncthreads();
+  if (threadIdx.x != 0) return;
+  if (sp.mask & 1)
+    for (int j = 0; j < 6; ++j) {
+      fin[j] = waves_combine<4>(j == 3 ? OP_MAX : OP_SUM, wv[j]);
+      sp.tr[j] = fin[j];
+    }
+  if (sp.mask & 2)
+    for (int j = 0; j < 4; ++j) {
+      double v = sp.blk[6 + j];
+      for (int r = 1; r < sp.nranks; ++r) v += sp.blk[(int64_t)r * sp.chunk + 6 + j];
+      fin[6 + j] = v;
+      sp.rt[j] = v;
+    }
+  if (sp.pub.host != nullptr)
+    publish_packet(sp.pub.s, sp.pub.ns, sp.pub.host, sp.pub.host_seq, sp.pub.seq, fin, sp.tr_off,
+                   (sp.mask & 1) ? 6 : 0, fin + 6, sp.rt_off, (sp.mask & 2) ? 4 : 0);
+}
+
+__global__ __launch_bounds__(256) void k_shard_combine(ShardPub sp) { shard_combine_block(sp); }
+
+// Row-sharded ProxGD trial, the replicated half (solver.cpp iter_proxgd_shard): each rank ran
+// k_prox_pgd on its n / G rows and the rows of p were all-gathered; every rank re-derives p_thr,
+// z and the masks of e from p with the comparisons and arithmetic k_prox_pgd uses, so the bits
+// equal the ones the trial kernel would have written for the whole of p. With sp.blk the last
+// workgroup combines the gathered sums (and publishes the packet) beside the rows.
+template <typename T, int LPR, int EPL>
+__global__ __launch_bounds__(256) void k_trial_split(const T* __restrict__ p, const T* __restrict__ xt,
+                                                     T* __restrict__ pthr, T* __restrict__ z,
+                                                     unsigned* __restrict__ zf, int64_t n, int64_t l,
+                                                     double t_, double thres_, int emode, ShardPub sp) {
+  if (sp.blk != nullptr && blockIdx.x == gridDim.x - 1) {
+    shard_combine_block(sp);
+    return;
+  }
+  const T t = (T)t_, thres = (T)thres_;
+  GLX_ROW_LOOP_BEGIN_NB(LPR, gridDim.x - (sp.blk != nullptr ? 1u : 0u))
+  T pth[EPL], zv[EPL];
+  bool ok[EPL];
+  unsigned mk = 0;
+#pragma unroll
+  for (int e = 0; e < EPL; ++e) {
+    const int64_t j = sub + (int64_t)e * LPR;
+    ok[e] = rv && j < l;
+    const T pv = ok[e] ? p[base + j] : T(0);
+    const bool small = tabs(pv) < thres;
+    pth[e] = small ? T(0) : pv;
+    if (emode) {
+      zv[e] = small ? pv : T(0);
+    } else {
+      const T xv = ok[e] ? xt[base + j] : T(0);
+      const T G = (xv - pv) / t;
+      zv[e] = xv - t * G;
+    }
+    if (ok[e] && small && pv != T(0) && sub + e * LPR < 32) mk |= 1u << (sub + e * LPR);
+  }
+  const unsigned rowe = row_or<LPR>(mk);
+  if (zf != nullptr && rv && sub == 0) zf[row] = rowe;
+  if constexpr (LPR == 16) {
+    __shared__ unsigned msk[16];
+    if (zf != nullptr) zf_store_group16(msk, rowe, rv, sub, zf, n, (int)l, row - (threadIdx.x >> 4));
+  }
+#pragma unroll
+  for (int e = 0; e < EPL; ++e) {
+    const int64_t j = sub + (int64_t)e * LPR;
+    if (ok[e]) {
+      pthr[base + j] = pth[e];
+      if (z != nullptr) z[base + j] = zv[e];
+    }
+  }
+  GLX_ROW_LOOP_END
+}
+
 // FISTA / FGD trial (gl_FProxGD_primal.py:92-102, gl_FGD_primal.py:209-212), fused with the
 // next iteration's combine so that A @ [xc | y_next] is one pass over A:
 //   xc     = prox(y - t g, t)        (PROX) or y - t g (FGD's identity prox)
@@ -687,6 +787,23 @@ void launch_prox_pgd(const T* x, const T* g, int S, T* gout, T* p, T* pthr, T* z
   });
 }
 template <typename T>
+void launch_trial_split(const T* p, const T* xt, T* pthr, T* z, unsigned* zf, int64_t n, int64_t l,
+                        double t, double thres, bool emode, const ShardPub& sp, hipStream_t st) {
+  dispatch_row(l, [&](auto lpr, auto epl) {
+    hipLaunchKernelGGL((k_trial_split<T, decltype(lpr)::value, decltype(epl)::value>),
+                       dim3(row_grid(n, lpr) + (sp.blk != nullptr ? 1u : 0u)), dim3(256), 0, st, p, xt,
+                       pthr, z, zf, n, l, t, thres, emode ? 1 : 0, sp);
+  });
+}
+void launch_shard_combine(const ShardPub& sp, hipStream_t st) {
+  hipLaunchKernelGGL(k_shard_combine, dim3(1), dim3(256), 0, st, sp);
+}
+int prox_blocks(int64_t n, int64_t l) {
+  int b = 0;
+  dispatch_row(l, [&](auto lpr, auto) { b = (int)row_grid_pub(n, lpr, Pub{}); });
+  return b;
+}
+template <typename T>
 void launch_fista_trial(bool prox, const T* y, const T* g, int S, T* gout, const T* xk, T* xc,
                         T* vnext, T* ynext, int64_t n, int64_t l, double t, double mu, double thres,
                         double theta, double theta_next, double delta, Red red, hipStream_t st,
@@ -790,6 +907,8 @@ void launch_publish(const double* s, int ns, double* host, unsigned* host_seq, u
   template void launch_finalize_fista<T>(const T*, int, const T*, int, const T*, T*, const T*, T*,  \
                                          int64_t, double, double, double, const T*, int64_t,        \
                                          const double*, const unsigned*, int, Red, hipStream_t, Ctl);\
+  template void launch_trial_split<T>(const T*, const T*, T*, T*, unsigned*, int64_t, int64_t,       \
+                                      double, double, bool, const ShardPub&, hipStream_t);            \
   template void launch_prox_pgd<T>(const T*, const T*, int, T*, T*, T*, T*, int64_t, int64_t,       \
                                    double, double, double, Red, hipStream_t, Pub, unsigned*);       \
   template void launch_fista_trial<T>(bool, const T*, const T*, int, T*, const T*, T*, T*, T*,      \

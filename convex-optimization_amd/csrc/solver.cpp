@@ -54,6 +54,7 @@ enum {
   S_XRN = 14,   // sum ||x_i|| of the current iterate   } rownorm_max: [sum, max]
   S_XMAX = 15,  // max |x|
   S_RG = 16,    // standalone residual finalize (FISTA y): [sum r^2, ...]
+  S_TRN = 16,   // row-sharded ProxGD: the speculated next trial's sums (6; the FISTA / SGD slots)
   S_REGY = 20,  // FGD smooth regulariser at y
   S_DRN = 21,   // row-norm sum written by the SGD/GD step (+1: max)
   NSCAL = 24,   // the host packet copies slots [0, NSCAL)
@@ -91,6 +92,11 @@ constexpr int kKeepMiB = 192;    // Infinity-Cache hand-off between the non-temp
 // window + 2, so that the all-reduces queued behind a cancelling decision (they cannot be
 // gated) never land in the set the host resumes from
 constexpr int kMaxGSets = kCtlMaxBatch / 2 + 2;
+// row-sharded ProxGD (iter_proxgd_shard): each rank's chunk of sums that rides the all-gather
+// (the finalize's at [6, 10), the trial's workgroup partials from kShardPartOff, ShardPub), for
+// up to kMaxShardRanks ranks
+constexpr int kShardChunkMax = kShardPartOff + 6 * kMaxBlocks;
+constexpr int kMaxShardRanks = 64;
 
 // device-controlled batches' window: opts.dc_window (> 0: that window, < 0: off), else
 // GLX_DC_BATCH, else the measured default (0 = the host decides every iteration): kDcWindow for
@@ -292,6 +298,9 @@ class Session : public SessionBase {
     double* dcr = static_cast<double*>(c.take(sizeof(double) * kCtlRec * kCtlMaxBatch));
     // split-candidate mode: per-row column masks of e = p - p_thr (z's buffer; bit c = e[k][c] != 0)
     unsigned* zf = static_cast<unsigned*>(c.take(zf_bytes(P.n)));   // + the column bitmaps
+    double* sblk = P.comm != nullptr && P.method == GLX_PROXGD
+                       ? static_cast<double*>(c.take(sizeof(double) * kShardChunkMax * kMaxShardRanks))
+                       : nullptr;
     double* fh = static_cast<double*>(c.take(sizeof(double) * (fh_cap + 1)));
     double* sp100 = static_cast<double*>(c.take(sizeof(double) * (fh_cap / 100 + 2)));
     const int gb = gemv_blocks_for(P);
@@ -309,6 +318,7 @@ class Session : public SessionBase {
       s->dc_abort_ = reinterpret_cast<int*>(dcs + 8);
       s->dc_rec_ = dcr;
       s->zf_ = zf;
+      s->blk_ = sblk;
       s->E_ = ec;
       for (int k = 0; k < 3; ++k) s->SXO_[k] = sxo[k];
       s->sp100_ = sp100;
@@ -456,11 +466,47 @@ class Session : public SessionBase {
       std::memset(dc_ring_, 0, sizeof(double) * kCtlRec * kCtlMaxBatch);   // tags start at 1
       GLX_HIP(hipHostGetDevicePointer(reinterpret_cast<void**>(&dc_ring_dev_), dc_ring_, 0));
     }
+    // Row-sharded ProxGD (round 5, iter_proxgd_shard): with a communicator of G > 1 ranks the
+    // gradient is reduce-scattered, the trial runs on this rank's n / G rows and p's rows are
+    // all-gathered (opts.shard_rows: 0 auto = on where n % G == 0, 1 on, 2 off; GLX_SHARD_ROWS overrides). Host
+    // control only (a device-control window keeps the all-reduce schedule). GLX_SHARD_MODEL=G at
+    // world size 1 (bench.py --force-comm): the per-rank timing model of G ranks — the trial on
+    // n / G rows, every line-search test accepted — whose iterates are NOT a solve.
+    if (comm_ != nullptr && P.method == GLX_PROXGD && dc_window_ == 0) {
+      int want = O.shard_rows;
+      if (const char* e = std::getenv("GLX_SHARD_ROWS")) want = std::atoi(e) == 0 ? 2 : 1;
+      cranks_ = comm_size(comm_);
+      int vr = cranks_;
+      if (cranks_ == 1) {
+        const char* mdl = std::getenv("GLX_SHARD_MODEL");
+        vr = mdl ? std::max(1, std::atoi(mdl)) : 1;
+        shard_model_ = vr > 1;
+      }
+      const bool fits = vr <= kMaxShardRanks && n_ % vr == 0;
+      if (want == 1 && vr > 1 && !fits)
+        throw Error{GLX_E_INVALID, "row-sharded ProxGD needs n % ranks == 0 and at most 64 ranks "
+                                   "(opts.shard_rows = 0 / 2: the all-reduce schedule)"};
+      if (want != 2 && vr > 1 && fits) {   // auto: the all-reduce schedule where it does not fit
+        shard_ = true;
+        sranks_ = vr;
+        srank_ = shard_model_ ? 0 : comm_rank(comm_);
+        srows_ = n_ / vr;
+        srow0_ = (int64_t)srank_ * srows_;
+        nbp_ = prox_blocks(srows_, l_);
+        schunk_ = kShardPartOff + 6 * nbp_;
+        // A e from the bitmap / list gathers reads e only where its masks are set, where e = p:
+        // the gathered p serves as e and z is not re-derived (the row form reads whole rows)
+        zskip_ = emode_ && gform_ != 1;
+      } else {
+        shard_model_ = false;
+      }
+    }
     GLX_HIP(hipMemsetAsync(ticket_, 0, kTicketBytes, st_));
     GLX_HIP(hipMemsetAsync(pcnt_, 0, sizeof(unsigned) * (P.n / 64 + 64), st_));
     GLX_HIP(hipMemsetAsync(fcnt_, 0, sizeof(unsigned) * (ax_fin_counters(plan_) + 64), st_));
     GLX_HIP(hipMemsetAsync(flag_, 0, 256, st_));
     GLX_HIP(hipMemsetAsync(scal_, 0, sizeof(double) * NSCAL_DEV, st_));
+    if (blk_) GLX_HIP(hipMemsetAsync(blk_, 0, sizeof(double) * kShardChunkMax * kMaxShardRanks, st_));
     mus_[0] = 100 * P.mu0;
     mus_[1] = 10 * P.mu0;
     mus_[2] = P.mu0;
@@ -598,6 +644,10 @@ class Session : public SessionBase {
     else if (gform_ == 2) s += "gather k_e_lists+k_at_gather";
     else s += "gather k_at_gather_bm";
     if (fin_ok_) s += " + finalize folded into A p_thr";
+    if (shard_)
+      s += "; rows=sharded x" + std::to_string(sranks_) + (shard_model_ ? " (timing model)" : "") +
+           " (reduce-scatter of A^T r, k_prox_pgd on n/" + std::to_string(sranks_) +
+           " rows, all-gather of p, k_trial_split)";
     s += "; dc_window=" + std::to_string(dc_window_);
     return s;
   }
@@ -1031,6 +1081,7 @@ class Session : public SessionBase {
   // this trial ready (same mu and t); (2) otherwise A^T r with the trial fused into it
   // (launch_atr_prox); (3) otherwise the gradient (speculative or not) and k_prox_pgd.
   void iter_proxgd() {
+    if (shard_) { iter_proxgd_shard(); return; }
     if (!state_valid_) proxgd_prologue(thr_from_trial_);
     record(f_cur_, s_cur_);
     if (stop_rule()) { end_phase(true); return; }
@@ -1154,19 +1205,20 @@ class Session : public SessionBase {
   }
 
   // accepted trial: the packet (hs_) holds its sums
-  void proxgd_accept(int rpt, bool exact) {
-    stats_[0] += hs_[S_TR + 4];
-    stats_[1] += hs_[S_TR + 5];
+  // trs: the packet slots that hold the trial's sums (S_TR; row-sharded: S_TR or S_TRN)
+  void proxgd_accept(int rpt, bool exact, int trs = S_TR) {
+    stats_[0] += hs_[trs + 4];
+    stats_[1] += hs_[trs + 5];
     stats_[2] += 1;
-    split_hist_.push_back(hs_[S_TR + 5]);
+    split_hist_.push_back(hs_[trs + 5]);
     irg_ = rpt;
     gx_ = 0.5 * hs_[S_RT + 1];
     // exact: A p from the batch; split-candidate: A p - b = (A p_thr - b) + A e; dense z
     // batch (GLX_SPLIT_CAND=0): A z - b (z = x - t G_t is ulp-close to p) unless the
     // threshold changed nothing, in which case A p_thr - b == A p - b exactly
     const double sq_x = exact ? hs_[S_RT + 2]
-                              : ((emode_ || hs_[S_TR + 4] != 0) ? hs_[S_RT] : hs_[S_RT + 1]);
-    f_cur_ = 0.5 * sq_x + P_.mu0 * hs_[S_TR + 2];
+                              : ((emode_ || hs_[trs + 4] != 0) ? hs_[S_RT] : hs_[S_RT + 1]);
+    f_cur_ = 0.5 * sq_x + P_.mu0 * hs_[trs + 2];
     s_cur_ = hs_[S_RT + 3] / (double)nl_;
     state_valid_ = true;
   }
@@ -1180,6 +1232,190 @@ class Session : public SessionBase {
     spec_set_ = nset(gset_);
     spec_trial_mu_ = mu_;
     spec_trial_t_ = O_.alpha0;
+  }
+
+  // ------------------------------------------------------------------ row-sharded ProxGD
+  // (round 5; VERDICT round 4: reduce-scatter -> prox on n/G rows -> all-gather). Per iteration
+  // on every rank: A@[e | p_thr] over this rank's rows of A and its finalize (partial residual
+  // sums, the sparsity count over this rank's rows of p); A^T r of the candidate, reduce-scattered
+  // (this rank's n / G rows of the gradient); the next trial, k_prox_pgd on those rows (partial
+  // trial sums); one RCCL group that all-gathers p's rows and every rank's block of partial sums,
+  // combined in rank order (k_shard_combine: every rank holds the same bits); then the replicated
+  // k_trial_split re-derives p_thr, z and the masks of e from the gathered p. The host decides
+  // from the combined sums, with the next trial and its A@X already queued (the speculative path
+  // of iter_proxgd). The all-gathered blocks replace the 8-byte all-reduces of the residual sums.
+  // Bytes per iteration and rank: reduce-scatter + all-gather of n x l, the same as one ring
+  // all-reduce of the gradient; the row-wise work (k_prox_pgd, the count) is divided by G.
+  double* blk_own() { return blk_ + (int64_t)(shard_model_ ? 0 : srank_) * schunk_; }
+  int tr_other() const { return tr_slot_ == S_TR ? S_TRN : S_TR; }
+  void shard_gradient(const T* r, int set) {
+    T* G = Gs_[set];
+    T* Gp = Gps_[set];
+    hipEvent_t e0 = prof_begin(1);
+    launch_atr<T>(plan_, A_, r, Gp, st_);
+    check_launch();
+    prof_end(1, e0);
+    ++atr_calls_;
+    if (plan_.atr_S > 1) {
+      launch_sum_partials<T>(Gp, plan_.atr_S, G, nl_, st_);
+      check_launch();
+    }
+    comm_reduce_scatter(comm_, G, srows_ * l_, P_.dtype, st_);
+  }
+  // the trial on this rank's rows: p, p_thr, z rows into X_[op], X_[opt], X_[oz]; its workgroup
+  // partials into this rank's chunk (Red::parts_only)
+  void shard_prox(const T* xt, const T* G, int op, int opt, int oz, double t) {
+    const int64_t o = srow0_ * l_;
+    Red rd = red_to(scal_ + S_TR);
+    rd.part = blk_own() + kShardPartOff;
+    rd.parts_only = 1;
+    launch_prox_pgd<T>(xt + o, G + o, 1, nullptr, X_[op] + o, X_[opt] + o, X_[oz] + o, srows_, l_, t,
+                       mu_, O_.thres, rd, st_, Pub{}, nullptr);
+    check_launch();
+  }
+  // one RCCL group: p's rows (op >= 0) and every rank's chunk of sums
+  void shard_exchange(int op) {
+    if (shard_model_ && op >= 0) {   // timing model: this rank's rows stand in for the others'
+      const size_t bytes = sizeof(T) * (size_t)(srows_ * l_);   // (so e's row count is realistic)
+      for (int r = 1; r < sranks_; ++r)
+        GLX_HIP(hipMemcpyAsync(X_[op] + (size_t)r * srows_ * l_, X_[op], bytes, hipMemcpyDeviceToDevice, st_));
+    }
+    comm_group_begin(comm_);
+    if (op >= 0) comm_all_gather(comm_, X_[op], srows_ * l_, P_.dtype, st_);
+    comm_all_gather(comm_, blk_, schunk_, GLX_F64, st_);
+    comm_group_end(comm_);
+  }
+  // mask & 1: the trial's sums -> scal_[tr_dst], mask & 2: the finalize's -> scal_[S_RT];
+  // seq != NULL: the packet follows (*seq = its number)
+  ShardPub shard_pub(int mask, int tr_dst, unsigned* seq) {
+    ShardPub sp;
+    sp.blk = blk_;
+    sp.nranks = cranks_;
+    sp.chunk = schunk_;
+    sp.nbp = nbp_;
+    sp.mask = mask;
+    sp.tr = scal_ + tr_dst;
+    sp.rt = scal_ + S_RT;
+    sp.tr_off = tr_dst;
+    sp.rt_off = S_RT;
+    if (seq != nullptr) sp.pub = make_pub(nullptr, seq);
+    return sp;
+  }
+  // p_thr, z (unless zskip_) and e's masks from the gathered p, the sums combined beside the rows
+  void shard_derive(int ixt, int op, int opt, int oz, double t, const ShardPub& sp) {
+    launch_trial_split<T>(X_[op], X_[ixt], X_[opt], zskip_ ? nullptr : X_[oz], ezf(), n_, l_, t,
+                          O_.thres, emode_, sp, st_);
+    check_launch();
+  }
+  // the trial's pass over this rank's rows of A and its finalize: sums -> the chunk's [6, 10), the
+  // count over this rank's rows of cx against the combined max at cmax
+  void shard_fin(int nsrc, const T* const* xs, T* const* rs, const T* cx, const double* cmax, bool skip_ax) {
+    const bool chain = emode_;
+    const bool gat = chain && smode_ == 1;
+    if (!skip_ax) {
+      if (gat) cand_ax(xs);
+      else spec_ax(nsrc, xs);
+    }
+    T* rsc[3] = {chain ? nullptr : rs[0], rs[1], rs[2]};
+    const int64_t o = srow0_ * l_;
+    launch_finalize_residual<T>(Pp_, gat ? ax_split(plan_, 1) : ax_split(plan_, nsrc), B_, nsrc, rsc,
+                                ml_, nullptr, 0, 1, cx + o, srows_ * l_, cmax, nullptr, 0.0,
+                                scal_ + S_DRN, red_to(blk_own() + 6), st_, nullptr, nullptr, 0,
+                                chain ? 1 : 0, gat ? gsplit_ : 0, Ctl{});
+    check_launch();
+  }
+  void iter_proxgd_shard() {
+    if (!state_valid_) proxgd_prologue(thr_from_trial_);   // x replicated: all-reduced sums
+    record(f_cur_, s_cur_);
+    if (stop_rule()) { end_phase(true); return; }
+    const bool ls = O_.step_type == GLX_STEP_LINE_SEARCH && O_.ls_maxit > 0;
+    const double t0 = ls ? O_.alpha0 : schedule(inner_);
+    bool first_done = false;
+    if (spec_trial_ready_) {   // the previous iteration's speculated trial (its sums in tr_slot_)
+      spec_trial_ready_ = false;
+      use_gset(spec_set_);
+      first_done = (spec_trial_mu_ == mu_ && spec_trial_t_ == t0);
+      if (!first_done) ax_queued_ = false;
+    } else {
+      shard_gradient(R_[irg_], gset_);
+    }
+    const bool exact = O_.exact_objective != 0;
+    const int rz = (irg_ + 1) % kRes, rpt = (irg_ + 2) % kRes, rp = (irg_ + 3) % kRes;
+    const int nsrc = exact ? 3 : 2;
+    auto trial = [&](double tt) {
+      shard_prox(X_[ixt_], G_, ip_, ipt_, iz_, tt);
+      shard_exchange(ip_);
+      shard_derive(ixt_, ip_, ipt_, iz_, tt, shard_pub(1, tr_slot_, nullptr));
+    };
+    double t = t0;
+    bool accepted = false, spec_trial = false;
+    if (ls) {
+      for (int it = 0; it < O_.ls_maxit; ++it) {
+        if (!(it == 0 && first_done)) trial(t);
+        const T* xs[3] = {zskip_ ? X_[ip_] : X_[iz_], X_[ipt_], X_[ip_]};
+        T* rs[3] = {R_[rz], R_[rpt], R_[rp]};
+        const bool skip_ax = it == 0 && first_done && ax_queued_;
+        ax_queued_ = false;
+        shard_fin(nsrc, xs, rs, X_[ip_], scal_ + tr_slot_ + 3, skip_ax);
+        unsigned seq = 0;
+        if (want_spec(it)) {
+          // the next iteration's gradient and first trial at the candidate p_thr (the other
+          // gradient set, the spare buffers, the other trial slot); their exchange carries this
+          // trial's residual sums, and the next trial's A@X is queued before the host waits
+          const int ns = nset(gset_);
+          const int ot = tr_other();
+          shard_gradient(R_[rpt], ns);
+          shard_prox(X_[ipt_], Gs_[ns], if1_, if2_, iz_, O_.alpha0);
+          shard_exchange(if1_);
+          // the packet (this trial's residual sums, the next trial's sums) rides the next trial's
+          // dense pass as its publisher workgroup: a workgroup of the 8 MiB-writing k_trial_split
+          // that stores to host memory stretched that kernel from 5.6 to 17.8 us (its end-of-
+          // kernel release), a separate k_publish costs ~4.5 us (profiles/r5_shard/)
+          shard_derive(ipt_, if1_, if2_, iz_, O_.alpha0, shard_pub(3, ot, nullptr));
+          const T* sx[3] = {zskip_ ? X_[if1_] : X_[iz_], X_[if2_], X_[if1_]};
+          const bool carry = spin_readback_ && attach_ok_ && ax_pub_ok(plan_, smode_ == 1 ? 1 : nsrc);
+          Pub pb;
+          if (carry) pb = make_pub(nullptr, &seq);
+          else seq = post_readback();
+          if (smode_ == 1) cand_ax(sx, pb);
+          else spec_ax(nsrc, sx, pb);
+          ax_queued_ = true;
+          spec_trial = true;
+        } else {
+          shard_exchange(-1);
+          launch_shard_combine(shard_pub(2, tr_slot_, spin_readback_ ? &seq : nullptr), st_);
+          check_launch();
+          if (!spin_readback_) seq = post_readback();
+        }
+        wait_readback(seq);
+        const double gz = 0.5 * hs_[S_RT];
+        if (shard_model_ || gz <= gx_ - t * hs_[tr_slot_ + 0] + 0.5 * t * hs_[tr_slot_ + 1]) {
+          accepted = true;
+          spec_on_ = (it == 0);
+          break;
+        }
+        spec_trial = false;
+        spec_on_ = false;
+        ax_queued_ = false;   // the speculated trial and its A@X are dropped
+        t *= O_.ls_coeff;
+      }
+      if (!accepted) trial(t);   // the untested last step (:99)
+    } else if (!first_done) {
+      trial(t);
+    }
+    if (accepted) {
+      proxgd_accept(rpt, exact, tr_slot_);
+    } else {
+      state_valid_ = false;
+      thr_from_trial_ = true;
+    }
+    if (spec_trial) {
+      proxgd_spec_rotate();
+      tr_slot_ = tr_other();
+    } else {
+      std::swap(ix_, ip_);
+      std::swap(ixt_, ipt_);
+    }
   }
 
   // ------------------------------------------------------------------ device-controlled ProxGD
@@ -1892,6 +2128,15 @@ class Session : public SessionBase {
   unsigned* fcnt_ = nullptr;   // per-row-block counters (the dense pass's folded finalize)
   bool fin_ok_ = false;        // the split-candidate ProxGD finalize folded into the dense pass
   unsigned* zf_ = nullptr;     // per-row column masks of e (split-candidate mode)
+  // row-sharded ProxGD (iter_proxgd_shard): this rank's rows [srow0_, srow0_ + srows_) of n,
+  // sranks_ row blocks (cranks_ communicator ranks; they differ only in the timing model)
+  bool shard_ = false, shard_model_ = false;
+  int srank_ = 0, sranks_ = 1, cranks_ = 1;
+  int64_t srow0_ = 0, srows_ = 0;
+  int nbp_ = 0, schunk_ = 0;   // k_prox_pgd's workgroups on srows_ rows; doubles per rank's chunk
+  bool zskip_ = false;         // the gathered p serves as e (bitmap / list gathers)
+  double* blk_ = nullptr;      // kMaxShardRanks chunks of sums (kShardChunkMax doubles each)
+  int tr_slot_ = S_TR;         // the packet slots of the current trial's sums
   T* At_ = nullptr;            // A^T (split-candidate gather form)
   void* glists_ = nullptr;     // the gather's per-column index lists of e
   int smode_ = 0, gsplit_ = 1;

@@ -29,7 +29,8 @@ class GlxOpts(ctypes.Structure):
                 ("ls_coeff", c_double), ("ls_maxit", c_int32), ("delta", c_double),
                 ("continuous_subgradient", c_int32), ("exact_objective", c_int32),
                 ("profile", c_int32), ("max_total_iters", c_int64), ("ax_variant", c_int32),
-                ("split_cand", c_int32), ("dc_window", c_int32), ("reserved", c_int32 * 5)]
+                ("split_cand", c_int32), ("dc_window", c_int32), ("shard_rows", c_int32),
+                ("reserved", c_int32 * 4)]
 
 
 class GlxProblem(ctypes.Structure):
@@ -97,6 +98,8 @@ _SIGS = {
     "glx_comm_create": (c_int, [POINTER(c_void_p), POINTER(c_uint8), c_int, c_int]),
     "glx_comm_create_host": (c_int, [POINTER(c_void_p), c_int, c_int, c_void_p, c_void_p]),
     "glx_comm_allreduce": (c_int, [c_void_p, c_void_p, c_int64, c_int, c_void_p]),
+    "glx_comm_reduce_scatter": (c_int, [c_void_p, c_void_p, c_int64, c_int, c_void_p]),
+    "glx_comm_all_gather": (c_int, [c_void_p, c_void_p, c_int64, c_int, c_void_p]),
     "glx_comm_destroy": (None, [c_void_p]),
 }
 

@@ -2,8 +2,11 @@
 
 The bootstrap (exchanging RCCL's unique id) rides on ``torch.distributed`` with whatever
 backend the launcher initialised (gloo is enough); every GPU collective of the solve itself
-is issued by libglx on the compute stream (csrc/comm.cpp): one sum all-reduce of the n x l
-gradient per A^T r, plus 8-byte all-reduces of squared residual norms.
+is issued by libglx on the compute stream (csrc/comm.cpp). ProxGD's row-sharded schedule
+(the default where n divides by the world size): a reduce-scatter of the n x l gradient per
+A^T r and one grouped all-gather of the new iterate's rows with every rank's partial sums per
+trial; otherwise one sum all-reduce of the gradient plus 8-byte all-reduces of squared
+residual norms.
 """
 from __future__ import annotations
 
@@ -82,6 +85,23 @@ class Comm:
         stream = ctypes.c_void_p(torch.cuda.current_stream(t.device).cuda_stream)
         check(lib().glx_comm_allreduce(self.handle, ctypes.c_void_p(t.data_ptr()), t.numel(), dt, stream))
         return t
+
+    def _chunked(self, fn, t: torch.Tensor) -> torch.Tensor:
+        if t.numel() % self.world:
+            raise ValueError("the tensor must hold world-size equal chunks")
+        dt = _lib.GLX_F64 if t.dtype == torch.float64 else _lib.GLX_F32
+        stream = ctypes.c_void_p(torch.cuda.current_stream(t.device).cuda_stream)
+        check(fn(self.handle, ctypes.c_void_p(t.data_ptr()), t.numel() // self.world, dt, stream))
+        return t
+
+    def reduce_scatter_(self, t: torch.Tensor) -> torch.Tensor:
+        """In place over world-size chunks: chunk ``rank`` becomes the sum over ranks of that
+        chunk (the other chunks are left undefined)."""
+        return self._chunked(lib().glx_comm_reduce_scatter, t)
+
+    def all_gather_(self, t: torch.Tensor) -> torch.Tensor:
+        """In place over world-size chunks: chunk ``rank`` is sent, every chunk received."""
+        return self._chunked(lib().glx_comm_all_gather, t)
 
     def close(self):
         if self.handle:

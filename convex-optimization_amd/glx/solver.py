@@ -16,7 +16,9 @@ provides device memory, the stream and the multi-process bootstrap. There is no 
 Build-only option keys (ignored by the reference): ``exact_objective`` (ProxGD: recompute
 A@x for every objective instead of reusing the accepted trial residual), ``profile``,
 ``max_total_iters``, ``ax_variant``, ``split_cand`` (0 auto, 1 on, 2 off), ``dc_window``
-(device-controlled line search: 0 auto, -1 off, k iterations in flight), ``device``, ``comm``.
+(device-controlled line search: 0 auto, -1 off, k iterations in flight), ``shard_rows``
+(ProxGD with a communicator: 0 auto = the row-sharded schedule, 1 on, 2 off = the gradient
+all-reduce schedule), ``device``, ``comm``.
 """
 from __future__ import annotations
 
@@ -39,7 +41,7 @@ _REF_KEYS = {
     "delta": "delta",
 }
 _BUILD_KEYS = {"exact_objective", "profile", "max_total_iters", "ax_variant", "split_cand",
-               "dc_window"}
+               "dc_window", "shard_rows"}
 
 
 def _device(opts: Dict[str, Any]) -> torch.device:
@@ -266,6 +268,7 @@ def solve(name: str, x0, A, b, mu_0, opts: Optional[Dict[str, Any]] = None, comm
     try:
         s.run(0)
         res = s.finish()
+        plan = s.describe()
         if logger.isEnabledFor(logging.DEBUG):
             _replay_log(s, res, float(mu_0))
     finally:
@@ -274,5 +277,6 @@ def solve(name: str, x0, A, b, mu_0, opts: Optional[Dict[str, Any]] = None, comm
     x = xd.cpu().numpy() if numpy_in else xd
     out = {"tt": res["tt"], "fval": res["fval"], "f_hist": res["f_hist"],
            "f_hist_best": res["f_hist_best"],
-           "glx": {"ax_calls": res["ax_calls"], "atr_calls": res["atr_calls"], "syncs": res["syncs"]}}
+           "glx": {"ax_calls": res["ax_calls"], "atr_calls": res["atr_calls"], "syncs": res["syncs"],
+                   "plan": plan}}
     return x, res["k"], out

@@ -78,7 +78,13 @@ typedef struct glx_opts {
                                      (GLX_DC_BATCH env, else the measured default: 8 for
                                      FProxGD with a communicator, off otherwise), -1 = off,
                                      k in 1..32 = up to k iterations queued ahead of the host   */
-  int32_t reserved[5];
+  int32_t shard_rows;             /* ProxGD with a communicator of G > 1 ranks: 0 = auto (on),
+                                     1 = on, 2 = off. On: the row-sharded schedule — the gradient
+                                     is reduce-scattered, the prox / trial runs on this rank's
+                                     n / G rows and the new iterate's rows are all-gathered
+                                     (needs n % G == 0); off: the gradient is all-reduced and
+                                     every rank runs the row-wise step on all n rows            */
+  int32_t reserved[4];
 } glx_opts;
 
 /* One problem instance. For multi-GPU runs A and b are this rank's row shard
@@ -231,7 +237,7 @@ int glx_kernel_workspace_bytes(int dtype, int64_t m, int64_t n, int64_t l, size_
  * A @ X with 1, 2, 3 right-hand sides and for A^T R (NUL-terminated, truncated to cap). */
 int glx_plan_describe(int dtype, int64_t m, int64_t n, int64_t l, char* out, size_t cap);
 
-/* ---- multi-GPU (row-sharded A, one RCCL all-reduce of A^T r per gradient) ---- */
+/* ---- multi-GPU (row-sharded A; A^T r all-reduced, or reduce-scattered with the row-sharded step) ---- */
 #define GLX_COMM_ID_BYTES 128
 int  glx_comm_unique_id(uint8_t id[GLX_COMM_ID_BYTES]);
 int  glx_comm_create(glx_comm** out, const uint8_t id[GLX_COMM_ID_BYTES], int nranks, int rank);
@@ -243,6 +249,13 @@ typedef int (*glx_host_allreduce_fn)(void* host_buf, int64_t count, int dtype, v
 int  glx_comm_create_host(glx_comm** out, int nranks, int rank, glx_host_allreduce_fn fn, void* user);
 /* in-place sum all-reduce of `count` elements of dtype on `stream` (exposed for tests) */
 int  glx_comm_allreduce(glx_comm* c, void* buf, int64_t count, int dtype, void* stream);
+/* The row-sharded schedule's collectives (round 5, exposed for tests), in place over nranks
+ * chunks of `count` elements: reduce-scatter leaves in chunk `rank` the sum over ranks of that
+ * chunk (other chunks undefined); all-gather sends chunk `rank` and receives every chunk. The
+ * host transport runs both through the all-reduce callback (all-gather exactly: the chunks it
+ * does not own are -0.0). */
+int  glx_comm_reduce_scatter(glx_comm* c, void* buf, int64_t count, int dtype, void* stream);
+int  glx_comm_all_gather(glx_comm* c, void* buf, int64_t count, int dtype, void* stream);
 void glx_comm_destroy(glx_comm* c);
 
 #ifdef __cplusplus

@@ -36,6 +36,8 @@ def main():
                     help="alpha0 = scale / (sqrt(m) + sqrt(n))^2 (> 1: line-search rejections)")
     ap.add_argument("--shm", action="store_true",
                     help="one host copy of the instance in /dev/shm, each rank generating its own rows")
+    ap.add_argument("--shard-rows", type=int, default=None,
+                    help="opts shard_rows (ProxGD: 0 auto, 1 the row-sharded step, 2 all-reduce)")
     ap.add_argument("--out", required=True)
     a = ap.parse_args()
 
@@ -49,6 +51,11 @@ def main():
     dist.init_process_group("gloo", rank=rank, world_size=world)
     comm = Comm.host_staged() if a.transport == "host" else Comm.from_torch_distributed()
 
+    if a.solver == "collectives":
+        collectives_check(comm, rank, world, a.out)
+        comm.close()
+        dist.destroy_process_group()
+        return
     r0, r1 = shard_rows(a.m, world, rank)
     shm_path = None
     if a.shm:
@@ -61,10 +68,12 @@ def main():
     opts = {"alpha0": a.alpha_scale * numpy_ref.step_size_for(a.m, a.n), "maxit": a.maxit}
     if a.csf:
         opts["continuous_subgradient_flag"] = True
+    if a.shard_rows is not None:
+        opts["shard_rows"] = a.shard_rows
     x, k, out = glx.solve(a.solver, x0, A[r0:r1], b[r0:r1], mu, dict(opts), comm=comm)
     digest = hashlib.sha256(np.ascontiguousarray(x).tobytes()).hexdigest()
     mine = {"rank": rank, "k": int(k), "fval": float(out["fval"]), "x_sha": digest,
-            "f_hist": [float(v) for v in out["f_hist"]]}
+            "f_hist": [float(v) for v in out["f_hist"]], "plan": out["glx"]["plan"]}
     gathered = [None] * world
     dist.all_gather_object(gathered, mine)
     if rank == 0:
@@ -81,6 +90,37 @@ def main():
         if rank == 0:
             os.unlink(shm_path)
     dist.destroy_process_group()
+
+
+def collectives_check(comm, rank, world, out):
+    """glx_comm_reduce_scatter / glx_comm_all_gather on the host transport: chunk sums against
+    NumPy and a bit-exact gather (signed zeros, NaN and infinities included)."""
+    ok = True
+    for dt, npdt in ((torch.float64, np.float64), (torch.float32, np.float32)):
+        chunk = 1000
+        full = [np.random.default_rng(100 + r).standard_normal(world * chunk).astype(npdt) for r in range(world)]
+        t = torch.from_numpy(full[rank].copy()).cuda()
+        comm.reduce_scatter_(t)
+        torch.cuda.synchronize()
+        want = full[0][rank * chunk:(rank + 1) * chunk].astype(np.float64)
+        for r in range(1, world):
+            want = want + full[r][rank * chunk:(rank + 1) * chunk]
+        got = t.cpu().numpy()[rank * chunk:(rank + 1) * chunk].astype(np.float64)
+        ok &= bool(np.allclose(got, want, rtol=1e-5 if npdt == np.float32 else 1e-13, atol=1e-6))
+        src = [np.random.default_rng(200 + r).standard_normal(chunk).astype(npdt) for r in range(world)]
+        for r in range(world):
+            src[r][:4] = np.array([-0.0, 0.0, np.nan, -np.inf], dtype=npdt)
+        t = torch.full((world * chunk,), 7.0, dtype=dt, device="cuda")
+        t[rank * chunk:(rank + 1) * chunk] = torch.from_numpy(src[rank]).cuda()
+        comm.all_gather_(t)
+        torch.cuda.synchronize()
+        ok &= t.cpu().numpy().tobytes() == np.concatenate(src).tobytes()
+    import torch.distributed as dist
+    res = [None] * world
+    dist.all_gather_object(res, ok)
+    if rank == 0:
+        with open(out, "w") as fh:
+            json.dump({"ok": res}, fh)
 
 
 def shm_instance(path, m, n, l, seed, rank, r0, r1):

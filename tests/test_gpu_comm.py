@@ -47,6 +47,34 @@ def test_allreduce_identity_world1(comm):
     assert torch.equal(t, ref)
 
 
+def test_reduce_scatter_all_gather_world1(comm):
+    """RCCL reduce-scatter / all-gather at world size 1 (the row-sharded schedule's collectives):
+    identities."""
+    for dt in (torch.float64, torch.float32):
+        t = torch.randn(4096, dtype=dt, device="cuda")
+        ref = t.clone()
+        comm.reduce_scatter_(t)
+        comm.all_gather_(t)
+        torch.cuda.synchronize()
+        assert torch.equal(t, ref)
+
+
+def test_shard_timing_model_world1(comm, monkeypatch):
+    """GLX_SHARD_MODEL=8 at world size 1 (bench.py --force-comm): the per-rank schedule of 8
+    ranks — the trial on n / 8 rows — runs and says so; its iterates are not a solve."""
+    import glx
+    from oracle import numpy_ref
+    monkeypatch.setenv("GLX_SHARD_MODEL", "8")
+    A, b, u, x0, mu = numpy_ref.gen_data(256, 1024, 32, 7)
+    At, bt, xt = (torch.from_numpy(a).to("cuda", torch.float64) for a in (A, b, x0))
+    s = glx.Session("gl_ProxGD_primal", xt.clone(), At, bt, mu,
+                    {"alpha0": numpy_ref.step_size_for(256, 1024), "maxit": 10}, comm=comm)
+    assert "rows=sharded x8 (timing model)" in s.describe()
+    done = s.run(12)
+    s.close()
+    assert done == 12
+
+
 @pytest.mark.parametrize("solver,shape,dtype", [
     ("gl_ProxGD_primal", (512, 1024, 32), torch.float64),
     ("gl_FProxGD_primal", (512, 1024, 16), torch.float64),

@@ -1,8 +1,11 @@
-"""Row-sharded solves with world size 2 and 3 on ONE GPU (host-staged transport over gloo).
+"""Row-sharded solves with world size 2, 3 and 8 on ONE GPU (host-staged transport over gloo).
 
 Every rank runs the full libglx N-GPU path of solver.cpp — local A_g x - b_g and A_g^T r_g, the
 gradient and every squared-residual sum all-reduced, replicated row-wise steps and decisions —
 with the all-reduces staged through host memory instead of RCCL (RCCL needs one GPU per rank).
+ProxGD where n divides by the world size takes the row-sharded schedule instead (round 5,
+iter_proxgd_shard): the gradient reduce-scattered, the trial on n / G rows, p's rows and the
+partial sums all-gathered and combined in rank order (test_row_sharded_*).
 Checks: every rank returns the same k, fval and bit-identical x; k equals the unsharded oracle's
 and fval / f_hist agree to 1e-8 relative (fp64), as in tests/test_gpu_parity.py.
 """
@@ -38,7 +41,9 @@ def run_sharded(tmp_path, world, solver, m, n, l, dtype="f64", maxit=20, extra=(
            "--maxit", str(maxit), "--out", str(out)] + list(extra)
     env = dict(os.environ, OMP_NUM_THREADS=str(threads))
     p = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=timeout)
-    assert p.returncode == 0, p.stdout[-3000:] + p.stderr[-3000:]
+    if p.returncode != 0:   # the first worker traceback, not just the launcher's summary
+        i = p.stderr.find("Traceback")
+        raise AssertionError(p.stderr[max(0, i):max(0, i) + 4000] + "\n...\n" + p.stderr[-1500:])
     with open(out) as fh:
         return json.load(fh)
 
@@ -147,3 +152,83 @@ def test_sharded_c5_global_world8(tmp_path):
     assert fh.shape == fo.shape
     assert np.max(np.abs(fh - fo) / np.abs(fo)) < 1e-8
     assert v["x_maxdiff"] <= 1e-6 * v["x_scale"]
+
+
+def _check_identical_and_oracle(v, world, bar=1e-8):
+    ranks = v["ranks"]
+    assert len(ranks) == world
+    for r in ranks[1:]:   # every rank combines the same gathered sums: identical bits everywhere
+        assert r["k"] == ranks[0]["k"] and r["fval"] == ranks[0]["fval"] and r["x_sha"] == ranks[0]["x_sha"]
+        assert r["f_hist"] == ranks[0]["f_hist"]
+    assert ranks[0]["k"] == v["oracle_k"]
+    rel = abs(ranks[0]["fval"] - v["oracle_fval"]) / abs(v["oracle_fval"])
+    assert rel < bar, rel
+    fh, fo = np.asarray(ranks[0]["f_hist"]), np.asarray(v["oracle_f_hist"])
+    assert fh.shape == fo.shape
+    assert np.max(np.abs(fh - fo) / np.abs(fo)) < bar
+    return ranks[0]
+
+
+@pytest.mark.parametrize("world,shape,extra", [
+    (2, (515, 1024, 16), ()),
+    (3, (515, 1536, 32), ()),
+    (8, (1024, 1024, 32), ()),
+    (2, (512, 1024, 32), ("--alpha-scale", "2.5")),   # rejected first trials, retried on n/G rows
+    (3, (600, 768, 5), ()),                           # l = 5: LPR 8 rows, no column bitmaps
+])
+def test_row_sharded_proxgd(tmp_path, world, shape, extra):
+    """ProxGD's row-sharded schedule (reduce-scatter of A^T r, k_prox_pgd on n / G rows, one
+    all-gather of p's rows and the partial sums, k_trial_split) against the unsharded oracle
+    (gl_ProxGD_primal.py:73-132): k identical, f_hist within 1e-8, bit-identical on every rank."""
+    v = run_sharded(tmp_path, world, "gl_ProxGD_primal", *shape, maxit=25,
+                    extra=("--shard-rows", "1") + tuple(extra), timeout=150)
+    r0 = _check_identical_and_oracle(v, world)
+    assert ("rows=sharded x%d" % world) in r0["plan"], r0["plan"]
+    assert v["x_maxdiff"] <= 1e-6 * v["x_scale"]
+
+
+def test_row_sharded_split_candidate(tmp_path, monkeypatch):
+    """The split-candidate trial under the row-sharded schedule: the masks and bitmaps of e are
+    re-derived from the gathered p by k_trial_split and the bitmap gather reads e from them."""
+    monkeypatch.setenv("GLX_SPLIT_CAND", "1")
+    v = run_sharded(tmp_path, 2, "gl_ProxGD_primal", 512, 1024, 32, maxit=25,
+                    extra=("--shard-rows", "1"))
+    r0 = _check_identical_and_oracle(v, 2)
+    assert "gather k_at_gather_bm" in r0["plan"] and "rows=sharded x2" in r0["plan"], r0["plan"]
+
+
+def test_row_sharded_matches_allreduce_schedule(tmp_path):
+    """Both multi-GPU schedules on the same instance: same k, f_hist within 1e-12 of each other
+    (they differ only in the order the trial sums are added)."""
+    a = run_sharded(tmp_path, 2, "gl_ProxGD_primal", 515, 1024, 32, maxit=25, extra=("--shard-rows", "1"))
+    b = run_sharded(tmp_path, 2, "gl_ProxGD_primal", 515, 1024, 32, maxit=25, extra=("--shard-rows", "2"))
+    ra, rb = a["ranks"][0], b["ranks"][0]
+    assert "rows=sharded" in ra["plan"] and "rows=sharded" not in rb["plan"]
+    assert ra["k"] == rb["k"]
+    fa, fb = np.asarray(ra["f_hist"]), np.asarray(rb["f_hist"])
+    assert np.max(np.abs(fa - fb) / np.abs(fb)) < 1e-12
+
+
+def test_row_sharded_fp32(tmp_path):
+    """fp32 ProxGD (the dense [z | p_thr] batch: k_trial_split re-derives z = x - t G_t)."""
+    v = run_sharded(tmp_path, 2, "gl_ProxGD_primal", 512, 1024, 16, dtype="f32", maxit=10,
+                    extra=("--shard-rows", "1"))
+    ranks = v["ranks"]
+    assert ranks[0]["x_sha"] == ranks[1]["x_sha"] and "rows=sharded" in ranks[0]["plan"]
+    assert abs(ranks[0]["fval"] - v["oracle_fval"]) / abs(v["oracle_fval"]) < 1e-5   # as test_sharded_fp32
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_host_reduce_scatter_all_gather(tmp_path, world):
+    """The row-sharded schedule's collectives on the host transport: reduce-scatter sums match
+    NumPy, the all-gather is bit-exact (-0.0, NaN, -inf chunks included)."""
+    v = run_sharded(tmp_path, world, "collectives", 1, 1, 1)
+    assert v["ok"] == [True] * world
+
+
+def test_row_sharded_needs_divisible_rows(tmp_path):
+    """shard_rows = 1 with n % G != 0 is refused; auto (0) keeps the all-reduce schedule."""
+    v = run_sharded(tmp_path, 3, "gl_ProxGD_primal", 515, 1024, 16, maxit=5, extra=("--shard-rows", "0"))
+    assert "rows=sharded" not in v["ranks"][0]["plan"]
+    with pytest.raises(AssertionError, match="n % ranks == 0"):
+        run_sharded(tmp_path, 3, "gl_ProxGD_primal", 515, 1024, 16, maxit=5, extra=("--shard-rows", "1"))
