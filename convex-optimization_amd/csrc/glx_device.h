@@ -166,6 +166,46 @@ __device__ inline void publish_packet(const double* s, int ns, double* host, uns
   __hip_atomic_store(host_seq, seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
+// Pub's deferred reductions, by the publishing workgroup (all its threads call this; the first
+// 256 work): each value over its partials strided over 256 threads in slot order, the butterfly,
+// the four waves in order — grid_reduce's order for a 256-thread launch, whichever kernel (4 or 8
+// waves) publishes. Thread 0 stores the results to dout (and then reads them back itself when it
+// copies the packet).
+template <int NW>
+__device__ inline void defer_reduce(const Pub& pub) {
+  static_assert(NW == 4 || NW == 8, "4- or 8-wave workgroups");
+  if (pub.dpart[0] == nullptr && pub.dpart[1] == nullptr) return;
+  __shared__ double dsh[2][6][4];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  if (threadIdx.x < 256) {
+#pragma unroll
+    for (int d = 0; d < 2; ++d) {
+      if (pub.dpart[d] == nullptr) continue;
+      const int nv = pub.dnv[d];
+      double acc[6];
+#pragma unroll
+      for (int j = 0; j < 6; ++j) acc[j] = identity((pub.dmax[d] >> j) & 1);
+      for (int i = threadIdx.x; i < pub.dnp[d]; i += 256)
+#pragma unroll
+        for (int j = 0; j < 6; ++j)
+          if (j < nv) acc[j] = combine((pub.dmax[d] >> j) & 1, acc[j], pub.dpart[d][i * nv + j]);
+#pragma unroll
+      for (int j = 0; j < 6; ++j)
+#pragma unroll
+        for (int off = 32; off > 0; off >>= 1)
+          acc[j] = combine((pub.dmax[d] >> j) & 1, acc[j], __shfl_xor(acc[j], off));
+      if (lane == 0)
+#pragma unroll
+        for (int j = 0; j < 6; ++j) dsh[d][j][wave] = acc[j];
+    }
+  }
+  __syncthreads();
+  if (threadIdx.x == 0)
+    for (int d = 0; d < 2; ++d)
+      if (pub.dpart[d] != nullptr)
+        for (int j = 0; j < pub.dnv[d]; ++j) pub.dout[d][j] = waves_combine<4>((pub.dmax[d] >> j) & 1, dsh[d][j]);
+}
+
 // A launch that carries the scalar packet gets one extra workgroup, the FIRST (blockIdx.x 0;
 // the other workgroups index themselves with blockIdx.x - 1), that writes it and then joins the
 // grid reduction with identity values (the reduction counts every workgroup). Workgroups are
@@ -177,6 +217,7 @@ __device__ inline void publish_packet(const double* s, int ns, double* host, uns
 template <int NV, unsigned MAXMASK, int NW = 4>
 __device__ inline bool publisher_first(const Pub& pub, const Red& red, int nparts = -1) {
   if (pub.host == nullptr || blockIdx.x != 0) return false;
+  defer_reduce<NW>(pub);
   if (threadIdx.x == 0)
     publish_packet(pub.s, pub.ns, pub.host, pub.host_seq, pub.seq, pub.s2, pub.off2, pub.n2,
                    pub.s3, pub.off3, pub.n3);
@@ -196,6 +237,7 @@ __device__ inline int work_slot(const Pub& pub) { return (int)blockIdx.x - (pub.
 template <int NV, unsigned MAXMASK, int NW = 4>
 __device__ inline bool publisher_last(const Pub& pub, const Red& red) {
   if (pub.host == nullptr || blockIdx.x != gridDim.x - 1) return false;
+  defer_reduce<NW>(pub);
   if (threadIdx.x == 0)
     publish_packet(pub.s, pub.ns, pub.host, pub.host_seq, pub.seq, pub.s2, pub.off2, pub.n2,
                    pub.s3, pub.off3, pub.n3);

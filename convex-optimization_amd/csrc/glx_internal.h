@@ -136,6 +136,14 @@ struct Pub {
   int off2 = 0, n2 = 0;
   const double* s3 = nullptr;   // host[off3 .. off3 + n3) come from s3 (a snapshot)
   int off3 = 0, n3 = 0;
+  // Round 5, deferred reductions: workgroup partials (Red::parts_only layout: dnv values per
+  // slot, dnp slots) that the publishing workgroup reduces (dmax bit j: max) into dout[0, dnv)
+  // before it copies the packet, so the kernels that produced them skip their grid reduction's
+  // serial tail (solver.cpp defer_)
+  const double* dpart[2] = {nullptr, nullptr};
+  int dnp[2] = {0, 0}, dnv[2] = {0, 0};
+  unsigned dmax[2] = {0u, 0u};
+  double* dout[2] = {nullptr, nullptr};
 };
 
 // Round 5: the split-candidate trial's residual finalize folded into the dense pass A p_thr
@@ -332,7 +340,9 @@ void launch_finalize_residual(const T* P, int S, const T* B, int nsrc, T* const*
                               const double* cmax, double* fh, double fh_mu, const double* fh_rn,
                               Red red, hipStream_t st, const double* snap_src = nullptr,
                               double* snap_dst = nullptr, int nsnap = 0, int chain = 0, int S0 = 0,
-                              Ctl ctl = Ctl{});
+                              Ctl ctl = Ctl{}, const double* cmax_parts = nullptr, int cmax_np = 0);
+// (cmax_parts: *cmax is still pending as the max column (index 3) of cmax_np trial partials,
+// Red::parts_only layout of 6 values, reduced by every workgroup for itself)
 // state[0..3] = s0..s3, *abort = 0 (one thread; the seed of a device-controlled batch)
 // the decision of a device-controlled ProxGD iteration with a communicator (one thread): out =
 // the all-reduced residual sums (a gradient set's tail); no-op once *c.abort != 0; the record
@@ -351,15 +361,16 @@ template <typename T>
 void launch_prox_pgd(const T* x, const T* g, int S, T* gout, T* p, T* pthr, T* z, int64_t n,
                      int64_t l, double t, double mu, double thres, Red red, hipStream_t st,
                      Pub pub = Pub{}, unsigned* zf = nullptr);
-// The row-sharded trial's all-gathered sums: blk holds nranks chunks of `chunk` doubles, [6, 10)
-// a finalize's sums (launch_finalize_residual's out), [kShardPartOff + 6 b, + 6) the trial's
-// (launch_prox_pgd's out) as the partials of its nbp workgroups (Red::parts_only). Combined in a
+// The row-sharded trial's all-gathered sums: blk holds nranks chunks of `chunk` doubles, from
+// kShardPartOff the workgroup partials (Red::parts_only) of the trial (launch_prox_pgd's out, 6
+// per workgroup, nbp workgroups) and then of its finalize (launch_finalize_residual's out, 4 per
+// workgroup, nbf workgroups). Combined in a
 // fixed order (sums; trial slot 3: max, NaN-propagating), identical on every rank: mask & 1 ->
 // tr[0, 6), mask & 2 -> rt[0, 4); with pub.host the scalar packet follows with these values.
 constexpr int kShardPartOff = 16;
 struct ShardPub {
   const double* blk = nullptr;
-  int nranks = 1, chunk = 0, nbp = 0, mask = 0;
+  int nranks = 1, chunk = 0, nbp = 0, nbf = 0, mask = 0;
   double* tr = nullptr;
   double* rt = nullptr;
   int tr_off = 0, rt_off = 0;   // their packet slots
@@ -368,6 +379,10 @@ struct ShardPub {
 void launch_shard_combine(const ShardPub& sp, hipStream_t st);
 // workgroups of launch_prox_pgd over n rows of l columns (without a packet)
 int prox_blocks(int64_t n, int64_t l);
+// reducing slots of launch_atr_prox (Red::parts_only partials: 6 values each)
+int atr_prox_slots(const GemmPlan& p, bool pub);
+// workgroups of launch_finalize_residual for these slabs and count length
+int finalize_blocks(int64_t ml, int S, int S0, int64_t cn);
 // Row-sharded schedule (round 5, solver.cpp iter_proxgd_shard): the replicated half of a ProxGD
 // trial, from the all-gathered p (n x l): pthr = p with |p| < thres zeroed; z = e = p - pthr
 // (emode) or z = xt - t (xt - p) / t (launch_prox_pgd's dense z, xt = the thresholded iterate);
@@ -445,6 +460,8 @@ template <typename T>
 void launch_sum_cols(const T* Gp, int S, T* G, int64_t n, hipStream_t st);
 // host[0..ns) = s[0..ns) except host[off2..off2+n2) = s2[0..n2) when s2 != NULL, then
 // *host_seq = seq (system-scope release); host memory is mapped
+// the packet of `pub` with its deferred reductions first (pub.host == NULL: the reductions only)
+void launch_publish_pub(const Pub& pub, hipStream_t st);
 void launch_publish(const double* s, int ns, double* host, unsigned* host_seq, unsigned seq,
                     hipStream_t st, const double* s2 = nullptr, int off2 = 0, int n2 = 0);
 

@@ -600,6 +600,10 @@ void launch_atr(const GemmPlan& p, const T* A, const T* R, T* Gp, hipStream_t st
 }
 
 
+int atr_prox_slots(const GemmPlan& p, bool pub) {
+  return (int)(p.n / (p.atr_wl == 3 ? 32 : 64)) + (pub ? 1 : 0);
+}
+
 bool atr_prox_ok(const GemmPlan& p) {
   if (p.atr_wl == 3)   // the 32-column panel: f64, no K splits (session_plan)
     return p.atr_kind == 1 && p.esize == 8 && p.atr_S == 1 && (p.l == 16 || p.l == 32) &&

@@ -106,7 +106,8 @@ __global__ __launch_bounds__(256) void k_finalize_residual(
     T* __restrict__ R2, int64_t ml, const int* __restrict__ gate, int epoch, int gate_mode,
     const T* __restrict__ cx, int64_t cn, const double* __restrict__ cmax, double* __restrict__ fh,
     double fh_mu, const double* __restrict__ fh_rn, Red red, const double* __restrict__ snap_src,
-    double* __restrict__ snap_dst, int nsnap, int chain, const T* __restrict__ P0, int S0, Ctl ctl) {
+    double* __restrict__ snap_dst, int nsnap, int chain, const T* __restrict__ P0, int S0, Ctl ctl,
+    const double* __restrict__ cmp, int cmnp) {
   // a cancelled launch (device-controlled batch) stores nothing and returns before the
   // reduction; the flag is tested at the first store, so its load overlaps the slab loads
   const bool skipped = red_skipped(red);
@@ -119,7 +120,20 @@ __global__ __launch_bounds__(256) void k_finalize_residual(
   if (!live && gate_mode == 0) return;  // uniform over the grid: nobody touches the ticket
   double v[4] = {0.0, 0.0, 0.0, 0.0};
   T* rs[3] = {R0, R1, R2};
-  const T thr = cx != nullptr ? (T)1e-6 * (T)(*cmax) : T(0);
+  double cm = 0.0;
+  if (cx != nullptr && cmp != nullptr) {   // max |p| still as the trial's partials (deferred)
+    __shared__ double wmax[4];
+    double mv = -__builtin_inf();
+    for (int i = threadIdx.x; i < cmnp; i += 256) mv = nan_max(mv, cmp[i * 6 + 3]);
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) mv = nan_max(mv, __shfl_xor(mv, off));
+    if ((threadIdx.x & 63) == 0) wmax[threadIdx.x >> 6] = mv;
+    __syncthreads();
+    cm = nan_max(nan_max(wmax[0], wmax[1]), nan_max(wmax[2], wmax[3]));
+  } else if (cx != nullptr) {
+    cm = *cmax;
+  }
+  const T thr = cx != nullptr ? (T)1e-6 * (T)cm : T(0);
   const int sub = threadIdx.x % G;
   const int64_t tid = (int64_t)blockIdx.x * 256 + threadIdx.x;
   const int64_t stride = (int64_t)gridDim.x * 256;
@@ -299,11 +313,11 @@ __global__ __launch_bounds__(256) void k_prox_pgd(const T* __restrict__ x, const
 // finalize's sums rank by rank. Writes tr / rt and, with sp.pub.host, the scalar packet with
 // these values in place (read from LDS, not back from memory).
 __device__ inline void shard_combine_block(const ShardPub& sp) {
-  __shared__ double wv[6][4];
+  __shared__ double wv[10][4];
   __shared__ double fin[10];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  double acc[10] = {0.0, 0.0, 0.0, -__builtin_inf(), 0.0, 0.0, 0.0, 0.0, 0.0, 0.0};
   if (sp.mask & 1) {
-    double acc[6] = {0.0, 0.0, 0.0, -__builtin_inf(), 0.0, 0.0};
     const int np = sp.nranks * sp.nbp;
     for (int i = threadIdx.x; i < np; i += 256) {
       const int r = i / sp.nbp, b = i - r * sp.nbp;
@@ -311,29 +325,31 @@ __device__ inline void shard_combine_block(const ShardPub& sp) {
 #pragma unroll
       for (int j = 0; j < 6; ++j) acc[j] = combine(j == 3 ? OP_MAX : OP_SUM, acc[j], q[j]);
     }
-#pragma unroll
-    for (int j = 0; j < 6; ++j)
-#pragma unroll
-      for (int off = 32; off > 0; off >>= 1)
-        acc[j] = combine(j == 3 ? OP_MAX : OP_SUM, acc[j], __shfl_xor(acc[j], off));
-    if (lane == 0)
-#pragma unroll
-      for (int j = 0; j < 6; ++j) wv[j][wave] = acc[j];
   }
+  if (sp.mask & 2) {
+    const int np = sp.nranks * sp.nbf;
+    for (int i = threadIdx.x; i < np; i += 256) {
+      const int r = i / sp.nbf, b = i - r * sp.nbf;
+      const double* q = sp.blk + (int64_t)r * sp.chunk + kShardPartOff + 6 * sp.nbp + b * 4;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc[6 + j] += q[j];
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < 10; ++j)
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1)
+      acc[j] = combine(j == 3 ? OP_MAX : OP_SUM, acc[j], __shfl_xor(acc[j], off));
+  if (lane == 0)
+#pragma unroll
+    for (int j = 0; j < 10; ++j) wv[j][wave] = acc[j];
   __syncthreads();
   if (threadIdx.x != 0) return;
+  for (int j = 0; j < 10; ++j) fin[j] = waves_combine<4>(j == 3 ? OP_MAX : OP_SUM, wv[j]);
   if (sp.mask & 1)
-    for (int j = 0; j < 6; ++j) {
-      fin[j] = waves_combine<4>(j == 3 ? OP_MAX : OP_SUM, wv[j]);
-      sp.tr[j] = fin[j];
-    }
+    for (int j = 0; j < 6; ++j) sp.tr[j] = fin[j];
   if (sp.mask & 2)
-    for (int j = 0; j < 4; ++j) {
-      double v = sp.blk[6 + j];
-      for (int r = 1; r < sp.nranks; ++r) v += sp.blk[(int64_t)r * sp.chunk + 6 + j];
-      fin[6 + j] = v;
-      sp.rt[j] = v;
-    }
+    for (int j = 0; j < 4; ++j) sp.rt[j] = fin[6 + j];
   if (sp.pub.host != nullptr)
     publish_packet(sp.pub.s, sp.pub.ns, sp.pub.host, sp.pub.host_seq, sp.pub.seq, fin, sp.tr_off,
                    (sp.mask & 1) ? 6 : 0, fin + 6, sp.rt_off, (sp.mask & 2) ? 4 : 0);
@@ -643,6 +659,14 @@ __global__ __launch_bounds__(256) void k_thr_axpby(T* __restrict__ xk, const T* 
   }
 }
 
+// the deferred reductions of a packet, then the packet (host == NULL: the reductions only)
+__global__ __launch_bounds__(256) void k_publish_pub(Pub pub) {
+  defer_reduce<4>(pub);
+  if (threadIdx.x == 0 && pub.host != nullptr)
+    publish_packet(pub.s, pub.ns, pub.host, pub.host_seq, pub.seq, pub.s2, pub.off2, pub.n2, pub.s3,
+                   pub.off3, pub.n3);
+}
+
 // publish the scalar packet to host-mapped memory: data, then (system-scope release) seq
 __global__ void k_publish(const double* __restrict__ s, int ns, double* host, unsigned* host_seq,
                           unsigned seq, const double* __restrict__ s2, int off2, int n2) {
@@ -717,32 +741,37 @@ static inline unsigned row_grid_pub(int64_t n, int lpr, const Pub& pub) {
   return std::min<unsigned>(row_grid(n, lpr), (unsigned)kMaxBlocks - 1) + (pub.host ? 1u : 0u);
 }
 
-template <typename T>
-void launch_finalize_residual(const T* P, int S, const T* B, int nsrc, T* const* R, int64_t ml,
-                              const int* gate, int epoch, int gate_mode, const T* cx, int64_t cn,
-                              const double* cmax, double* fh, double fh_mu, const double* fh_rn,
-                              Red red, hipStream_t st, const double* snap_src, double* snap_dst,
-                              int nsnap, int chain, int S0, Ctl ctl) {
-  if (chain && (nsrc != 2 || gate != nullptr)) throw Error{GLX_E_INVALID, "finalize: chain needs 2 ungated sources"};
-  if (S0 <= 0) S0 = S;
-  const int G = finalize_groups(S > S0 ? S : S0);
-  if (G > 8) throw Error{GLX_E_INVALID, "finalize: more than 64 K-split slabs"};
-  const int64_t work = ml * G > cn ? ml * G : cn;
-  // work items per workgroup (GLX_FIN_PER_BLOCK): one per thread, within the 1024-block cap.
-  // Measured (profiles/r2_fin*): 512 -> 256 takes C2 from 256 to 512 workgroups, +2.3 %;
-  // NS and the 1024-row shape sit at the cap either way; 1024-4096 lost 0-24 %.
+// work items per workgroup of k_finalize_residual (GLX_FIN_PER_BLOCK): one per thread, within
+// the 1024-block cap. Measured (profiles/r2_fin*): 512 -> 256 takes C2 from 256 to 512 workgroups,
+// +2.3 %; NS and the 1024-row shape sit at the cap either way; 1024-4096 lost 0-24 %.
+static int finalize_per_block() {
   static const int per_block = [] {
     const char* e = std::getenv("GLX_FIN_PER_BLOCK");
     const int v = e ? std::atoi(e) : 0;
     return v >= 256 ? v : 256;
   }();
-  const dim3 grid(grid_for(work, per_block));
+  return per_block;
+}
+template <typename T>
+void launch_finalize_residual(const T* P, int S, const T* B, int nsrc, T* const* R, int64_t ml,
+                              const int* gate, int epoch, int gate_mode, const T* cx, int64_t cn,
+                              const double* cmax, double* fh, double fh_mu, const double* fh_rn,
+                              Red red, hipStream_t st, const double* snap_src, double* snap_dst,
+                              int nsnap, int chain, int S0, Ctl ctl, const double* cmax_parts,
+                              int cmax_np) {
+  if (chain && (nsrc != 2 || gate != nullptr)) throw Error{GLX_E_INVALID, "finalize: chain needs 2 ungated sources"};
+  if (S0 <= 0) S0 = S;
+  const int G = finalize_groups(S > S0 ? S : S0);
+  if (G > 8) throw Error{GLX_E_INVALID, "finalize: more than 64 K-split slabs"};
+  const int64_t work = ml * G > cn ? ml * G : cn;
+  const dim3 grid(grid_for(work, finalize_per_block()));
   T* r1 = nsrc > 1 ? R[1] : nullptr;
   T* r2 = nsrc > 2 ? R[2] : nullptr;
   auto go = [&](auto ns, auto g) {
     hipLaunchKernelGGL((k_finalize_residual<T, decltype(ns)::value, decltype(g)::value>), grid,
                        dim3(256), 0, st, P, S, B, R[0], r1, r2, ml, gate, epoch, gate_mode, cx, cn,
-                       cmax, fh, fh_mu, fh_rn, red, snap_src, snap_dst, nsnap, chain, P, S0, ctl);
+                       cmax, fh, fh_mu, fh_rn, red, snap_src, snap_dst, nsnap, chain, P, S0, ctl,
+                       cmax_parts, cmax_np);
   };
   auto by_g = [&](auto ns) {
     if (G == 1) go(ns, std::integral_constant<int, 1>{});
@@ -797,6 +826,12 @@ void launch_trial_split(const T* p, const T* xt, T* pthr, T* z, unsigned* zf, in
 }
 void launch_shard_combine(const ShardPub& sp, hipStream_t st) {
   hipLaunchKernelGGL(k_shard_combine, dim3(1), dim3(256), 0, st, sp);
+}
+int finalize_blocks(int64_t ml, int S, int S0, int64_t cn) {
+  if (S0 <= 0) S0 = S;
+  const int G = finalize_groups(S > S0 ? S : S0);
+  const int64_t work = ml * G > cn ? ml * G : cn;
+  return (int)grid_for(work, finalize_per_block());
 }
 int prox_blocks(int64_t n, int64_t l) {
   int b = 0;
@@ -892,6 +927,9 @@ void launch_ctl_seed(double* state, int* abort, double s0, double s1, double s2,
   hipLaunchKernelGGL(k_ctl_seed, dim3(1), dim3(64), 0, st, state, abort, s0, s1, s2, s3);
 }
 
+void launch_publish_pub(const Pub& pub, hipStream_t st) {
+  hipLaunchKernelGGL(k_publish_pub, dim3(1), dim3(256), 0, st, pub);
+}
 void launch_publish(const double* s, int ns, double* host, unsigned* host_seq, unsigned seq,
                     hipStream_t st, const double* s2, int off2, int n2) {
   hipLaunchKernelGGL(k_publish, dim3(1), dim3(64), 0, st, s, ns, host, host_seq, seq, s2, off2,
@@ -902,7 +940,8 @@ void launch_publish(const double* s, int ns, double* host, unsigned* host_seq, u
   template void launch_finalize_residual<T>(const T*, int, const T*, int, T* const*, int64_t,       \
                                             const int*, int, int, const T*, int64_t, const double*, \
                                             double*, double, const double*, Red, hipStream_t,       \
-                                            const double*, double*, int, int, int, Ctl);            \
+                                            const double*, double*, int, int, int, Ctl,             \
+                                            const double*, int);                                    \
   template void launch_sum_partials<T>(const T*, int, T*, int64_t, hipStream_t);                    \
   template void launch_finalize_fista<T>(const T*, int, const T*, int, const T*, T*, const T*, T*,  \
                                          int64_t, double, double, double, const T*, int64_t,        \

@@ -95,7 +95,7 @@ constexpr int kMaxGSets = kCtlMaxBatch / 2 + 2;
 // row-sharded ProxGD (iter_proxgd_shard): each rank's chunk of sums that rides the all-gather
 // (the finalize's at [6, 10), the trial's workgroup partials from kShardPartOff, ShardPub), for
 // up to kMaxShardRanks ranks
-constexpr int kShardChunkMax = kShardPartOff + 6 * kMaxBlocks;
+constexpr int kShardChunkMax = kShardPartOff + (6 + 4) * kMaxBlocks;
 constexpr int kMaxShardRanks = 64;
 
 // device-controlled batches' window: opts.dc_window (> 0: that window, < 0: off), else
@@ -298,6 +298,10 @@ class Session : public SessionBase {
     double* dcr = static_cast<double*>(c.take(sizeof(double) * kCtlRec * kCtlMaxBatch));
     // split-candidate mode: per-row column masks of e = p - p_thr (z's buffer; bit c = e[k][c] != 0)
     unsigned* zf = static_cast<unsigned*>(c.take(zf_bytes(P.n)));   // + the column bitmaps
+    // deferred reductions (defer_): two trial partial buffers (the kernel that reduces one may run
+    // beside the next trial writing the other) and the finalize's
+    double* tpart = static_cast<double*>(c.take(sizeof(double) * 2 * 6 * kMaxBlocks));
+    double* fpart = static_cast<double*>(c.take(sizeof(double) * 4 * kMaxBlocks));
     double* sblk = P.comm != nullptr && P.method == GLX_PROXGD
                        ? static_cast<double*>(c.take(sizeof(double) * kShardChunkMax * kMaxShardRanks))
                        : nullptr;
@@ -319,6 +323,9 @@ class Session : public SessionBase {
       s->dc_rec_ = dcr;
       s->zf_ = zf;
       s->blk_ = sblk;
+      s->tpart_[0] = tpart;
+      s->tpart_[1] = tpart + 6 * kMaxBlocks;
+      s->fpart_ = fpart;
       s->E_ = ec;
       for (int k = 0; k < 3; ++k) s->SXO_[k] = sxo[k];
       s->sp100_ = sp100;
@@ -493,7 +500,11 @@ class Session : public SessionBase {
         srows_ = n_ / vr;
         srow0_ = (int64_t)srank_ * srows_;
         nbp_ = prox_blocks(srows_, l_);
-        schunk_ = kShardPartOff + 6 * nbp_;
+        // the trial finalize's workgroups (its sources: 2 in the split / dense modes, 3 exact)
+        const int fsrc = O.exact_objective != 0 ? 3 : 2;
+        nbf_ = finalize_blocks(ml_, emode_ && smode_ == 1 ? ax_split(plan_, 1) : ax_split(plan_, fsrc),
+                               emode_ && smode_ == 1 ? gsplit_ : 0, srows_ * l_);
+        schunk_ = kShardPartOff + 6 * nbp_ + 4 * nbf_;
         // A e from the bitmap / list gathers reads e only where its masks are set, where e = p:
         // the gathered p serves as e and z is not re-derived (the row form reads whole rows)
         zskip_ = emode_ && gform_ != 1;
@@ -501,6 +512,14 @@ class Session : public SessionBase {
         shard_model_ = false;
       }
     }
+    // Round 5, deferred reductions (single GPU, host control, ProxGD): the fused trial (k_atr_prox)
+    // and the residual finalize leave their sums as workgroup partials (Red::parts_only) instead
+    // of running the grid reduction's serial tail (two arrival counters, the last workgroup's
+    // loads: ~3 us at the end of each kernel); the workgroup that publishes the next packet
+    // reduces them first (Pub::dpart, defer_reduce), and the finalize takes max |p| from the
+    // trial's partials itself. GLX_DEFER_RED=0: off.
+    defer_ = comm_ == nullptr && dc_window_ == 0 && P.method == GLX_PROXGD && spin_readback_ &&
+             !fin_ok_ && !env_is("GLX_DEFER_RED", "0");
     GLX_HIP(hipMemsetAsync(ticket_, 0, kTicketBytes, st_));
     GLX_HIP(hipMemsetAsync(pcnt_, 0, sizeof(unsigned) * (P.n / 64 + 64), st_));
     GLX_HIP(hipMemsetAsync(fcnt_, 0, sizeof(unsigned) * (ax_fin_counters(plan_) + 64), st_));
@@ -792,14 +811,26 @@ class Session : public SessionBase {
       else spec_ax(nsrc, xs);
     }
     T* rsc[3] = {chain ? nullptr : rs[0], rs[1], rs[2]};
-    launch_finalize_residual<T>(Pp_, gat ? ax_split(plan_, 1) : ax_split(plan_, nsrc), B_, nsrc, rsc,
+    Red rd = defer ? red_to(defer) : red(slot);
+    const bool dfin = defer_ && defer == nullptr && !snap_trial && (comm_ ? nullptr : fh) == nullptr &&
+                      dc_ctl_.rec == nullptr;
+    // max |p| of a trial whose sums are still partials
+    const bool dmax = cx != nullptr && cmax == scal_ + S_TR + 3 && ptr_.part != nullptr;
+    const int S = gat ? ax_split(plan_, 1) : ax_split(plan_, nsrc);
+    if (dfin) {
+      rd.part = fpart_;
+      rd.parts_only = 1;
+    }
+    launch_finalize_residual<T>(Pp_, S, B_, nsrc, rsc,
                                 ml_, nullptr, 0, 1, cx,
                                 cx ? nl_ : 0, cmax, comm_ ? nullptr : fh, fh_mu, scal_ + S_DRN,
-                                defer ? red_to(defer) : red(slot), st_,
+                                rd, st_,
                                 snap_trial ? scal_ + S_TR : nullptr,
                                 snap_trial ? scal_ + S_SNAP : nullptr, snap_trial ? 6 : 0,
-                                chain ? 1 : 0, gat ? gsplit_ : 0, dc_ctl_);
+                                chain ? 1 : 0, gat ? gsplit_ : 0, dc_ctl_,
+                                dmax ? ptr_.part : nullptr, dmax ? ptr_.np : 0);
     check_launch();
+    if (dfin) pfin_ = Pend{fpart_, finalize_blocks(ml_, S, gat ? gsplit_ : 0, cx ? nl_ : 0), 4, 0u, scal_ + slot};
     if (defer) return;
     if (comm_) {
       comm_allreduce(comm_, scal_ + slot, nsrc, GLX_F64, st_);
@@ -943,6 +974,23 @@ class Session : public SessionBase {
   // extra != NULL: the packet's S_RT..S_RT+3 come from extra[0..4) (a gradient set's tail)
   unsigned post_readback(const double* extra = nullptr) {
     ++syncs_;
+    if (pending()) {   // deferred reductions: reduced by the publishing kernel first
+      Pub pb;
+      pb.s = scal_;
+      pb.ns = NSCAL;
+      pb.s2 = extra;
+      pb.off2 = S_RT;
+      pb.n2 = extra ? 4 : 0;
+      attach_pending(pb);
+      if (spin_readback_) {
+        pb.host = hs_dev_;
+        pb.host_seq = hseq_dev_;
+        pb.seq = ++seq_;
+      }
+      launch_publish_pub(pb, st_);
+      check_launch();
+      if (spin_readback_) return pb.seq;
+    }
     if (!spin_readback_) {   // GLX_READBACK=sync: stream-ordered copies, then an event wait
       GLX_HIP(hipMemcpyAsync(hs_, scal_, sizeof(double) * NSCAL, hipMemcpyDeviceToHost, st_));
       if (extra) GLX_HIP(hipMemcpyAsync(hs_ + S_RT, extra, 4 * sizeof(double), hipMemcpyDeviceToHost, st_));
@@ -967,8 +1015,31 @@ class Session : public SessionBase {
     pb.s2 = extra;
     pb.off2 = S_RT;
     pb.n2 = extra ? 4 : 0;
+    attach_pending(pb);
     *seq_out = pb.seq;
     return pb;
+  }
+  // deferred reductions (defer_): partials not yet reduced into their scalar slots
+  struct Pend {
+    const double* part = nullptr;
+    int np = 0, nv = 0;
+    unsigned mx = 0;
+    double* out = nullptr;
+  };
+  bool pending() const { return ptr_.part != nullptr || pfin_.part != nullptr; }
+  // the kernel carrying pb reduces the pending partials before it copies the packet
+  void attach_pending(Pub& pb) {
+    int d = 0;
+    for (Pend* q : {&ptr_, &pfin_}) {
+      if (q->part == nullptr) continue;
+      pb.dpart[d] = q->part;
+      pb.dnp[d] = q->np;
+      pb.dnv[d] = q->nv;
+      pb.dmax[d] = q->mx;
+      pb.dout[d] = q->out;
+      ++d;
+      *q = Pend{};
+    }
   }
   void wait_readback(unsigned seq) {
     if (!spin_readback_) {
@@ -1121,6 +1192,7 @@ class Session : public SessionBase {
                          (first && g.first != G_) ? G_ : nullptr, X_[ip_], X_[ipt_], X_[iz_], n_,
                          l_, tt, mu_, O_.thres, red(S_TR), st_, Pub{}, ezf());
       check_launch();
+      ptr_ = Pend{};   // S_TR holds this trial's sums
     };
     if (ls) {
       t = t0;
@@ -1275,11 +1347,6 @@ class Session : public SessionBase {
   }
   // one RCCL group: p's rows (op >= 0) and every rank's chunk of sums
   void shard_exchange(int op) {
-    if (shard_model_ && op >= 0) {   // timing model: this rank's rows stand in for the others'
-      const size_t bytes = sizeof(T) * (size_t)(srows_ * l_);   // (so e's row count is realistic)
-      for (int r = 1; r < sranks_; ++r)
-        GLX_HIP(hipMemcpyAsync(X_[op] + (size_t)r * srows_ * l_, X_[op], bytes, hipMemcpyDeviceToDevice, st_));
-    }
     comm_group_begin(comm_);
     if (op >= 0) comm_all_gather(comm_, X_[op], srows_ * l_, P_.dtype, st_);
     comm_all_gather(comm_, blk_, schunk_, GLX_F64, st_);
@@ -1293,6 +1360,7 @@ class Session : public SessionBase {
     sp.nranks = cranks_;
     sp.chunk = schunk_;
     sp.nbp = nbp_;
+    sp.nbf = nbf_;
     sp.mask = mask;
     sp.tr = scal_ + tr_dst;
     sp.rt = scal_ + S_RT;
@@ -1318,9 +1386,12 @@ class Session : public SessionBase {
     }
     T* rsc[3] = {chain ? nullptr : rs[0], rs[1], rs[2]};
     const int64_t o = srow0_ * l_;
+    Red rd = red_to(scal_ + S_RT);   // its workgroup partials ride the all-gather too
+    rd.part = blk_own() + kShardPartOff + 6 * nbp_;
+    rd.parts_only = 1;
     launch_finalize_residual<T>(Pp_, gat ? ax_split(plan_, 1) : ax_split(plan_, nsrc), B_, nsrc, rsc,
                                 ml_, nullptr, 0, 1, cx + o, srows_ * l_, cmax, nullptr, 0.0,
-                                scal_ + S_DRN, red_to(blk_own() + 6), st_, nullptr, nullptr, 0,
+                                scal_ + S_DRN, rd, st_, nullptr, nullptr, 0,
                                 chain ? 1 : 0, gat ? gsplit_ : 0, Ctl{});
     check_launch();
   }
@@ -1640,9 +1711,16 @@ class Session : public SessionBase {
     // in a device-controlled batch this speculative kernel also runs when the decision before it
     // stops the phase (abort = that decision's tag): the next phase starts from its gradient, as
     // on the host path; the speculative kernels queued after it do not run
+    Red rd = red(S_TR, dc_pass_);
+    if (defer_) {   // its trial sums stay partials (the other buffer than the one pb may reduce)
+      tb_ ^= 1;
+      rd.part = tpart_[tb_];
+      rd.parts_only = 1;
+    }
     launch_atr_prox<T>(plan_, A_, r, Gs_[set], x, X_[op], X_[opt], X_[oz], t, mu_, O_.thres,
-                       red(S_TR, dc_pass_), st_, pb, Gps_[set], pcnt_, ezf());
+                       rd, st_, pb, Gps_[set], pcnt_, ezf());
     check_launch();
+    if (defer_) ptr_ = Pend{tpart_[tb_], atr_prox_slots(plan_, pb.host != nullptr), 6, 0x8u, scal_ + S_TR};
     prof_end(1, e0);
     ++atr_calls_;
   }
@@ -2133,9 +2211,16 @@ class Session : public SessionBase {
   bool shard_ = false, shard_model_ = false;
   int srank_ = 0, sranks_ = 1, cranks_ = 1;
   int64_t srow0_ = 0, srows_ = 0;
-  int nbp_ = 0, schunk_ = 0;   // k_prox_pgd's workgroups on srows_ rows; doubles per rank's chunk
+  int nbp_ = 0, nbf_ = 0;      // k_prox_pgd's workgroups on srows_ rows, the trial finalize's
+  int schunk_ = 0;             // doubles per rank's chunk
   bool zskip_ = false;         // the gathered p serves as e (bitmap / list gathers)
   double* blk_ = nullptr;      // kMaxShardRanks chunks of sums (kShardChunkMax doubles each)
+  // deferred reductions (defer_, single GPU): the trial's and the finalize's pending partials
+  bool defer_ = false;
+  double* tpart_[2] = {nullptr, nullptr};
+  double* fpart_ = nullptr;
+  int tb_ = 0;
+  Pend ptr_, pfin_;
   int tr_slot_ = S_TR;         // the packet slots of the current trial's sums
   T* At_ = nullptr;            // A^T (split-candidate gather form)
   void* glists_ = nullptr;     // the gather's per-column index lists of e

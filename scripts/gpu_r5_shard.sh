@@ -21,5 +21,5 @@ unset GLX_SHARD_MODEL
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/tr_ar -o run -- python3 bench.py --m 1024 --force-comm --steps 200 --warmup 20 --no-cpu-baseline --no-whole-solve > $O/tr_ar.log 2>&1 || exit 1
 export GLX_SHARD_MODEL=8
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/tr_shard -o run -- python3 bench.py --m 1024 --force-comm --steps 200 --warmup 20 --no-cpu-baseline --no-whole-solve > $O/tr_shard.log 2>&1 || exit 1
-find $O -name "*kernel_stats.csv" | head
+python3 scripts/trace_db_summary.py $(find $O -name "*.db") | tee -a $O/status.txt
 echo done >> $O/status.txt

@@ -339,3 +339,31 @@ def test_folded_finalize_matches_separate_kernel(monkeypatch):
     assert k0 == k1 == 180
     assert np.array_equal(x0_, x1)
     assert np.max(np.abs(f1 - f0) / np.abs(f0)) < 1e-13
+
+
+@pytest.mark.parametrize("alpha_scale", [1.0, 2.5])
+def test_deferred_reductions_match(monkeypatch, alpha_scale):
+    """Round 5: ProxGD's fused trial and its residual finalize leave their sums as workgroup
+    partials that the next publishing workgroup reduces (GLX_DEFER_RED, default on). Same
+    decisions and bit-identical iterates as the grid reductions; the recorded objective moves by
+    summation order only. alpha_scale 2.5: rejected first trials (the pending sums of a dropped
+    speculative trial are discarded, the retrial's k_prox_pgd reduces in full)."""
+    from oracle import numpy_ref
+    m, n, l = 2048, 4096, 32
+    A, b, u, x0, mu = numpy_ref.gen_data(m, n, l, 5)
+    opts = {"alpha0": alpha_scale * numpy_ref.step_size_for(m, n), "maxit": 40}
+    import importlib
+    fn = getattr(importlib.import_module("gl_ProxGD_primal"), "gl_ProxGD_primal")
+    At, bt = torch.from_numpy(A).cuda(), torch.from_numpy(b).cuda()
+    runs = []
+    for d in ("0", "1"):
+        monkeypatch.setenv("GLX_DEFER_RED", d)
+        x, k, out = fn(torch.from_numpy(x0).cuda(), At, bt, mu, dict(opts))
+        runs.append((x.cpu().numpy(), k, np.asarray([float(v) for v in out["f_hist"]])))
+    (x0_, k0, f0), (x1, k1, f1) = runs
+    assert k0 == k1
+    assert np.array_equal(x0_, x1)
+    assert np.max(np.abs(f1 - f0) / np.abs(f0)) < 1e-13
+    xr, kr, outr = numpy_ref.gl_ProxGD_primal(x0, A, b, mu, dict(opts))
+    assert k1 == kr
+    assert np.max(np.abs(f1 - np.asarray(outr["f_hist"])) / np.abs(np.asarray(outr["f_hist"]))) < 1e-8
