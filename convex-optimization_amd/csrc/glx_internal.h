@@ -340,9 +340,10 @@ void launch_finalize_residual(const T* P, int S, const T* B, int nsrc, T* const*
                               const double* cmax, double* fh, double fh_mu, const double* fh_rn,
                               Red red, hipStream_t st, const double* snap_src = nullptr,
                               double* snap_dst = nullptr, int nsnap = 0, int chain = 0, int S0 = 0,
-                              Ctl ctl = Ctl{}, const double* cmax_parts = nullptr, int cmax_np = 0);
+                              Ctl ctl = Ctl{}, const double* cmax_parts = nullptr, int cmax_np = 0,
+                              int cmax_nv = 6);
 // (cmax_parts: *cmax is still pending as the max column (index 3) of cmax_np trial partials,
-// Red::parts_only layout of 6 values, reduced by every workgroup for itself)
+// Red::parts_only layout of cmax_nv values, reduced by every workgroup for itself)
 // state[0..3] = s0..s3, *abort = 0 (one thread; the seed of a device-controlled batch)
 // the decision of a device-controlled ProxGD iteration with a communicator (one thread): out =
 // the all-reduced residual sums (a gradient set's tail); no-op once *c.abort != 0; the record
@@ -383,6 +384,7 @@ int prox_blocks(int64_t n, int64_t l);
 int atr_prox_slots(const GemmPlan& p, bool pub);
 // workgroups of launch_finalize_residual for these slabs and count length
 int finalize_blocks(int64_t ml, int S, int S0, int64_t cn);
+int finalize_fista_blocks(int64_t ml, int S, int S0, int64_t cn);
 // Row-sharded schedule (round 5, solver.cpp iter_proxgd_shard): the replicated half of a ProxGD
 // trial, from the all-gathered p (n x l): pthr = p with |p| < thres zeroed; z = e = p - pthr
 // (emode) or z = xt - t (xt - p) / t (launch_prox_pgd's dense z, xt = the thresholded iterate);
@@ -413,7 +415,8 @@ template <typename T>
 void launch_finalize_fista(const T* P, int S, const T* Pe, int S0, const T* B, T* Ry, const T* sxo,
                            T* sxo_out, int64_t ml, double a1, double b1, double theta, const T* cx,
                            int64_t cn, const double* cmax, const unsigned* counts, int nl, Red red,
-                           hipStream_t st, Ctl ctl = Ctl{});
+                           hipStream_t st, Ctl ctl = Ctl{}, const double* cmax_parts = nullptr,
+                           int cmax_np = 0, int cmax_nv = 4);
 // plain prox of W (glx_prox): out: [sum ||x_i||, max |x|]
 template <typename T>
 void launch_prox_plain(const T* w, T* x, int64_t n, int64_t l, double t, double mu, double thres,

@@ -100,6 +100,21 @@ __global__ void k_ctl_seed(double* state, int* abort, double s0, double s1, doub
   }
 }
 
+// *cmax, or (cmp != NULL: the trial's sums still pending as Red::parts_only partials, cmnv values
+// per slot) the max of their column 3 over cmnp slots, by every workgroup for itself (all 256
+// threads call this; the result is order-independent)
+__device__ inline double pending_max(const double* cmax, const double* __restrict__ cmp, int cmnp, int cmnv) {
+  if (cmp == nullptr) return *cmax;
+  __shared__ double wmax[4];
+  double mv = -__builtin_inf();
+  for (int i = threadIdx.x; i < cmnp; i += 256) mv = nan_max(mv, cmp[i * cmnv + 3]);
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) mv = nan_max(mv, __shfl_xor(mv, off));
+  if ((threadIdx.x & 63) == 0) wmax[threadIdx.x >> 6] = mv;
+  __syncthreads();
+  return nan_max(nan_max(wmax[0], wmax[1]), nan_max(wmax[2], wmax[3]));
+}
+
 template <typename T, int NSRC, int G>
 __global__ __launch_bounds__(256) void k_finalize_residual(
     const T* __restrict__ P, int S, const T* __restrict__ B, T* __restrict__ R0, T* __restrict__ R1,
@@ -107,7 +122,7 @@ __global__ __launch_bounds__(256) void k_finalize_residual(
     const T* __restrict__ cx, int64_t cn, const double* __restrict__ cmax, double* __restrict__ fh,
     double fh_mu, const double* __restrict__ fh_rn, Red red, const double* __restrict__ snap_src,
     double* __restrict__ snap_dst, int nsnap, int chain, const T* __restrict__ P0, int S0, Ctl ctl,
-    const double* __restrict__ cmp, int cmnp) {
+    const double* __restrict__ cmp, int cmnp, int cmnv) {
   // a cancelled launch (device-controlled batch) stores nothing and returns before the
   // reduction; the flag is tested at the first store, so its load overlaps the slab loads
   const bool skipped = red_skipped(red);
@@ -120,20 +135,7 @@ __global__ __launch_bounds__(256) void k_finalize_residual(
   if (!live && gate_mode == 0) return;  // uniform over the grid: nobody touches the ticket
   double v[4] = {0.0, 0.0, 0.0, 0.0};
   T* rs[3] = {R0, R1, R2};
-  double cm = 0.0;
-  if (cx != nullptr && cmp != nullptr) {   // max |p| still as the trial's partials (deferred)
-    __shared__ double wmax[4];
-    double mv = -__builtin_inf();
-    for (int i = threadIdx.x; i < cmnp; i += 256) mv = nan_max(mv, cmp[i * 6 + 3]);
-#pragma unroll
-    for (int off = 32; off > 0; off >>= 1) mv = nan_max(mv, __shfl_xor(mv, off));
-    if ((threadIdx.x & 63) == 0) wmax[threadIdx.x >> 6] = mv;
-    __syncthreads();
-    cm = nan_max(nan_max(wmax[0], wmax[1]), nan_max(wmax[2], wmax[3]));
-  } else if (cx != nullptr) {
-    cm = *cmax;
-  }
-  const T thr = cx != nullptr ? (T)1e-6 * (T)cm : T(0);
+  const T thr = cx != nullptr ? (T)1e-6 * (T)pending_max(cmax, cmp, cmnp, cmnv) : T(0);
   const int sub = threadIdx.x % G;
   const int64_t tid = (int64_t)blockIdx.x * 256 + threadIdx.x;
   const int64_t stride = (int64_t)gridDim.x * 256;
@@ -189,7 +191,8 @@ __global__ __launch_bounds__(256) void k_finalize_fista(
     const T* __restrict__ P, int S, const T* __restrict__ Pe, int S0, const T* __restrict__ B,
     T* __restrict__ Ry, const T* __restrict__ sxo, T* __restrict__ sxo_out, int64_t ml, double a1_,
     double b1_, double theta_, const T* __restrict__ cx, int64_t cn, const double* __restrict__ cmax,
-    const unsigned* __restrict__ counts, int nl, Red red, Ctl ctl) {
+    const unsigned* __restrict__ counts, int nl, Red red, Ctl ctl, const double* __restrict__ cmp,
+    int cmnp, int cmnv) {
   const bool skipped = red_skipped(red);   // cancelled in a device-controlled batch
   double pre[10];
   if (ctl.rec != nullptr && threadIdx.x == 0) {
@@ -199,7 +202,7 @@ __global__ __launch_bounds__(256) void k_finalize_fista(
   const T a1 = (T)a1_, b1 = (T)b1_, theta = (T)theta_;
   double v[4] = {0.0, 0.0, 0.0, 0.0};
   if (blockIdx.x == 0 && (int)threadIdx.x < nl) v[2] = (double)counts[threadIdx.x];
-  const T thr = cx != nullptr ? (T)1e-6 * (T)(*cmax) : T(0);
+  const T thr = cx != nullptr ? (T)1e-6 * (T)pending_max(cmax, cmp, cmnp, cmnv) : T(0);
   const int sub = threadIdx.x % G;
   const int64_t tid = (int64_t)blockIdx.x * 256 + threadIdx.x;
   const int64_t stride = (int64_t)gridDim.x * 256;
@@ -758,7 +761,7 @@ void launch_finalize_residual(const T* P, int S, const T* B, int nsrc, T* const*
                               const double* cmax, double* fh, double fh_mu, const double* fh_rn,
                               Red red, hipStream_t st, const double* snap_src, double* snap_dst,
                               int nsnap, int chain, int S0, Ctl ctl, const double* cmax_parts,
-                              int cmax_np) {
+                              int cmax_np, int cmax_nv) {
   if (chain && (nsrc != 2 || gate != nullptr)) throw Error{GLX_E_INVALID, "finalize: chain needs 2 ungated sources"};
   if (S0 <= 0) S0 = S;
   const int G = finalize_groups(S > S0 ? S : S0);
@@ -771,7 +774,7 @@ void launch_finalize_residual(const T* P, int S, const T* B, int nsrc, T* const*
     hipLaunchKernelGGL((k_finalize_residual<T, decltype(ns)::value, decltype(g)::value>), grid,
                        dim3(256), 0, st, P, S, B, R[0], r1, r2, ml, gate, epoch, gate_mode, cx, cn,
                        cmax, fh, fh_mu, fh_rn, red, snap_src, snap_dst, nsnap, chain, P, S0, ctl,
-                       cmax_parts, cmax_np);
+                       cmax_parts, cmax_np, cmax_nv);
   };
   auto by_g = [&](auto ns) {
     if (G == 1) go(ns, std::integral_constant<int, 1>{});
@@ -787,14 +790,16 @@ template <typename T>
 void launch_finalize_fista(const T* P, int S, const T* Pe, int S0, const T* B, T* Ry, const T* sxo,
                            T* sxo_out, int64_t ml, double a1, double b1, double theta, const T* cx,
                            int64_t cn, const double* cmax, const unsigned* counts, int nl, Red red,
-                           hipStream_t st, Ctl ctl) {
+                           hipStream_t st, Ctl ctl, const double* cmax_parts, int cmax_np,
+                           int cmax_nv) {
   const int G = finalize_groups(S > S0 ? S : S0);
   if (G > 8) throw Error{GLX_E_INVALID, "finalize: more than 64 K-split slabs"};
   const int64_t work = ml * G > cn ? ml * G : cn;
   const dim3 grid(grid_for(work, 256 * 2));
   auto go = [&](auto g) {
     hipLaunchKernelGGL((k_finalize_fista<T, decltype(g)::value>), grid, dim3(256), 0, st, P, S, Pe,
-                       S0, B, Ry, sxo, sxo_out, ml, a1, b1, theta, cx, cn, cmax, counts, nl, red, ctl);
+                       S0, B, Ry, sxo, sxo_out, ml, a1, b1, theta, cx, cn, cmax, counts, nl, red, ctl,
+                       cmax_parts, cmax_np, cmax_nv);
   };
   if (G == 1) go(std::integral_constant<int, 1>{});
   else if (G == 2) go(std::integral_constant<int, 2>{});
@@ -832,6 +837,11 @@ int finalize_blocks(int64_t ml, int S, int S0, int64_t cn) {
   const int G = finalize_groups(S > S0 ? S : S0);
   const int64_t work = ml * G > cn ? ml * G : cn;
   return (int)grid_for(work, finalize_per_block());
+}
+int finalize_fista_blocks(int64_t ml, int S, int S0, int64_t cn) {
+  const int G = finalize_groups(S > S0 ? S : S0);
+  const int64_t work = ml * G > cn ? ml * G : cn;
+  return (int)grid_for(work, 256 * 2);
 }
 int prox_blocks(int64_t n, int64_t l) {
   int b = 0;
@@ -941,11 +951,12 @@ void launch_publish(const double* s, int ns, double* host, unsigned* host_seq, u
                                             const int*, int, int, const T*, int64_t, const double*, \
                                             double*, double, const double*, Red, hipStream_t,       \
                                             const double*, double*, int, int, int, Ctl,             \
-                                            const double*, int);                                    \
+                                            const double*, int, int);                               \
   template void launch_sum_partials<T>(const T*, int, T*, int64_t, hipStream_t);                    \
   template void launch_finalize_fista<T>(const T*, int, const T*, int, const T*, T*, const T*, T*,  \
                                          int64_t, double, double, double, const T*, int64_t,        \
-                                         const double*, const unsigned*, int, Red, hipStream_t, Ctl);\
+                                         const double*, const unsigned*, int, Red, hipStream_t, Ctl,\
+                                         const double*, int, int);                                  \
   template void launch_trial_split<T>(const T*, const T*, T*, T*, unsigned*, int64_t, int64_t,       \
                                       double, double, bool, const ShardPub&, hipStream_t);            \
   template void launch_prox_pgd<T>(const T*, const T*, int, T*, T*, T*, T*, int64_t, int64_t,       \

@@ -518,8 +518,9 @@ class Session : public SessionBase {
     // loads: ~3 us at the end of each kernel); the workgroup that publishes the next packet
     // reduces them first (Pub::dpart, defer_reduce), and the finalize takes max |p| from the
     // trial's partials itself. GLX_DEFER_RED=0: off.
-    defer_ = comm_ == nullptr && dc_window_ == 0 && P.method == GLX_PROXGD && spin_readback_ &&
-             !fin_ok_ && !env_is("GLX_DEFER_RED", "0");
+    defer_ = comm_ == nullptr && dc_window_ == 0 &&
+             (P.method == GLX_PROXGD || P.method == GLX_FPROXGD) && spin_readback_ && !fin_ok_ &&
+             !env_is("GLX_DEFER_RED", "0");
     GLX_HIP(hipMemsetAsync(ticket_, 0, kTicketBytes, st_));
     GLX_HIP(hipMemsetAsync(pcnt_, 0, sizeof(unsigned) * (P.n / 64 + 64), st_));
     GLX_HIP(hipMemsetAsync(fcnt_, 0, sizeof(unsigned) * (ax_fin_counters(plan_) + 64), st_));
@@ -815,9 +816,10 @@ class Session : public SessionBase {
     const bool dfin = defer_ && defer == nullptr && !snap_trial && (comm_ ? nullptr : fh) == nullptr &&
                       dc_ctl_.rec == nullptr;
     // max |p| of a trial whose sums are still partials
-    const bool dmax = cx != nullptr && cmax == scal_ + S_TR + 3 && ptr_.part != nullptr;
+    const bool dmax = cx != nullptr && ptr_.part != nullptr && cmax == ptr_.out + 3;
     const int S = gat ? ax_split(plan_, 1) : ax_split(plan_, nsrc);
     if (dfin) {
+      flush_fin_pending();
       rd.part = fpart_;
       rd.parts_only = 1;
     }
@@ -828,7 +830,7 @@ class Session : public SessionBase {
                                 snap_trial ? scal_ + S_TR : nullptr,
                                 snap_trial ? scal_ + S_SNAP : nullptr, snap_trial ? 6 : 0,
                                 chain ? 1 : 0, gat ? gsplit_ : 0, dc_ctl_,
-                                dmax ? ptr_.part : nullptr, dmax ? ptr_.np : 0);
+                                dmax ? ptr_.part : nullptr, dmax ? ptr_.np : 0, dmax ? ptr_.nv : 6);
     check_launch();
     if (dfin) pfin_ = Pend{fpart_, finalize_blocks(ml_, S, gat ? gsplit_ : 0, cx ? nl_ : 0), 4, 0u, scal_ + slot};
     if (defer) return;
@@ -1027,6 +1029,20 @@ class Session : public SessionBase {
     double* out = nullptr;
   };
   bool pending() const { return ptr_.part != nullptr || pfin_.part != nullptr; }
+  // a finalize's partials still pending when the next finalize would overwrite them (FProxGD's
+  // g(y) residual ahead of the trial's batch): reduced on their own first
+  void flush_fin_pending() {
+    if (pfin_.part == nullptr) return;
+    Pub pb;
+    pb.dpart[0] = pfin_.part;
+    pb.dnp[0] = pfin_.np;
+    pb.dnv[0] = pfin_.nv;
+    pb.dmax[0] = pfin_.mx;
+    pb.dout[0] = pfin_.out;
+    pfin_ = Pend{};
+    launch_publish_pub(pb, st_);
+    check_launch();
+  }
   // the kernel carrying pb reduces the pending partials before it copies the packet
   void attach_pending(Pub& pb) {
     int d = 0;
@@ -1793,6 +1809,7 @@ class Session : public SessionBase {
                             X_[iyn_], n_, l_, tt, mu_, O_.thres, theta, theta_next, O_.delta,
                             red(S_TR), st_, Pub{}, fec(), fzf());
       check_launch();
+      ptr_ = Pend{};   // S_TR holds this trial's sums
     };
     const int i_rn = smooth ? 3 : 2, i_max = smooth ? 4 : 3;
     bool fs_batch = false;
@@ -2078,11 +2095,23 @@ class Session : public SessionBase {
                          const double* cmax, unsigned* pub_seq, double* defer) {
     const T* xs[3] = {E_, X_[ic_], nullptr};
     cand_ax(xs);
+    Red rd = defer ? Red{part_, ticket_, defer} : red(slot);
+    const bool dfin = defer_ && defer == nullptr;
+    const bool dmax = cx != nullptr && ptr_.part != nullptr && cmax == ptr_.out + 3;
+    if (dfin) {
+      flush_fin_pending();
+      rd.part = fpart_;
+      rd.parts_only = 1;
+    }
     launch_finalize_fista<T>(Pp_ + (size_t)gsplit_ * ml_, ax_split(plan_, 1), Pp_, gsplit_, B_, ry,
                              SXO_[kslot_], SXO_[(kslot_ + 1) % 3], ml_, 1.0 - theta_next,
                              theta_next, theta, cx, nl_, cmax, gather_counts(glists_, n_), gcount_n(),
-                             defer ? Red{part_, ticket_, defer} : red(slot), st_);
+                             rd, st_, Ctl{}, dmax ? ptr_.part : nullptr, dmax ? ptr_.np : 0,
+                             dmax ? ptr_.nv : 4);
     check_launch();
+    if (dfin)
+      pfin_ = Pend{fpart_, finalize_fista_blocks(ml_, ax_split(plan_, 1), gsplit_, cx ? nl_ : 0), 4, 0u,
+                   scal_ + slot};
     if (defer) return;
     if (comm_) comm_allreduce(comm_, scal_ + slot, 2, GLX_F64, st_);
     if (pub_seq != nullptr) *pub_seq = post_readback();
@@ -2108,9 +2137,16 @@ class Session : public SessionBase {
     Pub pb = dc_pub_;   // in a device-controlled batch: the decision record (fista_dc_queue)
     if (pub_seq) pb = make_pub(extra, pub_seq);
     hipEvent_t e0 = prof_begin(1);
+    Red rd = red(S_TR, dc_pass_);
+    if (defer_) {   // its trial sums stay partials (as atr_prox)
+      tb_ ^= 1;
+      rd.part = tpart_[tb_];
+      rd.parts_only = 1;
+    }
     launch_atr_fista<T>(plan_, A_, r, Gs_[set], yv, xk, X_[oc], X_[ov], X_[oy], t, mu_, O_.thres,
-                        theta, theta_next, red(S_TR, dc_pass_), st_, pb, Gps_[set], pcnt_, fec(), fzf());
+                        theta, theta_next, rd, st_, pb, Gps_[set], pcnt_, fec(), fzf());
     check_launch();
+    if (defer_) ptr_ = Pend{tpart_[tb_], atr_prox_slots(plan_, pb.host != nullptr), 4, 0x8u, scal_ + S_TR};
     prof_end(1, e0);
     ++atr_calls_;
   }

@@ -341,19 +341,21 @@ def test_folded_finalize_matches_separate_kernel(monkeypatch):
     assert np.max(np.abs(f1 - f0) / np.abs(f0)) < 1e-13
 
 
-@pytest.mark.parametrize("alpha_scale", [1.0, 2.5])
-def test_deferred_reductions_match(monkeypatch, alpha_scale):
+@pytest.mark.parametrize("solver,alpha_scale", [("gl_ProxGD_primal", 1.0), ("gl_ProxGD_primal", 2.5),
+                                               ("gl_FProxGD_primal", 1.0), ("gl_FProxGD_primal", 3.0)])
+def test_deferred_reductions_match(monkeypatch, solver, alpha_scale):
     """Round 5: ProxGD's fused trial and its residual finalize leave their sums as workgroup
     partials that the next publishing workgroup reduces (GLX_DEFER_RED, default on). Same
     decisions and bit-identical iterates as the grid reductions; the recorded objective moves by
     summation order only. alpha_scale 2.5: rejected first trials (the pending sums of a dropped
-    speculative trial are discarded, the retrial's k_prox_pgd reduces in full)."""
+    speculative trial are discarded, the retrial's k_prox_pgd reduces in full). FProxGD: the fused
+    backtracking trial (k_atr_fista) and its batch's finalize the same way."""
     from oracle import numpy_ref
     m, n, l = 2048, 4096, 32
     A, b, u, x0, mu = numpy_ref.gen_data(m, n, l, 5)
     opts = {"alpha0": alpha_scale * numpy_ref.step_size_for(m, n), "maxit": 40}
     import importlib
-    fn = getattr(importlib.import_module("gl_ProxGD_primal"), "gl_ProxGD_primal")
+    fn = getattr(importlib.import_module(solver), solver)
     At, bt = torch.from_numpy(A).cuda(), torch.from_numpy(b).cuda()
     runs = []
     for d in ("0", "1"):
@@ -364,6 +366,6 @@ def test_deferred_reductions_match(monkeypatch, alpha_scale):
     assert k0 == k1
     assert np.array_equal(x0_, x1)
     assert np.max(np.abs(f1 - f0) / np.abs(f0)) < 1e-13
-    xr, kr, outr = numpy_ref.gl_ProxGD_primal(x0, A, b, mu, dict(opts))
+    xr, kr, outr = numpy_ref.SOLVERS[solver](x0, A, b, mu, dict(opts))
     assert k1 == kr
     assert np.max(np.abs(f1 - np.asarray(outr["f_hist"])) / np.abs(np.asarray(outr["f_hist"]))) < 1e-8
