@@ -6,7 +6,9 @@ each solving its row shard of the same instance; the decisions run on the device
 gradient all-reduce. Every run must be bit-identical to host control (GLX_DC_BATCH=0) — same k,
 f_hist to the last bit, fval, iterate and threshold statistics — and identical on both ranks.
 fp32 keeps host control with a communicator (its trial sums do not ride the gradient
-all-reduce), so its twin checks that it stays host-controlled and identical.
+all-reduce), so its twin checks that it stays host-controlled and identical. Host control here is
+the gradient all-reduce schedule (opts shard_rows = 2), the one device control runs: ProxGD's
+row-sharded schedule (host control only) adds its trial sums in another order.
 """
 import json
 import os
@@ -35,7 +37,8 @@ def _twin(tmp_path, shape, dtype="f64", scale=1.0, opts=None, env=None, windows=
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes", "1", "--nproc-per-node", "2",
            "--master-addr", "127.0.0.1", "--master-port", str(_port()),
            os.path.join(ROOT, "tests", "dc_dist_worker.py"), "--shape", ",".join(map(str, shape)),
-           "--dtype", dtype, "--alpha-scale", str(scale), "--opts", json.dumps(opts or {}),
+           "--dtype", dtype, "--alpha-scale", str(scale),
+           "--opts", json.dumps(dict({"shard_rows": 2}, **(opts or {}))),
            "--env", json.dumps(env or {}), "--windows", windows, "--slices", str(slices),
            "--out", str(out), "--method", method] + ([] if mu is None else ["--mu", repr(mu)])
     p = subprocess.run(cmd, env=dict(os.environ, OMP_NUM_THREADS="1"), capture_output=True,
