@@ -115,6 +115,21 @@ __device__ inline double pending_max(const double* cmax, const double* __restric
   return nan_max(nan_max(wmax[0], wmax[1]), nan_max(wmax[2], wmax[3]));
 }
 
+// count(|cx| > 1e-6 cm) over this thread's indices tid, tid + stride, ...: the first kCountAhead
+// values already in cxv (loaded ahead), the rest read here
+constexpr int kCountAhead = 2;
+template <typename T>
+__device__ inline double count_above(const T* __restrict__ cx, int64_t cn, const T (&cxv)[kCountAhead],
+                                     int64_t tid, int64_t stride, double cm) {
+  const T thr = (T)1e-6 * (T)cm;
+  double c = 0.0;
+#pragma unroll
+  for (int q = 0; q < kCountAhead; ++q)
+    if (tid + q * stride < cn) c += (tabs(cxv[q]) > thr) ? 1.0 : 0.0;
+  for (int64_t idx = tid + kCountAhead * stride; idx < cn; idx += stride) c += (tabs(cx[idx]) > thr) ? 1.0 : 0.0;
+  return c;
+}
+
 template <typename T, int NSRC, int G>
 __global__ __launch_bounds__(256) void k_finalize_residual(
     const T* __restrict__ P, int S, const T* __restrict__ B, T* __restrict__ R0, T* __restrict__ R1,
@@ -135,10 +150,15 @@ __global__ __launch_bounds__(256) void k_finalize_residual(
   if (!live && gate_mode == 0) return;  // uniform over the grid: nobody touches the ticket
   double v[4] = {0.0, 0.0, 0.0, 0.0};
   T* rs[3] = {R0, R1, R2};
-  const T thr = cx != nullptr ? (T)1e-6 * (T)pending_max(cmax, cmp, cmnp, cmnv) : T(0);
   const int sub = threadIdx.x % G;
   const int64_t tid = (int64_t)blockIdx.x * 256 + threadIdx.x;
   const int64_t stride = (int64_t)gridDim.x * 256;
+  // the count's first kCountAhead values are loaded before the slab loads (their latencies
+  // overlap); the threshold (max |cx|) is known only later
+  T cxv[kCountAhead];
+#pragma unroll
+  for (int q = 0; q < kCountAhead; ++q)
+    cxv[q] = (cx != nullptr && tid + q * stride < cn) ? cx[tid + q * stride] : T(0);
   // residual elements: G lanes per element; the lanes of a group share idx, so they enter and
   // leave the loop together and the butterfly only reads active partners
   for (int64_t idx = tid / G; idx < ml; idx += stride / G) {
@@ -168,9 +188,8 @@ __global__ __launch_bounds__(256) void k_finalize_residual(
       if (sub == 0) v[sr] += (double)(r * r);
     }
   }
-  if (skipped) return;   // (threads without a residual element)
-  if (cx != nullptr)
-    for (int64_t idx = tid; idx < cn; idx += stride) v[3] += (tabs(cx[idx]) > thr) ? 1.0 : 0.0;
+  if (skipped) return;   // (threads without a residual element; uniform over the grid)
+  if (cx != nullptr) v[3] = count_above(cx, cn, cxv, tid, stride, pending_max(cmax, cmp, cmnp, cmnv));
   const bool last = grid_reduce<4, 0u>(v, red);
   if (last && fh != nullptr && threadIdx.x == 0) *fh = 0.5 * red.out[0] + fh_mu * (*fh_rn);
   // snapshot of the preceding trial's sums for a packet published after the next trial has
@@ -202,10 +221,13 @@ __global__ __launch_bounds__(256) void k_finalize_fista(
   const T a1 = (T)a1_, b1 = (T)b1_, theta = (T)theta_;
   double v[4] = {0.0, 0.0, 0.0, 0.0};
   if (blockIdx.x == 0 && (int)threadIdx.x < nl) v[2] = (double)counts[threadIdx.x];
-  const T thr = cx != nullptr ? (T)1e-6 * (T)pending_max(cmax, cmp, cmnp, cmnv) : T(0);
   const int sub = threadIdx.x % G;
   const int64_t tid = (int64_t)blockIdx.x * 256 + threadIdx.x;
   const int64_t stride = (int64_t)gridDim.x * 256;
+  T cxv[kCountAhead];   // (as k_finalize_residual)
+#pragma unroll
+  for (int q = 0; q < kCountAhead; ++q)
+    cxv[q] = (cx != nullptr && tid + q * stride < cn) ? cx[tid + q * stride] : T(0);
   for (int64_t idx = tid / G; idx < ml; idx += stride / G) {
     const T bv = B[idx];
     const T sx = group_slab_sum<T, G>(P, S, ml, idx, sub);
@@ -223,8 +245,7 @@ __global__ __launch_bounds__(256) void k_finalize_fista(
     }
   }
   if (skipped) return;
-  if (cx != nullptr)
-    for (int64_t idx = tid; idx < cn; idx += stride) v[3] += (tabs(cx[idx]) > thr) ? 1.0 : 0.0;
+  if (cx != nullptr) v[3] = count_above(cx, cn, cxv, tid, stride, pending_max(cmax, cmp, cmnp, cmnv));
   const bool last = grid_reduce<4, 0u>(v, red);
   if (last && ctl.rec != nullptr && threadIdx.x == 0) ctl_decide(ctl, red.out, pre);
 }

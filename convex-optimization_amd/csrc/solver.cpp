@@ -518,8 +518,16 @@ class Session : public SessionBase {
     // loads: ~3 us at the end of each kernel); the workgroup that publishes the next packet
     // reduces them first (Pub::dpart, defer_reduce), and the finalize takes max |p| from the
     // trial's partials itself. GLX_DEFER_RED=0: off.
-    defer_ = comm_ == nullptr && dc_window_ == 0 &&
-             (P.method == GLX_PROXGD || P.method == GLX_FPROXGD) && spin_readback_ && !fin_ok_ &&
+    // Only where the packet that follows is carried by the next speculative kernel (carry_): a
+    // standalone k_publish_pub that reduces them and then writes the packet measured 17-19 us
+    // against 4 us for k_publish (profiles/r5_probe/), so the non-speculative paths keep the
+    // in-kernel reduction.
+    // ProxGD only: FProxGD's k_atr_fista measured no gain (NS FProxGD 2583 / 2582, C3 4527 / 4535
+    // it/s over 200 steps, profiles/r5_defer3/) and lost 8 % on the rejection-heavy probe
+    // (its publisher's reduction stretched the 33 us fused kernel by ~4 us); GLX_DEFER_RED=2 takes
+    // it for FProxGD too.
+    const bool dmeth = P.method == GLX_PROXGD || (P.method == GLX_FPROXGD && env_is("GLX_DEFER_RED", "2"));
+    defer_ = comm_ == nullptr && dc_window_ == 0 && dmeth && spin_readback_ && attach_ok_ && !fin_ok_ &&
              !env_is("GLX_DEFER_RED", "0");
     GLX_HIP(hipMemsetAsync(ticket_, 0, kTicketBytes, st_));
     GLX_HIP(hipMemsetAsync(pcnt_, 0, sizeof(unsigned) * (P.n / 64 + 64), st_));
@@ -813,8 +821,8 @@ class Session : public SessionBase {
     }
     T* rsc[3] = {chain ? nullptr : rs[0], rs[1], rs[2]};
     Red rd = defer ? red_to(defer) : red(slot);
-    const bool dfin = defer_ && defer == nullptr && !snap_trial && (comm_ ? nullptr : fh) == nullptr &&
-                      dc_ctl_.rec == nullptr;
+    const bool dfin = defer_ && carry_ && pub_seq == nullptr && defer == nullptr && !snap_trial &&
+                      (comm_ ? nullptr : fh) == nullptr && dc_ctl_.rec == nullptr;
     // max |p| of a trial whose sums are still partials
     const bool dmax = cx != nullptr && ptr_.part != nullptr && cmax == ptr_.out + 3;
     const int S = gat ? ax_split(plan_, 1) : ax_split(plan_, nsrc);
@@ -1184,7 +1192,9 @@ class Session : public SessionBase {
       first_done = (spec_trial_mu_ == mu_ && spec_trial_t_ == t0);   // else: a phase change
       if (!first_done) ax_queued_ = false;
     } else if (fused_ok_) {
+      carry_ = want_spec(0);   // the batch's packet will ride the speculative kernel
       atr_prox(R_[irg_], gset_, X_[ixt_], ip_, ipt_, iz_, t0);
+      carry_ = false;
       g = {G_, 1};
       first_done = true;
     } else {
@@ -1236,8 +1246,10 @@ class Session : public SessionBase {
         // that k_prox_pgd overwrites) come from a snapshot this finalize takes
         const bool axp = spec && fused_ok_ && comm_ != nullptr && late_pub && attach_ok_ &&
                          spec_ax_pub_ && ax_pub_ok(plan_, smode_ == 1 ? 1 : nsrc);
+        carry_ = late_pub;
         residuals(nsrc, xs, rs, S_RT, X_[ip_], scal_ + S_TR + 3, nullptr, 0.0,
                   late_pub ? nullptr : &seq, merge ? tail(nset(gset_)) : nullptr, skip_ax, axp, emode_);
+        carry_ = false;
         std::pair<const T*, int> sg;
         if (spec && fused_ok_) {
           // the next iteration's A^T r and first trial at the candidate p_thr, into the other
@@ -1728,7 +1740,11 @@ class Session : public SessionBase {
     // stops the phase (abort = that decision's tag): the next phase starts from its gradient, as
     // on the host path; the speculative kernels queued after it do not run
     Red rd = red(S_TR, dc_pass_);
-    if (defer_) {   // its trial sums stay partials (the other buffer than the one pb may reduce)
+    // its trial sums stay partials (the other buffer than the one pb may reduce) when the packet
+    // that needs them is carried by a later speculative kernel: this one's own trial is the next
+    // iteration's (pub_seq), or the caller's batch is carried (carry_)
+    const bool dtr = defer_ && (pub_seq != nullptr || carry_);
+    if (dtr) {
       tb_ ^= 1;
       rd.part = tpart_[tb_];
       rd.parts_only = 1;
@@ -1736,7 +1752,7 @@ class Session : public SessionBase {
     launch_atr_prox<T>(plan_, A_, r, Gs_[set], x, X_[op], X_[opt], X_[oz], t, mu_, O_.thres,
                        rd, st_, pb, Gps_[set], pcnt_, ezf());
     check_launch();
-    if (defer_) ptr_ = Pend{tpart_[tb_], atr_prox_slots(plan_, pb.host != nullptr), 6, 0x8u, scal_ + S_TR};
+    ptr_ = dtr ? Pend{tpart_[tb_], atr_prox_slots(plan_, pb.host != nullptr), 6, 0x8u, scal_ + S_TR} : Pend{};
     prof_end(1, e0);
     ++atr_calls_;
   }
@@ -1777,7 +1793,9 @@ class Session : public SessionBase {
         gy_pending_ = true;
       }
       if (fuse) {
+        carry_ = want_spec(0);
         atr_fista(R_[iry_], gset_, X_[iy_], X_[ix_], ic_, ivn_, iyn_, t0, theta, theta_next);
+        carry_ = false;
         g = {G_, 1};
         first_done = true;
       } else {
@@ -1824,6 +1842,7 @@ class Session : public SessionBase {
         const bool merge = spec && fuse && merge_tail();
         const bool late_pub = merge || (spec && fuse && attach_ok_ && comm_ == nullptr);
         fs_batch = fsplit_ && kslot_ >= 0 && dense_left_ == 0;
+        carry_ = late_pub;
         if (fs_batch) {   // A xc dense, A e_c gathered, A y_next by linearity
           fista_split_batch(R_[ryn], theta, theta_next, S_RT, X_[ic_], scal_ + S_TR + i_max,
                             late_pub ? nullptr : &seq, merge ? tail(nset(gset_)) : nullptr);
@@ -1831,6 +1850,7 @@ class Session : public SessionBase {
           residuals(2, xs, rs, S_RT, X_[ic_], scal_ + S_TR + i_max, nullptr, 0.0,   // A @ [x | y_next]
                     late_pub ? nullptr : &seq, merge ? tail(nset(gset_)) : nullptr);
         }
+        carry_ = false;
         std::pair<const T*, int> sg;
         if (spec && fuse) {
           // the next iteration's gradient at y_next and its first trial (t, theta' = theta_next)
@@ -2096,7 +2116,7 @@ class Session : public SessionBase {
     const T* xs[3] = {E_, X_[ic_], nullptr};
     cand_ax(xs);
     Red rd = defer ? Red{part_, ticket_, defer} : red(slot);
-    const bool dfin = defer_ && defer == nullptr;
+    const bool dfin = defer_ && carry_ && pub_seq == nullptr && defer == nullptr;
     const bool dmax = cx != nullptr && ptr_.part != nullptr && cmax == ptr_.out + 3;
     if (dfin) {
       flush_fin_pending();
@@ -2138,7 +2158,8 @@ class Session : public SessionBase {
     if (pub_seq) pb = make_pub(extra, pub_seq);
     hipEvent_t e0 = prof_begin(1);
     Red rd = red(S_TR, dc_pass_);
-    if (defer_) {   // its trial sums stay partials (as atr_prox)
+    const bool dtr = defer_ && (pub_seq != nullptr || carry_);   // (as atr_prox)
+    if (dtr) {
       tb_ ^= 1;
       rd.part = tpart_[tb_];
       rd.parts_only = 1;
@@ -2146,7 +2167,7 @@ class Session : public SessionBase {
     launch_atr_fista<T>(plan_, A_, r, Gs_[set], yv, xk, X_[oc], X_[ov], X_[oy], t, mu_, O_.thres,
                         theta, theta_next, rd, st_, pb, Gps_[set], pcnt_, fec(), fzf());
     check_launch();
-    if (defer_) ptr_ = Pend{tpart_[tb_], atr_prox_slots(plan_, pb.host != nullptr), 4, 0x8u, scal_ + S_TR};
+    ptr_ = dtr ? Pend{tpart_[tb_], atr_prox_slots(plan_, pb.host != nullptr), 4, 0x8u, scal_ + S_TR} : Pend{};
     prof_end(1, e0);
     ++atr_calls_;
   }
@@ -2257,6 +2278,7 @@ class Session : public SessionBase {
   double* fpart_ = nullptr;
   int tb_ = 0;
   Pend ptr_, pfin_;
+  bool carry_ = false;         // while queuing: the next packet rides the speculative kernel
   int tr_slot_ = S_TR;         // the packet slots of the current trial's sums
   T* At_ = nullptr;            // A^T (split-candidate gather form)
   void* glists_ = nullptr;     // the gather's per-column index lists of e

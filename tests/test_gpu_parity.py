@@ -358,7 +358,7 @@ def test_deferred_reductions_match(monkeypatch, solver, alpha_scale):
     fn = getattr(importlib.import_module(solver), solver)
     At, bt = torch.from_numpy(A).cuda(), torch.from_numpy(b).cuda()
     runs = []
-    for d in ("0", "1"):
+    for d in ("0", "1" if solver == "gl_ProxGD_primal" else "2"):   # (FProxGD: opt-in, 2)
         monkeypatch.setenv("GLX_DEFER_RED", d)
         x, k, out = fn(torch.from_numpy(x0).cuda(), At, bt, mu, dict(opts))
         runs.append((x.cpu().numpy(), k, np.asarray([float(v) for v in out["f_hist"]])))
