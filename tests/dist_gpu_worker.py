@@ -38,6 +38,7 @@ def main():
                     help="one host copy of the instance in /dev/shm, each rank generating its own rows")
     ap.add_argument("--shard-rows", type=int, default=None,
                     help="opts shard_rows (ProxGD: 0 auto, 1 the row-sharded step, 2 all-reduce)")
+    ap.add_argument("--opts", default="{}", help="more solver options (JSON)")
     ap.add_argument("--out", required=True)
     a = ap.parse_args()
 
@@ -70,6 +71,7 @@ def main():
         opts["continuous_subgradient_flag"] = True
     if a.shard_rows is not None:
         opts["shard_rows"] = a.shard_rows
+    opts.update(json.loads(a.opts))
     x, k, out = glx.solve(a.solver, x0, A[r0:r1], b[r0:r1], mu, dict(opts), comm=comm)
     digest = hashlib.sha256(np.ascontiguousarray(x).tobytes()).hexdigest()
     mine = {"rank": rank, "k": int(k), "fval": float(out["fval"]), "x_sha": digest,

@@ -187,6 +187,18 @@ def test_row_sharded_proxgd(tmp_path, world, shape, extra):
     assert v["x_maxdiff"] <= 1e-6 * v["x_scale"]
 
 
+@pytest.mark.parametrize("extra_opts", [{"step_type": "fixed"}, {"exact_objective": 1}])
+def test_row_sharded_other_modes(tmp_path, extra_opts):
+    """The row-sharded schedule with the fixed step (every trial untested: the prologue's
+    all-reduced sums each iteration) and with exact_objective (A p as a third right-hand side from
+    the gathered p), world 2, against the unsharded oracle."""
+    import json as _json
+    v = run_sharded(tmp_path, 2, "gl_ProxGD_primal", 512, 1024, 32, maxit=25,
+                    extra=("--shard-rows", "1", "--opts", _json.dumps(extra_opts)))
+    r0 = _check_identical_and_oracle(v, 2)
+    assert "rows=sharded x2" in r0["plan"]
+
+
 def test_row_sharded_split_candidate(tmp_path, monkeypatch):
     """The split-candidate trial under the row-sharded schedule: the masks and bitmaps of e are
     re-derived from the gathered p by k_trial_split and the bitmap gather reads e from them."""
