@@ -56,14 +56,20 @@ static inline int finalize_groups(int S) {
   return g;
 }
 
+// group_slab_sum in two halves, so a caller can issue the loads of several sources before the
+// first add (round 5: the finalize's two sources, one round trip instead of two)
 template <typename T, int G>
-__device__ inline T group_slab_sum(const T* __restrict__ P, int S, int64_t ml, int64_t idx, int sub) {
+__device__ inline int group_slab_load(const T* __restrict__ P, int S, int64_t ml, int64_t idx, int sub,
+                                      T (&a)[kSlabLoads]) {
   const int per = (S + G - 1) / G;
   const int k0 = sub * per;
   const int cnt = S - k0 < per ? S - k0 : per;   // <= 0 for an empty trailing lane
-  T a[kSlabLoads];
 #pragma unroll
   for (int k = 0; k < kSlabLoads; ++k) a[k] = k < cnt ? P[(int64_t)(k0 + k) * ml + idx] : T(0);
+  return cnt;
+}
+template <typename T, int G>
+__device__ inline T group_slab_fold(const T (&a)[kSlabLoads], int cnt) {
   T v = a[0];
 #pragma unroll
   for (int k = 1; k < kSlabLoads; ++k)
@@ -71,6 +77,12 @@ __device__ inline T group_slab_sum(const T* __restrict__ P, int S, int64_t ml, i
 #pragma unroll
   for (int off = 1; off < G; off <<= 1) v = v + __shfl_xor(v, off);
   return v;
+}
+template <typename T, int G>
+__device__ inline T group_slab_sum(const T* __restrict__ P, int S, int64_t ml, int64_t idx, int sub) {
+  T a[kSlabLoads];
+  const int cnt = group_slab_load<T, G>(P, S, ml, idx, sub, a);
+  return group_slab_fold<T, G>(a, cnt);
 }
 
 // Device-controlled ProxGD with a communicator (solver.cpp dc_queue): the trial's residual sums
@@ -164,8 +176,11 @@ __global__ __launch_bounds__(256) void k_finalize_residual(
   for (int64_t idx = tid / G; idx < ml; idx += stride / G) {
     const T bv = B[idx];
     if (NSRC == 2 && chain) {   // split-candidate: R0 = (A p_thr - b) + A e (always live)
-      const T r1 = group_slab_sum<T, G>(P + (int64_t)S0 * ml, S, ml, idx, sub) - bv;
-      const T r0 = r1 + group_slab_sum<T, G>(P0, S0, ml, idx, sub);
+      T a1[kSlabLoads], a0[kSlabLoads];
+      const int c1 = group_slab_load<T, G>(P + (int64_t)S0 * ml, S, ml, idx, sub, a1);
+      const int c0 = group_slab_load<T, G>(P0, S0, ml, idx, sub, a0);
+      const T r1 = group_slab_fold<T, G>(a1, c1) - bv;
+      const T r0 = r1 + group_slab_fold<T, G>(a0, c0);
       if (skipped) return;
       if (sub == 1 % G) rs[1][idx] = r1;
       if (R0 != nullptr && sub == 0) rs[0][idx] = r0;
@@ -175,11 +190,18 @@ __global__ __launch_bounds__(256) void k_finalize_residual(
       }
       continue;
     }
+    T a[NSRC][kSlabLoads];   // every source's slab loads issued before the first add
+    int cs[NSRC];
+    if (live) {
+#pragma unroll
+      for (int sr = 0; sr < NSRC; ++sr)
+        cs[sr] = group_slab_load<T, G>(P + (int64_t)sr * S * ml, S, ml, idx, sub, a[sr]);
+    }
 #pragma unroll
     for (int sr = 0; sr < NSRC; ++sr) {
       T r;
       if (live) {
-        r = group_slab_sum<T, G>(P + (int64_t)sr * S * ml, S, ml, idx, sub) - bv;
+        r = group_slab_fold<T, G>(a[sr], cs[sr]) - bv;
         if (skipped) return;
         if (sub == sr % G) rs[sr][idx] = r;
       } else {
