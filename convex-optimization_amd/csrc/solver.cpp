@@ -1481,10 +1481,12 @@ class Session : public SessionBase {
           ax_queued_ = true;
           spec_trial = true;
         } else {
+          // the combine and a plain k_publish: one kernel that combines and then writes the packet
+          // measured 17-19 us against ~4 us for k_publish (as k_publish_pub, profiles/r5_probe/)
           shard_exchange(-1);
-          launch_shard_combine(shard_pub(2, tr_slot_, spin_readback_ ? &seq : nullptr), st_);
+          launch_shard_combine(shard_pub(2, tr_slot_, nullptr), st_);
           check_launch();
-          if (!spin_readback_) seq = post_readback();
+          seq = post_readback();
         }
         wait_readback(seq);
         const double gz = 0.5 * hs_[S_RT];
