@@ -387,10 +387,16 @@ def main():
         pw = glx.Session(args.method, xw, A, b, mu, dict(opts, profile=0, max_total_iters=0),
                          comm=comm)
         t_pw = time.perf_counter()
-        while time.perf_counter() - t_pw < args.prewarm_s:
+        while True:
             got = pw.run(16)
             prewarm["iters"] += got
-            if pw.finished or got == 0:
+            # every rank must run the same number of chunks (each issues collectives): continue
+            # only while the clock has time left on EVERY rank (min over ranks)
+            go = torch.tensor([0 if (pw.finished or got == 0 or time.perf_counter() - t_pw >= args.prewarm_s)
+                               else 1], dtype=torch.int64)
+            if dist is not None:
+                dist.all_reduce(go, op=dist.ReduceOp.MIN)
+            if int(go.item()) == 0:
                 break
         prewarm["seconds"] = round(time.perf_counter() - t_pw, 3)
         # closed before the timed warmup: only one session's workspace (with
