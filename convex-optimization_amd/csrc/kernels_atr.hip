@@ -36,7 +36,9 @@ namespace glx {
 // 256 MiB Infinity Cache for the next pass over A (A@X) to hit.
 
 // panel width (columns of A = rows of G) of a wave layout, and its MFMA output groups e
-template <int WL> constexpr int atr_pw() { return WL == 3 ? 32 : 64; }
+template <int WL> constexpr int atr_pw() { return (WL == 3 || WL == 4) ? 32 : 64; }
+// waves per workgroup: WL 2 (64-column panel) and WL 4 (32-column panel, round 5) have eight
+template <int WL> constexpr int atr_waves() { return (WL == 2 || WL == 4) ? 8 : 4; }
 template <int WL> constexpr int atr_ne() { return atr_pw<WL>() / 16; }
 
 template <typename T, int NT, int PF, int WL, bool NTL>
@@ -47,9 +49,9 @@ __device__ inline int64_t atr_panel(const T* __restrict__ A, const T* __restrict
   typedef typename M::acc_t C;
   constexpr int L = 16 * NT;
   constexpr bool RW = WL != 1;   // the block's waves split the rows of one panel
-  constexpr int NWV = WL == 2 ? 8 : 4;
+  constexpr int NWV = atr_waves<WL>();
   constexpr int PW = atr_pw<WL>(), NE = atr_ne<WL>();
-  static_assert(WL != 3 || sizeof(T) == 8, "the 32-column panel is f64 (one 16-B load per row)");
+  static_assert((WL != 3 && WL != 4) || sizeof(T) == 8, "the 32-column panel is f64 (one 16-B load per row)");
   __shared__ C red[RW ? 4 : 1][RW ? 4 * NT : 1][64];   // [wave][e * NT + nt][lane]
 
   const int lane = threadIdx.x & 63;
@@ -142,17 +144,17 @@ __device__ inline int64_t atr_panel(const T* __restrict__ A, const T* __restrict
   }
   GLX_CLK(2);
 
-  if constexpr (WL == 2) {   // waves 4..7 into 0..3: acc(w) + acc(w + 4)
+  if constexpr (WL == 2 || WL == 4) {   // waves 4..7 into 0..3: acc(w) + acc(w + 4)
     if (wave >= 4) {
 #pragma unroll
-      for (int e = 0; e < 4; ++e)
+      for (int e = 0; e < NE; ++e)
 #pragma unroll
         for (int nt = 0; nt < NT; ++nt) red[wave - 4][e * NT + nt][lane] = acc[e][nt];
     }
     __syncthreads();
     if (wave < 4) {
 #pragma unroll
-      for (int e = 0; e < 4; ++e)
+      for (int e = 0; e < NE; ++e)
 #pragma unroll
         for (int nt = 0; nt < NT; ++nt) acc[e][nt] += red[wave][e * NT + nt][lane];
     }
@@ -265,7 +267,7 @@ __device__ inline bool atr_split_combine(typename MF<T>::acc_t (&acc)[4][NT], T*
 }
 
 template <typename T, int NT, int PF, int WL, bool NTL>
-__global__ __launch_bounds__(WL == 2 ? 512 : 256) void k_atr_mfma(const T* __restrict__ A, const T* __restrict__ R,
+__global__ __launch_bounds__(atr_waves<WL>() * 64) void k_atr_mfma(const T* __restrict__ A, const T* __restrict__ R,
                                                   T* __restrict__ Gp, int64_t m, int64_t n, int S,
                                                   int keep_mib) {
   typedef MF<T> M;
@@ -294,7 +296,7 @@ __global__ __launch_bounds__(WL == 2 ? 512 : 256) void k_atr_mfma(const T* __res
 // wave writes its rows of G and runs the trial on them (prox_pgd_row, the same arithmetic as
 // k_prox_pgd) with x = the thresholded iterate; the six trial sums are reduced over the grid.
 template <typename T, int NT, int PF, bool NTL, bool SPLIT, int WL>
-__global__ __launch_bounds__(WL == 2 ? 512 : 256, ((WL == 0 || WL == 3) && sizeof(T) == 8) ? 2 : 1) void k_atr_prox(const T* __restrict__ A, const T* __restrict__ R,
+__global__ __launch_bounds__(atr_waves<WL>() * 64, ((WL == 0 || WL == 3) && sizeof(T) == 8) ? 2 : 1) void k_atr_prox(const T* __restrict__ A, const T* __restrict__ R,
                                                   T* __restrict__ G, int64_t m, int64_t n,
                                                   const T* __restrict__ x, T* __restrict__ p,
                                                   T* __restrict__ pthr, T* __restrict__ z,
@@ -315,7 +317,7 @@ __global__ __launch_bounds__(WL == 2 ? 512 : 256, ((WL == 0 || WL == 3) && sizeo
   // the extra workgroup (n / 64 * S + 1 in all); with K splits only the panel owners and the
   // publisher reduce (nparts)
   const int nparts = SPLIT ? (int)(n / 64) + (pub.host ? 1 : 0) : -1;
-  constexpr int NW = WL == 2 ? 8 : 4;
+  constexpr int NW = atr_waves<WL>();
   if (publisher_first<6, 0x8u, NW>(pub, red, nparts)) return;
   typedef MF<T> M;
   constexpr int L = 16 * NT;
@@ -399,7 +401,7 @@ __global__ __launch_bounds__(WL == 2 ? 512 : 256, ((WL == 0 || WL == 3) && sizeo
 // fista_row (the arithmetic of k_fista_trial) on its 16 gradient rows, with y the extrapolated
 // point and xk the current iterate; writes G, xc, v_next, y_next and reduces the four sums.
 template <typename T, int NT, int PF, bool NTL, bool SPLIT, int WL>
-__global__ __launch_bounds__(WL == 2 ? 512 : 256, ((WL == 0 || WL == 3) && sizeof(T) == 8) ? 2 : 1) void k_atr_fista(const T* __restrict__ A, const T* __restrict__ R,
+__global__ __launch_bounds__(atr_waves<WL>() * 64, ((WL == 0 || WL == 3) && sizeof(T) == 8) ? 2 : 1) void k_atr_fista(const T* __restrict__ A, const T* __restrict__ R,
                                                    T* __restrict__ G, int64_t m, int64_t n,
                                                    const T* __restrict__ y, const T* __restrict__ xk,
                                                    T* __restrict__ xc, T* __restrict__ vnext,
@@ -415,7 +417,7 @@ __global__ __launch_bounds__(WL == 2 ? 512 : 256, ((WL == 0 || WL == 3) && sizeo
     return;
   }
   const int nparts = SPLIT ? (int)(n / 64) + (pub.host ? 1 : 0) : -1;   // see k_atr_prox
-  constexpr int NW = WL == 2 ? 8 : 4;
+  constexpr int NW = atr_waves<WL>();
   if (publisher_first<4, 0x8u, NW>(pub, red, nparts)) return;
   typedef MF<T> M;
   constexpr int L = 16 * NT;
@@ -552,7 +554,7 @@ template <typename T, int NT, int PF, int WL, bool NTL>
 static void atr_mfma_go(const GemmPlan& p, const T* A, const T* R, T* Gp, hipStream_t st) {
   const dim3 grid((unsigned)(p.n / (WL == 1 ? 256 : atr_pw<WL>())), (unsigned)p.atr_S);
   static const size_t pad = lds_pad(k_atr_mfma<T, NT, PF, WL, NTL>, "GLX_ATR_LDS_PAD");
-  glx_launch((k_atr_mfma<T, NT, PF, WL, NTL>), grid, dim3(WL == 2 ? 512 : 256), pad, st, A, R, Gp, p.m, p.n, p.atr_S,
+  glx_launch((k_atr_mfma<T, NT, PF, WL, NTL>), grid, dim3(atr_waves<WL>() * 64), pad, st, A, R, Gp, p.m, p.n, p.atr_S,
              p.atr_keep_mib);
 }
 
@@ -580,6 +582,14 @@ static void atr_mfma_nt(const GemmPlan& p, const T* A, const T* R, T* Gp, hipStr
         break;
       }
       throw Error{GLX_E_INVALID, "A^T R: the 32-column panel is f64"};
+    case 48:
+    case 148:
+      if constexpr (sizeof(T) == 8) {
+        if (p.atr_ntl) atr_mfma_go<T, NT, 8, 4, true>(p, A, R, Gp, st);
+        else atr_mfma_go<T, NT, 8, 4, false>(p, A, R, Gp, st);
+        break;
+      }
+      throw Error{GLX_E_INVALID, "A^T R: the 32-column panel is f64"};
     default: atr_mfma_go<T, NT, 2, 0, false>(p, A, R, Gp, st); break;
   }
 }
@@ -601,11 +611,11 @@ void launch_atr(const GemmPlan& p, const T* A, const T* R, T* Gp, hipStream_t st
 
 
 int atr_prox_slots(const GemmPlan& p, bool pub) {
-  return (int)(p.n / (p.atr_wl == 3 ? 32 : 64)) + (pub ? 1 : 0);
+  return (int)(p.n / ((p.atr_wl == 3 || p.atr_wl == 4) ? 32 : 64)) + (pub ? 1 : 0);
 }
 
 bool atr_prox_ok(const GemmPlan& p) {
-  if (p.atr_wl == 3)   // the 32-column panel: f64, no K splits (session_plan)
+  if (p.atr_wl == 3 || p.atr_wl == 4)   // the 32-column panels: f64, no K splits (session_plan)
     return p.atr_kind == 1 && p.esize == 8 && p.atr_S == 1 && (p.l == 16 || p.l == 32) &&
            p.n % 32 == 0 && p.n / 32 < kMaxBlocks;
   return p.atr_kind == 1 && (p.atr_wl == 0 || p.atr_wl == 2) && p.atr_S >= 1 && p.atr_S <= 8 &&
@@ -619,8 +629,8 @@ static void atr_prox_go(const GemmPlan& p, const T* A, const T* R, T* G, const T
                         T* pthr, T* z, double t, double mu, double thres, Red red, hipStream_t st,
                         Pub pub, T* Gp, unsigned* pcnt, unsigned* zf) {
   const dim3 grid((unsigned)(p.n / atr_pw<WL>() * p.atr_S + (pub.host ? 1 : 0)));
-  const dim3 block(WL == 2 ? 512 : 256);
-  if (WL != 3 && p.atr_S > 1) {
+  const dim3 block(atr_waves<WL>() * 64);
+  if (WL != 3 && WL != 4 && p.atr_S > 1) {
     glx_launch((k_atr_prox<T, NT, PF, NTL, true, WL>), grid, block, 0, st, A, R, G, p.m,
                        p.n, x, pp, pthr, z, t, t * mu, thres, red, pub, p.atr_S, Gp, pcnt, zf, p.atr_keep_mib);
     return;
@@ -649,6 +659,14 @@ static void atr_prox_nt(const GemmPlan& p, const T* A, const T* R, T* G, const T
         break;
       }
       throw Error{GLX_E_INVALID, "A^T R: the 32-column panel is f64"};
+    case 48:
+    case 148:
+      if constexpr (sizeof(T) == 8) {
+        if (p.atr_ntl) atr_prox_go<T, NT, 8, true, 4>(p, A, R, G, x, pp, pthr, z, t, mu, thres, red, st, pub, Gp, pcnt, zf);
+        else atr_prox_go<T, NT, 8, false, 4>(p, A, R, G, x, pp, pthr, z, t, mu, thres, red, st, pub, Gp, pcnt, zf);
+        break;
+      }
+      throw Error{GLX_E_INVALID, "A^T R: the 32-column panel is f64"};
     default: atr_prox_go<T, NT, 8, false, 0>(p, A, R, G, x, pp, pthr, z, t, mu, thres, red, st, pub, Gp, pcnt, zf); break;
   }
 }
@@ -668,8 +686,8 @@ static void atr_fista_go(const GemmPlan& p, const T* A, const T* R, T* G, const 
                          double theta_next, Red red, hipStream_t st, Pub pub, T* Gp, unsigned* pcnt,
                          T* ec, unsigned* zf) {
   const dim3 grid((unsigned)(p.n / atr_pw<WL>() * p.atr_S + (pub.host ? 1 : 0)));
-  const dim3 block(WL == 2 ? 512 : 256);
-  if (WL != 3 && p.atr_S > 1) {
+  const dim3 block(atr_waves<WL>() * 64);
+  if (WL != 3 && WL != 4 && p.atr_S > 1) {
     glx_launch((k_atr_fista<T, NT, PF, NTL, true, WL>), grid, block, 0, st, A, R, G, p.m,
                        p.n, y, xk, xc, vn, yn, t, t * mu, thres, theta, 1.0 - theta_next,
                        theta_next, red, pub, p.atr_S, Gp, pcnt, ec, zf, p.atr_keep_mib);
@@ -697,6 +715,14 @@ static void atr_fista_nt(const GemmPlan& p, const T* A, const T* R, T* G, const 
       if constexpr (sizeof(T) == 8) {
         if (p.atr_ntl) atr_fista_go<T, NT, 8, true, 3>(p, A, R, G, y, xk, xc, vn, yn, t, mu, thres, theta, theta_next, red, st, pub, Gp, pcnt, ec, zf);
         else atr_fista_go<T, NT, 8, false, 3>(p, A, R, G, y, xk, xc, vn, yn, t, mu, thres, theta, theta_next, red, st, pub, Gp, pcnt, ec, zf);
+        break;
+      }
+      throw Error{GLX_E_INVALID, "A^T R: the 32-column panel is f64"};
+    case 48:
+    case 148:
+      if constexpr (sizeof(T) == 8) {
+        if (p.atr_ntl) atr_fista_go<T, NT, 8, true, 4>(p, A, R, G, y, xk, xc, vn, yn, t, mu, thres, theta, theta_next, red, st, pub, Gp, pcnt, ec, zf);
+        else atr_fista_go<T, NT, 8, false, 4>(p, A, R, G, y, xk, xc, vn, yn, t, mu, thres, theta, theta_next, red, st, pub, Gp, pcnt, ec, zf);
         break;
       }
       throw Error{GLX_E_INVALID, "A^T R: the 32-column panel is f64"};

@@ -230,7 +230,7 @@ static GemmPlan session_plan(const glx_problem& P, const glx_opts& O) {
     const char* nw = std::getenv("GLX_ATR_NARROW");
     if (!(nw && std::strcmp(nw, "0") == 0)) {
       GemmPlan f = p;
-      f.atr_wl = 3;
+      f.atr_wl = (nw && std::strcmp(nw, "8") == 0) ? 4 : 3;   // GLX_ATR_NARROW=8: eight waves
       f.atr_pf = 8;
       f.atr_S = 1;
       if (atr_prox_ok(f)) return f;

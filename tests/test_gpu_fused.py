@@ -156,16 +156,18 @@ def test_fused_trial_eight_wave_panel(monkeypatch, method, S):
     assert np.max(np.abs(f_g - f_r) / np.abs(f_r)) < 1e-8
 
 
-# Round 5: the 32-column A^T R panel (WL 3, f64, one K split) in the fused kernels: the iterate is
-# bit-identical to the unfused path on the same tile and within the north-star bar of the oracle.
+# Round 5: the 32-column A^T R panels (WL 3: four waves, WL 4: eight, f64, one K split) in the
+# fused kernels: the iterate is bit-identical to the unfused path on the same tile and within the
+# north-star bar of the oracle.
+@pytest.mark.parametrize("code,wl", [("1038", "WL3"), ("1048", "WL4")])
 @pytest.mark.parametrize("method", METHODS)
-def test_fused_trial_narrow_panel(monkeypatch, method):
+def test_fused_trial_narrow_panel(monkeypatch, method, code, wl):
     from oracle import numpy_ref
     from glx import _lib
-    monkeypatch.setenv("GLX_ATR_VARIANT", "1038")
+    monkeypatch.setenv("GLX_ATR_VARIANT", code)
     monkeypatch.setenv("GLX_ATR_S", "1")
     d = _lib.plan_describe(_lib.GLX_F64, *SHAPE)
-    assert "WL3" in d and "S=1" in d, d
+    assert wl in d and "S=1" in d, d
     A, b, x0, mu, alpha0 = _instance()
     opts = {"alpha0": alpha0, "maxit": 25}
     x_f, r_f = _run(monkeypatch, True, True, opts, method)

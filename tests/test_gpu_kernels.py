@@ -200,7 +200,7 @@ def test_residual_batch_split_groups(monkeypatch, dtype, split):
 @pytest.mark.parametrize("dtype", ["f64", "f32"])
 @pytest.mark.parametrize("shape", [(256, 512, 32), (512, 1024, 16), (1000, 1024, 32), (4096, 8192, 16),
                                    (8, 256, 32), (2052, 2048, 32)])
-@pytest.mark.parametrize("code", [8, 1008, 14, 1114, 28, 1024, 1028, 38, 1038])
+@pytest.mark.parametrize("code", [8, 1008, 14, 1114, 28, 1024, 1028, 38, 1038, 48, 1048])
 def test_gradient_atr_codes(monkeypatch, shape, dtype, code):
     monkeypatch.setenv("GLX_ATR_VARIANT", str(code))
     k = _glx()
