@@ -106,8 +106,15 @@ constexpr int kMaxShardRanks = 64;
 // turn); FProxGD NS 2454-2478 vs 2456-2465 (whole solve 2058-2060 vs 2036-2038), C3 3702 vs
 // 3687-3703, C5's shard 1227-1231 vs 1230-1234, the 1024-row comm shard 9802-9829 vs 10517-10587
 // (+7.5 %: the host path leaves the GPU idle while it decides behind the short speculative trial).
-static int dc_window_opt(const glx_problem& P, const glx_opts& O) {
+// Round 5: also kDcWindow for ProxGD on the unfused speculative form (unfused: Session's
+// dc_unfused_ok) when A is at most kDcSmallBytes — launch-bound shapes, where the host's turn per
+// iteration is a large share: C1 (512, 1024, 2) 200-step windows 24 250 / 24 253 it/s with host
+// control against 25 477 / 25 591 with window 8 (and 22 079 / 21 752 on the rounds-1-4 form;
+// profiles/r5_unfused/).
+static constexpr double kDcSmallBytes = 64.0 * 1024 * 1024;
+static int dc_window_opt(const glx_problem& P, const glx_opts& O, bool unfused = false) {
   int w = (P.method == GLX_FPROXGD && P.comm != nullptr) ? kDcWindow : 0;
+  if (unfused && (double)P.m * (double)P.n * 8.0 <= kDcSmallBytes) w = kDcWindow;
   if (O.dc_window != 0) {
     w = O.dc_window;
   } else if (const char* dc = std::getenv("GLX_DC_BATCH")) {
@@ -344,6 +351,24 @@ class Session : public SessionBase {
     return gemv_fused_blocks((int)sizeof(T), P.m, P.n, P.l);
   }
 
+  // Round 5: ProxGD on one GPU whose plan cannot fuse the trial into A^T r (l not in {16, 32},
+  // n % 64 != 0, ...; C1's (512, 1024, 2)) runs the communicator path's form instead: A^T r, then
+  // k_prox_pgd from its slabs, queued speculatively the same way (the packet riding k_prox_pgd),
+  // so device control (dc_queue_comm) applies to these shapes too. GLX_UNFUSED_SPEC=0: off (the
+  // gradient and the trial as separate host-driven steps, rounds 1-4).
+  static bool unfused_spec_ok(const glx_problem& P, const glx_opts& O, const GemmPlan& plan) {
+    const char* e = std::getenv("GLX_UNFUSED_SPEC");
+    const char* fz = std::getenv("GLX_FUSED_TRIAL");
+    return P.comm == nullptr && P.method == GLX_PROXGD && !atr_prox_ok(plan) &&
+           (O.step_type == GLX_STEP_LINE_SEARCH || O.step_type == GLX_STEP_FIXED) &&
+           !(e && std::strcmp(e, "0") == 0) && !(fz && std::strcmp(fz, "0") == 0);
+  }
+  // device control on that form: as with a communicator (fp64: the finalize's sums go to the
+  // gradient set's tail, read as doubles), line search, fast objective mode
+  static bool dc_unfused_ok(const glx_problem& P, const glx_opts& O, const GemmPlan& plan) {
+    return unfused_spec_ok(P, O, plan) && P.dtype == GLX_F64 && O.step_type == GLX_STEP_LINE_SEARCH &&
+           O.ls_maxit > 0 && O.exact_objective == 0;
+  }
   // device control with a communicator: ProxGD, fp64 (the trial sums ride the gradient
   // all-reduce), line search, fast objective mode
   static bool dc_comm_ok(const glx_problem& P, const glx_opts& O) {
@@ -365,16 +390,17 @@ class Session : public SessionBase {
                           (O.step_type == GLX_STEP_LINE_SEARCH || O.step_type == GLX_STEP_FIXED) &&
                           !env_is("GLX_FUSED_TRIAL", "0");
     const bool method = P.method == GLX_PROXGD || P.method == GLX_FPROXGD;
-    if (!(fuse_any && method && spin && O.exact_objective == 0 && ls &&
+    const bool unf = dc_unfused_ok(P, O, plan) && attach;
+    if (!((fuse_any || unf) && method && spin && O.exact_objective == 0 && ls &&
           (P.comm == nullptr || (dc_comm_ok(P, O) && attach))))
       return 0;
-    return dc_window_opt(P, O);
+    return dc_window_opt(P, O, unf && P.comm == nullptr);
   }
   // a ring of window + 2 gradient sets only where device control with a communicator actually
   // runs (it was sized on the request, not on the window that takes effect)
   static int gsets_for(const glx_problem& P, const glx_opts& O, const GemmPlan& plan) {
     const int w = dc_window_eff(P, O, plan);
-    return (w > 0 && dc_comm_ok(P, O)) ? w + 2 : 2;
+    return (w > 0 && (dc_comm_ok(P, O) || dc_unfused_ok(P, O, plan))) ? w + 2 : 2;
   }
 
   static int64_t fh_capacity(const glx_problem& P, const glx_opts& O) {
@@ -431,7 +457,8 @@ class Session : public SessionBase {
     const bool fuse_any = (comm_ != nullptr || atr_prox_ok(plan_)) &&
                           (O.step_type == GLX_STEP_LINE_SEARCH || O.step_type == GLX_STEP_FIXED) &&
                           !(fz && std::strcmp(fz, "0") == 0);
-    fused_ok_ = fuse_any && P.method == GLX_PROXGD;
+    unfused_spec_ = unfused_spec_ok(P, O, plan_);
+    fused_ok_ = (fuse_any || unfused_spec_) && P.method == GLX_PROXGD;
     // ProxGD's fast objective mode evaluates the candidate as A p = A p_thr + A e, e = p - p_thr
     // nonzero only where the hard threshold zeroed p (see iter_proxgd, split_mode)
     emode_ = smode_ != 0 && P.method == GLX_PROXGD;
@@ -664,7 +691,7 @@ class Session : public SessionBase {
   // the kernels this session actually launches (bench.py re-derived the plan)
   std::string describe() const override {
     std::string s = describe_plan(plan_);
-    if (comm_ == nullptr && fused_ok_) s += " +trial (k_atr_prox)";
+    if (comm_ == nullptr && fused_ok_) s += unfused_spec_ ? " +trial (k_prox_pgd behind A^T r)" : " +trial (k_atr_prox)";
     if (comm_ == nullptr && fused_fista_ok_) s += " +trial (k_atr_fista)";
     s += "; split=";
     if (smode_ == 0) s += "dense";
@@ -1536,7 +1563,7 @@ class Session : public SessionBase {
   bool dc_ready() const {
     // (with a communicator the first trial's A@X is normally already queued: the batch uses it)
     return dc_window_ > 0 && spec_trial_ready_ && spec_trial_mu_ == mu_ &&
-           spec_trial_t_ == O_.alpha0 && want_spec(0) && (comm_ != nullptr || !ax_queued_);
+           spec_trial_t_ == O_.alpha0 && want_spec(0) && (comm_ != nullptr || unfused_spec_ || !ax_queued_);
   }
   // Gated (cancellable) launches: the finalize (it would overwrite the decision state and the
   // gradient residual of the iteration the host resumes) and the speculative fused kernel (the
@@ -1579,13 +1606,13 @@ class Session : public SessionBase {
     const int ns = nset(q.gset);
     residuals(2, xs, rs, S_RT, X_[q.ip], scal_ + S_TR + 3, nullptr, 0.0, nullptr, tail(ns), true,
               false, emode_);
-    gradient(R_[rpt], ns, 2);
+    const std::pair<const T*, int> g = gradient(R_[rpt], ns, 2);   // (one GPU: A^T r's slabs)
     const int64_t slot = (tag % kCtlMaxBatch) * kCtlRec;
     launch_ctl_decide(dc_make_ctl(tag), tail(ns), dc_ring_dev_ + slot,
                       reinterpret_cast<unsigned*>(dc_ring_dev_ + slot + kCtlRec - 1), (unsigned)tag, st_);
     check_launch();
-    launch_prox_pgd<T>(X_[q.ipt], Gs_[ns], 1, nullptr, X_[q.if1], X_[q.if2], X_[q.iz], n_, l_,
-                       O_.alpha0, mu_, O_.thres, red(S_TR), st_, Pub{}, ezf());
+    launch_prox_pgd<T>(X_[q.ipt], g.first, g.second, g.first != Gs_[ns] ? Gs_[ns] : nullptr, X_[q.if1],
+                       X_[q.if2], X_[q.iz], n_, l_, O_.alpha0, mu_, O_.thres, red(S_TR), st_, Pub{}, ezf());
     check_launch();
     const T* sx[3] = {X_[q.iz], X_[q.if2], X_[q.if1]};   // [z | p_thr | p] of that trial
     if (smode_ == 1) cand_ax(sx);
@@ -1659,7 +1686,7 @@ class Session : public SessionBase {
     const int64_t w = std::min<int64_t>(dc_window_, budget);
     auto push = [&]() {   // tags are never reused: dc_tag_ = the last one queued
       dc_tag_ = tag0 + 1 + queued++;
-      if (comm_) dc_queue_comm(q, dc_tag_, queued == 1);
+      if (comm_ || unfused_spec_) dc_queue_comm(q, dc_tag_, queued == 1);
       else dc_queue(q, dc_tag_);
     };
     while (queued < w) push();
@@ -1675,7 +1702,7 @@ class Session : public SessionBase {
           // k_prox_pgd and everything behind it), which proxgd_spec_rotate declared ready: keep
           // its gradient set (the all-reduce in front of the decision completed) but never its
           // trial, even where the next phase's mu equals this one's (mu0 = 0).
-          if (comm_) {
+          if (comm_ || unfused_spec_) {
             spec_trial_mu_ = NAN;
             ax_queued_ = false;
           }
@@ -1712,7 +1739,7 @@ class Session : public SessionBase {
       prev = code;
     }
     // with a communicator the last segment queued the next trial's A@X
-    ax_queued_ = comm_ != nullptr;
+    ax_queued_ = comm_ != nullptr || unfused_spec_;
   }
 
   // A^T r fused with a ProxGD trial at x (gradient set `set`, outputs X_[op], X_[opt], X_[oz]).
@@ -1724,15 +1751,17 @@ class Session : public SessionBase {
   void atr_prox(const T* r, int set, const T* x, int op, int opt, int oz, double t, int tail_n = 0,
                 unsigned* pub_seq = nullptr, Pub* pub_out = nullptr) {
     const double* extra = tail_n ? tail(set) : nullptr;
-    if (comm_) {
+    if (comm_ || unfused_spec_) {
       const std::pair<const T*, int> g = gradient(r, set, tail_n);
       Pub pb;
       if (pub_seq && pub_out) *pub_out = make_pub(extra, pub_seq);
       else if (pub_seq && attach_ok_) pb = make_pub(extra, pub_seq);
       else if (pub_seq) *pub_seq = post_readback(extra);
-      launch_prox_pgd<T>(x, g.first, g.second, nullptr, X_[op], X_[opt], X_[oz], n_, l_, t, mu_,
-                         O_.thres, red(S_TR), st_, pb, ezf());
+      // (one GPU: g is A^T r's slabs; the trial stores their sum as the set's G for retrials)
+      launch_prox_pgd<T>(x, g.first, g.second, g.first != Gs_[set] ? Gs_[set] : nullptr, X_[op], X_[opt],
+                         X_[oz], n_, l_, t, mu_, O_.thres, red(S_TR, dc_pass_), st_, pb, ezf());
       check_launch();
+      ptr_ = Pend{};   // S_TR holds this trial's sums
       return;
     }
     Pub pb = dc_pub_;   // without a communicator pub_seq is only passed when attaching
@@ -2280,6 +2309,7 @@ class Session : public SessionBase {
   double* fpart_ = nullptr;
   int tb_ = 0;
   Pend ptr_, pfin_;
+  bool unfused_spec_ = false;  // one GPU, a plan without the fused trial: the communicator form
   bool carry_ = false;         // while queuing: the next packet rides the speculative kernel
   int tr_slot_ = S_TR;         // the packet slots of the current trial's sums
   T* At_ = nullptr;            // A^T (split-candidate gather form)

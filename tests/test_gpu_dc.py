@@ -65,6 +65,11 @@ CASES = [
     ((512, 1024, 16), np.float64, 2.5, {}, 1e-4),   # rejections inside device-controlled runs
     ((512, 1024, 16), np.float32, 1.0, {}, 0.5),
     ((1024, 2048, 32), np.float64, 1.0, {"maxit": 400}, 0.5),
+    # round 5: plans without the fused trial (C1's l = 2; n % 64 != 0) on the communicator
+    # form of the speculative trial (A^T r, then k_prox_pgd from its slabs, dc_queue_comm)
+    ((512, 1024, 2), np.float64, 1.0, {"maxit": 300}, 0.5),
+    ((512, 1024, 2), np.float64, 2.5, {"maxit": 120}, 0.0),
+    ((300, 1000, 4), np.float64, 1.0, {"maxit": 200}, 0.5),
 ]
 
 
@@ -173,3 +178,16 @@ def test_fista_oracle_parity_with_device_control(monkeypatch):
     assert r["k"] == kr
     assert abs(r["fval"] - outr["fval"]) <= 1e-10 * abs(outr["fval"])
     assert r["stats"][7] > 0
+
+
+
+@pytest.mark.parametrize("shape,scale", [((512, 1024, 2), 1.0), ((512, 1024, 2), 2.5), ((300, 1000, 4), 1.0),
+                                         ((256, 512, 8), 1.0)])
+def test_unfused_speculative_form_bit_identical(monkeypatch, shape, scale):
+    """Round 5: with a plan that cannot fuse the trial into A^T r, host control runs the
+    speculative trial as A^T r + k_prox_pgd from its slabs (GLX_UNFUSED_SPEC, default on): the
+    same arithmetic in the same order as the separate gradient and trial (GLX_UNFUSED_SPEC=0)."""
+    a = _run(monkeypatch, 0, shape, alpha_scale=scale, opts={"maxit": 200})
+    b = _run(monkeypatch, 0, shape, alpha_scale=scale, opts={"maxit": 200}, env={"GLX_UNFUSED_SPEC": "0"})
+    _same(a, b)
+    assert a[1]["syncs"] <= b[1]["syncs"]
