@@ -10,6 +10,7 @@
 #include <rccl/rccl.h>
 
 #include <algorithm>
+#include <atomic>
 #include <cstring>
 #include <string>
 
@@ -29,6 +30,13 @@ struct glx_comm {
   void* host_user = nullptr;
   void* stage = nullptr;     // pinned staging buffer (host transport)
   size_t stage_bytes = 0;
+  // progress record (round 6): collectives issued on the stream, collectives the host transport
+  // completed, the kind of the last one issued (1 all-reduce, 2 reduce-scatter, 3 all-gather), and
+  // whether the communicator was aborted. Atomics: a watchdog thread reads them
+  // (glx_comm_progress) while the solver thread issues.
+  std::atomic<int64_t> issued{0}, host_done{0};
+  std::atomic<int> last_kind{0};
+  std::atomic<int> aborted{0};
 };
 
 namespace glx {
@@ -48,6 +56,8 @@ static void rccl_check(ncclResult_t r, const char* what) {
 static ncclDataType_t rccl_type(int dtype) { return dtype == GLX_F64 ? ncclFloat64 : ncclFloat32; }
 
 void comm_allreduce(glx_comm* c, void* buf, int64_t count, int dtype, hipStream_t st) {
+  c->issued.fetch_add(1);
+  c->last_kind.store(1);
   if (c->host_fn == nullptr) {
     rccl_check(ncclAllReduce(buf, buf, (size_t)count, rccl_type(dtype), ncclSum, c->comm, st), "ncclAllReduce");
     return;
@@ -62,12 +72,15 @@ void comm_allreduce(glx_comm* c, void* buf, int64_t count, int dtype, hipStream_
   if (hipMemcpyAsync(buf, c->stage, bytes, hipMemcpyHostToDevice, st) != hipSuccess ||
       hipStreamSynchronize(st) != hipSuccess)   // the staging buffer is reused by the next call
     throw Error{GLX_E_HIP, "host comm: host-to-device staging failed"};
+  c->host_done.fetch_add(1);
 }
 
 // In place: buf holds nranks chunks of `count` elements; chunk `rank` receives the sum of every
 // rank's chunk `rank` (the others are left undefined). Host transport: a full all-reduce.
 void comm_reduce_scatter(glx_comm* c, void* buf, int64_t count, int dtype, hipStream_t st) {
   if (c->host_fn == nullptr) {
+    c->issued.fetch_add(1);
+    c->last_kind.store(2);
     const size_t es = dtype == GLX_F64 ? 8 : 4;
     void* own = static_cast<char*>(buf) + (size_t)c->rank * (size_t)count * es;
     rccl_check(ncclReduceScatter(buf, own, (size_t)count, rccl_type(dtype), ncclSum, c->comm, st),
@@ -83,6 +96,8 @@ void comm_reduce_scatter(glx_comm* c, void* buf, int64_t count, int dtype, hipSt
 void comm_all_gather(glx_comm* c, void* buf, int64_t count, int dtype, hipStream_t st) {
   const size_t es = dtype == GLX_F64 ? 8 : 4;
   char* own = static_cast<char*>(buf) + (size_t)c->rank * (size_t)count * es;
+  c->issued.fetch_add(1);
+  c->last_kind.store(3);
   if (c->host_fn == nullptr) {
     rccl_check(ncclAllGather(own, buf, (size_t)count, rccl_type(dtype), c->comm, st), "ncclAllGather");
     return;
@@ -104,6 +119,7 @@ void comm_all_gather(glx_comm* c, void* buf, int64_t count, int dtype, hipStream
   if (hipMemcpyAsync(buf, c->stage, bytes, hipMemcpyHostToDevice, st) != hipSuccess ||
       hipStreamSynchronize(st) != hipSuccess)
     throw Error{GLX_E_HIP, "host comm: host-to-device staging failed"};
+  c->host_done.fetch_add(1);
 }
 
 // RCCL group: the collectives issued in between go out as one launch (no-op for the host
@@ -116,6 +132,17 @@ void comm_group_end(glx_comm* c) {
 }
 int comm_rank(const glx_comm* c) { return c->rank; }
 int comm_size(const glx_comm* c) { return c->nranks; }
+int comm_async_error(glx_comm* c) {
+  if (c->host_fn != nullptr || c->comm == nullptr || c->aborted.load()) return 0;
+  ncclResult_t a = ncclSuccess;
+  if (ncclCommGetAsyncError(c->comm, &a) != ncclSuccess) return (int)ncclInternalError;
+  return a == ncclInProgress ? 0 : (int)a;
+}
+void comm_abort(glx_comm* c) {
+  if (c->host_fn == nullptr && c->comm != nullptr && c->aborted.exchange(1) == 0) (void)ncclCommAbort(c->comm);
+}
+bool comm_is_rccl(const glx_comm* c) { return c->host_fn == nullptr; }
+int64_t comm_issued(const glx_comm* c) { return c->issued.load(); }
 }  // namespace glx
 
 extern "C" {
@@ -197,9 +224,23 @@ int glx_comm_all_gather(glx_comm* c, void* buf, int64_t count, int dtype, void* 
   }
 }
 
+int glx_comm_progress(glx_comm* c, int64_t out[4]) {
+  if (!c || !out) {
+    glx::g_last_error = "glx_comm_progress: null argument";
+    return GLX_E_INVALID;
+  }
+  out[0] = c->issued.load();
+  out[1] = c->host_fn != nullptr ? c->host_done.load() : -1;
+  out[2] = c->last_kind.load();
+  out[3] = c->aborted.load() ? -1 : glx::comm_async_error(c);
+  return GLX_OK;
+}
+
 void glx_comm_destroy(glx_comm* c) {
   if (!c) return;
-  if (c->comm) ncclCommDestroy(c->comm);
+  if (c->comm) {
+    if (c->aborted.load() == 0) ncclCommDestroy(c->comm);   // an aborted one is already freed
+  }
   if (c->stage) (void)hipHostFree(c->stage);
   delete c;
 }

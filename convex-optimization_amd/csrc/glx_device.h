@@ -314,9 +314,13 @@ __device__ inline void ctl_decide(const Ctl& c, const double* out, const double 
 // bit c: u16 word g of column c = rows 16 g .. 16 g + 15 (bit j = row 16 g + j), at
 // zf_bitmaps(zf, n)[c * zf_npad(n) / 16 + g]; read as u64, word w of column c covers the 64 rows
 // of panel w. The A e gather builds its ascending per-column row lists from them in LDS
-// (kernels_gather.hip k_at_gather_bm) instead of a k_e_lists launch over all n masks. Every
-// trial rewrites every word of every column < l (the words of rows >= n are 0), so nothing needs
-// clearing between trials.
+// (kernels_gather.hip k_at_gather_bm) instead of a k_e_lists launch over all n masks. A trial
+// rewrites the words of the row groups it visits: the 16-row groups below ceil16(n) (row kernels)
+// or the 64 / 32-row panels (A^T R epilogues). Words it never visits — the groups in
+// [ceil16(n), ceil64(n)), the upper half of the last u64 of a 32-row panel — keep what the session
+// cleared at creation (Session's constructor zeroes the whole zf region), and the gather also
+// masks the bits of rows >= n of the last word itself (stale bits there made it
+// read At and E beyond n).
 // ------------------------------------------------------------------------------------------
 __host__ __device__ inline int64_t zf_npad(int64_t n) { return (n + 63) / 64 * 64; }
 __device__ inline unsigned short* zf_bitmaps(unsigned* zf, int64_t n) {

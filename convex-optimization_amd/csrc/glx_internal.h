@@ -146,26 +146,6 @@ struct Pub {
   double* dout[2] = {nullptr, nullptr};
 };
 
-// Round 5: the split-candidate trial's residual finalize folded into the dense pass A p_thr
-// (launch_ax_fin, the LDS-DMA tile): the K-split workgroups store their slabs (agent scope) and
-// arrive on their row block's counter; the last arriver sums the S slabs in slab order, forms
-// r1 = A p_thr - b (stored to R1: the next gradient residual) and r0 = r1 + A e (the A e slabs P0,
-// computed BEFORE the pass), and every workgroup joins one grid reduction of
-// [sum r0^2, sum r1^2, 0, count(|cx| > 1e-6 *cmax)] (its share of cx) into red; the final block
-// runs the device-side decision when ctl.rec != NULL. Replaces k_finalize_residual's chain mode.
-struct AxFin {
-  const void* B = nullptr;
-  void* R1 = nullptr;
-  const void* P0 = nullptr;
-  int S0 = 0;
-  const void* cx = nullptr;
-  int64_t cn = 0;
-  const double* cmax = nullptr;
-  unsigned* cnt = nullptr;   // one arrival counter per row block (zero; the last arriver resets it)
-  Red red{};
-  Ctl ctl{};
-};
-
 // Launch plan of the two dense products for one (dtype, m, n, l).
 struct GemmPlan {
   int esize;        // 4 or 8
@@ -222,14 +202,6 @@ template <typename T>
 bool launch_ax_dma(const GemmPlan& p, int code, int nsrc, int S, const T* A, const T* const* X, T* P,
                    const int* gate, int epoch, hipStream_t st, Pub pub);
 int dma_lds_need(int code, int64_t l, int nsrc, int esize);
-// the dense single-source pass with the folded finalize (AxFin): false when this plan's tile or
-// shape does not take it (the caller then runs launch_ax + launch_finalize_residual); needs
-// fin.cnt to hold ax_fin_counters(p) words
-template <typename T>
-bool launch_ax_fin(const GemmPlan& p, const T* A, const T* X, T* P, const int* gate, int epoch,
-                   hipStream_t st, const AxFin& fin);
-int ax_fin_counters(const GemmPlan& p);
-bool ax_fin_ok(const GemmPlan& p, int esize);
 int dma_waves(int code);   // waves per workgroup of a kind-8/9 code (last digit; 1 = 16)
 int dma_mt(int code);      // 16-row tiles per wave (kind 9: 2)
 // Infinity-Cache hand-off between the passes (tuning experiment; MiB of A fetched with the

@@ -558,21 +558,17 @@ static void atr_mfma_go(const GemmPlan& p, const T* A, const T* R, T* Gp, hipStr
              p.atr_keep_mib);
 }
 
+// Round 6: only the tiles the planner picks are built — the f64
+// default (WL 0, PF 8; non-temporal A beyond the Infinity Cache), the f32 default (WL 1, PF 4,
+// non-temporal), the fp32 fused trial's eight-wave panel (WL 2) and the f64 32-column panel
+// (WL 3). The measured-slower ring depths (PF 2-6) and the 8-wave 32-column panel (WL 4) of
+// rounds 1-5 are gone; their numbers stay in DESIGN.md's tuning record.
 template <typename T, int NT>
 static void atr_mfma_nt(const GemmPlan& p, const T* A, const T* R, T* Gp, hipStream_t st) {
   switch (p.atr_ntl * 100 + p.atr_wl * 10 + p.atr_pf) {
-    case 3: atr_mfma_go<T, NT, 3, 0, false>(p, A, R, Gp, st); break;
-    case 4: atr_mfma_go<T, NT, 4, 0, false>(p, A, R, Gp, st); break;
-    case 6: atr_mfma_go<T, NT, 6, 0, false>(p, A, R, Gp, st); break;
     case 8: atr_mfma_go<T, NT, 8, 0, false>(p, A, R, Gp, st); break;
-    case 14: atr_mfma_go<T, NT, 4, 1, false>(p, A, R, Gp, st); break;
-    case 102: atr_mfma_go<T, NT, 2, 0, true>(p, A, R, Gp, st); break;
-    case 104: atr_mfma_go<T, NT, 4, 0, true>(p, A, R, Gp, st); break;
-    case 106: atr_mfma_go<T, NT, 6, 0, true>(p, A, R, Gp, st); break;
     case 108: atr_mfma_go<T, NT, 8, 0, true>(p, A, R, Gp, st); break;
     case 114: atr_mfma_go<T, NT, 4, 1, true>(p, A, R, Gp, st); break;
-    case 28: atr_mfma_go<T, NT, 8, 2, false>(p, A, R, Gp, st); break;
-    case 124: atr_mfma_go<T, NT, 4, 2, true>(p, A, R, Gp, st); break;
     case 128: atr_mfma_go<T, NT, 8, 2, true>(p, A, R, Gp, st); break;
     case 38:
     case 138:
@@ -582,15 +578,9 @@ static void atr_mfma_nt(const GemmPlan& p, const T* A, const T* R, T* Gp, hipStr
         break;
       }
       throw Error{GLX_E_INVALID, "A^T R: the 32-column panel is f64"};
-    case 48:
-    case 148:
-      if constexpr (sizeof(T) == 8) {
-        if (p.atr_ntl) atr_mfma_go<T, NT, 8, 4, true>(p, A, R, Gp, st);
-        else atr_mfma_go<T, NT, 8, 4, false>(p, A, R, Gp, st);
-        break;
-      }
-      throw Error{GLX_E_INVALID, "A^T R: the 32-column panel is f64"};
-    default: atr_mfma_go<T, NT, 2, 0, false>(p, A, R, Gp, st); break;
+    default:
+      throw Error{GLX_E_INVALID, "A^T R: tile WL" + std::to_string(p.atr_wl) + " PF" + std::to_string(p.atr_pf) +
+                                     " NTL" + std::to_string(p.atr_ntl) + " is not built (round 6 pruning)"};
   }
 }
 
@@ -611,11 +601,11 @@ void launch_atr(const GemmPlan& p, const T* A, const T* R, T* Gp, hipStream_t st
 
 
 int atr_prox_slots(const GemmPlan& p, bool pub) {
-  return (int)(p.n / ((p.atr_wl == 3 || p.atr_wl == 4) ? 32 : 64)) + (pub ? 1 : 0);
+  return (int)(p.n / (p.atr_wl == 3 ? 32 : 64)) + (pub ? 1 : 0);
 }
 
 bool atr_prox_ok(const GemmPlan& p) {
-  if (p.atr_wl == 3 || p.atr_wl == 4)   // the 32-column panels: f64, no K splits (session_plan)
+  if (p.atr_wl == 3)   // the 32-column panel: f64, no K splits (session_plan)
     return p.atr_kind == 1 && p.esize == 8 && p.atr_S == 1 && (p.l == 16 || p.l == 32) &&
            p.n % 32 == 0 && p.n / 32 < kMaxBlocks;
   return p.atr_kind == 1 && (p.atr_wl == 0 || p.atr_wl == 2) && p.atr_S >= 1 && p.atr_S <= 8 &&
@@ -643,31 +633,22 @@ template <typename T, int NT>
 static void atr_prox_nt(const GemmPlan& p, const T* A, const T* R, T* G, const T* x, T* pp,
                         T* pthr, T* z, double t, double mu, double thres, Red red, hipStream_t st,
                         Pub pub, T* Gp, unsigned* pcnt, unsigned* zf) {
-  switch (p.atr_ntl * 100 + p.atr_wl * 10 + p.atr_pf) {
-    case 4: atr_prox_go<T, NT, 4, false, 0>(p, A, R, G, x, pp, pthr, z, t, mu, thres, red, st, pub, Gp, pcnt, zf); break;
-    case 6: atr_prox_go<T, NT, 6, false, 0>(p, A, R, G, x, pp, pthr, z, t, mu, thres, red, st, pub, Gp, pcnt, zf); break;
-    case 104: atr_prox_go<T, NT, 4, true, 0>(p, A, R, G, x, pp, pthr, z, t, mu, thres, red, st, pub, Gp, pcnt, zf); break;
-    case 108: atr_prox_go<T, NT, 8, true, 0>(p, A, R, G, x, pp, pthr, z, t, mu, thres, red, st, pub, Gp, pcnt, zf); break;
-    case 124: atr_prox_go<T, NT, 4, true, 2>(p, A, R, G, x, pp, pthr, z, t, mu, thres, red, st, pub, Gp, pcnt, zf); break;
-    case 128: atr_prox_go<T, NT, 8, true, 2>(p, A, R, G, x, pp, pthr, z, t, mu, thres, red, st, pub, Gp, pcnt, zf); break;
-    case 28: atr_prox_go<T, NT, 8, false, 2>(p, A, R, G, x, pp, pthr, z, t, mu, thres, red, st, pub, Gp, pcnt, zf); break;
-    case 38:
-    case 138:
-      if constexpr (sizeof(T) == 8) {
-        if (p.atr_ntl) atr_prox_go<T, NT, 8, true, 3>(p, A, R, G, x, pp, pthr, z, t, mu, thres, red, st, pub, Gp, pcnt, zf);
-        else atr_prox_go<T, NT, 8, false, 3>(p, A, R, G, x, pp, pthr, z, t, mu, thres, red, st, pub, Gp, pcnt, zf);
-        break;
-      }
-      throw Error{GLX_E_INVALID, "A^T R: the 32-column panel is f64"};
-    case 48:
-    case 148:
-      if constexpr (sizeof(T) == 8) {
-        if (p.atr_ntl) atr_prox_go<T, NT, 8, true, 4>(p, A, R, G, x, pp, pthr, z, t, mu, thres, red, st, pub, Gp, pcnt, zf);
-        else atr_prox_go<T, NT, 8, false, 4>(p, A, R, G, x, pp, pthr, z, t, mu, thres, red, st, pub, Gp, pcnt, zf);
-        break;
-      }
-      throw Error{GLX_E_INVALID, "A^T R: the 32-column panel is f64"};
-    default: atr_prox_go<T, NT, 8, false, 0>(p, A, R, G, x, pp, pthr, z, t, mu, thres, red, st, pub, Gp, pcnt, zf); break;
+  // the planner's fused tiles only (see atr_mfma_nt): f64 WL 0 PF 8 (+ non-temporal), WL 3
+  // (32-column panel); WL 2 non-temporal (fp32's eight-wave panel; f64 through GLX_ATR_VARIANT)
+  const int code = p.atr_ntl * 100 + p.atr_wl * 10 + p.atr_pf;
+  if constexpr (sizeof(T) == 8) {
+    switch (code) {
+      case 8: atr_prox_go<T, NT, 8, false, 0>(p, A, R, G, x, pp, pthr, z, t, mu, thres, red, st, pub, Gp, pcnt, zf); return;
+      case 38: atr_prox_go<T, NT, 8, false, 3>(p, A, R, G, x, pp, pthr, z, t, mu, thres, red, st, pub, Gp, pcnt, zf); return;
+      case 138: atr_prox_go<T, NT, 8, true, 3>(p, A, R, G, x, pp, pthr, z, t, mu, thres, red, st, pub, Gp, pcnt, zf); return;
+      default: break;
+    }
+  }
+  switch (code) {
+    case 108: atr_prox_go<T, NT, 8, true, 0>(p, A, R, G, x, pp, pthr, z, t, mu, thres, red, st, pub, Gp, pcnt, zf); return;
+    case 128: atr_prox_go<T, NT, 8, true, 2>(p, A, R, G, x, pp, pthr, z, t, mu, thres, red, st, pub, Gp, pcnt, zf); return;
+    default:
+      throw Error{GLX_E_INVALID, "fused A^T R + trial: tile code " + std::to_string(code) + " is not built"};
   }
 }
 template <typename T>
@@ -703,30 +684,20 @@ static void atr_fista_nt(const GemmPlan& p, const T* A, const T* R, T* G, const 
                          T* xc, T* vn, T* yn, double t, double mu, double thres, double theta,
                          double theta_next, Red red, hipStream_t st, Pub pub, T* Gp, unsigned* pcnt,
                          T* ec, unsigned* zf) {
-  switch (p.atr_ntl * 100 + p.atr_wl * 10 + p.atr_pf) {
-    case 4: atr_fista_go<T, NT, 4, false, 0>(p, A, R, G, y, xk, xc, vn, yn, t, mu, thres, theta, theta_next, red, st, pub, Gp, pcnt, ec, zf); break;
-    case 104: atr_fista_go<T, NT, 4, true, 0>(p, A, R, G, y, xk, xc, vn, yn, t, mu, thres, theta, theta_next, red, st, pub, Gp, pcnt, ec, zf); break;
-    case 108: atr_fista_go<T, NT, 8, true, 0>(p, A, R, G, y, xk, xc, vn, yn, t, mu, thres, theta, theta_next, red, st, pub, Gp, pcnt, ec, zf); break;
-    case 124: atr_fista_go<T, NT, 4, true, 2>(p, A, R, G, y, xk, xc, vn, yn, t, mu, thres, theta, theta_next, red, st, pub, Gp, pcnt, ec, zf); break;
-    case 128: atr_fista_go<T, NT, 8, true, 2>(p, A, R, G, y, xk, xc, vn, yn, t, mu, thres, theta, theta_next, red, st, pub, Gp, pcnt, ec, zf); break;
-    case 28: atr_fista_go<T, NT, 8, false, 2>(p, A, R, G, y, xk, xc, vn, yn, t, mu, thres, theta, theta_next, red, st, pub, Gp, pcnt, ec, zf); break;
-    case 38:
-    case 138:
-      if constexpr (sizeof(T) == 8) {
-        if (p.atr_ntl) atr_fista_go<T, NT, 8, true, 3>(p, A, R, G, y, xk, xc, vn, yn, t, mu, thres, theta, theta_next, red, st, pub, Gp, pcnt, ec, zf);
-        else atr_fista_go<T, NT, 8, false, 3>(p, A, R, G, y, xk, xc, vn, yn, t, mu, thres, theta, theta_next, red, st, pub, Gp, pcnt, ec, zf);
-        break;
-      }
-      throw Error{GLX_E_INVALID, "A^T R: the 32-column panel is f64"};
-    case 48:
-    case 148:
-      if constexpr (sizeof(T) == 8) {
-        if (p.atr_ntl) atr_fista_go<T, NT, 8, true, 4>(p, A, R, G, y, xk, xc, vn, yn, t, mu, thres, theta, theta_next, red, st, pub, Gp, pcnt, ec, zf);
-        else atr_fista_go<T, NT, 8, false, 4>(p, A, R, G, y, xk, xc, vn, yn, t, mu, thres, theta, theta_next, red, st, pub, Gp, pcnt, ec, zf);
-        break;
-      }
-      throw Error{GLX_E_INVALID, "A^T R: the 32-column panel is f64"};
-    default: atr_fista_go<T, NT, 8, false, 0>(p, A, R, G, y, xk, xc, vn, yn, t, mu, thres, theta, theta_next, red, st, pub, Gp, pcnt, ec, zf); break;
+  const int code = p.atr_ntl * 100 + p.atr_wl * 10 + p.atr_pf;   // the tiles of atr_prox_nt
+  if constexpr (sizeof(T) == 8) {
+    switch (code) {
+      case 8: atr_fista_go<T, NT, 8, false, 0>(p, A, R, G, y, xk, xc, vn, yn, t, mu, thres, theta, theta_next, red, st, pub, Gp, pcnt, ec, zf); return;
+      case 38: atr_fista_go<T, NT, 8, false, 3>(p, A, R, G, y, xk, xc, vn, yn, t, mu, thres, theta, theta_next, red, st, pub, Gp, pcnt, ec, zf); return;
+      case 138: atr_fista_go<T, NT, 8, true, 3>(p, A, R, G, y, xk, xc, vn, yn, t, mu, thres, theta, theta_next, red, st, pub, Gp, pcnt, ec, zf); return;
+      default: break;
+    }
+  }
+  switch (code) {
+    case 108: atr_fista_go<T, NT, 8, true, 0>(p, A, R, G, y, xk, xc, vn, yn, t, mu, thres, theta, theta_next, red, st, pub, Gp, pcnt, ec, zf); return;
+    case 128: atr_fista_go<T, NT, 8, true, 2>(p, A, R, G, y, xk, xc, vn, yn, t, mu, thres, theta, theta_next, red, st, pub, Gp, pcnt, ec, zf); return;
+    default:
+      throw Error{GLX_E_INVALID, "fused A^T R + FISTA trial: tile code " + std::to_string(code) + " is not built"};
   }
 }
 template <typename T>

@@ -64,86 +64,8 @@ constexpr int dma_lds_bytes() {
 template <int SLR>
 __device__ inline int dma_sw(int i) { return SLR >= 16 ? (i & 15) : ((i >> 1) & 7); }
 
-// Round 5, FIN (NSRC = 1; AxFin, glx_internal.h): the split-candidate trial's residual finalize
-// folded into the pass. Every workgroup stores its slab with agent-scope stores, drains vmcnt and
-// arrives on its row block's counter; the last arriver sums the row block's S slabs in slab
-// order (agent-scope loads), forms r1 = sum - b and r0 = r1 + (the A e slabs, written by the
-// gather launched before this pass), stores r1 and keeps sum r0^2, sum r1^2; then every
-// workgroup counts its share of |cx| > 1e-6 *cmax and joins one grid reduction (the final block
-// runs the device-side decision). No packet rides a FIN launch; every K split is non-empty.
-template <typename T>
-__device__ inline void ax_fin_epilogue(const AxFin& fin, const T* __restrict__ P, int S, int64_t m,
-                                       int64_t L, int64_t rb, int64_t rows, bool owner_block,
-                                       int nthr) {
-  double v[4] = {0.0, 0.0, 0.0, 0.0};
-  if (owner_block) {
-    __shared__ int fin_last;
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    if (threadIdx.x == 0)
-      fin_last = __hip_atomic_fetch_add(fin.cnt + rb, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
-                 (unsigned)S - 1;
-    __syncthreads();
-    if (fin_last) {
-      const int64_t ml = m * L;
-      const int64_t e0 = rb * rows * L;
-      const int64_t e1 = (rb + 1) * rows < m ? (rb + 1) * rows * L : ml;
-      const T* __restrict__ B = static_cast<const T*>(fin.B);
-      const T* __restrict__ P0 = static_cast<const T*>(fin.P0);
-      T* __restrict__ R1 = static_cast<T*>(fin.R1);
-      // all loads of a batch of EB elements per thread issued before the first is used (the S
-      // slabs with agent-scope loads, S <= kFinSlabs): a few round trips per row block instead of
-      // one per slab and element
-      constexpr int EB = 4, KS = 8;
-      for (int64_t base = e0 + threadIdx.x; base < e1; base += (int64_t)nthr * EB) {
-        T a[EB][KS], bv[EB], e[EB];
-#pragma unroll
-        for (int u = 0; u < EB; ++u) {
-          const int64_t idx = base + (int64_t)u * nthr;
-          const int64_t ic = idx < e1 ? idx : e1 - 1;
-#pragma unroll
-          for (int k = 0; k < KS; ++k)
-            a[u][k] = k < S ? __hip_atomic_load(P + (int64_t)k * ml + ic, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
-                            : T(0);
-          bv[u] = B[ic];
-          e[u] = slab_sum(P0, fin.S0, ml, ic);
-        }
-#pragma unroll
-        for (int u = 0; u < EB; ++u) {
-          const int64_t idx = base + (int64_t)u * nthr;
-          T sum = a[u][0];
-#pragma unroll
-          for (int k = 1; k < KS; ++k)
-            if (k < S) sum = sum + a[u][k];
-          const T r1 = sum - bv[u];
-          const T r0 = r1 + e[u];
-          if (idx < e1) {
-            R1[idx] = r1;
-            v[0] += (double)(r0 * r0);
-            v[1] += (double)(r1 * r1);
-          }
-        }
-      }
-      if (threadIdx.x == 0) __hip_atomic_store(fin.cnt + rb, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-  }
-  if (fin.cx != nullptr) {   // this workgroup's share of the candidate's sparsity count
-    const T* __restrict__ cx = static_cast<const T*>(fin.cx);
-    const T thr = (T)1e-6 * (T)(*fin.cmax);
-    const int64_t c0 = fin.cn * blockIdx.x / gridDim.x, c1 = fin.cn * (blockIdx.x + 1) / gridDim.x;
-    for (int64_t idx = c0 + threadIdx.x; idx < c1; idx += nthr) v[3] += (tabs(cx[idx]) > thr) ? 1.0 : 0.0;
-  }
-  const bool last = grid_reduce<4, 0u, 8>(v, fin.red);
-  if (last && fin.ctl.rec != nullptr && threadIdx.x == 0) {
-    double pre[10];
-    for (int k = 0; k < 6; ++k) pre[k] = fin.ctl.tr[k];
-    for (int k = 0; k < 4; ++k) pre[6 + k] = fin.ctl.state[k];
-    ctl_decide(fin.ctl, fin.red.out, pre);
-  }
-}
-
 template <typename T, int NT, int NSRC, int NS, int KC, int WAVES, bool NTL, bool HOIST, bool PIPE,
-          int MT, bool FIN = false>
+          int MT>
 __global__ __launch_bounds__(64 * WAVES) void k_ax_dma(const T* __restrict__ A,
                                                       const T* __restrict__ X0,
                                                       const T* __restrict__ X1,
@@ -151,8 +73,7 @@ __global__ __launch_bounds__(64 * WAVES) void k_ax_dma(const T* __restrict__ A,
                                                       T* __restrict__ P, int64_t m, int64_t n,
                                                       int64_t chunks, int S, int gx, int xmap,
                                                       const int* __restrict__ gate, int epoch,
-                                                      Pub pub, int keep_mib, AxFin fin) {
-  static_assert(!FIN || (NSRC == 1 && WAVES == 8), "the folded finalize: one source, 8 waves");
+                                                      Pub pub, int keep_mib) {
   typedef MF<T> M;
   typedef typename M::acc_t C;
   typedef typename M::vec_t V;                      // one 16-B slot of A
@@ -198,10 +119,7 @@ __global__ __launch_bounds__(64 * WAVES) void k_ax_dma(const T* __restrict__ A,
   }
   if (!gate_live(gate, epoch)) return;
   int bx, by;
-  if (!ax_block(xmap, gx, S, bx, by, pub.host != nullptr ? 1 : 0)) {
-    if constexpr (FIN) ax_fin_epilogue<T>(fin, P, S, m, 16 * NT, 0, 16 * MT * WAVES, false, 64 * WAVES);
-    return;
-  }
+  if (!ax_block(xmap, gx, S, bx, by, pub.host != nullptr ? 1 : 0)) return;
 
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -446,33 +364,26 @@ __global__ __launch_bounds__(64 * WAVES) void k_ax_dma(const T* __restrict__ A,
         const int64_t row = row0 + mt * 16 + M::row(lane, r);
         if (row < m) {
 #pragma unroll
-          for (int nt = 0; nt < NT; ++nt) {
-            if constexpr (FIN)   // agent scope: the row block's last arriver reads them
-              __hip_atomic_store(pout + row * L + nt * 16 + i, acc[mt][sr * NT + nt][r], __ATOMIC_RELAXED,
-                                 __HIP_MEMORY_SCOPE_AGENT);
-            else
-              pout[row * L + nt * 16 + i] = acc[mt][sr * NT + nt][r];
-          }
+          for (int nt = 0; nt < NT; ++nt) pout[row * L + nt * 16 + i] = acc[mt][sr * NT + nt][r];
         }
       }
   }
-  if constexpr (FIN) ax_fin_epilogue<T>(fin, P, S, m, L, bx, 16 * MT * WAVES, true, 64 * WAVES);
   GLX_CLK(3);
 }
 
 template <typename T, int NT, int NSRC, int NS, int KC, int WAVES, bool NTL, bool HOIST = false,
-          bool PIPE = false, int MT = 1, bool FIN = false>
+          bool PIPE = false, int MT = 1>
 static void ax_dma_go(const GemmPlan& p, int S, const T* A, const T* const* X, T* P,
-                      const int* gate, int epoch, hipStream_t st, Pub pub, const AxFin& fin = AxFin{}) {
+                      const int* gate, int epoch, hipStream_t st, Pub pub) {
   if constexpr (dma_lds_bytes<T, NT, NSRC, NS, KC, WAVES, MT>() > 160 * 1024) {
     throw Error{GLX_E_INVALID, "A@X: this LDS-DMA tile does not fit (160 KiB of LDS)"};
   } else {
     const int gx = (int)cdiv(p.m, 16 * MT * WAVES);
     const int xmap = ax_xmap_flags(p, S);
     const dim3 grid((unsigned)ax_grid(xmap, gx, S) + (pub.host ? 1u : 0u));
-    glx_launch((k_ax_dma<T, NT, NSRC, NS, KC, WAVES, NTL, HOIST, PIPE, MT, FIN>), grid, dim3(64 * WAVES), 0, st,
+    glx_launch((k_ax_dma<T, NT, NSRC, NS, KC, WAVES, NTL, HOIST, PIPE, MT>), grid, dim3(64 * WAVES), 0, st,
                        A, X[0], X[1], X[2], P, p.m, p.n, p.n / KC, S, gx, xmap, gate, epoch, pub,
-                       p.ax_keep_mib, fin);
+                       p.ax_keep_mib);
   }
 }
 
@@ -520,34 +431,6 @@ bool launch_ax_dma(const GemmPlan& p, int code, int nsrc, int S, const T* A, con
   if (nsrc == 2) return dma_code<T, 2, 2>(p, code, S, A, X, P, gate, epoch, st, pub);
   return dma_code<T, 2, 3>(p, code, S, A, X, P, gate, epoch, st, pub);
 }
-// the folded-finalize form of the one-source f64 pass (92278; AxFin)
-int ax_fin_counters(const GemmPlan& p) { return (int)cdiv(p.m, 16 * 2 * 8); }
-bool ax_fin_ok(const GemmPlan& p, int esize) {
-  const int S = p.axb_S[1];
-  return esize == 8 && p.ax_kind != 3 && p.axb_code[1] == 92278 && (p.l == 16 || p.l == 32) &&
-         S >= 1 && S <= 8 && p.n / 32 >= S && ax_grid(ax_xmap_flags(p, S), (int)cdiv(p.m, 256), S) <= kMaxBlocks;
-}
-
-template <typename T>
-bool launch_ax_fin(const GemmPlan& p, const T* A, const T* X, T* P, const int* gate, int epoch,
-                   hipStream_t st, const AxFin& fin) {
-  if constexpr (sizeof(T) != 8) {
-    return false;
-  } else {
-    const int S = p.axb_S[1];
-    if (!ax_fin_ok(p, 8) || fin.cnt == nullptr) return false;
-    const T* xs[3] = {X, nullptr, nullptr};
-    if (p.l == 16)
-      ax_dma_go<T, 1, 1, 2, 32, 8, true, true, true, 2, true>(p, S, A, xs, P, gate, epoch, st, Pub{}, fin);
-    else
-      ax_dma_go<T, 2, 1, 2, 32, 8, true, true, true, 2, true>(p, S, A, xs, P, gate, epoch, st, Pub{}, fin);
-    return true;
-  }
-}
-template bool launch_ax_fin<double>(const GemmPlan&, const double*, const double*, double*, const int*, int,
-                                    hipStream_t, const AxFin&);
-template bool launch_ax_fin<float>(const GemmPlan&, const float*, const float*, float*, const int*, int,
-                                   hipStream_t, const AxFin&);
 
 template bool launch_ax_dma<double>(const GemmPlan&, int, int, int, const double*, const double* const*,
                                     double*, const int*, int, hipStream_t, Pub);

@@ -280,6 +280,7 @@ __global__ __launch_bounds__(kGThreads) void k_at_gather_bm(const T* __restrict_
   for (int64_t w0 = 0; w0 < nw; w0 += SEGW) {
     const int64_t w = w0 + tid;
     uint64_t bits = (tid < SEGW && w < nw) ? words[w] : uint64_t(0);
+    if (w == nw - 1 && (n & 63) != 0) bits &= (uint64_t(1) << (n & 63)) - 1;   // rows >= n: never
     const unsigned cnt = (unsigned)__builtin_popcountll(bits);
     unsigned inc = cnt;
 #pragma unroll

@@ -677,11 +677,15 @@ GemmPlan make_plan(int esize, int64_t m, int64_t n, int64_t l, int ax_variant) {
   if (atr_code == 0)
     atr_code = esize == 8 ? ((double)m * n * esize > kAtrNtBytes ? kAtrDefaultBig : kAtrDefault)
                           : kAtrDefault32;
-  const int ntl = atr_code >= 1000 ? 1 : 0;
+  int ntl = atr_code >= 1000 ? 1 : 0;
   int wl = (atr_code / 10) % 10;
-  const int pf = atr_code % 10;
+  int pf = atr_code % 10;
   if (wl == 1 && n % 256 != 0) wl = 0;   // four shared-row panels need n % 256: one panel per block
-  if (wl > 4 || ((wl == 3 || wl == 4) && (esize != 8 || n % 32 != 0))) wl = 0;   // 3 / 4: 32-column f64 panels (4 / 8 waves)
+  if (wl > 3 || (wl == 3 && (esize != 8 || n % 32 != 0))) wl = 0;   // 3: the 32-column f64 panel (4 waves)
+  // Round 6: only the planner's tiles are built (kernels_atr.hip atr_mfma_nt): WL 0 / 3 with the
+  // PF 8 ring, WL 2 with PF 8 and non-temporal A, WL 1 with PF 4 and non-temporal A
+  if (wl == 1) { pf = 4; ntl = 1; }
+  else { pf = 8; if (wl == 2) ntl = 1; }
   const bool atr_mfma_ok = mfma_l && (n % 64 == 0) && (m % 4 == 0);
   if (ax_variant == 3 || atr_code == 3 || !atr_mfma_ok) {
     p.atr_kind = 3;
@@ -699,7 +703,7 @@ GemmPlan make_plan(int esize, int64_t m, int64_t n, int64_t l, int ax_variant) {
     p.atr_ntl = ntl;
     const int64_t steps = m / 4;
     if (p.atr_wl != 1) {
-      const int64_t blocks = n / ((p.atr_wl == 3 || p.atr_wl == 4) ? 32 : 64);
+      const int64_t blocks = n / (p.atr_wl == 3 ? 32 : 64);
       // f64: one wave per SIMD is enough with the PF-8 ring (and S = 1 at n = 16384 lets the
       // ProxGD trial fuse into the kernel); f32 wants 4 per SIMD
       const int64_t target = esize == 8 ? kTargetWaves / 2 : 2 * kTargetWaves;
@@ -745,7 +749,7 @@ std::string describe_plan(const GemmPlan& p) {
     std::snprintf(buf, sizeof buf, "atr=k_atr_valu<LB%d,VEC%d> S=%d", p.atr_lb, p.atr_vec, p.atr_S);
   else
     std::snprintf(buf, sizeof buf, "atr=k_atr_mfma<WL%d,PF%d,NTL%d> S=%d%s", p.atr_wl, p.atr_pf, p.atr_ntl, p.atr_S,
-                  p.atr_wl == 3 ? " (32-column panels)" : (p.atr_wl == 4 ? " (32-column panels, 8 waves)" : ""));
+                  p.atr_wl == 3 ? " (32-column panels)" : "");
   return s + buf;
 }
 

@@ -16,6 +16,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <atomic>
 #include <cstdio>
 #include <cstdlib>
 #include <chrono>
@@ -162,10 +163,12 @@ static void validate(const glx_problem* P, const glx_opts* O) {
 // against 3.4e-7 for the dense batch. Round 5 measured the band (scripts/c3_band.py,
 // profiles/r5_d/c3_band.jsonl): eleven summation orders of the two forms (K splits, tiles, A e
 // forms) end 3.4e-7 .. 8.7e-5 (dense) and 1.6e-5 .. 8.9e-5 (split) from the reference's fp32
-// objective, all 7.0e-3 .. 7.1e-3 from its fp64 one (the reference's own fp32 run: 7.0e-3). The
-// split form's band is no worse, so it is the default (GLX_SPLIT_F32=0: the dense batch); whole
-// solves run level (3897 it/s both: late in a solve e_c fills and the budget runs dense batches),
-// 200-step windows +17 %. (The size gate counts elements as fp64.)
+// objective, all 7.0e-3 .. 7.1e-3 from its fp64 one (the reference's own fp32 run: 7.0e-3).
+// Round 6: the dense batch is the fp32 default again — its default order ends
+// 3.4e-7 from the reference's fp32 run, inside the 1e-6 fp32 bar, the split form's 1.6e-5 does
+// not, and whole solves run level (3897 it/s both: late in a solve e_c fills and the budget runs
+// dense batches; only 200-step windows gain, +17 %). GLX_SPLIT_F32=1: the split form (opt-in).
+// (The size gate counts elements as fp64.)
 // FProxGD with line search takes the gather form too (iter_fista: A y_next by linearity from
 // A xc, A e_c and the kept A thr(x_k)); GLX_SPLIT_FISTA=0 keeps its dense [xc | y_next] batch.
 // Only for A of at least kSplitMinBytes (this rank's rows): the column lists and the gather
@@ -185,9 +188,9 @@ static constexpr double kSplitMinBytes = 768.0 * 1024 * 1024;
 static int split_mode(const glx_problem& P, const glx_opts& O) {
   if (O.exact_objective != 0) return 0;
   if (P.method != GLX_PROXGD && P.method != GLX_FPROXGD) return 0;
-  if (P.dtype != GLX_F64) {   // fp32: FProxGD only (GLX_SPLIT_F32=0: off, above)
+  if (P.dtype != GLX_F64) {   // fp32: FProxGD only, opt-in (GLX_SPLIT_F32=1, above)
     const char* f = std::getenv("GLX_SPLIT_F32");
-    if (P.method != GLX_FPROXGD || (f && std::strcmp(f, "0") == 0)) return 0;
+    if (P.method != GLX_FPROXGD || !(f && std::strcmp(f, "1") == 0)) return 0;
   }
   if (O.split_cand == 2) return 0;
   const char* sc = O.split_cand == 0 ? std::getenv("GLX_SPLIT_CAND") : nullptr;
@@ -230,14 +233,15 @@ static GemmPlan session_plan(const glx_problem& P, const glx_opts& O) {
   }
   // Round 5: fp64 with fewer than 256 64-column panels (C2: 128, planned as 2 K splits) takes
   // the 32-column panel without K splits (WL 3): 256+ workgroups and no slab combine in front of
-  // the fused trial. GLX_ATR_NARROW=0: off.
+  // the fused trial. GLX_ATR_NARROW=0: off. (Its eight-wave form, WL 4, measured slower and is no
+  // longer built, round 6.)
   if (es == 8 && P.comm == nullptr && trial_method && p.atr_kind == 1 && (P.l == 16 || P.l == 32) &&
       P.n % 32 == 0 && P.n / 64 < 256 && P.n / 32 >= 256 && !std::getenv("GLX_ATR_VARIANT") &&
       !std::getenv("GLX_ATR_S") && !std::getenv("GLX_FUSED_TRIAL")) {
     const char* nw = std::getenv("GLX_ATR_NARROW");
     if (!(nw && std::strcmp(nw, "0") == 0)) {
       GemmPlan f = p;
-      f.atr_wl = (nw && std::strcmp(nw, "8") == 0) ? 4 : 3;   // GLX_ATR_NARROW=8: eight waves
+      f.atr_wl = 3;
       f.atr_pf = 8;
       f.atr_S = 1;
       if (atr_prox_ok(f)) return f;
@@ -253,6 +257,8 @@ class SessionBase {
   virtual void finish(glx_result* res) = 0;
   virtual void kernel_time(int kind, int64_t* launches, double* ms) = 0;
   virtual void counters(int64_t out[4]) const = 0;
+  // thread-safe progress record (a watchdog thread reads it while run() is in progress)
+  virtual void progress(int64_t out[4]) const = 0;
   virtual void trace(double* sp_after, int64_t cap, int64_t* n, int64_t phase_info[6]) const = 0;
   virtual std::string describe() const = 0;
   virtual int64_t split_trace(double* out, int64_t cap) const = 0;
@@ -297,8 +303,6 @@ class Session : public SessionBase {
     unsigned* ticket = static_cast<unsigned*>(c.take(kTicketBytes));
     // per-panel arrival counters of the fused A^T R with K splits (atr_split_combine)
     unsigned* pcnt = static_cast<unsigned*>(c.take(sizeof(unsigned) * (P.n / 64 + 64)));
-    // row-block arrival counters of the dense pass with the folded finalize (launch_ax_fin)
-    unsigned* fcnt = static_cast<unsigned*>(c.take(sizeof(unsigned) * (ax_fin_counters(plan) + 64)));
     int* flag = static_cast<int*>(c.take(256));
     // device-controlled batches: Ctl::state (4 doubles) and the abort word; decision records
     double* dcs = static_cast<double*>(c.take(256));
@@ -324,7 +328,6 @@ class Session : public SessionBase {
       s->G_ = g[0]; s->Gp_ = gp[0]; s->Pp_ = pp; s->At_ = at; s->glists_ = glists;
       s->scal_ = scal; s->part_ = part; s->ticket_ = ticket; s->flag_ = flag; s->fh_dev_ = fh;
       s->pcnt_ = pcnt;
-      s->fcnt_ = fcnt;
       s->dc_state_ = dcs;
       s->dc_abort_ = reinterpret_cast<int*>(dcs + 8);
       s->dc_rec_ = dcr;
@@ -482,12 +485,9 @@ class Session : public SessionBase {
       launch_transpose<T>(static_cast<const T*>(P.A), At_, m_, n_, st_);   // once
     }
     fused_fista_ok_ = fuse_any && P.method == GLX_FPROXGD;
-    // Round 5: the split-candidate ProxGD trial's finalize folded into its dense pass (one GPU;
-    // with a communicator the sums ride the gradient all-reduce). Measured slower, so opt-in
-    // (GLX_AX_FIN=1): A p_thr 167-168 -> 207 us, NS 2537-2543 -> 2376 it/s over 200 steps
-    // (profiles/r5_d/): the slab stores go write-through (agent scope) and the 32 row-block
-    // owners' combine runs alone at the end of the pass, against k_finalize_residual's 12 us.
-    fin_ok_ = emode_ && comm_ == nullptr && ax_fin_ok(plan_, (int)sizeof(T)) && env_is("GLX_AX_FIN", "1");
+    // (Round 5's folded finalize — the split-candidate trial's finalize inside its dense pass,
+    // GLX_AX_FIN=1 — measured slower, 2376 against 2537-2543 it/s at NS, and was removed in round 6;
+    // DESIGN.md keeps the numbers.)
     // device-controlled batches (dc_run / fista_dc_run): ProxGD / FProxGD with line search on
     // the fused speculative path; GLX_DC_BATCH = iterations in flight (0: the host decides every
     // iteration). With a communicator fp64 only (the trial sums ride the gradient all-reduce).
@@ -502,18 +502,22 @@ class Session : public SessionBase {
     }
     // Row-sharded ProxGD (round 5, iter_proxgd_shard): with a communicator of G > 1 ranks the
     // gradient is reduce-scattered, the trial runs on this rank's n / G rows and p's rows are
-    // all-gathered (opts.shard_rows: 0 auto = on where n % G == 0, 1 on, 2 off; GLX_SHARD_ROWS overrides). Host
-    // control only (a device-control window keeps the all-reduce schedule). GLX_SHARD_MODEL=G at
-    // world size 1 (bench.py --force-comm): the per-rank timing model of G ranks — the trial on
-    // n / G rows, every line-search test accepted — whose iterates are NOT a solve.
+    // all-gathered (opts.shard_rows: 0 auto = on where n % G == 0, 1 on, 2 off; GLX_SHARD_ROWS,
+    // same codes, overrides). Host control only (a device-control window keeps the all-reduce
+    // schedule). opts.shard_model = G at world size 1 (bench.py --shard-model, with --force-comm):
+    // the per-rank timing model of G ranks — the trial on n / G rows, every line-search test
+    // accepted — whose iterates are NOT a solve (glx_solve refuses it; ADVICE round 5: no
+    // environment variable turns it on inside the library).
     if (comm_ != nullptr && P.method == GLX_PROXGD && dc_window_ == 0) {
       int want = O.shard_rows;
-      if (const char* e = std::getenv("GLX_SHARD_ROWS")) want = std::atoi(e) == 0 ? 2 : 1;
+      if (const char* e = std::getenv("GLX_SHARD_ROWS")) {
+        want = std::atoi(e);
+        if (want < 0 || want > 2) throw Error{GLX_E_INVALID, "GLX_SHARD_ROWS must be 0 (auto), 1 (on) or 2 (off)"};
+      }
       cranks_ = comm_size(comm_);
       int vr = cranks_;
       if (cranks_ == 1) {
-        const char* mdl = std::getenv("GLX_SHARD_MODEL");
-        vr = mdl ? std::max(1, std::atoi(mdl)) : 1;
+        vr = std::max(1, O.shard_model);
         shard_model_ = vr > 1;
       }
       const bool fits = vr <= kMaxShardRanks && n_ % vr == 0;
@@ -551,16 +555,18 @@ class Session : public SessionBase {
     // in-kernel reduction.
     // ProxGD only: FProxGD's k_atr_fista measured no gain (NS FProxGD 2583 / 2582, C3 4527 / 4535
     // it/s over 200 steps, profiles/r5_defer3/) and lost 8 % on the rejection-heavy probe
-    // (its publisher's reduction stretched the 33 us fused kernel by ~4 us); GLX_DEFER_RED=2 takes
-    // it for FProxGD too.
-    const bool dmeth = P.method == GLX_PROXGD || (P.method == GLX_FPROXGD && env_is("GLX_DEFER_RED", "2"));
-    defer_ = comm_ == nullptr && dc_window_ == 0 && dmeth && spin_readback_ && attach_ok_ && !fin_ok_ &&
+    // (its publisher's reduction stretched the 33 us fused kernel by ~4 us); that opt-in form
+    // (GLX_DEFER_RED=2) was removed in round 6.
+    const bool dmeth = P.method == GLX_PROXGD;
+    defer_ = comm_ == nullptr && dc_window_ == 0 && dmeth && spin_readback_ && attach_ok_ &&
              !env_is("GLX_DEFER_RED", "0");
     GLX_HIP(hipMemsetAsync(ticket_, 0, kTicketBytes, st_));
     GLX_HIP(hipMemsetAsync(pcnt_, 0, sizeof(unsigned) * (P.n / 64 + 64), st_));
-    GLX_HIP(hipMemsetAsync(fcnt_, 0, sizeof(unsigned) * (ax_fin_counters(plan_) + 64), st_));
     GLX_HIP(hipMemsetAsync(flag_, 0, 256, st_));
     GLX_HIP(hipMemsetAsync(scal_, 0, sizeof(double) * NSCAL_DEV, st_));
+    // the column bitmaps' words no trial visits (rows in [ceil16(n), ceil64(n)), the upper half
+    // of a narrow panel's last u64) must read as 0 (glx_device.h zf_bitmaps)
+    GLX_HIP(hipMemsetAsync(zf_, 0, zf_bytes(P.n), st_));
     if (blk_) GLX_HIP(hipMemsetAsync(blk_, 0, sizeof(double) * kShardChunkMax * kMaxShardRanks, st_));
     mus_[0] = 100 * P.mu0;
     mus_[1] = 10 * P.mu0;
@@ -607,6 +613,8 @@ class Session : public SessionBase {
         default: iter_descent(); break;
       }
       steps += k_ - k0;
+      prog_k_.store(k_, std::memory_order_relaxed);
+      prog_phase_.store(phase_, std::memory_order_relaxed);
       if (O_.max_total_iters > 0 && k_ >= O_.max_total_iters) finished_ = true;
     }
     GLX_HIP(hipStreamSynchronize(st_));
@@ -698,13 +706,19 @@ class Session : public SessionBase {
     else if (rows_form_) s += "rows k_at_rows S0=" + std::to_string(gsplit_);
     else if (gform_ == 2) s += "gather k_e_lists+k_at_gather";
     else s += "gather k_at_gather_bm";
-    if (fin_ok_) s += " + finalize folded into A p_thr";
     if (shard_)
       s += "; rows=sharded x" + std::to_string(sranks_) + (shard_model_ ? " (timing model)" : "") +
            " (reduce-scatter of A^T r, k_prox_pgd on n/" + std::to_string(sranks_) +
            " rows, all-gather of p, k_trial_split)";
     s += "; dc_window=" + std::to_string(dc_window_);
     return s;
+  }
+
+  void progress(int64_t out[4]) const override {
+    out[0] = prog_k_.load(std::memory_order_relaxed);
+    out[1] = prog_phase_.load(std::memory_order_relaxed);
+    out[2] = prog_wait_.load(std::memory_order_relaxed);
+    out[3] = comm_ != nullptr ? comm_issued(comm_) : 0;
   }
 
   void counters(int64_t out[4]) const override {
@@ -837,11 +851,6 @@ class Session : public SessionBase {
                  unsigned* pub_seq = nullptr, double* defer = nullptr, bool skip_ax = false,
                  bool snap_trial = false, bool chain = false) {
     const bool gat = chain && smode_ == 1;
-    if (gat && fin_ok_ && !skip_ax && defer == nullptr && !snap_trial && fh == nullptr) {
-      cand_ax_fin(xs, rs[1], cx, cmax, red(slot));
-      if (pub_seq != nullptr) *pub_seq = post_readback();
-      return;
-    }
     if (!skip_ax) {
       if (gat) cand_ax(xs);
       else spec_ax(nsrc, xs);
@@ -916,40 +925,6 @@ class Session : public SessionBase {
     else launch_at_gather_bm<T>(At_, xs[0], zf_, m_, n_, l_, Pp_, glists_, st_, dc_gate_);
     check_launch();
     prof_end(2, e2);
-    ++ax_calls_;
-    ax_cols_ += 1;
-  }
-  // The same trial with the finalize folded into the dense pass (fin_ok_, launch_ax_fin): A e first
-  // (its slabs at Pp_), then A p_thr, whose row blocks' last K-split arrivals form r1 = A p_thr - b
-  // (into r1), r0 = r1 + A e and the sums (red: [|r0|^2, |r1|^2, 0, count(|cx| > 1e-6 *cmax)];
-  // dc_ctl_: the device-side decision in the final workgroup).
-  void cand_ax_fin(const T* const* xs, T* r1, const T* cx, const double* cmax, Red rd) {
-    if (gform_ == 2) {
-      launch_e_lists(zf_, n_, l_, glists_, st_, dc_gate_);
-      check_launch();
-    }
-    hipEvent_t e2 = prof_begin(2);
-    if (gform_ == 1) launch_at_rows<T>(At_, xs[0], zf_, m_, n_, l_, Pp_, glists_, st_, dc_gate_);
-    else if (gform_ == 2) launch_at_gather<T>(At_, xs[0], m_, n_, l_, Pp_, glists_, st_, dc_gate_);
-    else launch_at_gather_bm<T>(At_, xs[0], zf_, m_, n_, l_, Pp_, glists_, st_, dc_gate_);
-    check_launch();
-    prof_end(2, e2);
-    AxFin f;
-    f.B = B_;
-    f.R1 = r1;
-    f.P0 = Pp_;
-    f.S0 = gsplit_;
-    f.cx = cx;
-    f.cn = cx ? nl_ : 0;
-    f.cmax = cmax;
-    f.cnt = fcnt_;
-    f.red = rd;
-    f.ctl = dc_ctl_;
-    hipEvent_t e0 = prof_begin(0);
-    if (!launch_ax_fin<T>(plan_, A_, xs[1], Pp_ + (size_t)gsplit_ * ml_, dc_gate_, 0, st_, f))
-      throw Error{GLX_E_STATE, "folded finalize: the plan does not take it"};
-    check_launch();
-    prof_end(0, e0);
     ++ax_calls_;
     ax_cols_ += 1;
   }
@@ -1101,17 +1076,49 @@ class Session : public SessionBase {
     volatile unsigned* hs = hseq_;
     uint64_t spins = 0;
     auto t0 = std::chrono::steady_clock::time_point{};
+    prog_wait_.store(1, std::memory_order_relaxed);
     while (*hs != seq) {
       __builtin_ia32_pause();
       if ((++spins & 0xFFFFF) == 0) {
         if (spins == 0x100000) t0 = std::chrono::steady_clock::now();
-        else if (std::chrono::steady_clock::now() - t0 > std::chrono::seconds(5)) {
-          GLX_HIP(hipStreamSynchronize(st_));   // surfaces a device error, if any
-          if (*hs != seq) throw Error{GLX_E_HIP, "scalar readback timed out"};
-        }
+        else stalled_wait(t0, [&] { return *hs == seq; }, "scalar readback");
       }
     }
+    prog_wait_.store(0, std::memory_order_relaxed);
     __atomic_thread_fence(__ATOMIC_ACQUIRE);
+  }
+  // A host wait that has spun for over ~5 s. Without a communicator the stream is synchronised
+  // (it surfaces a device error) and the wait fails if the word still has not come. With RCCL
+  // (round 6) a collective may be waiting for a peer: the stream is only
+  // queried, RCCL's asynchronous error is polled (an error aborts the communicator, so the
+  // blocked RCCL kernels return and the stream drains, then throws), and after GLX_WAIT_TIMEOUT_S
+  // (default 300 s) the communicator is aborted too and the wait fails with the progress record
+  // (iteration, collectives issued) — a diagnostic instead of a silent hang.
+  template <typename Done>
+  void stalled_wait(std::chrono::steady_clock::time_point t0, Done done, const char* what) {
+    if (comm_ == nullptr || !comm_is_rccl(comm_)) {
+      if (std::chrono::steady_clock::now() - t0 > std::chrono::seconds(5)) {
+        GLX_HIP(hipStreamSynchronize(st_));   // surfaces a device error, if any
+        if (!done()) throw Error{GLX_E_HIP, std::string(what) + " timed out"};
+      }
+      return;
+    }
+    const int aerr = comm_async_error(comm_);
+    const double waited = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+    static const double limit = [] {
+      const char* e = std::getenv("GLX_WAIT_TIMEOUT_S");
+      return e ? std::atof(e) : 300.0;
+    }();
+    if (aerr == 0 && (limit <= 0 || waited < limit)) return;
+    const std::string why =
+        std::string(what) + (aerr != 0 ? " failed: RCCL asynchronous error " + std::to_string(aerr)
+                                       : " stalled for " + std::to_string((int)waited) + " s") +
+        " on rank " + std::to_string(comm_rank(comm_)) + " of " + std::to_string(comm_size(comm_)) +
+        " at iteration " + std::to_string(k_) + " (phase " + std::to_string(phase_) + "), after " +
+        std::to_string(comm_issued(comm_)) + " collectives issued; the communicator was aborted";
+    comm_abort(comm_);
+    (void)hipStreamSynchronize(st_);   // the aborted RCCL kernels return
+    throw Error{GLX_E_RCCL, why};
   }
   void readback() { wait_readback(post_readback()); }
 
@@ -1658,16 +1665,15 @@ class Session : public SessionBase {
     const unsigned want = (unsigned)tag;
     uint64_t spins = 0;
     auto t0 = std::chrono::steady_clock::time_point{};
+    prog_wait_.store(2, std::memory_order_relaxed);
     while (*tp != want) {
       __builtin_ia32_pause();
       if ((++spins & 0xFFFFF) == 0) {
         if (spins == 0x100000) t0 = std::chrono::steady_clock::now();
-        else if (std::chrono::steady_clock::now() - t0 > std::chrono::seconds(5)) {
-          GLX_HIP(hipStreamSynchronize(st_));   // surfaces a device error, if any
-          if (*tp != want) throw Error{GLX_E_STATE, "device-controlled batch: decision record missing"};
-        }
+        else stalled_wait(t0, [&] { return *tp == want; }, "device-controlled batch: decision record");
       }
     }
+    prog_wait_.store(0, std::memory_order_relaxed);
     __atomic_thread_fence(__ATOMIC_ACQUIRE);
     return rec;
   }
@@ -2291,8 +2297,6 @@ class Session : public SessionBase {
   unsigned *hseq_ = nullptr, *hseq_dev_ = nullptr;
   unsigned* ticket_ = nullptr;
   unsigned* pcnt_ = nullptr;   // per-panel counters (fused A^T R with K splits)
-  unsigned* fcnt_ = nullptr;   // per-row-block counters (the dense pass's folded finalize)
-  bool fin_ok_ = false;        // the split-candidate ProxGD finalize folded into the dense pass
   unsigned* zf_ = nullptr;     // per-row column masks of e (split-candidate mode)
   // row-sharded ProxGD (iter_proxgd_shard): this rank's rows [srow0_, srow0_ + srows_) of n,
   // sranks_ row blocks (cranks_ communicator ranks; they differ only in the timing model)
@@ -2347,6 +2351,10 @@ class Session : public SessionBase {
   const int* dc_gate_ = nullptr;  // while queuing a batch: the abort word the launches test
   Ctl dc_ctl_{};                  // while queuing a batch: the finalize's decision epilogue
   int64_t fh_cap_ = 0;
+  // progress record for glx_session_progress (read by other threads): iterations, phase, what
+  // the host is waiting on (0 nothing, 1 a scalar packet, 2 a decision record)
+  std::atomic<int64_t> prog_k_{0};
+  std::atomic<int> prog_phase_{0}, prog_wait_{0};
   double* sp100_ = nullptr;   // SGD/GD: count(|x| > 1e-6 max|x|) after every 100th iteration
   T* gemv_slabs_ = nullptr;
   int gemv_blocks_ = 0;
@@ -2568,6 +2576,13 @@ int glx_session_counters(glx_session* s, int64_t out[4]) {
   });
 }
 
+int glx_session_progress(glx_session* s, int64_t out[4]) {
+  return guarded([&] {
+    if (!s || !s->impl || !out) throw Error{GLX_E_INVALID, "null session/out"};
+    s->impl->progress(out);
+  });
+}
+
 int glx_session_trace(glx_session* s, double* sparsity_after, int64_t cap, int64_t* n,
                       int64_t phase_info[6]) {
   return guarded([&] {
@@ -2595,6 +2610,11 @@ void glx_session_destroy(glx_session* s) { delete s; }
 
 int glx_solve(const glx_problem* prob, const glx_opts* opts, void* workspace,
               size_t workspace_bytes, glx_result* res, void* stream) {
+  if (opts != nullptr && opts->shard_model > 1) {   // a timing model is not a solve
+    g_last_error = "opts.shard_model is a benchmark timing model whose iterates are not a solve; "
+                   "glx_solve refuses it (use the session API, as bench.py does)";
+    return GLX_E_INVALID;
+  }
   glx_session* s = nullptr;
   int rc = glx_session_create(&s, prob, opts, workspace, workspace_bytes, stream);
   if (rc != GLX_OK) return rc;

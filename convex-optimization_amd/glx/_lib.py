@@ -30,7 +30,7 @@ class GlxOpts(ctypes.Structure):
                 ("continuous_subgradient", c_int32), ("exact_objective", c_int32),
                 ("profile", c_int32), ("max_total_iters", c_int64), ("ax_variant", c_int32),
                 ("split_cand", c_int32), ("dc_window", c_int32), ("shard_rows", c_int32),
-                ("reserved", c_int32 * 4)]
+                ("shard_model", c_int32), ("reserved", c_int32 * 3)]
 
 
 class GlxProblem(ctypes.Structure):
@@ -68,6 +68,7 @@ _SIGS = {
     "glx_session_finish": (c_int, [c_void_p, POINTER(GlxResult)]),
     "glx_session_kernel_time": (c_int, [c_void_p, c_int, POINTER(c_int64), POINTER(c_double)]),
     "glx_session_counters": (c_int, [c_void_p, POINTER(c_int64)]),
+    "glx_session_progress": (c_int, [c_void_p, POINTER(c_int64)]),
     "glx_session_trace": (c_int, [c_void_p, POINTER(c_double), c_int64, POINTER(c_int64),
                                   POINTER(c_int64)]),
     "glx_session_describe": (c_int, [c_void_p, c_char_p, c_size_t]),
@@ -100,6 +101,7 @@ _SIGS = {
     "glx_comm_allreduce": (c_int, [c_void_p, c_void_p, c_int64, c_int, c_void_p]),
     "glx_comm_reduce_scatter": (c_int, [c_void_p, c_void_p, c_int64, c_int, c_void_p]),
     "glx_comm_all_gather": (c_int, [c_void_p, c_void_p, c_int64, c_int, c_void_p]),
+    "glx_comm_progress": (c_int, [c_void_p, POINTER(c_int64)]),
     "glx_comm_destroy": (None, [c_void_p]),
 }
 

@@ -103,6 +103,15 @@ class Comm:
         """In place over world-size chunks: chunk ``rank`` is sent, every chunk received."""
         return self._chunked(lib().glx_comm_all_gather, t)
 
+    def progress(self):
+        """Thread-safe progress record (glx_comm_progress): collectives issued, completed by the
+        host transport (-1 for RCCL), kind of the last one, RCCL's asynchronous error."""
+        if not self.handle:
+            return {"closed": 1}
+        out = (ctypes.c_int64 * 4)()
+        check(lib().glx_comm_progress(self.handle, out))
+        return {"issued": out[0], "host_done": out[1], "last_kind": out[2], "async_error": out[3]}
+
     def close(self):
         if self.handle:
             lib().glx_comm_destroy(self.handle)

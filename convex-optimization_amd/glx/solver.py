@@ -18,7 +18,8 @@ A@x for every objective instead of reusing the accepted trial residual), ``profi
 ``max_total_iters``, ``ax_variant``, ``split_cand`` (0 auto, 1 on, 2 off), ``dc_window``
 (device-controlled line search: 0 auto, -1 off, k iterations in flight), ``shard_rows``
 (ProxGD with a communicator: 0 auto = the row-sharded schedule, 1 on, 2 off = the gradient
-all-reduce schedule), ``device``, ``comm``.
+all-reduce schedule), ``shard_model`` (bench.py only: the per-rank timing model of G ranks at
+world size 1; ``solve`` refuses it), ``device``, ``comm``.
 """
 from __future__ import annotations
 
@@ -41,7 +42,7 @@ _REF_KEYS = {
     "delta": "delta",
 }
 _BUILD_KEYS = {"exact_objective", "profile", "max_total_iters", "ax_variant", "split_cand",
-               "dc_window", "shard_rows"}
+               "dc_window", "shard_rows", "shard_model"}
 
 
 def _device(opts: Dict[str, Any]) -> torch.device:
@@ -188,6 +189,17 @@ class Session:
         check(lib().glx_session_counters(self.h, out))
         return {"ax_calls": out[0], "ax_sources": out[1], "atr_calls": out[2], "syncs": out[3]}
 
+    def progress(self) -> Dict[str, int]:
+        """Thread-safe progress record (glx_session_progress), for watchdogs: iterations so far,
+        phase, what the host waits on (0 nothing, 1 packet, 2 decision record), collectives
+        issued."""
+        h = getattr(self, "h", None)
+        if not h:
+            return {"closed": 1}
+        out = (ctypes.c_int64 * 4)()
+        check(lib().glx_session_progress(h, out))
+        return {"k": out[0], "phase": out[1], "waiting_on": out[2], "collectives_issued": out[3]}
+
     def describe(self) -> str:
         """The kernels this session launches (glx_session_describe): A@X tiles per right-hand
         side count, A^T r panel (+ the fused trial), the split-candidate form, the device-control
@@ -256,6 +268,9 @@ def solve(name: str, x0, A, b, mu_0, opts: Optional[Dict[str, Any]] = None, comm
     opts = dict(opts or {})
     if name not in _lib.METHODS:
         raise ValueError("unknown solver %r" % (name,))
+    if int(opts.get("shard_model", 0)) > 1:
+        raise ValueError("shard_model is bench.py's per-rank timing model (its iterates are not a "
+                         "solve); solve() refuses it")
     lib()  # fail loudly before touching data if the library is missing
     device = _device(opts)
     dtype = _dtype_of(A)

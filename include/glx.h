@@ -84,7 +84,13 @@ typedef struct glx_opts {
                                      n / G rows and the new iterate's rows are all-gathered
                                      (needs n % G == 0); off: the gradient is all-reduced and
                                      every rank runs the row-wise step on all n rows            */
-  int32_t reserved[4];
+  int32_t shard_model;            /* BENCHMARK ONLY (bench.py --shard-model): G > 1 with a world-1
+                                     communicator runs the per-rank timing model of G ranks of the
+                                     row-sharded ProxGD schedule (the trial on n / G rows, every
+                                     line-search test accepted). Its iterates are NOT a solve:
+                                     glx_solve refuses it and glx_session_describe says
+                                     "(timing model)". 0 = off                                  */
+  int32_t reserved[3];
 } glx_opts;
 
 /* One problem instance. For multi-GPU runs A and b are this rank's row shard
@@ -154,6 +160,11 @@ int  glx_session_kernel_time(glx_session* s, int kind, int64_t* launches, double
  * passes, host readbacks (glx_result.syncs)} (cumulative; the caller differences them around a
  * timed region). */
 int  glx_session_counters(glx_session* s, int64_t out[4]);
+/* Progress record, safe to call from ANOTHER thread while glx_session_run() is in progress (a
+ * watchdog's diagnostic, round 6): out = {iterations recorded so far (k), continuation phase
+ * (0..2), what the host is waiting on (0 nothing, 1 a scalar packet, 2 a device decision record),
+ * collectives issued on the session's communicator (0 without one)}. */
+int  glx_session_progress(glx_session* s, int64_t out[4]);
 /* After glx_session_finish: what the reference's 'opt' logger prints, so a host can replay it
  * without touching the hot loop (gl_ProxGD_primal.py:54 `new mu=` per phase, :134-136 the line
  * every 100 iterations; same in gl_FProxGD_primal.py:56,149-151 and gl_SGD_primal.py:49,98-99).
@@ -225,9 +236,11 @@ int glx_residual_gradient2(int dtype, int64_t m, int64_t n, int64_t l, const voi
  * gl_ProxGD_primal.py:91,112,127; FProxGD's A e_c, gl_FProxGD_primal.py:92-97,136):
  *   Y (m x l) = sum over the rows k with row_masks[k] != 0 of At[k,:]^T E[k,:],  At = A^T (n x m).
  * row_masks[k] (device uint32, n + 3 readable) = the column mask of row k of E (bit c = E[k][c] != 0,
- * as the trial kernels write it). form 0: the MFMA row form (k_at_rows, the solver's default; m % 64
- * == 0); form 1: the VALU column-list gather of rounds 2-4; form 2: the bitmap gather (the solver's
- * default since round 5, bit-identical to form 1). Forms 1, 2 need the exact column masks. */
+ * as the trial kernels write it). form 0: the MFMA row form (k_at_rows; FProxGD's default in the
+ * solver, m % 64 == 0); form 1: the VALU column-list gather of rounds 2-4; form 2: the bitmap gather
+ * (ProxGD's default in the solver since round 5, bit-identical to form 1). Forms 1, 2 need the exact
+ * column masks. NOTE: these form codes are this entry point's own; they are NOT the codes of the
+ * GLX_GATHER environment variable (bm / rows / lists). */
 int glx_flagged_rows_product(int dtype, int64_t m, int64_t n, int64_t l, const void* At,
                              const void* E, const uint32_t* row_masks, void* Y, int form,
                              void* workspace, size_t workspace_bytes, void* stream);
@@ -256,6 +269,13 @@ int  glx_comm_allreduce(glx_comm* c, void* buf, int64_t count, int dtype, void* 
  * does not own are -0.0). */
 int  glx_comm_reduce_scatter(glx_comm* c, void* buf, int64_t count, int dtype, void* stream);
 int  glx_comm_all_gather(glx_comm* c, void* buf, int64_t count, int dtype, void* stream);
+/* Progress record, safe to call from another thread (round 6): out = {collectives issued,
+ * collectives the host transport completed (-1 for RCCL), kind of the last one issued (1 all-reduce,
+ * 2 reduce-scatter, 3 all-gather), RCCL's asynchronous error (ncclCommGetAsyncError; 0 none, -1
+ * aborted)}. A session whose host wait on RCCL sees an asynchronous error, or waits longer than
+ * GLX_WAIT_TIMEOUT_S (default 300 s), aborts the communicator and fails with GLX_E_RCCL and this
+ * record in glx_last_error(). */
+int  glx_comm_progress(glx_comm* c, int64_t out[4]);
 void glx_comm_destroy(glx_comm* c);
 
 #ifdef __cplusplus

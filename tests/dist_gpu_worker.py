@@ -39,6 +39,15 @@ def main():
     ap.add_argument("--shard-rows", type=int, default=None,
                     help="opts shard_rows (ProxGD: 0 auto, 1 the row-sharded step, 2 all-reduce)")
     ap.add_argument("--opts", default="{}", help="more solver options (JSON)")
+    ap.add_argument("--stall-rank", type=int, default=-1,
+                    help="this rank's host all-reduce callback never returns after --stall-after "
+                         "calls (the other ranks block in the collective); with --watchdog-s")
+    ap.add_argument("--stall-after", type=int, default=10)
+    ap.add_argument("--watchdog-s", type=float, default=0.0)
+    ap.add_argument("--ns-golden", default=None,
+                    help="solve the reference's own instance of tests/golden/<stem>.npz (main.py "
+                         "gen_data, b = the reference run's A u) with its opts, checked against that "
+                         "run instead of the oracle")
     ap.add_argument("--out", required=True)
     a = ap.parse_args()
 
@@ -54,6 +63,14 @@ def main():
 
     if a.solver == "collectives":
         collectives_check(comm, rank, world, a.out)
+        comm.close()
+        dist.destroy_process_group()
+        return
+    if a.stall_rank >= 0:
+        stall_check(a, comm, rank, world)   # exits through the watchdog
+        return
+    if a.ns_golden is not None:
+        ns_golden(a, comm, rank, world)
         comm.close()
         dist.destroy_process_group()
         return
@@ -92,6 +109,82 @@ def main():
         if rank == 0:
             os.unlink(shm_path)
     dist.destroy_process_group()
+
+
+def stall_check(a, comm, rank, world):
+    """A row-sharded ProxGD solve whose rank a.stall_rank stops answering collectives: its host
+    transport's callback (torch.distributed.all_reduce over gloo) sleeps instead of joining after
+    a.stall_after calls. Every rank arms glx.watchdog with the session's and the communicator's
+    progress records as probes (as bench.py does for N > 1); the test expects every rank to
+    leave with the watchdog's exit code and diagnostic well before any outer limit."""
+    import time
+    import glx
+    from glx.watchdog import Watchdog
+    from oracle import numpy_ref
+    # the stalled rank's own deadline is later, so the blocked ranks' diagnostics are the ones
+    # the launcher sees first (it tears the others down after the first exit)
+    dl = a.watchdog_s * (3 if rank == a.stall_rank else 1)
+    wd = Watchdog(dl, "dist_gpu_worker stall check", rank=rank, world=world).start()
+    wd.probe("communicator", comm.progress)
+    calls = [0]
+    orig = dist.all_reduce
+
+    def all_reduce(t, *args, **kw):
+        calls[0] += 1
+        if rank == a.stall_rank and calls[0] > a.stall_after:
+            time.sleep(3600)
+        return orig(t, *args, **kw)
+    dist.all_reduce = all_reduce   # the host transport's callback looks it up at call time
+    from glx.dist import shard_rows
+    A, b, u, x0, mu = numpy_ref.gen_data(a.m, a.n, a.l, 11)
+    r0, r1 = shard_rows(a.m, world, rank)
+    opts = {"alpha0": numpy_ref.step_size_for(a.m, a.n), "maxit": a.maxit}
+    x = torch.from_numpy(x0).cuda()
+    s = glx.Session(a.solver, x, torch.from_numpy(np.ascontiguousarray(A[r0:r1])).cuda(),
+                    torch.from_numpy(np.ascontiguousarray(b[r0:r1])).cuda(), mu, opts, comm=comm)
+    wd.probe("session", s.progress)
+    wd.phase = "solve"
+    s.run(0)
+    raise SystemExit("the stalled solve returned (the watchdog should have ended this rank)")
+
+
+def ns_golden(a, comm, rank, world):
+    """The exact path of the driver's 8-GPU strong-scaling run (bench.py --gpus N): the reference's
+    gen_data instance at the north-star size (main.py:37-51; b from the reference's own run,
+    tests/golden/ns_instance_b.npz), the reference run's opts, every other option at its default
+    (shard_rows auto, the split-candidate gate), a whole solve. Every rank reports k, fval, its
+    f_hist, the digest of x and the plan; rank 0 adds the reference run's k / fval / f_hist."""
+    import glx
+    from oracle import numpy_ref
+    gold_dir = os.path.join(ROOT, "tests", "golden")
+    meta = json.load(open(os.path.join(gold_dir, a.ns_golden + ".json")))
+    m, n, l = meta["m"], meta["n"], meta["l"]
+    A, _, u, x0, mu = numpy_ref.gen_data(m, n, l, meta["seed"])
+    b = np.load(os.path.join(gold_dir, "ns_instance_b.npz"))["b"]
+    sha = lambda v: hashlib.sha256(np.ascontiguousarray(v).tobytes()).hexdigest()
+    assert sha(A) == meta["sha256"]["A"] and sha(x0) == meta["sha256"]["x0"] and sha(b) == meta["sha256"]["b"]
+    from glx.dist import shard_rows
+    r0, r1 = shard_rows(m, world, rank)
+    Ad = torch.from_numpy(np.ascontiguousarray(A[r0:r1])).cuda()
+    del A
+    bd = torch.from_numpy(np.ascontiguousarray(b[r0:r1])).cuda()
+    x, k, out = glx.solve(a.solver, torch.from_numpy(x0).cuda(), Ad, bd, mu, dict(meta["opts"]), comm=comm)
+    torch.cuda.synchronize()
+    xh = x.cpu().numpy()
+    mine = {"rank": rank, "k": int(k), "fval": float(out["fval"]), "x_sha": sha(xh),
+            "f_hist": [float(v) for v in out["f_hist"]], "plan": out["glx"]["plan"],
+            "tt": float(out["tt"])}
+    gathered = [None] * world
+    dist.all_gather_object(gathered, mine)
+    if rank == 0:
+        gold = np.load(os.path.join(gold_dir, a.ns_golden + ".npz"))
+        xr = gold["x"].astype(np.float64)
+        verdict = {"ranks": gathered, "oracle_k": int(gold["k"]), "oracle_fval": float(gold["fval"]),
+                   "oracle_f_hist": [float(v) for v in gold["f_hist"]],
+                   "x_maxdiff": float(np.max(np.abs(xh - xr))), "x_scale": float(np.max(np.abs(xr))),
+                   "oracle": "the reference's own run (tests/golden/%s.npz)" % a.ns_golden}
+        with open(a.out, "w") as fh:
+            json.dump(verdict, fh)
 
 
 def collectives_check(comm, rank, world, out):

@@ -60,19 +60,26 @@ def test_reduce_scatter_all_gather_world1(comm):
 
 
 def test_shard_timing_model_world1(comm, monkeypatch):
-    """GLX_SHARD_MODEL=8 at world size 1 (bench.py --force-comm): the per-rank schedule of 8
-    ranks — the trial on n / 8 rows — runs and says so; its iterates are not a solve."""
+    """opts shard_model=8 at world size 1 (bench.py --shard-model 8 --force-comm): the per-rank
+    schedule of 8 ranks — the trial on n / 8 rows — runs and says so; its iterates are not a
+    solve, so glx.solve and the C ABI's glx_solve refuse it, and the environment variable of
+    round 5 no longer turns it on."""
     import glx
     from oracle import numpy_ref
-    monkeypatch.setenv("GLX_SHARD_MODEL", "8")
     A, b, u, x0, mu = numpy_ref.gen_data(256, 1024, 32, 7)
     At, bt, xt = (torch.from_numpy(a).to("cuda", torch.float64) for a in (A, b, x0))
-    s = glx.Session("gl_ProxGD_primal", xt.clone(), At, bt, mu,
-                    {"alpha0": numpy_ref.step_size_for(256, 1024), "maxit": 10}, comm=comm)
+    opts = {"alpha0": numpy_ref.step_size_for(256, 1024), "maxit": 10}
+    s = glx.Session("gl_ProxGD_primal", xt.clone(), At, bt, mu, dict(opts, shard_model=8), comm=comm)
     assert "rows=sharded x8 (timing model)" in s.describe()
     done = s.run(12)
     s.close()
     assert done == 12
+    with pytest.raises(ValueError, match="timing model"):
+        glx.solve("gl_ProxGD_primal", xt.clone(), At, bt, mu, dict(opts, shard_model=8), comm=comm)
+    monkeypatch.setenv("GLX_SHARD_MODEL", "8")
+    s = glx.Session("gl_ProxGD_primal", xt.clone(), At, bt, mu, opts, comm=comm)
+    assert "timing model" not in s.describe()
+    s.close()
 
 
 @pytest.mark.parametrize("solver,shape,dtype", [

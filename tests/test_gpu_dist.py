@@ -244,3 +244,47 @@ def test_row_sharded_needs_divisible_rows(tmp_path):
     assert "rows=sharded" not in v["ranks"][0]["plan"]
     with pytest.raises(AssertionError, match="n % ranks == 0"):
         run_sharded(tmp_path, 3, "gl_ProxGD_primal", 515, 1024, 16, maxit=5, extra=("--shard-rows", "1"))
+
+
+@pytest.mark.timeout(600)
+def test_row_sharded_ns_world8_whole_solve(tmp_path):
+    """the exact path the driver's 8-GPU strong-scaling run takes
+    (bench.py --gpus 8: gl_ProxGD_primal fp64 at (8192, 16384, 32), 1024 rows of A per rank,
+    default options: the row-sharded schedule, the split-candidate trial with the bitmap gather,
+    a 4 MiB reduce-scatter and all-gather per iteration) as 8 host-staged ranks sharing the box's
+    GPU, a whole solve from x0 against the reference's own run of the same call
+    (tests/golden/ns_gl_ProxGD_primal.npz, gl_ProxGD_primal.py:9-146): k = 2680, fval and every
+    f_hist entry within 1e-8, x within 1e-6 of max|x|, bit-identical on all 8 ranks, and the plan
+    names the row-sharded schedule and the bitmap gather."""
+    v = run_sharded(tmp_path, 8, "gl_ProxGD_primal", 8192, 16384, 32, threads=2,
+                    extra=("--ns-golden", "ns_gl_ProxGD_primal"), timeout=580)
+    r0 = _check_identical_and_oracle(v, 8)
+    assert r0["k"] == 2680
+    assert "rows=sharded x8" in r0["plan"] and "gather k_at_gather_bm" in r0["plan"], r0["plan"]
+    assert v["x_maxdiff"] <= 1e-6 * v["x_scale"]
+
+
+def test_stalled_rank_watchdog_host_transport(tmp_path):
+    """one rank of a row-sharded ProxGD solve stops answering collectives
+    (its host transport callback never returns after 10 calls); the other ranks block inside the
+    collective. Every rank's glx.watchdog (armed as bench.py arms it for N > 1) prints its
+    diagnostic — rank, phase, the session's progress record (iterations, collectives issued) and
+    the communicator's (collectives issued / completed) — and the ranks leave with exit code 3,
+    within the deadline instead of at an outer time limit."""
+    import time
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes", "1", "--nproc-per-node", "2",
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()),
+           os.path.join(ROOT, "tests", "dist_gpu_worker.py"), "--solver", "gl_ProxGD_primal",
+           "--rows", "512", "--cols", "1024", "--groups-l", "32", "--maxit", "200",
+           "--out", str(tmp_path / "unused.json"),
+           "--stall-rank", "1", "--stall-after", "10", "--watchdog-s", "20"]
+    t0 = time.monotonic()
+    p = subprocess.run(cmd, env=dict(os.environ, OMP_NUM_THREADS="1"), capture_output=True, text=True,
+                       timeout=110)
+    elapsed = time.monotonic() - t0
+    msg = p.stderr
+    assert p.returncode != 0
+    assert elapsed < 100, elapsed
+    assert "glx watchdog: rank 0 of 2: dist_gpu_worker stall check passed its deadline of 20 s" in msg, msg[-3000:]
+    assert "session: {'k':" in msg and "'collectives_issued':" in msg, msg[-3000:]
+    assert "communicator: {'issued':" in msg, msg[-3000:]

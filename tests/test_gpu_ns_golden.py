@@ -63,9 +63,10 @@ def test_whole_solve_north_star_size(instance, method):
     assert np.max(np.abs(x - xr)) <= 1e-6 * np.max(np.abs(xr))
 
 
-# C3's default path at the default summation order (round 5: the split-candidate batch) ends at
-# this objective, bit for bit run to run (every kernel's order is fixed): the tripwire below.
-C3_DEFAULT_FVAL = 124.66994187389328
+# C3's default path (round 6: the dense [xc | y_next] batch again) ends at this
+# objective, bit for bit run to run (every kernel's order is fixed): the tripwire below
+# (profiles/r5_d/c3_band.jsonl, variant "dense").
+C3_DEFAULT_FVAL = 124.66799582996916
 
 
 def test_whole_solve_c3_fp32():
@@ -73,19 +74,19 @@ def test_whole_solve_c3_fp32():
     solve against the reference's own fp32 run of the same call (tests/golden/make_golden_c3.py)
     and its fp64 run (ns_gl_FProxGD_primal).
 
-    The bar comes from the measured band (scripts/c3_band.py,
-    profiles/r5_d/c3_band.jsonl): the C3 solve stops at maxit (4500, not converged), and eleven
-    equally valid summation orders of the two batch forms (K splits 4/8/16, tiles, A e forms)
-    end 3.4e-7 .. 8.9e-5 from the reference's fp32 objective, every one of them 7.0e-3 .. 7.1e-3
-    from the fp64 objective — as the reference's own fp32 run is (7.0e-3). So:
-      - fval within 2.5e-4 of the reference's fp32 run (~3x the widest draw);
+    The C3 solve stops at maxit (4500, not converged), so its fp32 objective depends on the
+    summation order: eleven equally valid orders end 3.4e-7 .. 8.9e-5 from the reference's fp32
+    objective, every one 7.0e-3 .. 7.1e-3 from the fp64 objective, as the reference's own fp32 run
+    is (scripts/c3_band.py, profiles/r5_d/c3_band.jsonl). The default path is the order that meets
+    the fp32 bar of SURVEY §8d (the bar is not widened to fit a default):
+      - fval within 1e-6 of the reference's fp32 run (measured 3.4e-7);
       - fval within 1e-2 of the reference's fp64 run (the fp32 arithmetic's own distance, 7e-3);
       - k within 0.5 % (measured identical, 4500 = maxit); where k agrees, every f_hist entry
         within 5e-3 and x within 5e-2 of max|x| (mid-solve drift of two fp32 implementations,
         up to 1.8e-3 / 3.0e-2, profiles/r4_c3gold/);
       - tripwire: the default path's objective equals C3_DEFAULT_FVAL to 1e-12 — it pins the
-        default kernels' summation order, and moves (inside the band) when any fp32 order on
-        this path changes; re-record it then, after the band check."""
+        default kernels' summation order; a change of any fp32 order on this path must be
+        re-checked against the 1e-6 bar before it is re-recorded."""
     import importlib
     meta_path = os.path.join(GOLD, "c3_gl_FProxGD_primal.json")
     if not os.path.exists(meta_path):
@@ -108,7 +109,7 @@ def test_whole_solve_c3_fp32():
     kg = int(gold["k"])
     assert abs(k - kg) <= max(1, int(0.005 * kg)), (k, kg)
     fg, fv = float(gold["fval"]), float(out["fval"])
-    assert abs(fv - fg) <= 2.5e-4 * abs(fg), (fv, fg)
+    assert abs(fv - fg) <= 1e-6 * abs(fg), (fv, fg)
     assert abs(fv - gold64) <= 1e-2 * abs(gold64), (fv, gold64)
     if k == kg:
         got = np.asarray([float(v) for v in out["f_hist"]])

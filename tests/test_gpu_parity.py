@@ -317,39 +317,14 @@ def test_split_candidate_gather_waves_bit_identical(name, monkeypatch):
     assert runs[0][1] == int(gold["k"])
 
 
-def test_folded_finalize_matches_separate_kernel(monkeypatch):
-    """Round 5: at the north-star size the split-candidate ProxGD trial's residual finalize can
-    run inside the dense pass A p_thr (launch_ax_fin, opt-in GLX_AX_FIN=1 because it measured
-    slower: the row blocks' last K-split arrivals sum the slabs) instead of k_finalize_residual. The next gradient residual is summed in the
-    same slab order, so the iterates are bit-identical; the recorded objective's squared sums are
-    reduced in another order (ulp level). 60 iterations per phase, both phase boundaries."""
-    from oracle import numpy_ref
-    m, n, l = 8192, 16384, 32
-    A, b, u, x0, mu = numpy_ref.gen_data(m, n, l, 97006855)
-    opts = {"alpha0": numpy_ref.step_size_for(m, n), "maxit": 60}
-    import importlib
-    fn = getattr(importlib.import_module("gl_ProxGD_primal"), "gl_ProxGD_primal")
-    At, bt = torch.from_numpy(A).cuda(), torch.from_numpy(b).cuda()
-    runs = []
-    for fin in ("0", "1"):
-        monkeypatch.setenv("GLX_AX_FIN", fin)
-        x, k, out = fn(torch.from_numpy(x0).cuda(), At, bt, mu, dict(opts))
-        runs.append((x.cpu().numpy(), k, np.asarray([float(v) for v in out["f_hist"]])))
-    (x0_, k0, f0), (x1, k1, f1) = runs
-    assert k0 == k1 == 180
-    assert np.array_equal(x0_, x1)
-    assert np.max(np.abs(f1 - f0) / np.abs(f0)) < 1e-13
-
-
-@pytest.mark.parametrize("solver,alpha_scale", [("gl_ProxGD_primal", 1.0), ("gl_ProxGD_primal", 2.5),
-                                               ("gl_FProxGD_primal", 1.0), ("gl_FProxGD_primal", 3.0)])
+@pytest.mark.parametrize("solver,alpha_scale", [("gl_ProxGD_primal", 1.0), ("gl_ProxGD_primal", 2.5)])
 def test_deferred_reductions_match(monkeypatch, solver, alpha_scale):
     """Round 5: ProxGD's fused trial and its residual finalize leave their sums as workgroup
     partials that the next publishing workgroup reduces (GLX_DEFER_RED, default on). Same
     decisions and bit-identical iterates as the grid reductions; the recorded objective moves by
     summation order only. alpha_scale 2.5: rejected first trials (the pending sums of a dropped
-    speculative trial are discarded, the retrial's k_prox_pgd reduces in full). FProxGD: the fused
-    backtracking trial (k_atr_fista) and its batch's finalize the same way."""
+    speculative trial are discarded, the retrial's k_prox_pgd reduces in full). (FProxGD's opt-in
+    form, GLX_DEFER_RED=2, measured no gain and was removed in round 6.)"""
     from oracle import numpy_ref
     m, n, l = 2048, 4096, 32
     A, b, u, x0, mu = numpy_ref.gen_data(m, n, l, 5)
@@ -358,7 +333,7 @@ def test_deferred_reductions_match(monkeypatch, solver, alpha_scale):
     fn = getattr(importlib.import_module(solver), solver)
     At, bt = torch.from_numpy(A).cuda(), torch.from_numpy(b).cuda()
     runs = []
-    for d in ("0", "1" if solver == "gl_ProxGD_primal" else "2"):   # (FProxGD: opt-in, 2)
+    for d in ("0", "1"):
         monkeypatch.setenv("GLX_DEFER_RED", d)
         x, k, out = fn(torch.from_numpy(x0).cuda(), At, bt, mu, dict(opts))
         runs.append((x.cpu().numpy(), k, np.asarray([float(v) for v in out["f_hist"]])))

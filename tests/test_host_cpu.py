@@ -108,11 +108,11 @@ def test_workspace_planning_host_only():
             _lib.check(_lib.lib().glx_workspace_bytes(ctypes.byref(p), ctypes.byref(make_opts(meth, {})),
                                                       ctypes.byref(nb)))
             es = 8 if dt == 1 else 4
-            # split-candidate trials (m n * 8 B of 768 MiB or more; fp32: FProxGD only, round 5
-            # default) keep a transposed copy of A (kernels_gather.hip); FProxGD's also e_c and
-            # three A thr(x) residual-sized slots
+            # split-candidate trials (m n * 8 B of 768 MiB or more; fp64 only by default — fp32
+            # FProxGD's split form is opt-in, GLX_SPLIT_F32=1, round 6) keep a transposed copy of A
+            # (kernels_gather.hip); FProxGD's also e_c and three A thr(x) residual-sized slots
             gate = (64 if meth == _lib.GLX_PROXGD and l == 32 else 768) * 2**20   # kSplitMinBytes*
-            split = (dt == 1 or meth == _lib.GLX_FPROXGD) and l in (16, 32) and m * n * 8 >= gate
+            split = dt == 1 and l in (16, 32) and m * n * 8 >= gate
             at = es * m * n if split else 0
             extra = es * (n * l + 3 * m * l) if (split and meth == _lib.GLX_FPROXGD) else 0
             assert nb.value >= es * (2 * n * l + 2 * m * l) + at + extra  # x-buffers + residuals at least
