@@ -563,15 +563,24 @@ static void atr_mfma_go(const GemmPlan& p, const T* A, const T* R, T* Gp, hipStr
 // non-temporal), the fp32 fused trial's eight-wave panel (WL 2) and the f64 32-column panel
 // (WL 3). The measured-slower ring depths (PF 2-6) and the 8-wave 32-column panel (WL 4) of
 // rounds 1-5 are gone; their numbers stay in DESIGN.md's tuning record.
+// the switch key of a plan's A^T R tile: NTL * 1000 + WL * 100 + PF
+static inline int atr_key(const GemmPlan& p) { return p.atr_ntl * 1000 + p.atr_wl * 100 + p.atr_pf; }
+
 template <typename T, int NT>
 static void atr_mfma_nt(const GemmPlan& p, const T* A, const T* R, T* Gp, hipStream_t st) {
-  switch (p.atr_ntl * 100 + p.atr_wl * 10 + p.atr_pf) {
+  switch (atr_key(p)) {
     case 8: atr_mfma_go<T, NT, 8, 0, false>(p, A, R, Gp, st); break;
-    case 108: atr_mfma_go<T, NT, 8, 0, true>(p, A, R, Gp, st); break;
-    case 114: atr_mfma_go<T, NT, 4, 1, true>(p, A, R, Gp, st); break;
-    case 128: atr_mfma_go<T, NT, 8, 2, true>(p, A, R, Gp, st); break;
-    case 38:
-    case 138:
+    case 1008: atr_mfma_go<T, NT, 8, 0, true>(p, A, R, Gp, st); break;
+    case 1104: atr_mfma_go<T, NT, 4, 1, true>(p, A, R, Gp, st); break;
+    case 1208: atr_mfma_go<T, NT, 8, 2, true>(p, A, R, Gp, st); break;
+    case 1216:
+      if constexpr (sizeof(T) == 4) {   // round 6: f32's sixteen-step ring (C3)
+        atr_mfma_go<T, NT, 16, 2, true>(p, A, R, Gp, st);
+        break;
+      }
+      throw Error{GLX_E_INVALID, "A^T R: the sixteen-step ring is f32"};
+    case 308:
+    case 1308:
       if constexpr (sizeof(T) == 8) {
         if (p.atr_ntl) atr_mfma_go<T, NT, 8, 3, true>(p, A, R, Gp, st);
         else atr_mfma_go<T, NT, 8, 3, false>(p, A, R, Gp, st);
@@ -635,18 +644,23 @@ static void atr_prox_nt(const GemmPlan& p, const T* A, const T* R, T* G, const T
                         Pub pub, T* Gp, unsigned* pcnt, unsigned* zf) {
   // the planner's fused tiles only (see atr_mfma_nt): f64 WL 0 PF 8 (+ non-temporal), WL 3
   // (32-column panel); WL 2 non-temporal (fp32's eight-wave panel; f64 through GLX_ATR_VARIANT)
-  const int code = p.atr_ntl * 100 + p.atr_wl * 10 + p.atr_pf;
+  const int code = atr_key(p);
   if constexpr (sizeof(T) == 8) {
     switch (code) {
       case 8: atr_prox_go<T, NT, 8, false, 0>(p, A, R, G, x, pp, pthr, z, t, mu, thres, red, st, pub, Gp, pcnt, zf); return;
-      case 38: atr_prox_go<T, NT, 8, false, 3>(p, A, R, G, x, pp, pthr, z, t, mu, thres, red, st, pub, Gp, pcnt, zf); return;
-      case 138: atr_prox_go<T, NT, 8, true, 3>(p, A, R, G, x, pp, pthr, z, t, mu, thres, red, st, pub, Gp, pcnt, zf); return;
+      case 308: atr_prox_go<T, NT, 8, false, 3>(p, A, R, G, x, pp, pthr, z, t, mu, thres, red, st, pub, Gp, pcnt, zf); return;
+      case 1308: atr_prox_go<T, NT, 8, true, 3>(p, A, R, G, x, pp, pthr, z, t, mu, thres, red, st, pub, Gp, pcnt, zf); return;
       default: break;
+    }
+  } else {
+    if (code == 1216) {
+      atr_prox_go<T, NT, 16, true, 2>(p, A, R, G, x, pp, pthr, z, t, mu, thres, red, st, pub, Gp, pcnt, zf);
+      return;
     }
   }
   switch (code) {
-    case 108: atr_prox_go<T, NT, 8, true, 0>(p, A, R, G, x, pp, pthr, z, t, mu, thres, red, st, pub, Gp, pcnt, zf); return;
-    case 128: atr_prox_go<T, NT, 8, true, 2>(p, A, R, G, x, pp, pthr, z, t, mu, thres, red, st, pub, Gp, pcnt, zf); return;
+    case 1008: atr_prox_go<T, NT, 8, true, 0>(p, A, R, G, x, pp, pthr, z, t, mu, thres, red, st, pub, Gp, pcnt, zf); return;
+    case 1208: atr_prox_go<T, NT, 8, true, 2>(p, A, R, G, x, pp, pthr, z, t, mu, thres, red, st, pub, Gp, pcnt, zf); return;
     default:
       throw Error{GLX_E_INVALID, "fused A^T R + trial: tile code " + std::to_string(code) + " is not built"};
   }
@@ -684,18 +698,23 @@ static void atr_fista_nt(const GemmPlan& p, const T* A, const T* R, T* G, const 
                          T* xc, T* vn, T* yn, double t, double mu, double thres, double theta,
                          double theta_next, Red red, hipStream_t st, Pub pub, T* Gp, unsigned* pcnt,
                          T* ec, unsigned* zf) {
-  const int code = p.atr_ntl * 100 + p.atr_wl * 10 + p.atr_pf;   // the tiles of atr_prox_nt
+  const int code = atr_key(p);   // the tiles of atr_prox_nt
   if constexpr (sizeof(T) == 8) {
     switch (code) {
       case 8: atr_fista_go<T, NT, 8, false, 0>(p, A, R, G, y, xk, xc, vn, yn, t, mu, thres, theta, theta_next, red, st, pub, Gp, pcnt, ec, zf); return;
-      case 38: atr_fista_go<T, NT, 8, false, 3>(p, A, R, G, y, xk, xc, vn, yn, t, mu, thres, theta, theta_next, red, st, pub, Gp, pcnt, ec, zf); return;
-      case 138: atr_fista_go<T, NT, 8, true, 3>(p, A, R, G, y, xk, xc, vn, yn, t, mu, thres, theta, theta_next, red, st, pub, Gp, pcnt, ec, zf); return;
+      case 308: atr_fista_go<T, NT, 8, false, 3>(p, A, R, G, y, xk, xc, vn, yn, t, mu, thres, theta, theta_next, red, st, pub, Gp, pcnt, ec, zf); return;
+      case 1308: atr_fista_go<T, NT, 8, true, 3>(p, A, R, G, y, xk, xc, vn, yn, t, mu, thres, theta, theta_next, red, st, pub, Gp, pcnt, ec, zf); return;
       default: break;
+    }
+  } else {
+    if (code == 1216) {
+      atr_fista_go<T, NT, 16, true, 2>(p, A, R, G, y, xk, xc, vn, yn, t, mu, thres, theta, theta_next, red, st, pub, Gp, pcnt, ec, zf);
+      return;
     }
   }
   switch (code) {
-    case 108: atr_fista_go<T, NT, 8, true, 0>(p, A, R, G, y, xk, xc, vn, yn, t, mu, thres, theta, theta_next, red, st, pub, Gp, pcnt, ec, zf); return;
-    case 128: atr_fista_go<T, NT, 8, true, 2>(p, A, R, G, y, xk, xc, vn, yn, t, mu, thres, theta, theta_next, red, st, pub, Gp, pcnt, ec, zf); return;
+    case 1008: atr_fista_go<T, NT, 8, true, 0>(p, A, R, G, y, xk, xc, vn, yn, t, mu, thres, theta, theta_next, red, st, pub, Gp, pcnt, ec, zf); return;
+    case 1208: atr_fista_go<T, NT, 8, true, 2>(p, A, R, G, y, xk, xc, vn, yn, t, mu, thres, theta, theta_next, red, st, pub, Gp, pcnt, ec, zf); return;
     default:
       throw Error{GLX_E_INVALID, "fused A^T R + FISTA trial: tile code " + std::to_string(code) + " is not built"};
   }

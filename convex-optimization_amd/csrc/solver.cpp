@@ -228,6 +228,9 @@ static GemmPlan session_plan(const glx_problem& P, const glx_opts& O) {
     if (P.n / 64 >= 256) {
       f.atr_wl = 2;
       f.atr_S = 1;
+      // round 6: GLX_ATR_PF32=16, a sixteen-step ring (twice the A bytes in flight per wave)
+      const char* pf32 = std::getenv("GLX_ATR_PF32");
+      if (pf32 && std::atoi(pf32) == 16) f.atr_pf = 16;
     }
     if (atr_prox_ok(f)) return f;   // only where the trial actually fuses (GLX_ATR_FUSE_SPLIT)
   }

@@ -20,3 +20,9 @@ timeout -k 10 700 python -u -m pytest -v --timeout 120 --timeout-method thread -
   --ignore tests/test_gpu_ragged_split.py --ignore tests/test_gpu_comm.py > $OUT/pytest_all.log 2>&1
 echo "suite rc=$?"
 tail -3 $OUT/pytest_all.log
+# C3 A/B: the f32 A^T R ring depth (round 6)
+for pf in 8 16; do
+  GLX_ATR_PF32=$pf timeout -k 10 120 python bench.py --method gl_FProxGD_primal --dtype f32 --steps 200 --warmup 20 \
+    --no-cpu-baseline > $OUT/c3_pf$pf.json 2> $OUT/c3_pf$pf.err || { echo "c3 pf$pf failed"; exit 1; }
+done
+echo "c3 ab ok"
