@@ -202,6 +202,21 @@ template <typename T>
 bool launch_ax_dma(const GemmPlan& p, int code, int nsrc, int S, const T* A, const T* const* X, T* P,
                    const int* gate, int epoch, hipStream_t st, Pub pub);
 int dma_lds_need(int code, int64_t l, int nsrc, int esize);
+// Round 6: the split-candidate trial's A e inside the dense pass A p_thr (NS's one-source f64
+// LDS-DMA tile 92278): e's rows are staged beside p_thr's in every chunk and, for the entries the
+// column bitmaps behind zf flag (glx_device.h zf_bitmaps), A[:, k] e[k, c] is accumulated on VALU
+// from the A chunk already in LDS: no transposed copy of A and no gather pass. Pe[S][m][l]: the
+// A e slabs (one per K split, summed in slab order by the finalize's chain mode).
+struct EGat {
+  const void* E = nullptr;               // e (n x l): read only where its bitmaps are set
+  const unsigned short* bm = nullptr;    // zf_bitmaps(zf, n): column c's u16 words at c * bstride
+  int64_t bstride = 0;                   // zf_npad(n) / 16
+  void* Pe = nullptr;
+};
+bool ax_egat_ok(const GemmPlan& p, int esize);
+template <typename T>
+bool launch_ax_egat(const GemmPlan& p, const T* A, const T* X, T* P, const int* gate, int epoch,
+                    hipStream_t st, Pub pub, const EGat& eg);
 int dma_waves(int code);   // waves per workgroup of a kind-8/9 code (last digit; 1 = 16)
 int dma_mt(int code);      // 16-row tiles per wave (kind 9: 2)
 // Infinity-Cache hand-off between the passes (tuning experiment; MiB of A fetched with the

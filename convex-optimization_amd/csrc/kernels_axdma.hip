@@ -65,7 +65,7 @@ template <int SLR>
 __device__ inline int dma_sw(int i) { return SLR >= 16 ? (i & 15) : ((i >> 1) & 7); }
 
 template <typename T, int NT, int NSRC, int NS, int KC, int WAVES, bool NTL, bool HOIST, bool PIPE,
-          int MT>
+          int MT, bool EG = false>
 __global__ __launch_bounds__(64 * WAVES) void k_ax_dma(const T* __restrict__ A,
                                                       const T* __restrict__ X0,
                                                       const T* __restrict__ X1,
@@ -73,7 +73,7 @@ __global__ __launch_bounds__(64 * WAVES) void k_ax_dma(const T* __restrict__ A,
                                                       T* __restrict__ P, int64_t m, int64_t n,
                                                       int64_t chunks, int S, int gx, int xmap,
                                                       const int* __restrict__ gate, int epoch,
-                                                      Pub pub, int keep_mib) {
+                                                      Pub pub, int keep_mib, EGat eg) {
   typedef MF<T> M;
   typedef typename M::acc_t C;
   typedef typename M::vec_t V;                      // one 16-B slot of A
@@ -88,7 +88,9 @@ __global__ __launch_bounds__(64 * WAVES) void k_ax_dma(const T* __restrict__ A,
   constexpr int AW = 16 * MT * KC * (int)sizeof(T); // one wave's A chunk (MT 16-row tiles)
   constexpr int NIA = AW / 1024;                    // its LDS-DMA instructions
   constexpr int XS = KC * L * (int)sizeof(T);       // one source's X chunk
-  constexpr int XB = NSRC * XS;
+  // EG: e's rows of the chunk staged as one more source behind the NSRC MFMA sources
+  constexpr int NSX = NSRC + (EG ? 1 : 0);
+  constexpr int XB = NSX * XS;
   constexpr int NXT = XB / 1024;                    // the block's X instructions per chunk
   constexpr int NIX = (NXT + WAVES - 1) / WAVES;    // per wave (surplus ones load a dummy)
   constexpr bool XDUP = NIX * WAVES != NXT;
@@ -103,6 +105,8 @@ __global__ __launch_bounds__(64 * WAVES) void k_ax_dma(const T* __restrict__ A,
   static_assert(D >= 1 && WAITN <= 63, "vmcnt range");
   static_assert(LDSB <= 160 * 1024, "LDS");
   static_assert(MT == 1 || PIPE, "two row tiles per wave: pipelined form only");
+  static_assert(!EG || (NSRC == 1 && PIPE && HOIST && NS == 2 && KC == 32 && 64 % L == 0),
+                "the fused A e: one MFMA source, the pipelined two-slot tile");
   // PIPE && HOIST: the pipelined loop with the DMA issues and operand reads interleaved into
   // the MFMA stream (sched_group_barrier) instead of all issued in front of it
   // s_waitcnt vmcnt(WAITN) expcnt(7) lgkmcnt(0) (gfx9 encoding: vmcnt[3:0] bits 3:0, expcnt
@@ -149,7 +153,7 @@ __global__ __launch_bounds__(64 * WAVES) void k_ax_dma(const T* __restrict__ A,
     const int src = pu / (KC * NT), u = pu % (KC * NT);
     const int k = u / NT;
     const int us = u ^ ((k / EV) & (EV - 1));
-    const T* xb = src == 0 ? X0 : (src == 1 ? X1 : X2);
+    const T* xb = src == 0 ? X0 : (src == 1 ? (EG ? static_cast<const T*>(eg.E) : X1) : X2);
     xsrc[r] = xb + (cb * KC + us / NT) * L + (us % NT) * 16 + (lane % LPU) * EV;
     xdst[r] = tx < NXT ? WAVES * AW + tx * 1024 : -1;
   }
@@ -242,6 +246,52 @@ __global__ __launch_bounds__(64 * WAVES) void k_ax_dma(const T* __restrict__ A,
       }
   };
 
+  // ---- EG: A e on VALU from the staged chunks. Lane (c, h): column c = lane % L of e, the RPL
+  // rows h RPL .. h RPL + RPL - 1 of the wave's 16 MT rows. Per chunk the lane reads the u32 of
+  // column c's bitmap that covers the chunk's 32 k (loaded one chunk ahead, like the DMA ring,
+  // so the barrier's wait covers it) and, for every set bit k (ascending), adds A[row][k] e[k][c]
+  // for its rows with A and e read from the chunk's LDS image. Order: per K split, the block's
+  // (rotated) chunk walk, ascending k within a chunk; the finalize sums the S slabs in order.
+  constexpr int RPL = EG ? (16 * MT * L) / 64 : 1;
+  T accE[RPL];
+#pragma unroll
+  for (int r = 0; r < RPL; ++r) accE[r] = T(0);
+  const int ecol_c = lane % L;
+  const int rb0 = (lane / L) * RPL;
+  const unsigned short* ecol = EG ? eg.bm + (int64_t)ecol_c * eg.bstride : nullptr;
+  auto ebits = [&](int64_t c) -> unsigned {   // bitmap word of walk step c (0 past the range)
+    if constexpr (!EG) {
+      return 0u;
+    } else {
+      if (c >= nch) return 0u;
+      c += rot;
+      c = c >= nch ? c - nch : c;
+      return *reinterpret_cast<const unsigned*>(ecol + (cb + c) * (KC / 16));
+    }
+  };
+  auto ework = [&](int slot, unsigned bits) {
+    if constexpr (EG) {
+      const char* sb = lds + slot * SLOT;
+      while (bits != 0u) {
+        const int kk = __builtin_ctz(bits);
+        bits &= bits - 1u;
+        const int unit = (kk * NT + (ecol_c >> 4)) ^ ((kk / EV) & (EV - 1));
+        const T ev = *reinterpret_cast<const T*>(sb + WAVES * AW + NSRC * XS + unit * UB + (ecol_c & 15) * ES);
+        T ar[RPL];
+#pragma unroll
+        for (int r = 0; r < RPL; ++r) {
+          const int w = rb0 + r, ri = w & 15;
+          ar[r] = *reinterpret_cast<const T*>(sb + wave * AW + w * (SLR * 16) + 16 * ((kk / EV) ^ dma_sw<SLR>(ri)) +
+                                              ES * (kk % EV));
+        }
+#pragma unroll
+        for (int r = 0; r < RPL; ++r) accE[r] = accE[r] + ar[r] * ev;
+      }
+    }
+  };
+  unsigned ebr[2] = {0u, 0u};   // bitmap words of the next two walk steps
+  (void)ebr;
+
   if constexpr (PIPE) {
     // Software-pipelined: the operands of chunk c sit in registers (read one iteration earlier)
     // when chunk c's MFMAs issue, so the MFMA pipe does not idle on the LDS read latency after
@@ -286,13 +336,16 @@ __global__ __launch_bounds__(64 * WAVES) void k_ax_dma(const T* __restrict__ A,
                 acc[mt][src * NT + nt] = M::mma(a[mt][j][e], x[j][e][src][nt], acc[mt][src * NT + nt]);
     };
     GLX_CLK(1);
+    if constexpr (EG) ebr[0] = ebits(0);
 #pragma unroll
     for (int d = 0; d < D; ++d) issue(d, d);
     asm volatile("s_waitcnt vmcnt(%0)" ::"n"(WAITN) : "memory");
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
+    if constexpr (EG) ebr[1] = ebits(1);
     issue(D, D);          // NS = D + 1: slot D is free
     read_ops(0, av[0], xv[0]);
+    if constexpr (EG) ework(0, ebr[0]);   // chunk 0 before the loop's first barrier frees slot 0
     int cs = 1;           // slot of chunk c + 1
     int64_t c = 0;
     // two chunks per trip so the register sets keep static indices
@@ -307,6 +360,11 @@ __global__ __launch_bounds__(64 * WAVES) void k_ax_dma(const T* __restrict__ A,
         __builtin_amdgcn_s_barrier();
         __builtin_amdgcn_sched_barrier(0);
         const int is = cs == 0 ? NS - 1 : cs - 1;   // slot of chunk c + h = slot of c + h + 1 + D
+        unsigned eb_use = 0u;
+        if constexpr (EG) {   // this step's word (chunk c + h + 1) out, the word of c + h + 2 in
+          eb_use = ebr[h ^ 1];
+          ebr[h] = ebits(c + h + 1 + D);
+        }
         issue(c + h + 1 + D, is);
         read_ops(cs, av[h ^ 1], xv[h ^ 1]);         // next chunk's operands ...
         if constexpr (!HOIST) {
@@ -331,6 +389,10 @@ __global__ __launch_bounds__(64 * WAVES) void k_ax_dma(const T* __restrict__ A,
           }
           __builtin_amdgcn_sched_group_barrier(0x008, NMF - NI - (NRD + 1) / 2, 0);
         }
+        if constexpr (EG) {   // behind this chunk's MFMAs: chunk c + h + 1's A e (slot cs)
+          __builtin_amdgcn_sched_barrier(0);
+          if (c + h + 1 < nch) ework(cs, eb_use);
+        }
         cs = cs + 1 == NS ? 0 : cs + 1;
       }
     }
@@ -353,6 +415,14 @@ __global__ __launch_bounds__(64 * WAVES) void k_ax_dma(const T* __restrict__ A,
   }
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the surplus re-issues, before exit
+  if constexpr (EG) {
+    T* pe = static_cast<T*>(eg.Pe) + (int64_t)by * m * L;
+#pragma unroll
+    for (int r = 0; r < RPL; ++r) {
+      const int64_t row = row0 + rb0 + r;
+      if (row < m) pe[row * L + ecol_c] = accE[r];
+    }
+  }
 
 #pragma unroll
   for (int sr = 0; sr < NSRC; ++sr) {
@@ -372,18 +442,18 @@ __global__ __launch_bounds__(64 * WAVES) void k_ax_dma(const T* __restrict__ A,
 }
 
 template <typename T, int NT, int NSRC, int NS, int KC, int WAVES, bool NTL, bool HOIST = false,
-          bool PIPE = false, int MT = 1>
+          bool PIPE = false, int MT = 1, bool EG = false>
 static void ax_dma_go(const GemmPlan& p, int S, const T* A, const T* const* X, T* P,
-                      const int* gate, int epoch, hipStream_t st, Pub pub) {
-  if constexpr (dma_lds_bytes<T, NT, NSRC, NS, KC, WAVES, MT>() > 160 * 1024) {
+                      const int* gate, int epoch, hipStream_t st, Pub pub, const EGat& eg = EGat{}) {
+  if constexpr (dma_lds_bytes<T, NT, NSRC + (EG ? 1 : 0), NS, KC, WAVES, MT>() > 160 * 1024) {
     throw Error{GLX_E_INVALID, "A@X: this LDS-DMA tile does not fit (160 KiB of LDS)"};
   } else {
     const int gx = (int)cdiv(p.m, 16 * MT * WAVES);
     const int xmap = ax_xmap_flags(p, S);
     const dim3 grid((unsigned)ax_grid(xmap, gx, S) + (pub.host ? 1u : 0u));
-    glx_launch((k_ax_dma<T, NT, NSRC, NS, KC, WAVES, NTL, HOIST, PIPE, MT>), grid, dim3(64 * WAVES), 0, st,
+    glx_launch((k_ax_dma<T, NT, NSRC, NS, KC, WAVES, NTL, HOIST, PIPE, MT, EG>), grid, dim3(64 * WAVES), 0, st,
                        A, X[0], X[1], X[2], P, p.m, p.n, p.n / KC, S, gx, xmap, gate, epoch, pub,
-                       p.ax_keep_mib);
+                       p.ax_keep_mib, eg);
   }
 }
 
@@ -431,6 +501,32 @@ bool launch_ax_dma(const GemmPlan& p, int code, int nsrc, int S, const T* A, con
   if (nsrc == 2) return dma_code<T, 2, 2>(p, code, S, A, X, P, gate, epoch, st, pub);
   return dma_code<T, 2, 3>(p, code, S, A, X, P, gate, epoch, st, pub);
 }
+
+// the fused A e form of the one-source f64 pass 92278 (EGat)
+bool ax_egat_ok(const GemmPlan& p, int esize) {
+  return esize == 8 && p.ax_kind != 3 && p.axb_code[1] == 92278 && (p.l == 16 || p.l == 32) && p.n % 32 == 0 &&
+         p.n <= 65535;
+}
+template <typename T>
+bool launch_ax_egat(const GemmPlan& p, const T* A, const T* X, T* P, const int* gate, int epoch,
+                    hipStream_t st, Pub pub, const EGat& eg) {
+  if constexpr (sizeof(T) != 8) {
+    return false;
+  } else {
+    if (!ax_egat_ok(p, 8)) return false;
+    const T* xs[3] = {X, nullptr, nullptr};
+    const int S = p.axb_S[1];
+    if (p.l == 16)
+      ax_dma_go<T, 1, 1, 2, 32, 8, true, true, true, 2, true>(p, S, A, xs, P, gate, epoch, st, pub, eg);
+    else
+      ax_dma_go<T, 2, 1, 2, 32, 8, true, true, true, 2, true>(p, S, A, xs, P, gate, epoch, st, pub, eg);
+    return true;
+  }
+}
+template bool launch_ax_egat<double>(const GemmPlan&, const double*, const double*, double*, const int*, int,
+                                     hipStream_t, Pub, const EGat&);
+template bool launch_ax_egat<float>(const GemmPlan&, const float*, const float*, float*, const int*, int,
+                                    hipStream_t, Pub, const EGat&);
 
 template bool launch_ax_dma<double>(const GemmPlan&, int, int, int, const double*, const double* const*,
                                     double*, const int*, int, hipStream_t, Pub);

@@ -207,6 +207,18 @@ static int split_mode(const glx_problem& P, const glx_opts& O) {
   return gather_ok(P.n, P.l) ? 1 : 0;
 }
 
+// Round 6: ProxGD's split-candidate trial with A e fused into the dense pass (launch_ax_egat,
+// kernels_axdma.hip): where the session's one-source pass is the f64 LDS-DMA tile 92278 (NS) and
+// no gather form is forced (GLX_GATHER), GLX_AE_FUSED=0: off. The transposed copy of A is then
+// not needed (ProxGD's workspace shrinks by m x n) and no gather launches.
+static bool egat_mode(const glx_problem& P, const GemmPlan& plan, int smode) {
+  if (smode != 1 || P.method != GLX_PROXGD || P.dtype != GLX_F64) return false;
+  if (gather_form() >= 0) return false;
+  const char* e = std::getenv("GLX_AE_FUSED");
+  if (e && std::strcmp(e, "0") == 0) return false;
+  return ax_egat_ok(plan, 8);
+}
+
 static GemmPlan session_plan(const glx_problem& P, const glx_opts& O) {
   const int es = P.dtype == GLX_F64 ? 8 : 4;
   GemmPlan p = make_plan(es, P.m, P.n, P.l, O.ax_variant);
@@ -293,7 +305,8 @@ class Session : public SessionBase {
     const int64_t pslabs = std::max<int64_t>((int64_t)ax_split_max(plan) * 3,
                                              smode == 1 ? gather_split(P.m, P.n) + ax_split(plan, 1) : 0);
     T* pp = static_cast<T*>(c.take(sizeof(T) * ml * pslabs));
-    T* at = smode == 1 ? static_cast<T*>(c.take(sizeof(T) * P.m * P.n)) : nullptr;   // A^T
+    const bool eg = egat_mode(P, plan, smode);
+    T* at = (smode == 1 && !eg) ? static_cast<T*>(c.take(sizeof(T) * P.m * P.n)) : nullptr;   // A^T
     void* glists = smode == 1 ? c.take(gather_lists_bytes(P.n)) : nullptr;
     // split-candidate FISTA: e_c and a ring of three A thr(x) (x_k's, the trial's, the
     // speculated next trial's)
@@ -480,11 +493,13 @@ class Session : public SessionBase {
     if (gform_ == 1 && !gather_rows_ok(m_, n_)) gform_ = 0;
     rows_form_ = gform_ == 1;
     gsplit_ = rows_form_ ? gather_split(m_, n_) : 1;
+    egat_ = egat_mode(P, plan_, smode_);
+    if (egat_) gsplit_ = ax_split(plan_, 1);   // the A e slabs: one per K split of the dense pass
     {   // the VALU gather's budget counts nonzeros of e_c, the row form's flagged rows (round 5)
       const char* nb = std::getenv("GLX_SPLIT_NNZ");
       nnz_budget_ = (nb ? std::atof(nb) : (rows_form_ ? kRowsBudget : 0.35)) * (double)n_;
     }
-    if (smode_ == 1) {
+    if (smode_ == 1 && !egat_) {
       launch_transpose<T>(static_cast<const T*>(P.A), At_, m_, n_, st_);   // once
     }
     fused_fista_ok_ = fuse_any && P.method == GLX_FPROXGD;
@@ -706,6 +721,7 @@ class Session : public SessionBase {
     if (comm_ == nullptr && fused_fista_ok_) s += " +trial (k_atr_fista)";
     s += "; split=";
     if (smode_ == 0) s += "dense";
+    else if (egat_) s += "A e fused into the dense pass (k_ax_dma EG), S0=" + std::to_string(gsplit_);
     else if (rows_form_) s += "rows k_at_rows S0=" + std::to_string(gsplit_);
     else if (gform_ == 2) s += "gather k_e_lists+k_at_gather";
     else s += "gather k_at_gather_bm";
@@ -914,6 +930,22 @@ class Session : public SessionBase {
   // slabs, each workgroup compacts its K range's row flags itself), so no column lists.
   void cand_ax(const T* const* xs, Pub pb = Pub{}) {
     const T* xd[3] = {xs[1], nullptr, nullptr};
+    if (egat_) {   // round 6: A p_thr and A e in one pass (S slabs each: A e at Pp_, A p_thr behind)
+      EGat eg;
+      eg.E = xs[0];
+      const int64_t npad = (n_ + 63) / 64 * 64;   // glx_device.h zf_npad
+      eg.bm = reinterpret_cast<const unsigned short*>(zf_ + npad);
+      eg.bstride = npad / 16;
+      eg.Pe = Pp_;
+      hipEvent_t e0 = prof_begin(0);
+      if (!launch_ax_egat<T>(plan_, A_, xs[1], Pp_ + (size_t)gsplit_ * ml_, dc_gate_, 0, st_, pb, eg))
+        throw Error{GLX_E_STATE, "fused A e: the plan does not take it"};
+      check_launch();
+      prof_end(0, e0);
+      ++ax_calls_;
+      ax_cols_ += 1;
+      return;
+    }
     if (gform_ == 2) {
       launch_e_lists(zf_, n_, l_, glists_, st_, dc_gate_);
       check_launch();
@@ -2324,6 +2356,7 @@ class Session : public SessionBase {
   int smode_ = 0, gsplit_ = 1;
   int gform_ = 0;              // A e: 0 bitmap gather, 1 k_at_rows, 2 lists + gather (gather_form)
   bool rows_form_ = false;     // gform_ == 1: A e by k_at_rows (round 5), gsplit_ slabs
+  bool egat_ = false;          // round 6: A e inside the dense pass (launch_ax_egat), gsplit_ = its S
   // entries of the gather counts the FISTA finalize sums: flagged rows per K range (row form) or
   // nonzeros per column (VALU gather)
   int gcount_n() const { return rows_form_ ? gsplit_ : (int)l_; }
