@@ -202,13 +202,14 @@ template <typename T>
 bool launch_ax_dma(const GemmPlan& p, int code, int nsrc, int S, const T* A, const T* const* X, T* P,
                    const int* gate, int epoch, hipStream_t st, Pub pub);
 int dma_lds_need(int code, int64_t l, int nsrc, int esize);
-// Round 6: the split-candidate trial's A e inside the dense pass A p_thr (NS's one-source f64
-// LDS-DMA tile 92278): e's rows are staged beside p_thr's in every chunk and, for the entries the
-// column bitmaps behind zf flag (glx_device.h zf_bitmaps), A[:, k] e[k, c] is accumulated on VALU
-// from the A chunk already in LDS: no transposed copy of A and no gather pass. Pe[S][m][l]: the
-// A e slabs (one per K split, summed in slab order by the finalize's chain mode).
+// Round 6: the split-candidate trial's A e inside its dense pass (NS's one-source f64 LDS-DMA tile
+// 92278): the pass streams A p (X = the candidate p) on MFMA and, for the entries the column
+// bitmaps behind zf flag (glx_device.h zf_bitmaps; there e = p), accumulates A[:, k] e[k, c] on
+// VALU from the A and p chunks already in LDS: no transposed copy of A, no gather pass, no second
+// source. P[S][m][l] = A p slabs, Pe[S][m][l] = the A e slabs (one per K split); the finalize's
+// chain mode 2 forms A p - b and A p_thr - b = (A p - b) - A e.
 struct EGat {
-  const void* E = nullptr;               // e (n x l): read only where its bitmaps are set
+  const void* E = nullptr;               // unused (e is read from the staged p)
   const unsigned short* bm = nullptr;    // zf_bitmaps(zf, n): column c's u16 words at c * bstride
   int64_t bstride = 0;                   // zf_npad(n) / 16
   void* Pe = nullptr;
@@ -359,6 +360,7 @@ constexpr int kShardPartOff = 16;
 struct ShardPub {
   const double* blk = nullptr;
   int nranks = 1, chunk = 0, nbp = 0, nbf = 0, mask = 0;
+  int tv = 6;                   // values per trial partial (ProxGD 6, FProxGD 4; the max is value 3)
   double* tr = nullptr;
   double* rt = nullptr;
   int tr_off = 0, rt_off = 0;   // their packet slots
@@ -382,6 +384,14 @@ int finalize_fista_blocks(int64_t ml, int S, int S0, int64_t cn);
 template <typename T>
 void launch_trial_split(const T* p, const T* xt, T* pthr, T* z, unsigned* zf, int64_t n, int64_t l,
                         double t, double thres, bool emode, const ShardPub& sp, hipStream_t st);
+// Row-sharded FProxGD (round 6, solver.cpp iter_fista_shard): the replicated half of a FISTA
+// trial from the all-gathered xc (n x l): v_next = thr(xk) + (xc - thr(xk)) / theta and
+// y_next = (1 - theta') thr(xc) + theta' v_next with k_fista_trial's arithmetic (fista_row), so
+// the bits equal the ones that kernel would have written for the whole of xc. sp.blk != NULL: one
+// more workgroup combines the gathered sums (launch_shard_combine's work) beside the elements.
+template <typename T>
+void launch_fista_split(const T* xc, const T* xk, T* vnext, T* ynext, int64_t nl, double thres,
+                        double theta, double theta_next, const ShardPub& sp, hipStream_t st);
 
 // FISTA (prox = true) / FGD (prox = false: identity) trial fused with the next combine:
 // xc = prox(y - t g, t); vnext = thr(xk) + (xc - thr(xk))/theta;

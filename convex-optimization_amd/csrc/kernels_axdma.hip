@@ -88,9 +88,7 @@ __global__ __launch_bounds__(64 * WAVES) void k_ax_dma(const T* __restrict__ A,
   constexpr int AW = 16 * MT * KC * (int)sizeof(T); // one wave's A chunk (MT 16-row tiles)
   constexpr int NIA = AW / 1024;                    // its LDS-DMA instructions
   constexpr int XS = KC * L * (int)sizeof(T);       // one source's X chunk
-  // EG: e's rows of the chunk staged as one more source behind the NSRC MFMA sources
-  constexpr int NSX = NSRC + (EG ? 1 : 0);
-  constexpr int XB = NSX * XS;
+  constexpr int XB = NSRC * XS;
   constexpr int NXT = XB / 1024;                    // the block's X instructions per chunk
   constexpr int NIX = (NXT + WAVES - 1) / WAVES;    // per wave (surplus ones load a dummy)
   constexpr bool XDUP = NIX * WAVES != NXT;
@@ -153,7 +151,7 @@ __global__ __launch_bounds__(64 * WAVES) void k_ax_dma(const T* __restrict__ A,
     const int src = pu / (KC * NT), u = pu % (KC * NT);
     const int k = u / NT;
     const int us = u ^ ((k / EV) & (EV - 1));
-    const T* xb = src == 0 ? X0 : (src == 1 ? (EG ? static_cast<const T*>(eg.E) : X1) : X2);
+    const T* xb = src == 0 ? X0 : (src == 1 ? X1 : X2);
     xsrc[r] = xb + (cb * KC + us / NT) * L + (us % NT) * 16 + (lane % LPU) * EV;
     xdst[r] = tx < NXT ? WAVES * AW + tx * 1024 : -1;
   }
@@ -246,12 +244,14 @@ __global__ __launch_bounds__(64 * WAVES) void k_ax_dma(const T* __restrict__ A,
       }
   };
 
-  // ---- EG: A e on VALU from the staged chunks. Lane (c, h): column c = lane % L of e, the RPL
-  // rows h RPL .. h RPL + RPL - 1 of the wave's 16 MT rows. Per chunk the lane reads the u32 of
-  // column c's bitmap that covers the chunk's 32 k (loaded one chunk ahead, like the DMA ring,
-  // so the barrier's wait covers it) and, for every set bit k (ascending), adds A[row][k] e[k][c]
-  // for its rows with A and e read from the chunk's LDS image. Order: per K split, the block's
-  // (rotated) chunk walk, ascending k within a chunk; the finalize sums the S slabs in order.
+  // ---- EG: the MFMA source X0 is the candidate p itself (A p: the objective and the Armijo test)
+  // and A e, e = p where the hard threshold zeroes it, is accumulated on VALU from the staged
+  // chunks: lane (c, h) owns column c = lane % L of e and the RPL rows h RPL .. h RPL + RPL - 1 of
+  // the wave's 16 MT rows. Per chunk the lane reads the u32 of column c's bitmap that covers the
+  // chunk's 32 k (loaded one chunk ahead, like the DMA ring, so the barrier's wait covers it) and,
+  // for every set bit k (ascending), adds A[row][k] p[k][c] for its rows, A and p read from the
+  // chunk's LDS image. Order: per K split, the block's (rotated) chunk walk, ascending k within a
+  // chunk; the finalize sums the S slabs in order and forms A p_thr - b = (A p - b) - A e.
   constexpr int RPL = EG ? (16 * MT * L) / 64 : 1;
   T accE[RPL];
 #pragma unroll
@@ -276,7 +276,8 @@ __global__ __launch_bounds__(64 * WAVES) void k_ax_dma(const T* __restrict__ A,
         const int kk = __builtin_ctz(bits);
         bits &= bits - 1u;
         const int unit = (kk * NT + (ecol_c >> 4)) ^ ((kk / EV) & (EV - 1));
-        const T ev = *reinterpret_cast<const T*>(sb + WAVES * AW + NSRC * XS + unit * UB + (ecol_c & 15) * ES);
+        // e[k][c] = p[k][c] where the bitmap is set: read from the staged X chunk (source 0 = p)
+        const T ev = *reinterpret_cast<const T*>(sb + WAVES * AW + unit * UB + (ecol_c & 15) * ES);
         T ar[RPL];
 #pragma unroll
         for (int r = 0; r < RPL; ++r) {
@@ -445,7 +446,7 @@ template <typename T, int NT, int NSRC, int NS, int KC, int WAVES, bool NTL, boo
           bool PIPE = false, int MT = 1, bool EG = false>
 static void ax_dma_go(const GemmPlan& p, int S, const T* A, const T* const* X, T* P,
                       const int* gate, int epoch, hipStream_t st, Pub pub, const EGat& eg = EGat{}) {
-  if constexpr (dma_lds_bytes<T, NT, NSRC + (EG ? 1 : 0), NS, KC, WAVES, MT>() > 160 * 1024) {
+  if constexpr (dma_lds_bytes<T, NT, NSRC, NS, KC, WAVES, MT>() > 160 * 1024) {
     throw Error{GLX_E_INVALID, "A@X: this LDS-DMA tile does not fit (160 KiB of LDS)"};
   } else {
     const int gx = (int)cdiv(p.m, 16 * MT * WAVES);

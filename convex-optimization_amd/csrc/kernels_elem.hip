@@ -176,11 +176,19 @@ __global__ __launch_bounds__(256) void k_finalize_residual(
   for (int64_t idx = tid / G; idx < ml; idx += stride / G) {
     const T bv = B[idx];
     if (NSRC == 2 && chain) {   // split-candidate: R0 = (A p_thr - b) + A e (always live)
+      // chain 2 (round 6, the fused A e pass): the slabs behind P0 are A p, so R0 = A p - b and
+      // R1 = A p_thr - b = R0 - A e
       T a1[kSlabLoads], a0[kSlabLoads];
       const int c1 = group_slab_load<T, G>(P + (int64_t)S0 * ml, S, ml, idx, sub, a1);
       const int c0 = group_slab_load<T, G>(P0, S0, ml, idx, sub, a0);
-      const T r1 = group_slab_fold<T, G>(a1, c1) - bv;
-      const T r0 = r1 + group_slab_fold<T, G>(a0, c0);
+      T r1, r0;
+      if (chain == 2) {
+        r0 = group_slab_fold<T, G>(a1, c1) - bv;
+        r1 = r0 - group_slab_fold<T, G>(a0, c0);
+      } else {
+        r1 = group_slab_fold<T, G>(a1, c1) - bv;
+        r0 = r1 + group_slab_fold<T, G>(a0, c0);
+      }
       if (skipped) return;
       if (sub == 1 % G) rs[1][idx] = r1;
       if (R0 != nullptr && sub == 0) rs[0][idx] = r0;
@@ -367,16 +375,17 @@ __device__ inline void shard_combine_block(const ShardPub& sp) {
     const int np = sp.nranks * sp.nbp;
     for (int i = threadIdx.x; i < np; i += 256) {
       const int r = i / sp.nbp, b = i - r * sp.nbp;
-      const double* q = sp.blk + (int64_t)r * sp.chunk + kShardPartOff + b * 6;
+      const double* q = sp.blk + (int64_t)r * sp.chunk + kShardPartOff + b * sp.tv;
 #pragma unroll
-      for (int j = 0; j < 6; ++j) acc[j] = combine(j == 3 ? OP_MAX : OP_SUM, acc[j], q[j]);
+      for (int j = 0; j < 6; ++j)
+        if (j < sp.tv) acc[j] = combine(j == 3 ? OP_MAX : OP_SUM, acc[j], q[j]);
     }
   }
   if (sp.mask & 2) {
     const int np = sp.nranks * sp.nbf;
     for (int i = threadIdx.x; i < np; i += 256) {
       const int r = i / sp.nbf, b = i - r * sp.nbf;
-      const double* q = sp.blk + (int64_t)r * sp.chunk + kShardPartOff + 6 * sp.nbp + b * 4;
+      const double* q = sp.blk + (int64_t)r * sp.chunk + kShardPartOff + sp.tv * sp.nbp + b * 4;
 #pragma unroll
       for (int j = 0; j < 4; ++j) acc[6 + j] += q[j];
     }
@@ -393,12 +402,12 @@ __device__ inline void shard_combine_block(const ShardPub& sp) {
   if (threadIdx.x != 0) return;
   for (int j = 0; j < 10; ++j) fin[j] = waves_combine<4>(j == 3 ? OP_MAX : OP_SUM, wv[j]);
   if (sp.mask & 1)
-    for (int j = 0; j < 6; ++j) sp.tr[j] = fin[j];
+    for (int j = 0; j < sp.tv; ++j) sp.tr[j] = fin[j];
   if (sp.mask & 2)
     for (int j = 0; j < 4; ++j) sp.rt[j] = fin[6 + j];
   if (sp.pub.host != nullptr)
     publish_packet(sp.pub.s, sp.pub.ns, sp.pub.host, sp.pub.host_seq, sp.pub.seq, fin, sp.tr_off,
-                   (sp.mask & 1) ? 6 : 0, fin + 6, sp.rt_off, (sp.mask & 2) ? 4 : 0);
+                   (sp.mask & 1) ? sp.tv : 0, fin + 6, sp.rt_off, (sp.mask & 2) ? 4 : 0);
 }
 
 __global__ __launch_bounds__(256) void k_shard_combine(ShardPub sp) { shard_combine_block(sp); }
@@ -453,6 +462,31 @@ __global__ __launch_bounds__(256) void k_trial_split(const T* __restrict__ p, co
     }
   }
   GLX_ROW_LOOP_END
+}
+
+// Row-sharded FISTA trial, the replicated half (solver.cpp iter_fista_shard): v_next and y_next of
+// every element from the all-gathered xc with fista_row's comparisons and arithmetic; the last
+// workgroup (sp.blk) combines the gathered sums beside them.
+template <typename T>
+__global__ __launch_bounds__(256) void k_fista_split(const T* __restrict__ xc, const T* __restrict__ xk,
+                                                     T* __restrict__ vnext, T* __restrict__ ynext,
+                                                     int64_t nl, double thres_, double theta_, double a1_,
+                                                     double b1_, ShardPub sp) {
+  if (sp.blk != nullptr && blockIdx.x == gridDim.x - 1) {
+    shard_combine_block(sp);
+    return;
+  }
+  const T thres = (T)thres_, theta = (T)theta_, a1 = (T)a1_, b1 = (T)b1_;
+  const int64_t nb = gridDim.x - (sp.blk != nullptr ? 1 : 0);
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < nl; i += nb * 256) {
+    const T pv = xc[i];
+    T xo = xk[i];
+    if (tabs(xo) < thres) xo = T(0);
+    const T vn = xo + (pv - xo) / theta;
+    const T pt = tabs(pv) < thres ? T(0) : pv;
+    vnext[i] = vn;
+    ynext[i] = a1 * pt + b1 * vn;
+  }
 }
 
 // FISTA / FGD trial (gl_FProxGD_primal.py:92-102, gl_FGD_primal.py:209-212), fused with the
@@ -872,6 +906,13 @@ void launch_trial_split(const T* p, const T* xt, T* pthr, T* z, unsigned* zf, in
                        pthr, z, zf, n, l, t, thres, emode ? 1 : 0, sp);
   });
 }
+template <typename T>
+void launch_fista_split(const T* xc, const T* xk, T* vnext, T* ynext, int64_t nl, double thres,
+                        double theta, double theta_next, const ShardPub& sp, hipStream_t st) {
+  const int64_t nb = std::min<int64_t>((nl + 255) / 256, 1024);
+  hipLaunchKernelGGL(k_fista_split<T>, dim3((unsigned)nb + (sp.blk != nullptr ? 1u : 0u)), dim3(256), 0, st, xc,
+                     xk, vnext, ynext, nl, thres, theta, 1.0 - theta_next, theta_next, sp);
+}
 void launch_shard_combine(const ShardPub& sp, hipStream_t st) {
   hipLaunchKernelGGL(k_shard_combine, dim3(1), dim3(256), 0, st, sp);
 }
@@ -1002,6 +1043,8 @@ void launch_publish(const double* s, int ns, double* host, unsigned* host_seq, u
                                          const double*, int, int);                                  \
   template void launch_trial_split<T>(const T*, const T*, T*, T*, unsigned*, int64_t, int64_t,       \
                                       double, double, bool, const ShardPub&, hipStream_t);            \
+  template void launch_fista_split<T>(const T*, const T*, T*, T*, int64_t, double, double, double,   \
+                                      const ShardPub&, hipStream_t);                                  \
   template void launch_prox_pgd<T>(const T*, const T*, int, T*, T*, T*, T*, int64_t, int64_t,       \
                                    double, double, double, Red, hipStream_t, Pub, unsigned*);       \
   template void launch_fista_trial<T>(bool, const T*, const T*, int, T*, const T*, T*, T*, T*,      \

@@ -185,6 +185,41 @@ static void validate(const glx_problem* P, const glx_opts* O) {
 // (whole solves 10480 / 3943 vs 10847 / 4000: e_c fills late in a solve).
 static constexpr double kSplitMinBytesL32 = 64.0 * 1024 * 1024;
 static constexpr double kSplitMinBytes = 768.0 * 1024 * 1024;
+// Round 6: row-sharded FProxGD (iter_fista_shard) — the gradient
+// reduce-scattered, k_fista_trial on this rank's n / G rows, xc's rows all-gathered and v_next,
+// y_next re-derived from it on every rank (k_fista_split). Returns G where it applies, else 0.
+// opts.shard_rows (GLX_SHARD_ROWS): 1 on (needs n % G == 0), 2 off, 0 auto: on where this rank's
+// A is below kFistaShardMaxBytes and no device-control window is asked for. Host control only:
+// the device-controlled FISTA batch (fista_dc_run) decides from all-reduced gradient tails; the
+// sharded form would need its decision behind the all-gather, one more collective per queued
+// iteration, so big shards (C5: 2 GiB per rank, where the replicated row work is ~2 % of an
+// iteration) keep the all-reduce schedule with device control.
+static constexpr double kFistaShardMaxBytes = 768.0 * 1024 * 1024;
+static int shard_rows_opt(const glx_opts& O) {
+  int want = O.shard_rows;
+  if (const char* e = std::getenv("GLX_SHARD_ROWS")) {
+    want = std::atoi(e);
+    if (want < 0 || want > 2) throw Error{GLX_E_INVALID, "GLX_SHARD_ROWS must be 0 (auto), 1 (on) or 2 (off)"};
+  }
+  return want;
+}
+static int fista_shard_ranks(const glx_problem& P, const glx_opts& O) {
+  if (P.comm == nullptr || P.method != GLX_FPROXGD) return 0;
+  if (O.step_type != GLX_STEP_LINE_SEARCH && O.step_type != GLX_STEP_FIXED) return 0;
+  const int want = shard_rows_opt(O);
+  if (want == 2) return 0;
+  const glx_comm* c = static_cast<const glx_comm*>(P.comm);
+  const int vr = comm_size(c) == 1 ? std::max(1, O.shard_model) : comm_size(c);
+  if (vr <= 1) return 0;
+  const bool fits = vr <= 64 && P.n % vr == 0;
+  if (want == 1 && !fits)
+    throw Error{GLX_E_INVALID, "row-sharded FProxGD needs n % ranks == 0 and at most 64 ranks "
+                               "(opts.shard_rows = 0 / 2: the all-reduce schedule)"};
+  if (!fits) return 0;
+  if (want == 0 && ((double)P.m * (double)P.n * 8.0 >= kFistaShardMaxBytes || O.dc_window > 0)) return 0;
+  return vr;
+}
+
 static int split_mode(const glx_problem& P, const glx_opts& O) {
   if (O.exact_objective != 0) return 0;
   if (P.method != GLX_PROXGD && P.method != GLX_FPROXGD) return 0;
@@ -199,6 +234,7 @@ static int split_mode(const glx_problem& P, const glx_opts& O) {
   const double gate = (P.method == GLX_PROXGD && P.l == 32) ? kSplitMinBytesL32 : kSplitMinBytes;
   if (!force && (double)P.m * (double)P.n * 8.0 < gate) return 0;
   if (P.method == GLX_FPROXGD) {
+    if (fista_shard_ranks(P, O) > 0) return 0;   // the row-sharded FISTA runs the dense batch
     const char* sf = std::getenv("GLX_SPLIT_FISTA");
     if (sf && std::strcmp(sf, "0") == 0) return 0;
     const bool ls = O.step_type == GLX_STEP_LINE_SEARCH && O.ls_maxit > 0;
@@ -329,7 +365,7 @@ class Session : public SessionBase {
     // beside the next trial writing the other) and the finalize's
     double* tpart = static_cast<double*>(c.take(sizeof(double) * 2 * 6 * kMaxBlocks));
     double* fpart = static_cast<double*>(c.take(sizeof(double) * 4 * kMaxBlocks));
-    double* sblk = P.comm != nullptr && P.method == GLX_PROXGD
+    double* sblk = P.comm != nullptr && (P.method == GLX_PROXGD || P.method == GLX_FPROXGD)
                        ? static_cast<double*>(c.take(sizeof(double) * kShardChunkMax * kMaxShardRanks))
                        : nullptr;
     double* fh = static_cast<double*>(c.take(sizeof(double) * (fh_cap + 1)));
@@ -402,6 +438,7 @@ class Session : public SessionBase {
   // (dc_window_opt) where the fused speculative path, the spinning readback and, with a
   // communicator, the attached packet are all on; else 0 (the host decides)
   static int dc_window_eff(const glx_problem& P, const glx_opts& O, const GemmPlan& plan) {
+    if (fista_shard_ranks(P, O) > 0) return 0;   // row-sharded FProxGD: host control
     const bool ls = O.step_type == GLX_STEP_LINE_SEARCH && O.ls_maxit > 0;
     const bool spin = !env_is("GLX_READBACK", "sync");
     const bool attach = spin && !env_is("GLX_ATTACH_PUB", "0");
@@ -526,12 +563,25 @@ class Session : public SessionBase {
     // the per-rank timing model of G ranks — the trial on n / G rows, every line-search test
     // accepted — whose iterates are NOT a solve (glx_solve refuses it; ADVICE round 5: no
     // environment variable turns it on inside the library).
-    if (comm_ != nullptr && P.method == GLX_PROXGD && dc_window_ == 0) {
-      int want = O.shard_rows;
-      if (const char* e = std::getenv("GLX_SHARD_ROWS")) {
-        want = std::atoi(e);
-        if (want < 0 || want > 2) throw Error{GLX_E_INVALID, "GLX_SHARD_ROWS must be 0 (auto), 1 (on) or 2 (off)"};
+    if (comm_ != nullptr && P.method == GLX_FPROXGD) {
+      const int fr = fista_shard_ranks(P, O);
+      cranks_ = comm_size(comm_);
+      if (fr > 0) {
+        shard_ = true;
+        fshard_ = true;
+        shard_model_ = cranks_ == 1;
+        sranks_ = fr;
+        srank_ = shard_model_ ? 0 : comm_rank(comm_);
+        srows_ = n_ / fr;
+        srow0_ = (int64_t)srank_ * srows_;
+        nbp_ = prox_blocks(srows_, l_);   // k_fista_trial's grid is k_prox_pgd's
+        nbf_ = finalize_blocks(ml_, ax_split(plan_, 2), 0, srows_ * l_);
+        stv_ = 4;
+        schunk_ = kShardPartOff + stv_ * nbp_ + 4 * nbf_;
       }
+    }
+    if (comm_ != nullptr && P.method == GLX_PROXGD && dc_window_ == 0) {
+      const int want = shard_rows_opt(O);
       cranks_ = comm_size(comm_);
       int vr = cranks_;
       if (cranks_ == 1) {
@@ -553,7 +603,7 @@ class Session : public SessionBase {
         const int fsrc = O.exact_objective != 0 ? 3 : 2;
         nbf_ = finalize_blocks(ml_, emode_ && smode_ == 1 ? ax_split(plan_, 1) : ax_split(plan_, fsrc),
                                emode_ && smode_ == 1 ? gsplit_ : 0, srows_ * l_);
-        schunk_ = kShardPartOff + 6 * nbp_ + 4 * nbf_;
+        schunk_ = kShardPartOff + stv_ * nbp_ + 4 * nbf_;
         // A e from the bitmap / list gathers reads e only where its masks are set, where e = p:
         // the gathered p serves as e and z is not re-derived (the row form reads whole rows)
         zskip_ = emode_ && gform_ != 1;
@@ -725,7 +775,11 @@ class Session : public SessionBase {
     else if (rows_form_) s += "rows k_at_rows S0=" + std::to_string(gsplit_);
     else if (gform_ == 2) s += "gather k_e_lists+k_at_gather";
     else s += "gather k_at_gather_bm";
-    if (shard_)
+    if (shard_ && fshard_)
+      s += "; rows=sharded x" + std::to_string(sranks_) + (shard_model_ ? " (timing model)" : "") +
+           " (reduce-scatter of A^T r, k_fista_trial on n/" + std::to_string(sranks_) +
+           " rows, all-gather of xc, k_fista_split)";
+    else if (shard_)
       s += "; rows=sharded x" + std::to_string(sranks_) + (shard_model_ ? " (timing model)" : "") +
            " (reduce-scatter of A^T r, k_prox_pgd on n/" + std::to_string(sranks_) +
            " rows, all-gather of p, k_trial_split)";
@@ -892,7 +946,7 @@ class Session : public SessionBase {
                                 rd, st_,
                                 snap_trial ? scal_ + S_TR : nullptr,
                                 snap_trial ? scal_ + S_SNAP : nullptr, snap_trial ? 6 : 0,
-                                chain ? 1 : 0, gat ? gsplit_ : 0, dc_ctl_,
+                                chain ? (egat_ ? 2 : 1) : 0, gat ? gsplit_ : 0, dc_ctl_,
                                 dmax ? ptr_.part : nullptr, dmax ? ptr_.np : 0, dmax ? ptr_.nv : 6);
     check_launch();
     if (dfin) pfin_ = Pend{fpart_, finalize_blocks(ml_, S, gat ? gsplit_ : 0, cx ? nl_ : 0), 4, 0u, scal_ + slot};
@@ -930,7 +984,7 @@ class Session : public SessionBase {
   // slabs, each workgroup compacts its K range's row flags itself), so no column lists.
   void cand_ax(const T* const* xs, Pub pb = Pub{}) {
     const T* xd[3] = {xs[1], nullptr, nullptr};
-    if (egat_) {   // round 6: A p_thr and A e in one pass (S slabs each: A e at Pp_, A p_thr behind)
+    if (egat_) {   // round 6: A p and A e in one pass (S slabs each: A e at Pp_, A p behind)
       EGat eg;
       eg.E = xs[0];
       const int64_t npad = (n_ + 63) / 64 * 64;   // glx_device.h zf_npad
@@ -938,7 +992,7 @@ class Session : public SessionBase {
       eg.bstride = npad / 16;
       eg.Pe = Pp_;
       hipEvent_t e0 = prof_begin(0);
-      if (!launch_ax_egat<T>(plan_, A_, xs[1], Pp_ + (size_t)gsplit_ * ml_, dc_gate_, 0, st_, pb, eg))
+      if (!launch_ax_egat<T>(plan_, A_, xs[2], Pp_ + (size_t)gsplit_ * ml_, dc_gate_, 0, st_, pb, eg))
         throw Error{GLX_E_STATE, "fused A e: the plan does not take it"};
       check_launch();
       prof_end(0, e0);
@@ -1416,7 +1470,9 @@ class Session : public SessionBase {
   // Bytes per iteration and rank: reduce-scatter + all-gather of n x l, the same as one ring
   // all-reduce of the gradient; the row-wise work (k_prox_pgd, the count) is divided by G.
   double* blk_own() { return blk_ + (int64_t)(shard_model_ ? 0 : srank_) * schunk_; }
-  int tr_other() const { return tr_slot_ == S_TR ? S_TRN : S_TR; }
+  // the speculated next trial's sums: ProxGD S_TRN; FProxGD S_RO (S_TRN = S_RG holds g(y) of a
+  // prologue until the host has read it; S_RO is read right behind its own objective)
+  int tr_other() const { return tr_slot_ == S_TR ? (fshard_ ? S_RO : S_TRN) : S_TR; }
   void shard_gradient(const T* r, int set) {
     T* G = Gs_[set];
     T* Gp = Gps_[set];
@@ -1459,6 +1515,7 @@ class Session : public SessionBase {
     sp.nbp = nbp_;
     sp.nbf = nbf_;
     sp.mask = mask;
+    sp.tv = stv_;
     sp.tr = scal_ + tr_dst;
     sp.rt = scal_ + S_RT;
     sp.tr_off = tr_dst;
@@ -1484,12 +1541,12 @@ class Session : public SessionBase {
     T* rsc[3] = {chain ? nullptr : rs[0], rs[1], rs[2]};
     const int64_t o = srow0_ * l_;
     Red rd = red_to(scal_ + S_RT);   // its workgroup partials ride the all-gather too
-    rd.part = blk_own() + kShardPartOff + 6 * nbp_;
+    rd.part = blk_own() + kShardPartOff + stv_ * nbp_;
     rd.parts_only = 1;
     launch_finalize_residual<T>(Pp_, gat ? ax_split(plan_, 1) : ax_split(plan_, nsrc), B_, nsrc, rsc,
                                 ml_, nullptr, 0, 1, cx + o, srows_ * l_, cmax, nullptr, 0.0,
                                 scal_ + S_DRN, rd, st_, nullptr, nullptr, 0,
-                                chain ? 1 : 0, gat ? gsplit_ : 0, Ctl{});
+                                chain ? (egat_ ? 2 : 1) : 0, gat ? gsplit_ : 0, Ctl{});
     check_launch();
   }
   void iter_proxgd_shard() {
@@ -1845,6 +1902,7 @@ class Session : public SessionBase {
     const double theta_next = 2.0 / (double)(inner_ + 2);
     const bool ls = O_.step_type == GLX_STEP_LINE_SEARCH && O_.ls_maxit > 0;
     const double t0 = ls ? tk_ : schedule(inner_);
+    if (fshard_) { iter_fista_shard(theta, theta_next); return; }
     const bool fuse = fused_fista_ok_ && !smooth;
     if (fsplit_ && ls && kslot_ < 0 && dense_left_ == 0) fista_split_prologue();
     if (!smooth && fista_dc_ready(t0, theta)) { fista_dc_run(); return; }
@@ -1960,7 +2018,7 @@ class Session : public SessionBase {
   // After the search: x_k <- x, v_k <- v (:145, :147), y <- y_next; the packet (hs_) holds the
   // last trial's sums. spec_trial: the speculative fused kernel left the next first trial.
   void fista_update(bool accepted, bool spec_trial, double t, bool fs_batch, double theta_next,
-                    int ryn, int i_rn) {
+                    int ryn, int i_rn, int trs = S_TR) {
     const bool ls = O_.step_type == GLX_STEP_LINE_SEARCH && O_.ls_maxit > 0;
     if (spec_trial) {   // the speculative outputs become the next iteration's trial buffers
       const int ox = ix_, ov = iv_, oy = iy_;
@@ -1994,13 +2052,118 @@ class Session : public SessionBase {
       iry_ = ryn;
       gy_sq_ = hs_[S_RT + 1];
       y_ready_ = true;
-      f_cur_ = 0.5 * hs_[S_RT] + P_.mu0 * hs_[S_TR + i_rn];   // A x exact: same x as recorded
+      f_cur_ = 0.5 * hs_[S_RT] + P_.mu0 * hs_[trs + i_rn];   // A x exact: same x as recorded
       s_cur_ = hs_[S_RT + 3] / (double)nl_;
       f_known_ = true;
     } else {
       y_ready_ = false;
       f_known_ = false;
     }
+  }
+
+  // ------------------------------------------------------------------ row-sharded FProxGD
+  // (round 6; gl_FProxGD_primal.py:138-147 row-sharded). Per trial on
+  // every rank: k_fista_trial on this rank's n / G rows of y and the reduce-scattered gradient
+  // (xc's rows and the four trial sums as workgroup partials into this rank's chunk); one RCCL
+  // group all-gathers xc's rows and every rank's chunk; k_fista_split re-derives v_next and y_next
+  // of every row from the gathered xc (fista_row's arithmetic) and combines the sums in rank
+  // order; A @ [xc | y_next] over this rank's rows of A and its finalize (sums into the chunk, the
+  // count over this rank's rows of xc). As iter_proxgd_shard, the next gradient and first trial
+  // are queued speculatively behind the trial (their exchange carries its residual sums) and the
+  // packet rides the next trial's dense pass. Host control only (see fista_shard_ranks).
+  void fshard_trial(int ix, int iy, const T* G, int oc, int ovn, int oyn, double t, double theta,
+                    double theta_next) {
+    const int64_t o = srow0_ * l_;
+    Red rd = red_to(scal_ + S_TR);
+    rd.part = blk_own() + kShardPartOff;
+    rd.parts_only = 1;
+    launch_fista_trial<T>(true, X_[iy] + o, G + o, 1, nullptr, X_[ix] + o, X_[oc] + o, X_[ovn] + o,
+                          X_[oyn] + o, srows_, l_, t, mu_, O_.thres, theta, theta_next, O_.delta, rd, st_,
+                          Pub{}, nullptr, nullptr);
+    check_launch();
+  }
+  void fshard_derive(int ix, int oc, int ovn, int oyn, double theta, double theta_next, const ShardPub& sp) {
+    launch_fista_split<T>(X_[oc], X_[ix], X_[ovn], X_[oyn], nl_, O_.thres, theta, theta_next, sp, st_);
+    check_launch();
+  }
+  void iter_fista_shard(double theta, double theta_next) {
+    const bool ls = O_.step_type == GLX_STEP_LINE_SEARCH && O_.ls_maxit > 0;
+    const double t0 = ls ? tk_ : schedule(inner_);
+    bool first_done = false;
+    if (spec_trial_ready_) {   // the previous iteration's speculated trial (its sums in tr_slot_)
+      spec_trial_ready_ = false;
+      use_gset(spec_set_);
+      first_done = spec_trial_mu_ == mu_ && spec_trial_t_ == t0 && spec_trial_theta_ == theta;
+      if (!first_done) ax_queued_ = false;
+    } else {
+      if (!y_ready_) {
+        launch_thr_axpby<T>(X_[ix_], X_[iv_], X_[iy_], nl_, O_.thres, 1.0 - theta, theta, st_);
+        check_launch();
+        residual1(X_[iy_], R_[iry_], S_RG);   // g(y): its sums all-reduced (8 B)
+        gy_pending_ = true;
+      }
+      shard_gradient(R_[iry_], gset_);
+    }
+    const int rc = (iry_ + 1) % kRes, ryn = (iry_ + 2) % kRes;
+    auto trial = [&](double tt) {
+      fshard_trial(ix_, iy_, G_, ic_, ivn_, iyn_, tt, theta, theta_next);
+      shard_exchange(ic_);
+      fshard_derive(ix_, ic_, ivn_, iyn_, theta, theta_next, shard_pub(1, tr_slot_, nullptr));
+    };
+    double t = t0;
+    bool accepted = false, spec_trial = false;
+    if (ls) {
+      for (int it = 0; it < O_.ls_maxit; ++it) {
+        if (!(it == 0 && first_done)) trial(t);
+        const T* xs[3] = {X_[ic_], X_[iyn_], nullptr};
+        T* rs[3] = {R_[rc], R_[ryn], nullptr};
+        const bool skip_ax = it == 0 && first_done && ax_queued_;
+        ax_queued_ = false;
+        shard_fin(2, xs, rs, X_[ic_], scal_ + tr_slot_ + 3, skip_ax);
+        unsigned seq = 0;
+        if (want_spec(it)) {
+          // the next iteration's gradient at y_next and its first trial (t, theta_next and the one
+          // after), into the other gradient set, the spare buffers and the other trial slot
+          const int ns = nset(gset_);
+          const int ot = tr_other();
+          const double thnn = 2.0 / (double)(inner_ + 3);
+          shard_gradient(R_[ryn], ns);
+          fshard_trial(ic_, iyn_, Gs_[ns], ff1_, ff2_, ff3_, t, theta_next, thnn);
+          shard_exchange(ff1_);
+          fshard_derive(ic_, ff1_, ff2_, ff3_, theta_next, thnn, shard_pub(3, ot, nullptr));
+          const T* sx[3] = {X_[ff1_], X_[ff3_], nullptr};
+          const bool carry = spin_readback_ && attach_ok_ && ax_pub_ok(plan_, 2);
+          Pub pb;
+          if (carry) pb = make_pub(nullptr, &seq);
+          else seq = post_readback();
+          spec_ax(2, sx, pb);
+          ax_queued_ = true;
+          spec_trial = true;
+        } else {
+          shard_exchange(-1);
+          launch_shard_combine(shard_pub(2, tr_slot_, nullptr), st_);
+          check_launch();
+          seq = post_readback();
+        }
+        wait_readback(seq);
+        if (gy_pending_) { gy_sq_ = hs_[S_RG]; gy_pending_ = false; }
+        const double gy = 0.5 * gy_sq_, gxc = 0.5 * hs_[S_RT];
+        if (shard_model_ || gxc <= gy + hs_[tr_slot_ + 0] + hs_[tr_slot_ + 1] / (2 * t)) {
+          accepted = true;
+          spec_on_ = (it == 0);
+          break;
+        }
+        spec_trial = false;
+        spec_on_ = false;
+        ax_queued_ = false;   // the speculated trial and its A@X are dropped
+        t *= O_.ls_coeff;
+      }
+      if (!accepted) trial(t);   // the untested last step
+    } else if (!first_done) {
+      trial(t);
+    }
+    fista_update(accepted, spec_trial, t, false, theta_next, ryn, 2, tr_slot_);
+    if (spec_trial) tr_slot_ = tr_other();
   }
 
   // ------------------------------------------------------------------ device-controlled FProxGD
@@ -2336,6 +2499,8 @@ class Session : public SessionBase {
   // row-sharded ProxGD (iter_proxgd_shard): this rank's rows [srow0_, srow0_ + srows_) of n,
   // sranks_ row blocks (cranks_ communicator ranks; they differ only in the timing model)
   bool shard_ = false, shard_model_ = false;
+  bool fshard_ = false;        // round 6: row-sharded FProxGD (iter_fista_shard)
+  int stv_ = 6;                // values per trial workgroup partial in the chunk (FProxGD: 4)
   int srank_ = 0, sranks_ = 1, cranks_ = 1;
   int64_t srow0_ = 0, srows_ = 0;
   int nbp_ = 0, nbf_ = 0;      // k_prox_pgd's workgroups on srows_ rows, the trial finalize's

@@ -72,9 +72,10 @@ def test_sharded_matches_oracle(tmp_path, world, solver, shape):
 
 @pytest.mark.parametrize("solver", ["gl_ProxGD_primal", "gl_FProxGD_primal"])
 def test_sharded_split_candidate_forced(tmp_path, monkeypatch, solver):
-    # the split-candidate trial (default only for A >= 768 MiB per rank) forced at a small shard
+    # the split-candidate trial (default only for A >= 768 MiB per rank) forced at a small shard,
+    # on the all-reduce schedule (the row-sharded FProxGD runs the dense batch)
     monkeypatch.setenv("GLX_SPLIT_CAND", "1")
-    v = run_sharded(tmp_path, 2, solver, 512, 1024, 32, maxit=25)
+    v = run_sharded(tmp_path, 2, solver, 512, 1024, 32, maxit=25, extra=("--shard-rows", "2"))
     ranks = v["ranks"]
     assert ranks[0]["x_sha"] == ranks[1]["x_sha"] and ranks[0]["k"] == ranks[1]["k"]
     assert ranks[0]["k"] == v["oracle_k"]
@@ -288,3 +289,47 @@ def test_stalled_rank_watchdog_host_transport(tmp_path):
     assert "glx watchdog: rank 0 of 2: dist_gpu_worker stall check passed its deadline of 20 s" in msg, msg[-3000:]
     assert "session: {'k':" in msg and "'collectives_issued':" in msg, msg[-3000:]
     assert "communicator: {'issued':" in msg, msg[-3000:]
+
+
+@pytest.mark.parametrize("world,shape,extra", [
+    (2, (515, 1024, 16), ()),
+    (3, (515, 1536, 32), ()),
+    (8, (1024, 1024, 32), ()),
+    (2, (512, 1024, 32), ("--alpha-scale", "3.0")),   # backtracking: rejected trials on n/G rows
+    (3, (600, 768, 5), ()),
+])
+def test_row_sharded_fprox(tmp_path, world, shape, extra):
+    """Round 6: FProxGD's row-sharded schedule (reduce-scatter of A^T r,
+    k_fista_trial on n / G rows, one all-gather of xc's rows and the partial sums, k_fista_split
+    re-deriving v_next and y_next on every rank) against the unsharded oracle
+    (gl_FProxGD_primal.py:89-103, 136-147): k identical, f_hist within 1e-8, bit-identical on
+    every rank."""
+    v = run_sharded(tmp_path, world, "gl_FProxGD_primal", *shape, maxit=25,
+                    extra=("--shard-rows", "1") + tuple(extra), timeout=150)
+    r0 = _check_identical_and_oracle(v, world)
+    assert ("rows=sharded x%d" % world) in r0["plan"] and "k_fista_split" in r0["plan"], r0["plan"]
+    assert v["x_maxdiff"] <= 1e-6 * v["x_scale"]
+
+
+def test_row_sharded_fprox_matches_allreduce_schedule(tmp_path):
+    """Both FProxGD multi-GPU schedules on one instance: the all-reduce schedule with device
+    control and the row-sharded one agree (same k, f_hist within 1e-12: they differ only in the
+    order the trial sums are added)."""
+    a = run_sharded(tmp_path, 2, "gl_FProxGD_primal", 515, 1024, 32, maxit=25, extra=("--shard-rows", "1"))
+    b = run_sharded(tmp_path, 2, "gl_FProxGD_primal", 515, 1024, 32, maxit=25, extra=("--shard-rows", "2"))
+    ra, rb = a["ranks"][0], b["ranks"][0]
+    assert "rows=sharded" in ra["plan"] and "rows=sharded" not in rb["plan"]
+    assert ra["k"] == rb["k"]
+    fa, fb = np.asarray(ra["f_hist"]), np.asarray(rb["f_hist"])
+    assert np.max(np.abs(fa - fb) / np.abs(fb)) < 1e-12
+
+
+def test_row_sharded_fprox_c5_shard_shape(tmp_path):
+    """C5's per-rank shard (16384 rows x 16384 x 32 fp64) on the row-sharded FProxGD schedule
+    (forced: auto keeps the all-reduce schedule with device control for 2 GiB shards), world 2,
+    two iterations per phase, against the unsharded oracle."""
+    v = run_sharded(tmp_path, 2, "gl_FProxGD_primal", 32768, 16384, 32, maxit=2, threads=8,
+                    extra=("--shard-rows", "1"), timeout=140)
+    r0 = _check_identical_and_oracle(v, 2)
+    assert r0["k"] == 6 and "k_fista_split" in r0["plan"]
+    assert v["x_maxdiff"] <= 1e-6 * v["x_scale"]

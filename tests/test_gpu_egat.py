@@ -2,11 +2,11 @@
 kernels_axdma.hip; gl_ProxGD_primal.py:89-92 g(z) and :112 the objective of the candidate, from
 A p = A p_thr + A e).
 
-The dense pass A p_thr is the same LDS-DMA tile with or without the fused A e, so the next
-gradient residual (A p_thr - b) and therefore the iterate are bit-identical to the gather form
-(GLX_AE_FUSED=0: the transposed copy of A and k_at_gather_bm); only A e is summed in another order
-(per K split, the block's chunk walk), so the recorded objective moves at the ulp level. Against
-the oracle: the north-star bar (k identical, f_hist within 1e-8, x within 1e-6 of max|x|).
+The fused pass streams A p on MFMA (the objective and the Armijo test directly) and A e on VALU
+from the same LDS chunks; the next gradient residual is (A p - b) - A e instead of the gather
+form's direct A p_thr - b (GLX_AE_FUSED=0: the transposed copy of A and k_at_gather_bm), so the two
+forms agree to rounding (k identical, f_hist within 1e-11, x within 1e-9 of max|x|). Against the
+oracle: the north-star bar (k identical, f_hist within 1e-8, x within 1e-6 of max|x|).
 """
 import warnings
 
@@ -38,8 +38,8 @@ def test_fused_ae_matches_gather_and_oracle(monkeypatch, l, maxit):
     assert "A e fused into the dense pass" in pf, pf
     assert "gather k_at_gather_bm" in pg, pg
     assert kf == kg == 3 * maxit
-    assert np.array_equal(xf, xg)
-    assert np.max(np.abs(ff - fg) / np.abs(fg)) < 1e-12
+    assert np.max(np.abs(xf - xg)) <= 1e-9 * np.max(np.abs(xg))
+    assert np.max(np.abs(ff - fg) / np.abs(fg)) < 1e-11
     with warnings.catch_warnings():
         warnings.simplefilter("ignore")
         xr, kr, outr = numpy_ref.gl_ProxGD_primal(x0, A, b, mu, dict(opts))
@@ -50,8 +50,8 @@ def test_fused_ae_matches_gather_and_oracle(monkeypatch, l, maxit):
 
 
 def test_fused_ae_rejections(monkeypatch):
-    """alpha0 = 2.5 / L: rejected first trials (the retrial's k_prox_pgd writes e and its bitmaps,
-    the fused pass reads them) — bit-identical iterates to the gather form, 20 per phase."""
+    """alpha0 = 2.5 / L: rejected first trials (the retrial's k_prox_pgd writes p and its bitmaps,
+    the fused pass reads them): the gather form's iterates to rounding, 20 per phase."""
     from oracle import numpy_ref
     m, n, l = 8192, 16384, 32
     A, b, u, x0, mu = numpy_ref.gen_data(m, n, l, 5)
@@ -60,5 +60,5 @@ def test_fused_ae_rejections(monkeypatch):
     xf, kf, ff, _ = _run(monkeypatch, True, At, bt, x0, mu, opts)
     xg, kg, fg, _ = _run(monkeypatch, False, At, bt, x0, mu, opts)
     assert kf == kg
-    assert np.array_equal(xf, xg)
-    assert np.max(np.abs(ff - fg) / np.abs(fg)) < 1e-12
+    assert np.max(np.abs(xf - xg)) <= 1e-9 * np.max(np.abs(xg))
+    assert np.max(np.abs(ff - fg) / np.abs(fg)) < 1e-11

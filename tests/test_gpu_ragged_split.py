@@ -9,8 +9,8 @@ clears zf at creation and the gather masks rows >= n itself; these tests fill th
 0xFF bytes first (the worst stale content torch.empty could hand back) and compare the whole
 trajectory with the oracle (gl_ProxGD_primal.py:73-132) at the fp64 bar.
   - n = 1000 (n % 64 = 40): groups [1008, 1024) are never visited by the 16-row trials;
-  - n = 8224 (n % 64 = 32, the 32-column narrow A^T R panel WL 3 at 128 < 256 64-column panels):
-    the upper half of the last u64 is never written.
+  - n = 8224 (n % 64 = 32): the 16-row trial kernels never write the groups of rows
+    [8224, 8256) — the upper half of the last u64 of every column bitmap.
 """
 import warnings
 
@@ -52,8 +52,6 @@ def test_ragged_split_candidate_vs_oracle(dirty_workspace, m, n, maxit):
     x, k, out = gl_ProxGD_primal(x0, A, b, mu, dict(opts))
     plan = out["glx"]["plan"]
     assert "k_at_gather_bm" in plan, plan
-    if n == 8224:
-        assert "WL3" in plan and "32-column panels" in plan, plan
     assert k == kr, (k, kr)
     assert _rel(out["fval"], outr["fval"]) < 1e-8
     assert _rel([float(v) for v in out["f_hist"]], [float(v) for v in outr["f_hist"]]) < 1e-8
