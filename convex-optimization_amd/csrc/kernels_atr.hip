@@ -573,12 +573,6 @@ static void atr_mfma_nt(const GemmPlan& p, const T* A, const T* R, T* Gp, hipStr
     case 1008: atr_mfma_go<T, NT, 8, 0, true>(p, A, R, Gp, st); break;
     case 1104: atr_mfma_go<T, NT, 4, 1, true>(p, A, R, Gp, st); break;
     case 1208: atr_mfma_go<T, NT, 8, 2, true>(p, A, R, Gp, st); break;
-    case 1216:
-      if constexpr (sizeof(T) == 4) {   // round 6: f32's sixteen-step ring (C3)
-        atr_mfma_go<T, NT, 16, 2, true>(p, A, R, Gp, st);
-        break;
-      }
-      throw Error{GLX_E_INVALID, "A^T R: the sixteen-step ring is f32"};
     case 308:
     case 1308:
       if constexpr (sizeof(T) == 8) {
@@ -652,11 +646,6 @@ static void atr_prox_nt(const GemmPlan& p, const T* A, const T* R, T* G, const T
       case 1308: atr_prox_go<T, NT, 8, true, 3>(p, A, R, G, x, pp, pthr, z, t, mu, thres, red, st, pub, Gp, pcnt, zf); return;
       default: break;
     }
-  } else {
-    if (code == 1216) {
-      atr_prox_go<T, NT, 16, true, 2>(p, A, R, G, x, pp, pthr, z, t, mu, thres, red, st, pub, Gp, pcnt, zf);
-      return;
-    }
   }
   switch (code) {
     case 1008: atr_prox_go<T, NT, 8, true, 0>(p, A, R, G, x, pp, pthr, z, t, mu, thres, red, st, pub, Gp, pcnt, zf); return;
@@ -705,11 +694,6 @@ static void atr_fista_nt(const GemmPlan& p, const T* A, const T* R, T* G, const 
       case 308: atr_fista_go<T, NT, 8, false, 3>(p, A, R, G, y, xk, xc, vn, yn, t, mu, thres, theta, theta_next, red, st, pub, Gp, pcnt, ec, zf); return;
       case 1308: atr_fista_go<T, NT, 8, true, 3>(p, A, R, G, y, xk, xc, vn, yn, t, mu, thres, theta, theta_next, red, st, pub, Gp, pcnt, ec, zf); return;
       default: break;
-    }
-  } else {
-    if (code == 1216) {
-      atr_fista_go<T, NT, 16, true, 2>(p, A, R, G, y, xk, xc, vn, yn, t, mu, thres, theta, theta_next, red, st, pub, Gp, pcnt, ec, zf);
-      return;
     }
   }
   switch (code) {

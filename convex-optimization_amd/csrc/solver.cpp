@@ -244,14 +244,20 @@ static int split_mode(const glx_problem& P, const glx_opts& O) {
 }
 
 // Round 6: ProxGD's split-candidate trial with A e fused into the dense pass (launch_ax_egat,
-// kernels_axdma.hip): where the session's one-source pass is the f64 LDS-DMA tile 92278 (NS) and
-// no gather form is forced (GLX_GATHER), GLX_AE_FUSED=0: off. The transposed copy of A is then
-// not needed (ProxGD's workspace shrinks by m x n) and no gather launches.
+// kernels_axdma.hip: A p on MFMA, A e on VALU from the same LDS chunks; no transposed copy of A,
+// no gather launch) where the session's one-source pass is the f64 LDS-DMA tile 92278 (NS).
+// Opt-in (GLX_AE_FUSED=1): same box, 200-step windows / whole solves (profiles/r6_egat/): NS
+// 2 452-2 467 / 2 461-2 467 it/s fused against 2 454-2 470 / 2 427-2 434 with the gather — level
+// in the window, +1.5 % over a solve (the gather grows late in a solve), but the fused pass runs
+// 210-218 µs against 174-176 µs: its A e (VALU, after the chunk's MFMAs) leaves the MFMA pipe of
+// both waves of a SIMD idle. Interleaving it into the MFMA stream (straight-line, or on opposite
+// sides of the two waves' MFMAs) spilled 16-208 VGPRs at 256. The gather stays the default;
+// the fused form also halves the session's workspace (no m x n copy of A).
 static bool egat_mode(const glx_problem& P, const GemmPlan& plan, int smode) {
   if (smode != 1 || P.method != GLX_PROXGD || P.dtype != GLX_F64) return false;
   if (gather_form() >= 0) return false;
   const char* e = std::getenv("GLX_AE_FUSED");
-  if (e && std::strcmp(e, "0") == 0) return false;
+  if (!(e && std::strcmp(e, "1") == 0)) return false;
   return ax_egat_ok(plan, 8);
 }
 
@@ -276,9 +282,8 @@ static GemmPlan session_plan(const glx_problem& P, const glx_opts& O) {
     if (P.n / 64 >= 256) {
       f.atr_wl = 2;
       f.atr_S = 1;
-      // round 6: GLX_ATR_PF32=16, a sixteen-step ring (twice the A bytes in flight per wave)
-      const char* pf32 = std::getenv("GLX_ATR_PF32");
-      if (pf32 && std::atoi(pf32) == 16) f.atr_pf = 16;
+      // (round 6: a sixteen-step ring, twice the A bytes in flight per wave, measured slower:
+      // A^T R + trial 120.9 against 101.3 us at C3, 3 628 against 3 862 it/s, profiles/r6_egat/)
     }
     if (atr_prox_ok(f)) return f;   // only where the trial actually fuses (GLX_ATR_FUSE_SPLIT)
   }

@@ -113,10 +113,7 @@ def test_workspace_planning_host_only():
             # (kernels_gather.hip); FProxGD's also e_c and three A thr(x) residual-sized slots
             gate = (64 if meth == _lib.GLX_PROXGD and l == 32 else 768) * 2**20   # kSplitMinBytes*
             split = dt == 1 and l in (16, 32) and m * n * 8 >= gate
-            # round 6: ProxGD whose dense pass is the LDS-DMA tile (f64, A beyond 384 MiB, l 16 / 32)
-            # fuses A e into that pass and keeps no transposed copy
-            egat = meth == _lib.GLX_PROXGD and dt == 1 and l in (16, 32) and m * n * 8 > 384 * 2**20
-            at = es * m * n if (split and not egat) else 0
+            at = es * m * n if split else 0
             extra = es * (n * l + 3 * m * l) if (split and meth == _lib.GLX_FPROXGD) else 0
             assert nb.value >= es * (2 * n * l + 2 * m * l) + at + extra  # x-buffers + residuals at least
             assert nb.value < at + es * (m * n) // 4 + (64 << 20)   # else never close to the size of A
