@@ -92,15 +92,51 @@ def workspace(problem: GlxProblem, o: GlxOpts, device) -> torch.Tensor:
     return torch.empty(int(nbytes.value), dtype=torch.uint8, device=device)
 
 
-def _lambda_max(A: torch.Tensor, comm=None) -> float:
-    """``np.max(LA.eigvals(A.T @ A))`` (gl_SGD_primal.py:35-37) for the optional
-    continuous_subgradient_flag, evaluated on the device. With row-sharded A the Gram matrix is
-    the sum of the shards' (all-reduced once, before the solve)."""
-    a = A.to(torch.float64)
-    gram = a.T @ a
-    if comm is not None:
-        comm.allreduce_(gram)
-    return float(torch.linalg.eigvalsh(gram).max().item())
+def _lambda_max(A: torch.Tensor, comm=None, max_steps: int = 400) -> float:
+    """``np.max(LA.eigvals(A.T @ A))`` (gl_SGD_primal.py:35-37, gl_GD_primal.py:43-45) for the
+    optional continuous_subgradient_flag, without forming the n x n Gram matrix and without a
+    library eigensolver on the device: Lanczos on the operator v -> A^T (A v), whose two products
+    are libglx's own kernels (glx_residual with b = 0, glx_gradient; with row-sharded A the
+    product is all-reduced over the ranks, so every rank runs the same recurrence). The
+    recurrence and its full re-orthogonalisation run on the host in float64 on n-vectors; the
+    largest eigenvalue of the k x k tridiagonal matrix is taken once its Ritz residual
+    beta_k |s_k| is below 1e-13 of it (the eigenvalue itself is then accurate to ~1e-16 relative),
+    or when the Krylov space is all of R^n (k = n: exact). A fixed start vector (seeded), so the
+    result is the same on every rank and from run to run."""
+    import numpy as np
+    from . import kernels
+    a = A if A.dtype == torch.float64 else A.to(torch.float64)
+    m, n = a.shape
+    zero = torch.zeros((m, 1), dtype=torch.float64, device=a.device)
+    rng = np.random.default_rng(20240611)
+    q = rng.standard_normal(n)
+    q /= np.linalg.norm(q)
+    Q = np.zeros((min(n, max_steps) + 1, n))
+    alphas, betas = [], []
+    q_prev, beta = np.zeros(n), 0.0
+    theta = 0.0
+    for k in range(min(n, max_steps)):
+        Q[k] = q
+        r, _ = kernels.residual(a, torch.from_numpy(np.ascontiguousarray(q[:, None])).to(a.device), zero)   # A q
+        w_t = kernels.gradient(a, r)                                                   # A^T A q
+        if comm is not None:
+            comm.allreduce_(w_t)
+        w = w_t[:, 0].cpu().numpy()
+        alpha = float(q @ w)
+        w = w - alpha * q - beta * q_prev
+        for _ in range(2):   # full re-orthogonalisation against the basis so far
+            w -= Q[:k + 1].T @ (Q[:k + 1] @ w)
+        alphas.append(alpha)
+        beta = float(np.linalg.norm(w))
+        T = np.diag(alphas) + np.diag(betas, 1) + np.diag(betas, -1)
+        ev, evec = np.linalg.eigh(T)
+        theta = float(ev[-1])
+        # an invariant subspace (beta ~ 0), or the Ritz pair of theta converged
+        if beta <= 1e-14 * abs(theta) or (k >= 4 and abs(beta * evec[-1, -1]) <= 1e-13 * abs(theta)):
+            break
+        betas.append(beta)
+        q_prev, q = q, w / beta
+    return theta
 
 
 def _replay_log(s: "Session", res: Dict[str, Any], mu_0: float) -> None:

@@ -250,8 +250,9 @@ def test_full_size_vs_oracle(solver, dtype, shape):
 @pytest.mark.parametrize("solver", ["gl_SGD_primal", "gl_GD_primal"])
 def test_continuous_subgradient_flag(solver):
     """opts['continuous_subgradient_flag'] (gl_SGD_primal.py:35-37, gl_GD_primal.py:43-45):
-    alpha0 = 1 / max eig(A^T A). The build takes the eigenvalue with a symmetric solver on the
-    device, the oracle with np.linalg.eigvals as the reference does: alpha0 agrees to rounding."""
+    alpha0 = 1 / max eig(A^T A). The build takes the eigenvalue by Lanczos on v -> A^T (A v) with
+    libglx's own products (round 6: no Gram matrix, no library eigensolver on the device), the
+    oracle with np.linalg.eigvals as the reference does: alpha0 agrees to ~1e-14."""
     from oracle import numpy_ref
     A, b, u, x0, mu = numpy_ref.gen_data(300, 256, 2, 31)
     opts = {"continuous_subgradient_flag": True, "maxit": 30}
