@@ -6,7 +6,8 @@ mkdir -p $OUT
 export TMPDIR=/tmp
 B="python bench.py --steps 200 --warmup 20 --no-cpu-baseline --no-whole-solve --force-comm"
 # ProxGD 1024-row (8-GPU) shard, the row-sharded timing model: knobs of the small kernels
-for v in "base:" "gbm_novec:GLX_GATHER_BM=8,256,0" "gbm_seg128:GLX_GATHER_BM=8,128,1" "axs16:GLX_AX_S=16" "fin512:GLX_FIN_PER_BLOCK=512"; do
+for v in "base:" "gbm_novec:GLX_GATHER_BM=8,256,0" "gbm_seg128:GLX_GATHER_BM=8,128,1" "axs16:GLX_AX_S=16" "fin512:GLX_FIN_PER_BLOCK=512" \
+         "dma268:GLX_AX_VARIANT=92268" "atr38:GLX_ATR_VARIANT=38" "atrS2:GLX_ATR_S=2" "axl512:GLX_AXL_BLOCKS=512"; do
   name=${v%%:*}; envs=${v#*:}
   env $envs timeout -k 10 120 $B --m 1024 --shard-model 8 > $OUT/pg1024_$name.json 2> $OUT/pg1024_$name.err || { echo "pg1024 $name failed"; exit 1; }
 done
