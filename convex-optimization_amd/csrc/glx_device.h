@@ -308,6 +308,59 @@ __device__ inline void ctl_decide(const Ctl& c, const double* out, const double 
   for (int k = 0; k <= 10; ++k) c.rec[k] = rec[k];
 }
 
+// The all-gathered sums of the row-sharded trial, combined by one workgroup in a fixed order (the
+// same bits on every rank): the trial's nranks * nbp workgroup partials strided over 256 threads
+// in (rank, workgroup) order, then the butterfly and the four waves in order; the finalize's sums
+// rank by rank. Writes tr / rt and, with sp.pub.host, the scalar packet with these values in
+// place (read from LDS, not back from memory). Called by every thread of a 256- or 512-thread
+// workgroup (k_trial_split's extra workgroup, round 6 also the publisher of the fused dense pass,
+// kernels_gemm.hip k_ax_lds DRV): threads past 256 only pass the barrier, so the bits are the
+// same whichever kernel combines.
+__device__ inline void shard_combine_block(const ShardPub& sp) {
+  __shared__ double wv[10][4];
+  __shared__ double fin[10];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  double acc[10] = {0.0, 0.0, 0.0, -__builtin_inf(), 0.0, 0.0, 0.0, 0.0, 0.0, 0.0};
+  const bool in = threadIdx.x < 256;
+  if ((sp.mask & 1) && in) {
+    const int np = sp.nranks * sp.nbp;
+    for (int i = threadIdx.x; i < np; i += 256) {
+      const int r = i / sp.nbp, b = i - r * sp.nbp;
+      const double* q = sp.blk + (int64_t)r * sp.chunk + kShardPartOff + b * sp.tv;
+#pragma unroll
+      for (int j = 0; j < 6; ++j)
+        if (j < sp.tv) acc[j] = combine(j == 3 ? OP_MAX : OP_SUM, acc[j], q[j]);
+    }
+  }
+  if ((sp.mask & 2) && in) {
+    const int np = sp.nranks * sp.nbf;
+    for (int i = threadIdx.x; i < np; i += 256) {
+      const int r = i / sp.nbf, b = i - r * sp.nbf;
+      const double* q = sp.blk + (int64_t)r * sp.chunk + kShardPartOff + sp.tv * sp.nbp + b * 4;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc[6 + j] += q[j];
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < 10; ++j)
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1)
+      acc[j] = combine(j == 3 ? OP_MAX : OP_SUM, acc[j], __shfl_xor(acc[j], off));
+  if (lane == 0 && in)
+#pragma unroll
+    for (int j = 0; j < 10; ++j) wv[j][wave] = acc[j];
+  __syncthreads();
+  if (threadIdx.x != 0) return;
+  for (int j = 0; j < 10; ++j) fin[j] = waves_combine<4>(j == 3 ? OP_MAX : OP_SUM, wv[j]);
+  if (sp.mask & 1)
+    for (int j = 0; j < sp.tv; ++j) sp.tr[j] = fin[j];
+  if (sp.mask & 2)
+    for (int j = 0; j < 4; ++j) sp.rt[j] = fin[6 + j];
+  if (sp.pub.host != nullptr)
+    publish_packet(sp.pub.s, sp.pub.ns, sp.pub.host, sp.pub.host_seq, sp.pub.seq, fin, sp.tr_off,
+                   (sp.mask & 1) ? sp.tv : 0, fin + 6, sp.rt_off, (sp.mask & 2) ? 4 : 0);
+}
+
 // ------------------------------------------------------------------------------------------
 // Split-candidate column bitmaps (round 5). Behind the n per-row column masks zf[k] of e (bit c =
 // e[k][c] != 0) the trial kernels also write, per column c, a bitmap of the rows whose mask has

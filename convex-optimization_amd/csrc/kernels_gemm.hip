@@ -203,15 +203,97 @@ __device__ inline void lds_put(T* dst, typename MF<T>::vec_t v) {
   }
 }
 
-template <typename T, int MT, int NT, int NSRC, int PF, int VPL, int WAVES>
-__global__ __launch_bounds__(64 * WAVES) void k_ax_lds(const T* __restrict__ A,
+// One (row block, column) item of the split-candidate A e inside the fused dense pass (AxDerive
+// with ggx > 0): k_at_gather_bm's work (kernels_gather.hip) by a 512-thread workgroup, one output
+// row per thread — column c's ascending list of flagged rows built in LDS from its bitmap words,
+// then At's rows walked in that order with the same arithmetic, so A e has the same bits — with the
+// words read from the all-gathered sums chunks (d.blk) instead of zf.
+template <typename T, int L, int NTHR>
+__device__ inline void drv_gather_item(const AxDerive& d, int64_t m, int64_t n, int item) {
+  constexpr int SEGW = 256, NW = NTHR / 64, U = 8;
+  static_assert(NTHR >= SEGW, "one bitmap word per thread and segment");
+  __shared__ unsigned short lst[64 * SEGW];
+  __shared__ unsigned wsum[NW];
+  const T* At = static_cast<const T*>(d.At);
+  const T* E = static_cast<const T*>(d.E);
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int rb = item % d.ggx, c = item / d.ggx;
+  const int64_t nw = n / 64;             // n % 64 == 0 and srows % 64 == 0 (solver.cpp sgat_)
+  const int64_t wpr = d.srows / 64;      // bitmap words per rank
+  const int64_t r = (int64_t)rb * NTHR + tid;
+  const int64_t rr = r < m ? r : m - 1;
+  T acc = T(0);
+  for (int64_t w0 = 0; w0 < nw; w0 += SEGW) {
+    const int64_t w = w0 + tid;
+    uint64_t bits = 0;
+    if (tid < SEGW && w < nw) {
+      const int64_t rk = w / wpr, lw = w - rk * wpr;
+      const unsigned* zr = reinterpret_cast<const unsigned*>(d.blk + rk * d.bstride + d.moff);
+      const unsigned short* bm = reinterpret_cast<const unsigned short*>(zr + d.srows) + (int64_t)c * (d.srows / 16);
+      bits = reinterpret_cast<const uint64_t*>(bm)[lw];
+    }
+    const unsigned cnt = (unsigned)__builtin_popcountll(bits);
+    unsigned inc = cnt;
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+      const unsigned v = __shfl_up(inc, off);
+      if (lane >= off) inc += v;
+    }
+    if (lane == 63) wsum[wave] = inc;
+    __syncthreads();
+    unsigned pos = inc - cnt, total = 0;
+#pragma unroll
+    for (int q = 0; q < NW; ++q) {
+      if (q < wave) pos += wsum[q];
+      total += wsum[q];
+    }
+    while (bits != 0) {
+      const int j = __builtin_ctzll(bits);
+      bits &= bits - 1;
+      lst[pos++] = (unsigned short)((w - w0) * 64 + j);   // row - 64 w0
+    }
+    __syncthreads();
+    const int tot = (int)total;
+    const int64_t kb = w0 * 64;
+    int idx = 0;
+    for (; idx + U <= tot; idx += U) {
+      T a[U], ev[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int64_t k = kb + lst[idx + u];
+        a[u] = __builtin_nontemporal_load(At + k * m + rr);
+        ev[u] = E[k * L + c];
+      }
+#pragma unroll
+      for (int u = 0; u < U; ++u) acc = acc + a[u] * ev[u];
+    }
+    for (; idx < tot; ++idx) {
+      const int64_t k = kb + lst[idx];
+      acc = acc + __builtin_nontemporal_load(At + k * m + rr) * E[k * L + c];
+    }
+    __syncthreads();   // lst and wsum are rewritten by the next segment
+  }
+  if (r < m) static_cast<T*>(d.Pe)[r * L + c] = acc;
+}
+
+//
+// DRV (round 6, the row-sharded ProxGD trial; solver.cpp iter_proxgd_shard): X0 is the all-gathered
+// p, and the pass derives the trial's replicated half itself (launch_trial_split's work with e = p
+// and no z): each staged vector is thresholded (|p| < thres -> 0, k_trial_split's comparison) on
+// its way into LDS, so the MFMAs read p_thr; row block bx owns the chunks c with c % gx == bx and
+// stores their p_thr vectors, row masks of e (zf) and column bitmap words (one 16-row group per
+// chunk, emitted one barrier after the masks went to LDS); the publisher workgroup combines the
+// all-gathered sums (shard_combine_block) and publishes the packet with them. Saves the k_trial_split
+// launch (5.6-6.5 us at the 1024-row shard) between the all-gather and this pass.
+template <typename T, int MT, int NT, int NSRC, int PF, int VPL, int WAVES, bool DRV>
+__device__ __forceinline__ void ax_lds_body(const T* __restrict__ A,
                                                       const T* __restrict__ X0,
                                                       const T* __restrict__ X1,
                                                       const T* __restrict__ X2,
                                                       T* __restrict__ P, int64_t m, int64_t n,
                                                       int64_t chunks, int S, int gx, int xmap,
                                                       const int* __restrict__ gate, int epoch,
-                                                      Pub pub) {
+                                                      Pub pub, AxDerive drv) {
   typedef MF<T> M;
   typedef typename M::vec_t V;
   typedef typename M::acc_t C;
@@ -229,15 +311,27 @@ __global__ __launch_bounds__(64 * WAVES) void k_ax_lds(const T* __restrict__ A,
   constexpr bool XFULL = (XV % NTHR) == 0; // every thread moves XPT vectors: no predicate
   constexpr int VPR = L / E;              // vectors per X row
   static_assert(PF >= 2, "X(c+1) must sit in another ring slot than X(c + PF)");
+  static_assert(!DRV || (NSRC == 1 && CK == 16 && XPT == 1 && XV % 64 == 0 && VPR <= 64),
+                "the derive: one source, one 16-row group per chunk, whole waves stage it");
   __shared__ __attribute__((aligned(16))) T xs[2][XCH];
+  __shared__ unsigned dmsk[DRV ? 2 : 1][16];   // DRV: row masks of the staged chunk, per slot
   // pub.host: workgroup 0 hands the scalar packet to the host (no reduction to join here) while
   // the others run; with a short kernel in front (the N > 1 trial) a packet carried by THAT
   // kernel held up this launch by ~4 us (profiles/r1_tuning/small_kernels/ax_publisher.log)
   if (pub.host != nullptr && blockIdx.x == 0) {
-    if (threadIdx.x == 0)
+    if constexpr (DRV) {
+      shard_combine_block(drv.sp);   // drv.sp.pub == pub
+    } else if (threadIdx.x == 0) {
       publish_packet(pub.s, pub.ns, pub.host, pub.host_seq, pub.seq, pub.s2, pub.off2, pub.n2,
                      pub.s3, pub.off3, pub.n3);
+    }
     return;
+  }
+  if constexpr (DRV) {
+    if (drv.ggx > 0 && (int)blockIdx.x >= drv.gat0) {   // the A e workgroups (block-uniform)
+      drv_gather_item<T, L, 64 * WAVES>(drv, m, n, (int)blockIdx.x - drv.gat0);
+      return;
+    }
   }
   if (!gate_live(gate, epoch)) return;
   int bx, by;
@@ -306,10 +400,49 @@ __global__ __launch_bounds__(64 * WAVES) void k_ax_lds(const T* __restrict__ A,
       for (int v = 0; v < VPL; ++v)
         dst[mt][v] = load_vec<T, false>(ap[mt] + off * CK + v * E);
   };
-  auto put_x = [&](int slot, const V (&src)[XPT]) {
+  // off: the walk offset of the chunk (DRV: which chunk it is)
+  auto put_x = [&](int slot, V (&src)[XPT], int64_t off) {
+    if constexpr (DRV) {
+      const int64_t kc = kch(off);
+      const bool own = ((cb + kc) % gx) == bx;   // block-uniform
+      const T thres = (T)drv.thres;
+      V v = src[0];
+      unsigned mk = 0;
+      const int c0 = (threadIdx.x % VPR) * E;
+#pragma unroll
+      for (int e = 0; e < E; ++e) {
+        const bool small = tabs(v[e]) < thres;
+        if (small && v[e] != T(0)) mk |= 1u << (c0 + e);
+        v[e] = small ? T(0) : v[e];
+      }
+      src[0] = v;
+      const unsigned rowm = row_or<VPR>(mk);
+      if (own && xon[0]) {
+        const int64_t eo = (xg[0] - X0) + kc * CK * L;
+        *reinterpret_cast<V*>(static_cast<T*>(drv.pthr) + eo) = v;
+        if (drv.zf != nullptr && (threadIdx.x % VPR) == 0) {
+          const int k = (int)threadIdx.x / VPR;   // row within the chunk
+          drv.zf[(cb + kc) * CK + k] = rowm;
+          dmsk[slot][k] = rowm;
+        }
+      }
+    }
 #pragma unroll
     for (int j = 0; j < XPT; ++j)
       if (XFULL || xon[j]) lds_put<T, W16>(&xs[slot][xo[j]], src[j]);
+  };
+  // DRV: the column bitmap words of chunk c (its masks went to dmsk[c & 1] one barrier ago)
+  auto emit_bits = [&](int64_t c) {
+    if constexpr (DRV) {
+      const int64_t kc = kch(c);
+      if (drv.zf != nullptr && ((cb + kc) % gx) == bx && (int)threadIdx.x < L) {
+        unsigned b = 0;
+#pragma unroll
+        for (int j = 0; j < 16; ++j) b |= ((dmsk[c & 1][j] >> threadIdx.x) & 1u) << j;
+        zf_bitmaps(drv.zf, drv.n)[(int64_t)threadIdx.x * (zf_npad(drv.n) / 16) + (cb + kc)] =
+            (unsigned short)b;
+      }
+    }
   };
   // X(c) from LDS slot into registers
   auto read_x = [&](int slot, T (&xv)[NC][EL]) {
@@ -340,7 +473,7 @@ __global__ __launch_bounds__(64 * WAVES) void k_ax_lds(const T* __restrict__ A,
     load_x(xr[p], p);
     load_a(a[p], p);
   }
-  put_x(0, xr[0]);                 // chunk 0 -> slot 0
+  put_x(0, xr[0], 0);              // chunk 0 -> slot 0
   __syncthreads();
 
   // Main loop: PF chunks per trip, no predicates. Registers are consumed in place: a tile's
@@ -352,7 +485,8 @@ __global__ __launch_bounds__(64 * WAVES) void k_ax_lds(const T* __restrict__ A,
     for (int p = 0; p < PF; ++p) {
       const int64_t c = c0 + p;
       const int slot = (int)(c & 1);
-      put_x(slot ^ 1, xr[(p + 1) % PF]);   // X(c+1), loaded PF-1 chunks ago
+      emit_bits(c);
+      put_x(slot ^ 1, xr[(p + 1) % PF], c + 1);   // X(c+1), loaded PF-1 chunks ago
       load_x(xr[p], c + PF);       // xr[p] (X(c)) has been in LDS since chunk c-1
       T xv[NC][EL];
       read_x(slot, xv);
@@ -372,7 +506,8 @@ __global__ __launch_bounds__(64 * WAVES) void k_ax_lds(const T* __restrict__ A,
     const int64_t c = c0 + p;
     if (c < nch) {
       const int slot = (int)(c & 1);
-      if (c + 1 < nch) put_x(slot ^ 1, xr[(p + 1) % PF]);
+      emit_bits(c);
+      if (c + 1 < nch) put_x(slot ^ 1, xr[(p + 1) % PF], c + 1);
       T xv[NC][EL];
       read_x(slot, xv);
 #pragma unroll
@@ -397,6 +532,25 @@ __global__ __launch_bounds__(64 * WAVES) void k_ax_lds(const T* __restrict__ A,
   }
 }
 
+#define GLX_AX_LDS_ARGS                                                                          \
+  const T* __restrict__ A, const T* __restrict__ X0, const T* __restrict__ X1,                 \
+      const T* __restrict__ X2, T* __restrict__ P, int64_t m, int64_t n, int64_t chunks, int S, \
+      int gx, int xmap, const int* __restrict__ gate, int epoch, Pub pub, AxDerive drv
+template <typename T, int MT, int NT, int NSRC, int PF, int VPL, int WAVES>
+__global__ __launch_bounds__(64 * WAVES) void k_ax_lds(GLX_AX_LDS_ARGS) {
+  ax_lds_body<T, MT, NT, NSRC, PF, VPL, WAVES, false>(A, X0, X1, X2, P, m, n, chunks, S, gx, xmap, gate,
+                                                     epoch, pub, drv);
+}
+// the derive form: held to 128 VGPRs (4 waves per SIMD, two 8-wave workgroups per CU) so that its
+// A e workgroups find a slot beside the dense ones (at 133 VGPRs one workgroup per CU fits and
+// the gather waits for the dense workgroups to drain)
+template <typename T, int MT, int NT, int NSRC, int PF, int VPL, int WAVES>
+__global__ __launch_bounds__(64 * WAVES) __attribute__((amdgpu_waves_per_eu(4))) void k_ax_lds_drv(
+    GLX_AX_LDS_ARGS) {
+  ax_lds_body<T, MT, NT, NSRC, PF, VPL, WAVES, true>(A, X0, X1, X2, P, m, n, chunks, S, gx, xmap, gate,
+                                                    epoch, pub, drv);
+}
+#undef GLX_AX_LDS_ARGS
 
 template <typename T, int LB, int RW, bool VEC, int NSRC>
 __global__ __launch_bounds__(256) void k_ax_valu(const T* __restrict__ A, const T* __restrict__ X0,
@@ -797,17 +951,26 @@ static void ax_mfma_go(const GemmPlan& p, const T* A, const T* const* X, T* P, c
                      epoch);
 }
 
-template <typename T, int NT, int NSRC, int MT, int PF, int VPL, int WAVES>
+template <typename T, int NT, int NSRC, int MT, int PF, int VPL, int WAVES, bool DRV = false>
 static void ax_lds_go(const GemmPlan& p, int S, const T* A, const T* const* X, T* P,
-                      const int* gate, int epoch, hipStream_t st, Pub pub = Pub{}) {
+                      const int* gate, int epoch, hipStream_t st, Pub pub = Pub{},
+                      const AxDerive& drv = AxDerive{}) {
   constexpr int E = 16 / sizeof(T);
   const int gx = (int)cdiv(p.m, 16 * MT * WAVES);
   const int xmap = ax_xmap_flags(p, S);
-  const dim3 grid((unsigned)ax_grid(xmap, gx, S) + (pub.host ? 1u : 0u));
-  static const size_t pad = lds_pad(k_ax_lds<T, MT, NT, NSRC, PF, VPL, WAVES>, "GLX_AX_LDS_PAD");
-  glx_launch((k_ax_lds<T, MT, NT, NSRC, PF, VPL, WAVES>), grid,
-                     dim3(64 * WAVES), pad, st, A, X[0], X[1], X[2], P, p.m, p.n,
-                     p.n / (4 * VPL * E), S, gx, xmap, gate, epoch, pub);
+  const unsigned dense = (unsigned)ax_grid(xmap, gx, S) + (pub.host ? 1u : 0u);
+  AxDerive dv = drv;
+  dv.gat0 = (int)dense;
+  const dim3 grid(dense + (DRV ? (unsigned)(dv.ggx * p.l) : 0u));
+  if constexpr (DRV) {
+    static const size_t pad = lds_pad(k_ax_lds_drv<T, MT, NT, NSRC, PF, VPL, WAVES>, "GLX_AX_LDS_PAD");
+    glx_launch((k_ax_lds_drv<T, MT, NT, NSRC, PF, VPL, WAVES>), grid, dim3(64 * WAVES), pad, st, A, X[0],
+               X[1], X[2], P, p.m, p.n, p.n / (4 * VPL * E), S, gx, xmap, gate, epoch, pub, dv);
+  } else {
+    static const size_t pad = lds_pad(k_ax_lds<T, MT, NT, NSRC, PF, VPL, WAVES>, "GLX_AX_LDS_PAD");
+    glx_launch((k_ax_lds<T, MT, NT, NSRC, PF, VPL, WAVES>), grid, dim3(64 * WAVES), pad, st, A, X[0], X[1],
+               X[2], P, p.m, p.n, p.n / (4 * VPL * E), S, gx, xmap, gate, epoch, pub, dv);
+  }
 }
 
 // the planner's kind-5 tiles (lds_plan): 52228 (f64 batched / one RHS in the Infinity Cache),
@@ -878,6 +1041,33 @@ void launch_ax(const GemmPlan& p, int nsrc, const T* A, const T* const* X, T* P,
   if (p.l == 16) ax_mfma_nt<T, 1>(p, nsrc, A, X, P, gate, epoch, st, pub);
   else ax_mfma_nt<T, 2>(p, nsrc, A, X, P, gate, epoch, st, pub);
 }
+
+bool ax_derive_ok(const GemmPlan& p, int esize) {
+  return esize == 8 && p.ax_kind == 5 && p.axb_code[1] == 51328 && p.l == 32 && p.n % 16 == 0;
+}
+
+template <typename T>
+bool launch_ax_derive(const GemmPlan& p, const T* A, const T* Xp, T* P, hipStream_t st, Pub pub,
+                      const AxDerive& d) {
+  if constexpr (sizeof(T) != 8) {
+    return false;
+  } else {
+    if (!ax_derive_ok(p, 8) || pub.host == nullptr || d.pthr == nullptr) return false;
+    if (d.ggx > 0 && (p.n % 64 != 0 || d.srows % 64 != 0 || d.srows <= 0 || d.blk == nullptr ||
+                      (int64_t)d.ggx * kDrvGatRows < p.m || p.n > 65536))
+      return false;
+    AxDerive dd = d;
+    dd.sp.pub = pub;
+    dd.n = p.n;
+    const T* xs[3] = {Xp, nullptr, nullptr};
+    ax_lds_go<T, 2, 1, 1, 3, 2, 8, true>(p, p.axb_S[1], A, xs, P, nullptr, 0, st, pub, dd);
+    return true;
+  }
+}
+template bool launch_ax_derive<double>(const GemmPlan&, const double*, const double*, double*, hipStream_t, Pub,
+                                       const AxDerive&);
+template bool launch_ax_derive<float>(const GemmPlan&, const float*, const float*, float*, hipStream_t, Pub,
+                                      const AxDerive&);
 
 template void launch_ax<double>(const GemmPlan&, int, const double*, const double* const*, double*, const int*, int, hipStream_t, Pub);
 template void launch_ax<float>(const GemmPlan&, int, const float*, const float* const*, float*, const int*, int, hipStream_t, Pub);

@@ -98,6 +98,11 @@ constexpr int kMaxGSets = kCtlMaxBatch / 2 + 2;
 // up to kMaxShardRanks ranks
 constexpr int kShardChunkMax = kShardPartOff + (6 + 4) * kMaxBlocks;
 constexpr int kMaxShardRanks = 64;
+// the chunks' doubles: the sums of up to kMaxShardRanks ranks, plus (round 6, sgat_) every rank's
+// row masks and column bitmaps of e for its rows (n / 2 + l n / 64 doubles over all ranks)
+static int64_t shard_blk_doubles(int64_t n, int64_t l) {
+  return (int64_t)kShardChunkMax * kMaxShardRanks + n / 2 + l * n / 64 + 64;
+}
 
 // device-controlled batches' window: opts.dc_window (> 0: that window, < 0: off), else
 // GLX_DC_BATCH, else the measured default (0 = the host decides every iteration): kDcWindow for
@@ -371,7 +376,7 @@ class Session : public SessionBase {
     double* tpart = static_cast<double*>(c.take(sizeof(double) * 2 * 6 * kMaxBlocks));
     double* fpart = static_cast<double*>(c.take(sizeof(double) * 4 * kMaxBlocks));
     double* sblk = P.comm != nullptr && (P.method == GLX_PROXGD || P.method == GLX_FPROXGD)
-                       ? static_cast<double*>(c.take(sizeof(double) * kShardChunkMax * kMaxShardRanks))
+                       ? static_cast<double*>(c.take(sizeof(double) * shard_blk_doubles(P.n, P.l)))
                        : nullptr;
     double* fh = static_cast<double*>(c.take(sizeof(double) * (fh_cap + 1)));
     double* sp100 = static_cast<double*>(c.take(sizeof(double) * (fh_cap / 100 + 2)));
@@ -612,6 +617,18 @@ class Session : public SessionBase {
         // A e from the bitmap / list gathers reads e only where its masks are set, where e = p:
         // the gathered p serves as e and z is not re-derived (the row form reads whole rows)
         zskip_ = emode_ && gform_ != 1;
+        // Round 6: that derive (k_trial_split) fused into the next trial's dense pass where the
+        // plan's one-source tile takes it (k_ax_lds DRV: the 8-wave shard tile, f64, l = 32) and
+        // the packet rides the pass (iter_proxgd_shard's speculative step). GLX_SHARD_DERIVE=0: off.
+        sderive_ = zskip_ && smode_ == 1 && !egat_ && gform_ != 2 && ax_derive_ok(plan_, (int)sizeof(T)) &&
+                   !env_is("GLX_SHARD_DERIVE", "0");
+        // ... and A e too (AxDerive::ggx): k_prox_pgd writes the masks and bitmaps of its rows into
+        // the rank's sums chunk (behind the partials, moff_), all-gathered with them, and the gather
+        // runs as extra workgroups of the dense pass. GLX_SHARD_GAT=0: the separate k_at_gather_bm.
+        sgat_ = sderive_ && gform_ == 0 && n_ % 64 == 0 && srows_ % 64 == 0 && n_ <= 65536 &&
+                !env_is("GLX_SHARD_GAT", "0");
+        moff_ = schunk_;
+        if (sgat_) schunk_ += srows_ / 2 + l_ * srows_ / 64;
       } else {
         shard_model_ = false;
       }
@@ -640,7 +657,7 @@ class Session : public SessionBase {
     // the column bitmaps' words no trial visits (rows in [ceil16(n), ceil64(n)), the upper half
     // of a narrow panel's last u64) must read as 0 (glx_device.h zf_bitmaps)
     GLX_HIP(hipMemsetAsync(zf_, 0, zf_bytes(P.n), st_));
-    if (blk_) GLX_HIP(hipMemsetAsync(blk_, 0, sizeof(double) * kShardChunkMax * kMaxShardRanks, st_));
+    if (blk_) GLX_HIP(hipMemsetAsync(blk_, 0, sizeof(double) * shard_blk_doubles(n_, l_), st_));
     mus_[0] = 100 * P.mu0;
     mus_[1] = 10 * P.mu0;
     mus_[2] = P.mu0;
@@ -787,7 +804,7 @@ class Session : public SessionBase {
     else if (shard_)
       s += "; rows=sharded x" + std::to_string(sranks_) + (shard_model_ ? " (timing model)" : "") +
            " (reduce-scatter of A^T r, k_prox_pgd on n/" + std::to_string(sranks_) +
-           " rows, all-gather of p, k_trial_split)";
+           " rows, all-gather of p, " + (sderive_ ? (sgat_ ? "derive and A e in the dense pass" : "derive in the dense pass") : "k_trial_split") + ")";
     s += "; dc_window=" + std::to_string(dc_window_);
     return s;
   }
@@ -987,7 +1004,9 @@ class Session : public SessionBase {
   // pb: the dense launch carries that scalar packet.
   // Round 5 (rows_form_): A e is the A^T R panel over the flagged rows of At (k_at_rows: gsplit_
   // slabs, each workgroup compacts its K range's row flags itself), so no column lists.
-  void cand_ax(const T* const* xs, Pub pb = Pub{}) {
+  // dv (row-sharded ProxGD, sderive_): the dense pass reads p (xs[2]) and derives p_thr into xs[1]
+  // itself, with the masks and bitmaps the gather reads (k_ax_lds DRV)
+  void cand_ax(const T* const* xs, Pub pb = Pub{}, const AxDerive* dv = nullptr) {
     const T* xd[3] = {xs[1], nullptr, nullptr};
     if (egat_) {   // round 6: A p and A e in one pass (S slabs each: A e at Pp_, A p behind)
       EGat eg;
@@ -1010,9 +1029,20 @@ class Session : public SessionBase {
       check_launch();
     }
     hipEvent_t e0 = prof_begin(0);
-    launch_ax<T>(plan_, 1, A_, xd, Pp_ + (size_t)gsplit_ * ml_, dc_gate_, 0, st_, pb);
+    if (dv != nullptr) {
+      if (pb.s2 != nullptr || pb.dpart[0] != nullptr || pb.dpart[1] != nullptr || dc_gate_ != nullptr ||
+          !launch_ax_derive<T>(plan_, A_, xs[2], Pp_ + (size_t)gsplit_ * ml_, st_, pb, *dv))
+        throw Error{GLX_E_STATE, "row-sharded derive: the dense pass does not take it"};
+    } else {
+      launch_ax<T>(plan_, 1, A_, xd, Pp_ + (size_t)gsplit_ * ml_, dc_gate_, 0, st_, pb);
+    }
     check_launch();
     prof_end(0, e0);
+    if (dv != nullptr && dv->ggx > 0) {   // A e ran inside the dense pass
+      ++ax_calls_;
+      ax_cols_ += 1;
+      return;
+    }
     hipEvent_t e2 = prof_begin(2);
     if (gform_ == 1) launch_at_rows<T>(At_, xs[0], zf_, m_, n_, l_, Pp_, glists_, st_, dc_gate_);
     else if (gform_ == 2) launch_at_gather<T>(At_, xs[0], m_, n_, l_, Pp_, glists_, st_, dc_gate_);
@@ -1499,8 +1529,10 @@ class Session : public SessionBase {
     Red rd = red_to(scal_ + S_TR);
     rd.part = blk_own() + kShardPartOff;
     rd.parts_only = 1;
+    // sgat_: the masks and bitmaps of e for these rows into the chunk (the third output is then e)
+    unsigned* czf = sgat_ ? reinterpret_cast<unsigned*>(blk_own() + moff_) : nullptr;
     launch_prox_pgd<T>(xt + o, G + o, 1, nullptr, X_[op] + o, X_[opt] + o, X_[oz] + o, srows_, l_, t,
-                       mu_, O_.thres, rd, st_, Pub{}, nullptr);
+                       mu_, O_.thres, rd, st_, Pub{}, czf);
     check_launch();
   }
   // one RCCL group: p's rows (op >= 0) and every rank's chunk of sums
@@ -1601,14 +1633,35 @@ class Session : public SessionBase {
           // dense pass as its publisher workgroup: a workgroup of the 8 MiB-writing k_trial_split
           // that stores to host memory stretched that kernel from 5.6 to 17.8 us (its end-of-
           // kernel release), a separate k_publish costs ~4.5 us (profiles/r5_shard/)
-          shard_derive(ipt_, if1_, if2_, iz_, O_.alpha0, shard_pub(3, ot, nullptr));
-          const T* sx[3] = {zskip_ ? X_[if1_] : X_[iz_], X_[if2_], X_[if1_]};
           const bool carry = spin_readback_ && attach_ok_ && ax_pub_ok(plan_, smode_ == 1 ? 1 : nsrc);
+          const bool fused = carry && sderive_;   // round 6: the derive inside the dense pass
+          if (!fused) shard_derive(ipt_, if1_, if2_, iz_, O_.alpha0, shard_pub(3, ot, nullptr));
+          const T* sx[3] = {zskip_ ? X_[if1_] : X_[iz_], X_[if2_], X_[if1_]};
           Pub pb;
           if (carry) pb = make_pub(nullptr, &seq);
           else seq = post_readback();
-          if (smode_ == 1) cand_ax(sx, pb);
-          else spec_ax(nsrc, sx, pb);
+          if (fused) {
+            AxDerive dv;
+            dv.pthr = X_[if2_];
+            dv.zf = sgat_ ? nullptr : ezf();
+            dv.thres = O_.thres;
+            dv.sp = shard_pub(3, ot, nullptr);
+            if (sgat_) {
+              dv.ggx = (int)((m_ + kDrvGatRows - 1) / kDrvGatRows);
+              dv.At = At_;
+              dv.E = sx[0];
+              dv.Pe = Pp_;
+              dv.blk = blk_;
+              dv.bstride = shard_model_ ? 0 : schunk_;
+              dv.moff = moff_;
+              dv.srows = srows_;
+            }
+            cand_ax(sx, pb, &dv);
+          } else if (smode_ == 1) {
+            cand_ax(sx, pb);
+          } else {
+            spec_ax(nsrc, sx, pb);
+          }
           ax_queued_ = true;
           spec_trial = true;
         } else {
@@ -2511,6 +2564,9 @@ class Session : public SessionBase {
   int nbp_ = 0, nbf_ = 0;      // k_prox_pgd's workgroups on srows_ rows, the trial finalize's
   int schunk_ = 0;             // doubles per rank's chunk
   bool zskip_ = false;         // the gathered p serves as e (bitmap / list gathers)
+  bool sderive_ = false;       // round 6: the speculative derive inside the dense pass (AxDerive)
+  bool sgat_ = false;          // ... with the A e gather as its extra workgroups (chunk masks)
+  int64_t moff_ = 0;           // doubles into a rank's chunk: its row masks + column bitmaps (sgat_)
   double* blk_ = nullptr;      // kMaxShardRanks chunks of sums (kShardChunkMax doubles each)
   // deferred reductions (defer_, single GPU): the trial's and the finalize's pending partials
   bool defer_ = false;

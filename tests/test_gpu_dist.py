@@ -200,14 +200,28 @@ def test_row_sharded_other_modes(tmp_path, extra_opts):
     assert "rows=sharded x2" in r0["plan"]
 
 
-def test_row_sharded_split_candidate(tmp_path, monkeypatch):
-    """The split-candidate trial under the row-sharded schedule: the masks and bitmaps of e are
-    re-derived from the gathered p by k_trial_split and the bitmap gather reads e from them."""
+@pytest.mark.parametrize("extra", [(), ("--alpha-scale", "2.5")])
+def test_row_sharded_split_candidate(tmp_path, monkeypatch, extra):
+    """The split-candidate trial under the row-sharded schedule: p_thr, the masks and bitmaps of e
+    are re-derived from the gathered p and the bitmap gather reads e from them. Round 6: in the
+    speculative steady state the derive runs inside the next trial's dense pass (k_ax_lds DRV; its
+    publisher workgroup combines the gathered sums) with A e as its extra workgroups (bitmaps from the
+    all-gathered sums chunks), elsewhere in k_trial_split; GLX_SHARD_GAT=0 (the separate gather) and
+    GLX_SHARD_DERIVE=0 (k_trial_split throughout) give the same bits. alpha0 x 2.5: rejected first trials (the
+    host-path trial, then the fused form again once speculation resumes)."""
     monkeypatch.setenv("GLX_SPLIT_CAND", "1")
     v = run_sharded(tmp_path, 2, "gl_ProxGD_primal", 512, 1024, 32, maxit=25,
-                    extra=("--shard-rows", "1"))
+                    extra=("--shard-rows", "1") + tuple(extra))
     r0 = _check_identical_and_oracle(v, 2)
     assert "gather k_at_gather_bm" in r0["plan"] and "rows=sharded x2" in r0["plan"], r0["plan"]
+    assert "derive and A e in the dense pass" in r0["plan"], r0["plan"]
+    for env, name in (("GLX_SHARD_GAT", "derive in the dense pass"), ("GLX_SHARD_DERIVE", "k_trial_split")):
+        monkeypatch.setenv(env, "0")
+        w = run_sharded(tmp_path, 2, "gl_ProxGD_primal", 512, 1024, 32, maxit=25,
+                        extra=("--shard-rows", "1") + tuple(extra))
+        w0 = w["ranks"][0]
+        assert name in w0["plan"], w0["plan"]
+        assert w0["k"] == r0["k"] and w0["x_sha"] == r0["x_sha"] and w0["f_hist"] == r0["f_hist"]
 
 
 def test_row_sharded_matches_allreduce_schedule(tmp_path):
@@ -262,6 +276,7 @@ def test_row_sharded_ns_world8_whole_solve(tmp_path):
     r0 = _check_identical_and_oracle(v, 8)
     assert r0["k"] == 2680
     assert "rows=sharded x8" in r0["plan"] and "gather k_at_gather_bm" in r0["plan"], r0["plan"]
+    assert "derive and A e in the dense pass" in r0["plan"], r0["plan"]
     assert v["x_maxdiff"] <= 1e-6 * v["x_scale"]
 
 
