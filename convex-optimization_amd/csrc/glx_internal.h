@@ -392,25 +392,21 @@ void launch_trial_split(const T* p, const T* xt, T* pthr, T* z, unsigned* zf, in
 template <typename T>
 void launch_fista_split(const T* xc, const T* xk, T* vnext, T* ynext, int64_t nl, double thres,
                         double theta, double theta_next, const ShardPub& sp, hipStream_t st);
-// Round 6: the ProxGD half above (emode, no z) fused into the split-candidate dense pass A p_thr
-// (kernels_gemm.hip k_ax_lds DRV, the 8-wave shard tile 51328 at l = 32, f64): the pass reads the
-// gathered p, thresholds it on the way into LDS, stores p_thr, zf's row masks and column bitmaps
-// of the chunks its row block owns, and its publisher workgroup combines sp's sums and publishes
-// the packet (pub, required). n is set by the launcher. False: the plan does not take it.
-// With ggx > 0 the launch also carries the trial's A e (k_at_gather_bm's work and bits) as
-// ggx * l extra workgroups behind the dense ones, running beside the MFMA work: column c's row
-// list from the bitmap words every rank's k_prox_pgd wrote for its srows rows into its sums chunk
-// (blk + rank * bstride + moff: srows row masks, then the column bitmaps; all-gathered with the
-// sums, so ready before the pass starts; bstride 0 in the one-GPU timing model: rank 0's words
-// for every rank), then the walk over At's rows into the slab Pe; zf is then NULL.
+// Round 6: the ProxGD half above (emode, e = p, no z) fused into the split-candidate dense pass
+// A p_thr (kernels_gemm.hip k_ax_lds_drv, the 8-wave shard tile 51328 at l = 32, f64): the pass
+// reads the gathered p and thresholds it on the way into LDS; nd extra workgroups write p_thr,
+// ggx * l more compute the trial's A e (k_at_gather_bm's work and bits) into the slab Pe beside
+// the MFMA work — column c's row list from the bitmap words every rank's k_prox_pgd wrote for its
+// srows rows into its sums chunk (blk + rank * bstride + moff: srows row masks, then the column
+// bitmaps; all-gathered with the sums, so ready before the pass starts; bstride 0 in the one-GPU
+// timing model: rank 0's words for every rank); the publisher workgroup combines sp's sums and
+// publishes the packet (pub, required). False: the plan or the shape does not take it.
 struct AxDerive {
   void* pthr = nullptr;
-  unsigned* zf = nullptr;
   double thres = 0.0;
-  int64_t n = 0;
   ShardPub sp{};
-  int ggx = 0;                   // gather row blocks (512 rows each); 0: no gather workgroups
-  int gat0 = 0;                  // set by the launcher: the first gather workgroup
+  int ggx = 0;                   // gather row blocks (kDrvGatRows rows each)
+  int nd = 0, thr0 = 0, gat0 = 0;   // set by the launcher: p_thr workgroups, first p_thr / A e one
   const void* At = nullptr;
   const void* E = nullptr;       // e where its masks are set (the gathered p)
   void* Pe = nullptr;
@@ -418,8 +414,10 @@ struct AxDerive {
   int64_t bstride = 0, moff = 0, srows = 0;
 };
 bool ax_derive_ok(const GemmPlan& p, int esize);
-// rows of A per gather workgroup of the fused dense pass (AxDerive::ggx = ceil(m / this))
+// rows of A per gather workgroup of the fused dense pass (AxDerive::ggx = ceil(m / this)), and
+// its p_thr workgroups
 constexpr int kDrvGatRows = 512;
+constexpr int kDrvThrBlocks = 64;
 template <typename T>
 bool launch_ax_derive(const GemmPlan& p, const T* A, const T* Xp, T* P, hipStream_t st, Pub pub,
                       const AxDerive& d);

@@ -203,6 +203,24 @@ __device__ inline void lds_put(T* dst, typename MF<T>::vec_t v) {
   }
 }
 
+// p_thr = p with |p| < thres zeroed over the n l elements (k_trial_split's comparison), 16-B
+// vectors strided over the AxDerive::nd workgroups of the fused dense pass
+template <typename T, int NTHR>
+__device__ inline void drv_thr_item(const T* __restrict__ p, const AxDerive& d, int64_t nl, int item) {
+  typedef typename MF<T>::vec_t V;
+  constexpr int E = MF<T>::E;
+  const T thres = (T)d.thres;
+  const V* src = reinterpret_cast<const V*>(p);
+  V* dst = reinterpret_cast<V*>(static_cast<T*>(d.pthr));
+  const int64_t nv = nl / E;
+  for (int64_t i = (int64_t)item * NTHR + threadIdx.x; i < nv; i += (int64_t)d.nd * NTHR) {
+    V v = src[i];
+#pragma unroll
+    for (int e = 0; e < E; ++e) v[e] = tabs(v[e]) < thres ? T(0) : v[e];
+    dst[i] = v;
+  }
+}
+
 // One (row block, column) item of the split-candidate A e inside the fused dense pass (AxDerive
 // with ggx > 0): k_at_gather_bm's work (kernels_gather.hip) by a 512-thread workgroup, one output
 // row per thread — column c's ascending list of flagged rows built in LDS from its bitmap words,
@@ -218,7 +236,7 @@ __device__ inline void drv_gather_item(const AxDerive& d, int64_t m, int64_t n, 
   const T* E = static_cast<const T*>(d.E);
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int rb = item % d.ggx, c = item / d.ggx;
-  const int64_t nw = n / 64;             // n % 64 == 0 and srows % 64 == 0 (solver.cpp sgat_)
+  const int64_t nw = n / 64;             // n % 64 == 0 and srows % 64 == 0 (solver.cpp sderive_)
   const int64_t wpr = d.srows / 64;      // bitmap words per rank
   const int64_t r = (int64_t)rb * NTHR + tid;
   const int64_t rr = r < m ? r : m - 1;
@@ -278,13 +296,14 @@ __device__ inline void drv_gather_item(const AxDerive& d, int64_t m, int64_t n, 
 
 //
 // DRV (round 6, the row-sharded ProxGD trial; solver.cpp iter_proxgd_shard): X0 is the all-gathered
-// p, and the pass derives the trial's replicated half itself (launch_trial_split's work with e = p
-// and no z): each staged vector is thresholded (|p| < thres -> 0, k_trial_split's comparison) on
-// its way into LDS, so the MFMAs read p_thr; row block bx owns the chunks c with c % gx == bx and
-// stores their p_thr vectors, row masks of e (zf) and column bitmap words (one 16-row group per
-// chunk, emitted one barrier after the masks went to LDS); the publisher workgroup combines the
-// all-gathered sums (shard_combine_block) and publishes the packet with them. Saves the k_trial_split
-// launch (5.6-6.5 us at the 1024-row shard) between the all-gather and this pass.
+// p and the launch does the trial's replicated half itself. The dense workgroups threshold each
+// staged vector on its way into LDS (|p| < thres -> 0, k_trial_split's comparison; registers only:
+// a store or a branch in the ring loop makes the compiler drain vmcnt at its join points, which
+// measured +15 us per pass), so the MFMAs read p_thr; behind them AxDerive::nd workgroups write
+// p_thr (drv_thr_item) and ggx * l workgroups compute A e (drv_gather_item) beside the MFMA work;
+// the publisher workgroup combines the all-gathered sums (shard_combine_block) and publishes the
+// packet with them. Replaces k_trial_split and the k_at_gather_bm launch between the all-gather
+// and this pass.
 template <typename T, int MT, int NT, int NSRC, int PF, int VPL, int WAVES, bool DRV>
 __device__ __forceinline__ void ax_lds_body(const T* __restrict__ A,
                                                       const T* __restrict__ X0,
@@ -311,10 +330,8 @@ __device__ __forceinline__ void ax_lds_body(const T* __restrict__ A,
   constexpr bool XFULL = (XV % NTHR) == 0; // every thread moves XPT vectors: no predicate
   constexpr int VPR = L / E;              // vectors per X row
   static_assert(PF >= 2, "X(c+1) must sit in another ring slot than X(c + PF)");
-  static_assert(!DRV || (NSRC == 1 && CK == 16 && XPT == 1 && XV % 64 == 0 && VPR <= 64),
-                "the derive: one source, one 16-row group per chunk, whole waves stage it");
+  static_assert(!DRV || NSRC == 1, "the derive: one source");
   __shared__ __attribute__((aligned(16))) T xs[2][XCH];
-  __shared__ unsigned dmsk[DRV ? 2 : 1][16];   // DRV: row masks of the staged chunk, per slot
   // pub.host: workgroup 0 hands the scalar packet to the host (no reduction to join here) while
   // the others run; with a short kernel in front (the N > 1 trial) a packet carried by THAT
   // kernel held up this launch by ~4 us (profiles/r1_tuning/small_kernels/ax_publisher.log)
@@ -328,8 +345,12 @@ __device__ __forceinline__ void ax_lds_body(const T* __restrict__ A,
     return;
   }
   if constexpr (DRV) {
-    if (drv.ggx > 0 && (int)blockIdx.x >= drv.gat0) {   // the A e workgroups (block-uniform)
+    if ((int)blockIdx.x >= drv.gat0) {   // the A e workgroups (block-uniform)
       drv_gather_item<T, L, 64 * WAVES>(drv, m, n, (int)blockIdx.x - drv.gat0);
+      return;
+    }
+    if ((int)blockIdx.x >= drv.thr0) {   // the p_thr workgroups
+      drv_thr_item<T, 64 * WAVES>(X0, drv, n * L, (int)blockIdx.x - drv.thr0);
       return;
     }
   }
@@ -400,49 +421,17 @@ __device__ __forceinline__ void ax_lds_body(const T* __restrict__ A,
       for (int v = 0; v < VPL; ++v)
         dst[mt][v] = load_vec<T, false>(ap[mt] + off * CK + v * E);
   };
-  // off: the walk offset of the chunk (DRV: which chunk it is)
-  auto put_x = [&](int slot, V (&src)[XPT], int64_t off) {
-    if constexpr (DRV) {
-      const int64_t kc = kch(off);
-      const bool own = ((cb + kc) % gx) == bx;   // block-uniform
+  auto put_x = [&](int slot, V (&src)[XPT]) {
+    if constexpr (DRV) {   // p -> p_thr in registers (see the header)
       const T thres = (T)drv.thres;
-      V v = src[0];
-      unsigned mk = 0;
-      const int c0 = (threadIdx.x % VPR) * E;
 #pragma unroll
-      for (int e = 0; e < E; ++e) {
-        const bool small = tabs(v[e]) < thres;
-        if (small && v[e] != T(0)) mk |= 1u << (c0 + e);
-        v[e] = small ? T(0) : v[e];
-      }
-      src[0] = v;
-      const unsigned rowm = row_or<VPR>(mk);
-      if (own && xon[0]) {
-        const int64_t eo = (xg[0] - X0) + kc * CK * L;
-        *reinterpret_cast<V*>(static_cast<T*>(drv.pthr) + eo) = v;
-        if (drv.zf != nullptr && (threadIdx.x % VPR) == 0) {
-          const int k = (int)threadIdx.x / VPR;   // row within the chunk
-          drv.zf[(cb + kc) * CK + k] = rowm;
-          dmsk[slot][k] = rowm;
-        }
-      }
+      for (int j = 0; j < XPT; ++j)
+#pragma unroll
+        for (int e = 0; e < E; ++e) src[j][e] = tabs(src[j][e]) < thres ? T(0) : src[j][e];
     }
 #pragma unroll
     for (int j = 0; j < XPT; ++j)
       if (XFULL || xon[j]) lds_put<T, W16>(&xs[slot][xo[j]], src[j]);
-  };
-  // DRV: the column bitmap words of chunk c (its masks went to dmsk[c & 1] one barrier ago)
-  auto emit_bits = [&](int64_t c) {
-    if constexpr (DRV) {
-      const int64_t kc = kch(c);
-      if (drv.zf != nullptr && ((cb + kc) % gx) == bx && (int)threadIdx.x < L) {
-        unsigned b = 0;
-#pragma unroll
-        for (int j = 0; j < 16; ++j) b |= ((dmsk[c & 1][j] >> threadIdx.x) & 1u) << j;
-        zf_bitmaps(drv.zf, drv.n)[(int64_t)threadIdx.x * (zf_npad(drv.n) / 16) + (cb + kc)] =
-            (unsigned short)b;
-      }
-    }
   };
   // X(c) from LDS slot into registers
   auto read_x = [&](int slot, T (&xv)[NC][EL]) {
@@ -473,7 +462,7 @@ __device__ __forceinline__ void ax_lds_body(const T* __restrict__ A,
     load_x(xr[p], p);
     load_a(a[p], p);
   }
-  put_x(0, xr[0], 0);              // chunk 0 -> slot 0
+  put_x(0, xr[0]);                 // chunk 0 -> slot 0
   __syncthreads();
 
   // Main loop: PF chunks per trip, no predicates. Registers are consumed in place: a tile's
@@ -485,8 +474,7 @@ __device__ __forceinline__ void ax_lds_body(const T* __restrict__ A,
     for (int p = 0; p < PF; ++p) {
       const int64_t c = c0 + p;
       const int slot = (int)(c & 1);
-      emit_bits(c);
-      put_x(slot ^ 1, xr[(p + 1) % PF], c + 1);   // X(c+1), loaded PF-1 chunks ago
+      put_x(slot ^ 1, xr[(p + 1) % PF]);   // X(c+1), loaded PF-1 chunks ago
       load_x(xr[p], c + PF);       // xr[p] (X(c)) has been in LDS since chunk c-1
       T xv[NC][EL];
       read_x(slot, xv);
@@ -506,8 +494,7 @@ __device__ __forceinline__ void ax_lds_body(const T* __restrict__ A,
     const int64_t c = c0 + p;
     if (c < nch) {
       const int slot = (int)(c & 1);
-      emit_bits(c);
-      if (c + 1 < nch) put_x(slot ^ 1, xr[(p + 1) % PF], c + 1);
+      if (c + 1 < nch) put_x(slot ^ 1, xr[(p + 1) % PF]);
       T xv[NC][EL];
       read_x(slot, xv);
 #pragma unroll
@@ -960,8 +947,9 @@ static void ax_lds_go(const GemmPlan& p, int S, const T* A, const T* const* X, T
   const int xmap = ax_xmap_flags(p, S);
   const unsigned dense = (unsigned)ax_grid(xmap, gx, S) + (pub.host ? 1u : 0u);
   AxDerive dv = drv;
-  dv.gat0 = (int)dense;
-  const dim3 grid(dense + (DRV ? (unsigned)(dv.ggx * p.l) : 0u));
+  dv.thr0 = (int)dense;
+  dv.gat0 = (int)dense + dv.nd;
+  const dim3 grid(dense + (DRV ? (unsigned)(dv.nd + dv.ggx * p.l) : 0u));
   if constexpr (DRV) {
     static const size_t pad = lds_pad(k_ax_lds_drv<T, MT, NT, NSRC, PF, VPL, WAVES>, "GLX_AX_LDS_PAD");
     glx_launch((k_ax_lds_drv<T, MT, NT, NSRC, PF, VPL, WAVES>), grid, dim3(64 * WAVES), pad, st, A, X[0],
@@ -1053,12 +1041,12 @@ bool launch_ax_derive(const GemmPlan& p, const T* A, const T* Xp, T* P, hipStrea
     return false;
   } else {
     if (!ax_derive_ok(p, 8) || pub.host == nullptr || d.pthr == nullptr) return false;
-    if (d.ggx > 0 && (p.n % 64 != 0 || d.srows % 64 != 0 || d.srows <= 0 || d.blk == nullptr ||
-                      (int64_t)d.ggx * kDrvGatRows < p.m || p.n > 65536))
+    if (d.ggx <= 0 || p.n % 64 != 0 || d.srows % 64 != 0 || d.srows <= 0 || d.blk == nullptr ||
+        (int64_t)d.ggx * kDrvGatRows < p.m || p.n > 65536)
       return false;
     AxDerive dd = d;
     dd.sp.pub = pub;
-    dd.n = p.n;
+    dd.nd = kDrvThrBlocks;
     const T* xs[3] = {Xp, nullptr, nullptr};
     ax_lds_go<T, 2, 1, 1, 3, 2, 8, true>(p, p.axb_S[1], A, xs, P, nullptr, 0, st, pub, dd);
     return true;

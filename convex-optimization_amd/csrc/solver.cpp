@@ -98,7 +98,7 @@ constexpr int kMaxGSets = kCtlMaxBatch / 2 + 2;
 // up to kMaxShardRanks ranks
 constexpr int kShardChunkMax = kShardPartOff + (6 + 4) * kMaxBlocks;
 constexpr int kMaxShardRanks = 64;
-// the chunks' doubles: the sums of up to kMaxShardRanks ranks, plus (round 6, sgat_) every rank's
+// the chunks' doubles: the sums of up to kMaxShardRanks ranks, plus (round 6, sderive_) every rank's
 // row masks and column bitmaps of e for its rows (n / 2 + l n / 64 doubles over all ranks)
 static int64_t shard_blk_doubles(int64_t n, int64_t l) {
   return (int64_t)kShardChunkMax * kMaxShardRanks + n / 2 + l * n / 64 + 64;
@@ -620,15 +620,13 @@ class Session : public SessionBase {
         // Round 6: that derive (k_trial_split) fused into the next trial's dense pass where the
         // plan's one-source tile takes it (k_ax_lds DRV: the 8-wave shard tile, f64, l = 32) and
         // the packet rides the pass (iter_proxgd_shard's speculative step). GLX_SHARD_DERIVE=0: off.
-        sderive_ = zskip_ && smode_ == 1 && !egat_ && gform_ != 2 && ax_derive_ok(plan_, (int)sizeof(T)) &&
-                   !env_is("GLX_SHARD_DERIVE", "0");
-        // ... and A e too (AxDerive::ggx): k_prox_pgd writes the masks and bitmaps of its rows into
-        // the rank's sums chunk (behind the partials, moff_), all-gathered with them, and the gather
-        // runs as extra workgroups of the dense pass. GLX_SHARD_GAT=0: the separate k_at_gather_bm.
-        sgat_ = sderive_ && gform_ == 0 && n_ % 64 == 0 && srows_ % 64 == 0 && n_ <= 65536 &&
-                !env_is("GLX_SHARD_GAT", "0");
+        // With it the A e gather (AxDerive: extra workgroups of that pass): k_prox_pgd writes the
+        // masks and bitmaps of its rows into the rank's sums chunk (behind the partials, moff_),
+        // all-gathered with them, so the gather needs nothing the pass writes.
+        sderive_ = zskip_ && smode_ == 1 && !egat_ && gform_ == 0 && ax_derive_ok(plan_, (int)sizeof(T)) &&
+                   n_ % 64 == 0 && srows_ % 64 == 0 && n_ <= 65536 && !env_is("GLX_SHARD_DERIVE", "0");
         moff_ = schunk_;
-        if (sgat_) schunk_ += srows_ / 2 + l_ * srows_ / 64;
+        if (sderive_) schunk_ += srows_ / 2 + l_ * srows_ / 64;
       } else {
         shard_model_ = false;
       }
@@ -804,7 +802,7 @@ class Session : public SessionBase {
     else if (shard_)
       s += "; rows=sharded x" + std::to_string(sranks_) + (shard_model_ ? " (timing model)" : "") +
            " (reduce-scatter of A^T r, k_prox_pgd on n/" + std::to_string(sranks_) +
-           " rows, all-gather of p, " + (sderive_ ? (sgat_ ? "derive and A e in the dense pass" : "derive in the dense pass") : "k_trial_split") + ")";
+           " rows, all-gather of p, " + (sderive_ ? "derive and A e in the dense pass" : "k_trial_split") + ")";
     s += "; dc_window=" + std::to_string(dc_window_);
     return s;
   }
@@ -1038,7 +1036,7 @@ class Session : public SessionBase {
     }
     check_launch();
     prof_end(0, e0);
-    if (dv != nullptr && dv->ggx > 0) {   // A e ran inside the dense pass
+    if (dv != nullptr) {   // A e ran inside the dense pass
       ++ax_calls_;
       ax_cols_ += 1;
       return;
@@ -1529,8 +1527,8 @@ class Session : public SessionBase {
     Red rd = red_to(scal_ + S_TR);
     rd.part = blk_own() + kShardPartOff;
     rd.parts_only = 1;
-    // sgat_: the masks and bitmaps of e for these rows into the chunk (the third output is then e)
-    unsigned* czf = sgat_ ? reinterpret_cast<unsigned*>(blk_own() + moff_) : nullptr;
+    // sderive_: the masks and bitmaps of e for these rows into the chunk (the third output is then e)
+    unsigned* czf = sderive_ ? reinterpret_cast<unsigned*>(blk_own() + moff_) : nullptr;
     launch_prox_pgd<T>(xt + o, G + o, 1, nullptr, X_[op] + o, X_[opt] + o, X_[oz] + o, srows_, l_, t,
                        mu_, O_.thres, rd, st_, Pub{}, czf);
     check_launch();
@@ -1643,19 +1641,16 @@ class Session : public SessionBase {
           if (fused) {
             AxDerive dv;
             dv.pthr = X_[if2_];
-            dv.zf = sgat_ ? nullptr : ezf();
             dv.thres = O_.thres;
             dv.sp = shard_pub(3, ot, nullptr);
-            if (sgat_) {
-              dv.ggx = (int)((m_ + kDrvGatRows - 1) / kDrvGatRows);
-              dv.At = At_;
-              dv.E = sx[0];
-              dv.Pe = Pp_;
-              dv.blk = blk_;
-              dv.bstride = shard_model_ ? 0 : schunk_;
-              dv.moff = moff_;
-              dv.srows = srows_;
-            }
+            dv.ggx = (int)((m_ + kDrvGatRows - 1) / kDrvGatRows);
+            dv.At = At_;
+            dv.E = sx[0];
+            dv.Pe = Pp_;
+            dv.blk = blk_;
+            dv.bstride = shard_model_ ? 0 : schunk_;
+            dv.moff = moff_;
+            dv.srows = srows_;
             cand_ax(sx, pb, &dv);
           } else if (smode_ == 1) {
             cand_ax(sx, pb);
@@ -2565,8 +2560,7 @@ class Session : public SessionBase {
   int schunk_ = 0;             // doubles per rank's chunk
   bool zskip_ = false;         // the gathered p serves as e (bitmap / list gathers)
   bool sderive_ = false;       // round 6: the speculative derive inside the dense pass (AxDerive)
-  bool sgat_ = false;          // ... with the A e gather as its extra workgroups (chunk masks)
-  int64_t moff_ = 0;           // doubles into a rank's chunk: its row masks + column bitmaps (sgat_)
+  int64_t moff_ = 0;           // doubles into a rank's chunk: its row masks + column bitmaps (sderive_)
   double* blk_ = nullptr;      // kMaxShardRanks chunks of sums (kShardChunkMax doubles each)
   // deferred reductions (defer_, single GPU): the trial's and the finalize's pending partials
   bool defer_ = false;

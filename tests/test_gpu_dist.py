@@ -206,8 +206,8 @@ def test_row_sharded_split_candidate(tmp_path, monkeypatch, extra):
     are re-derived from the gathered p and the bitmap gather reads e from them. Round 6: in the
     speculative steady state the derive runs inside the next trial's dense pass (k_ax_lds DRV; its
     publisher workgroup combines the gathered sums) with A e as its extra workgroups (bitmaps from the
-    all-gathered sums chunks), elsewhere in k_trial_split; GLX_SHARD_GAT=0 (the separate gather) and
-    GLX_SHARD_DERIVE=0 (k_trial_split throughout) give the same bits. alpha0 x 2.5: rejected first trials (the
+    all-gathered sums chunks), elsewhere in k_trial_split and k_at_gather_bm; GLX_SHARD_DERIVE=0
+    (those two throughout) gives the same bits. alpha0 x 2.5: rejected first trials (the
     host-path trial, then the fused form again once speculation resumes)."""
     monkeypatch.setenv("GLX_SPLIT_CAND", "1")
     v = run_sharded(tmp_path, 2, "gl_ProxGD_primal", 512, 1024, 32, maxit=25,
@@ -215,13 +215,12 @@ def test_row_sharded_split_candidate(tmp_path, monkeypatch, extra):
     r0 = _check_identical_and_oracle(v, 2)
     assert "gather k_at_gather_bm" in r0["plan"] and "rows=sharded x2" in r0["plan"], r0["plan"]
     assert "derive and A e in the dense pass" in r0["plan"], r0["plan"]
-    for env, name in (("GLX_SHARD_GAT", "derive in the dense pass"), ("GLX_SHARD_DERIVE", "k_trial_split")):
-        monkeypatch.setenv(env, "0")
-        w = run_sharded(tmp_path, 2, "gl_ProxGD_primal", 512, 1024, 32, maxit=25,
-                        extra=("--shard-rows", "1") + tuple(extra))
-        w0 = w["ranks"][0]
-        assert name in w0["plan"], w0["plan"]
-        assert w0["k"] == r0["k"] and w0["x_sha"] == r0["x_sha"] and w0["f_hist"] == r0["f_hist"]
+    monkeypatch.setenv("GLX_SHARD_DERIVE", "0")
+    w = run_sharded(tmp_path, 2, "gl_ProxGD_primal", 512, 1024, 32, maxit=25,
+                    extra=("--shard-rows", "1") + tuple(extra))
+    w0 = w["ranks"][0]
+    assert "k_trial_split" in w0["plan"], w0["plan"]
+    assert w0["k"] == r0["k"] and w0["x_sha"] == r0["x_sha"] and w0["f_hist"] == r0["f_hist"]
 
 
 def test_row_sharded_matches_allreduce_schedule(tmp_path):
