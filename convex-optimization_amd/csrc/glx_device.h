@@ -319,28 +319,47 @@ __device__ inline void ctl_decide(const Ctl& c, const double* out, const double 
 __device__ inline void shard_combine_block(const ShardPub& sp) {
   __shared__ double wv[10][4];
   __shared__ double fin[10];
+  __shared__ double pre[kPublishMax];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   double acc[10] = {0.0, 0.0, 0.0, -__builtin_inf(), 0.0, 0.0, 0.0, 0.0, 0.0, 0.0};
   const bool in = threadIdx.x < 256;
-  if ((sp.mask & 1) && in) {
-    const int np = sp.nranks * sp.nbp;
-    for (int i = threadIdx.x; i < np; i += 256) {
-      const int r = i / sp.nbp, b = i - r * sp.nbp;
-      const double* q = sp.blk + (int64_t)r * sp.chunk + kShardPartOff + b * sp.tv;
+  const int np1 = (sp.mask & 1) ? sp.nranks * sp.nbp : 0;
+  const int np2 = (sp.mask & 2) ? sp.nranks * sp.nbf : 0;
+  const int npm = np1 > np2 ? np1 : np2;
+  // Round 6 (this block publishes from the fused dense pass, where the packet's latency is on the
+  // host's critical path): every load of a batch — KB trial and finalize partials per thread, and
+  // the packet's other scalars — is issued before the first add, one round trip instead of three;
+  // the adds keep the per-thread order i = t, t + 256, ... (the same bits as before)
+  const bool pubp = sp.pub.host != nullptr && sp.pub.ns <= kPublishMax;
+  const double pv = (pubp && (int)threadIdx.x < sp.pub.ns) ? sp.pub.s[threadIdx.x] : 0.0;
+  constexpr int KB = 4;
+  for (int i0 = (int)threadIdx.x; in && i0 < npm; i0 += 256 * KB) {
+    double q1[KB][6], q2[KB][4];
 #pragma unroll
-      for (int j = 0; j < 6; ++j)
-        if (j < sp.tv) acc[j] = combine(j == 3 ? OP_MAX : OP_SUM, acc[j], q[j]);
+    for (int k = 0; k < KB; ++k) {
+      const int i = i0 + 256 * k;
+      const int r1 = i < np1 ? i / sp.nbp : 0, b1 = i < np1 ? i - r1 * sp.nbp : 0;
+      const double* p1 = sp.blk + (int64_t)r1 * sp.chunk + kShardPartOff + b1 * sp.tv;
+#pragma unroll
+      for (int j = 0; j < 6; ++j) q1[k][j] = (i < np1 && j < sp.tv) ? p1[j] : 0.0;
+      const int r2 = i < np2 ? i / sp.nbf : 0, b2 = i < np2 ? i - r2 * sp.nbf : 0;
+      const double* p2 = sp.blk + (int64_t)r2 * sp.chunk + kShardPartOff + sp.tv * sp.nbp + b2 * 4;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) q2[k][j] = i < np2 ? p2[j] : 0.0;
+    }
+#pragma unroll
+    for (int k = 0; k < KB; ++k) {
+      const int i = i0 + 256 * k;
+      if (i < np1)
+#pragma unroll
+        for (int j = 0; j < 6; ++j)
+          if (j < sp.tv) acc[j] = combine(j == 3 ? OP_MAX : OP_SUM, acc[j], q1[k][j]);
+      if (i < np2)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[6 + j] += q2[k][j];
     }
   }
-  if ((sp.mask & 2) && in) {
-    const int np = sp.nranks * sp.nbf;
-    for (int i = threadIdx.x; i < np; i += 256) {
-      const int r = i / sp.nbf, b = i - r * sp.nbf;
-      const double* q = sp.blk + (int64_t)r * sp.chunk + kShardPartOff + sp.tv * sp.nbp + b * 4;
-#pragma unroll
-      for (int j = 0; j < 4; ++j) acc[6 + j] += q[j];
-    }
-  }
+  if (pubp && (int)threadIdx.x < sp.pub.ns) pre[threadIdx.x] = pv;
 #pragma unroll
   for (int j = 0; j < 10; ++j)
 #pragma unroll
@@ -357,8 +376,8 @@ __device__ inline void shard_combine_block(const ShardPub& sp) {
   if (sp.mask & 2)
     for (int j = 0; j < 4; ++j) sp.rt[j] = fin[6 + j];
   if (sp.pub.host != nullptr)
-    publish_packet(sp.pub.s, sp.pub.ns, sp.pub.host, sp.pub.host_seq, sp.pub.seq, fin, sp.tr_off,
-                   (sp.mask & 1) ? sp.tv : 0, fin + 6, sp.rt_off, (sp.mask & 2) ? 4 : 0);
+    publish_packet(pubp ? pre : sp.pub.s, sp.pub.ns, sp.pub.host, sp.pub.host_seq, sp.pub.seq, fin,
+                   sp.tr_off, (sp.mask & 1) ? sp.tv : 0, fin + 6, sp.rt_off, (sp.mask & 2) ? 4 : 0);
 }
 
 // ------------------------------------------------------------------------------------------

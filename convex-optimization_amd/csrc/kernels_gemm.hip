@@ -296,15 +296,16 @@ __device__ inline void drv_gather_item(const AxDerive& d, int64_t m, int64_t n, 
 
 //
 // DRV (round 6, the row-sharded ProxGD trial; solver.cpp iter_proxgd_shard): X0 is the all-gathered
-// p and the launch does the trial's replicated half itself. The dense workgroups threshold each
-// staged vector on its way into LDS (|p| < thres -> 0, k_trial_split's comparison; registers only:
-// a store or a branch in the ring loop makes the compiler drain vmcnt at its join points, which
-// measured +15 us per pass), so the MFMAs read p_thr; behind them AxDerive::nd workgroups write
+// p and the launch does the trial's replicated half itself. The dense workgroups threshold the
+// MFMA operands as they leave LDS (|p| < thres -> 0, k_trial_split's comparison; stores and
+// branches in the ring loop made the compiler drain vmcnt at its join points: +15 us per pass,
+// and thresholding the staged vectors before their LDS store shortened the X prefetch: +6 us),
+// so the MFMAs read p_thr; behind them AxDerive::nd workgroups write
 // p_thr (drv_thr_item) and ggx * l workgroups compute A e (drv_gather_item) beside the MFMA work;
 // the publisher workgroup combines the all-gathered sums (shard_combine_block) and publishes the
 // packet with them. Replaces k_trial_split and the k_at_gather_bm launch between the all-gather
 // and this pass.
-template <typename T, int MT, int NT, int NSRC, int PF, int VPL, int WAVES, bool DRV>
+template <typename T, int MT, int NT, int NSRC, int PF, int VPL, int WAVES, int DRV>
 __device__ __forceinline__ void ax_lds_body(const T* __restrict__ A,
                                                       const T* __restrict__ X0,
                                                       const T* __restrict__ X1,
@@ -337,7 +338,11 @@ __device__ __forceinline__ void ax_lds_body(const T* __restrict__ A,
   // kernel held up this launch by ~4 us (profiles/r1_tuning/small_kernels/ax_publisher.log)
   if (pub.host != nullptr && blockIdx.x == 0) {
     if constexpr (DRV) {
-      shard_combine_block(drv.sp);   // drv.sp.pub == pub
+      if (!(drv.probe & 4)) {
+        shard_combine_block(drv.sp);   // drv.sp.pub == pub
+      } else if (threadIdx.x == 0) {
+        publish_packet(pub.s, pub.ns, pub.host, pub.host_seq, pub.seq);
+      }
     } else if (threadIdx.x == 0) {
       publish_packet(pub.s, pub.ns, pub.host, pub.host_seq, pub.seq, pub.s2, pub.off2, pub.n2,
                      pub.s3, pub.off3, pub.n3);
@@ -346,11 +351,11 @@ __device__ __forceinline__ void ax_lds_body(const T* __restrict__ A,
   }
   if constexpr (DRV) {
     if ((int)blockIdx.x >= drv.gat0) {   // the A e workgroups (block-uniform)
-      drv_gather_item<T, L, 64 * WAVES>(drv, m, n, (int)blockIdx.x - drv.gat0);
+      if (!(drv.probe & 1)) drv_gather_item<T, L, 64 * WAVES>(drv, m, n, (int)blockIdx.x - drv.gat0);
       return;
     }
     if ((int)blockIdx.x >= drv.thr0) {   // the p_thr workgroups
-      drv_thr_item<T, 64 * WAVES>(X0, drv, n * L, (int)blockIdx.x - drv.thr0);
+      if (!(drv.probe & 2)) drv_thr_item<T, 64 * WAVES>(X0, drv, n * L, (int)blockIdx.x - drv.thr0);
       return;
     }
   }
@@ -422,7 +427,7 @@ __device__ __forceinline__ void ax_lds_body(const T* __restrict__ A,
         dst[mt][v] = load_vec<T, false>(ap[mt] + off * CK + v * E);
   };
   auto put_x = [&](int slot, V (&src)[XPT]) {
-    if constexpr (DRV) {   // p -> p_thr in registers (see the header)
+    if constexpr (DRV == 2) {   // p -> p_thr before the staging store (probe form)
       const T thres = (T)drv.thres;
 #pragma unroll
       for (int j = 0; j < XPT; ++j)
@@ -441,6 +446,11 @@ __device__ __forceinline__ void ax_lds_body(const T* __restrict__ A,
       const T* xp = &xs[slot][src * CK * LP + q * EL * LP + nt * 16 + i];
 #pragma unroll
       for (int e = 0; e < EL; ++e) xv[cc][e] = xp[e * LP];
+      if constexpr (DRV == 1) {   // p -> p_thr as the operands leave LDS (see the header)
+        const T thres = (T)drv.thres;
+#pragma unroll
+        for (int e = 0; e < EL; ++e) xv[cc][e] = tabs(xv[cc][e]) < thres ? T(0) : xv[cc][e];
+      }
     }
   };
   // MFMAs of row tile mt for one chunk, column tiles [C0, C1)
@@ -525,16 +535,14 @@ __device__ __forceinline__ void ax_lds_body(const T* __restrict__ A,
       int gx, int xmap, const int* __restrict__ gate, int epoch, Pub pub, AxDerive drv
 template <typename T, int MT, int NT, int NSRC, int PF, int VPL, int WAVES>
 __global__ __launch_bounds__(64 * WAVES) void k_ax_lds(GLX_AX_LDS_ARGS) {
-  ax_lds_body<T, MT, NT, NSRC, PF, VPL, WAVES, false>(A, X0, X1, X2, P, m, n, chunks, S, gx, xmap, gate,
+  ax_lds_body<T, MT, NT, NSRC, PF, VPL, WAVES, 0>(A, X0, X1, X2, P, m, n, chunks, S, gx, xmap, gate,
                                                      epoch, pub, drv);
 }
-// the derive form: held to 128 VGPRs (4 waves per SIMD, two 8-wave workgroups per CU) so that its
-// A e workgroups find a slot beside the dense ones (at 133 VGPRs one workgroup per CU fits and
-// the gather waits for the dense workgroups to drain)
-template <typename T, int MT, int NT, int NSRC, int PF, int VPL, int WAVES>
-__global__ __launch_bounds__(64 * WAVES) __attribute__((amdgpu_waves_per_eu(4))) void k_ax_lds_drv(
+// the derive form (its own kernel: the extra workgroups' code and LDS stay out of k_ax_lds)
+template <typename T, int MT, int NT, int NSRC, int PF, int VPL, int WAVES, int DRV>
+__global__ __launch_bounds__(64 * WAVES) void k_ax_lds_drv(
     GLX_AX_LDS_ARGS) {
-  ax_lds_body<T, MT, NT, NSRC, PF, VPL, WAVES, true>(A, X0, X1, X2, P, m, n, chunks, S, gx, xmap, gate,
+  ax_lds_body<T, MT, NT, NSRC, PF, VPL, WAVES, DRV>(A, X0, X1, X2, P, m, n, chunks, S, gx, xmap, gate,
                                                     epoch, pub, drv);
 }
 #undef GLX_AX_LDS_ARGS
@@ -938,7 +946,7 @@ static void ax_mfma_go(const GemmPlan& p, const T* A, const T* const* X, T* P, c
                      epoch);
 }
 
-template <typename T, int NT, int NSRC, int MT, int PF, int VPL, int WAVES, bool DRV = false>
+template <typename T, int NT, int NSRC, int MT, int PF, int VPL, int WAVES, int DRV = 0>
 static void ax_lds_go(const GemmPlan& p, int S, const T* A, const T* const* X, T* P,
                       const int* gate, int epoch, hipStream_t st, Pub pub = Pub{},
                       const AxDerive& drv = AxDerive{}) {
@@ -951,8 +959,8 @@ static void ax_lds_go(const GemmPlan& p, int S, const T* A, const T* const* X, T
   dv.gat0 = (int)dense + dv.nd;
   const dim3 grid(dense + (DRV ? (unsigned)(dv.nd + dv.ggx * p.l) : 0u));
   if constexpr (DRV) {
-    static const size_t pad = lds_pad(k_ax_lds_drv<T, MT, NT, NSRC, PF, VPL, WAVES>, "GLX_AX_LDS_PAD");
-    glx_launch((k_ax_lds_drv<T, MT, NT, NSRC, PF, VPL, WAVES>), grid, dim3(64 * WAVES), pad, st, A, X[0],
+    static const size_t pad = lds_pad(k_ax_lds_drv<T, MT, NT, NSRC, PF, VPL, WAVES, DRV>, "GLX_AX_LDS_PAD");
+    glx_launch((k_ax_lds_drv<T, MT, NT, NSRC, PF, VPL, WAVES, DRV>), grid, dim3(64 * WAVES), pad, st, A, X[0],
                X[1], X[2], P, p.m, p.n, p.n / (4 * VPL * E), S, gx, xmap, gate, epoch, pub, dv);
   } else {
     static const size_t pad = lds_pad(k_ax_lds<T, MT, NT, NSRC, PF, VPL, WAVES>, "GLX_AX_LDS_PAD");
@@ -1047,8 +1055,12 @@ bool launch_ax_derive(const GemmPlan& p, const T* A, const T* Xp, T* P, hipStrea
     AxDerive dd = d;
     dd.sp.pub = pub;
     dd.nd = kDrvThrBlocks;
+    // timing probe only (results are wrong): bit 0 skips the A e work, bit 1 the p_thr stores
+    dd.probe = env_int("GLX_DRV_PROBE", 0);
     const T* xs[3] = {Xp, nullptr, nullptr};
-    ax_lds_go<T, 2, 1, 1, 3, 2, 8, true>(p, p.axb_S[1], A, xs, P, nullptr, 0, st, pub, dd);
+    if (env_int("GLX_DRV_THR", 1) == 2) ax_lds_go<T, 2, 1, 1, 3, 2, 8, 2>(p, p.axb_S[1], A, xs, P, nullptr, 0, st, pub, dd);
+    else if (env_int("GLX_DRV_THR", 1) == 3) ax_lds_go<T, 2, 1, 1, 3, 2, 8, 3>(p, p.axb_S[1], A, xs, P, nullptr, 0, st, pub, dd);
+    else ax_lds_go<T, 2, 1, 1, 3, 2, 8, 1>(p, p.axb_S[1], A, xs, P, nullptr, 0, st, pub, dd);
     return true;
   }
 }

@@ -9,7 +9,7 @@ timeout -k 10 900 python -u -m pytest -x -v --timeout 600 --timeout-method threa
   > $OUT/pytest.log 2>&1 || { tail -40 $OUT/pytest.log; exit 1; }
 tail -3 $OUT/pytest.log
 B="python bench.py --steps 200 --warmup 20 --no-cpu-baseline --no-whole-solve --force-comm --m 1024 --shard-model 8"
-for v in "fused:" "split:GLX_SHARD_DERIVE=0" "fused2:"; do
+for v in "fused:" "nocomb:GLX_DRV_PROBE=4" "split:GLX_SHARD_DERIVE=0" "fused2:"; do
   name=${v%%:*}; envs=${v#*:}
   env $envs timeout -k 10 120 $B > $OUT/pg1024_$name.json 2> $OUT/pg1024_$name.err || { echo "pg1024 $name failed"; tail -5 $OUT/pg1024_$name.err; exit 1; }
 done
