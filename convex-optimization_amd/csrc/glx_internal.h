@@ -412,7 +412,6 @@ struct AxDerive {
   void* Pe = nullptr;
   const double* blk = nullptr;
   int64_t bstride = 0, moff = 0, srows = 0;
-  int probe = 0;                 // GLX_DRV_PROBE (timing probe of the pieces; wrong results)
 };
 bool ax_derive_ok(const GemmPlan& p, int esize);
 // rows of A per gather workgroup of the fused dense pass (AxDerive::ggx = ceil(m / this)), and

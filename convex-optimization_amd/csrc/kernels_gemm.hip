@@ -338,11 +338,7 @@ __device__ __forceinline__ void ax_lds_body(const T* __restrict__ A,
   // kernel held up this launch by ~4 us (profiles/r1_tuning/small_kernels/ax_publisher.log)
   if (pub.host != nullptr && blockIdx.x == 0) {
     if constexpr (DRV) {
-      if (!(drv.probe & 4)) {
-        shard_combine_block(drv.sp);   // drv.sp.pub == pub
-      } else if (threadIdx.x == 0) {
-        publish_packet(pub.s, pub.ns, pub.host, pub.host_seq, pub.seq);
-      }
+      shard_combine_block(drv.sp);   // drv.sp.pub == pub
     } else if (threadIdx.x == 0) {
       publish_packet(pub.s, pub.ns, pub.host, pub.host_seq, pub.seq, pub.s2, pub.off2, pub.n2,
                      pub.s3, pub.off3, pub.n3);
@@ -351,11 +347,11 @@ __device__ __forceinline__ void ax_lds_body(const T* __restrict__ A,
   }
   if constexpr (DRV) {
     if ((int)blockIdx.x >= drv.gat0) {   // the A e workgroups (block-uniform)
-      if (!(drv.probe & 1)) drv_gather_item<T, L, 64 * WAVES>(drv, m, n, (int)blockIdx.x - drv.gat0);
+      drv_gather_item<T, L, 64 * WAVES>(drv, m, n, (int)blockIdx.x - drv.gat0);
       return;
     }
     if ((int)blockIdx.x >= drv.thr0) {   // the p_thr workgroups
-      if (!(drv.probe & 2)) drv_thr_item<T, 64 * WAVES>(X0, drv, n * L, (int)blockIdx.x - drv.thr0);
+      drv_thr_item<T, 64 * WAVES>(X0, drv, n * L, (int)blockIdx.x - drv.thr0);
       return;
     }
   }
@@ -427,13 +423,6 @@ __device__ __forceinline__ void ax_lds_body(const T* __restrict__ A,
         dst[mt][v] = load_vec<T, false>(ap[mt] + off * CK + v * E);
   };
   auto put_x = [&](int slot, V (&src)[XPT]) {
-    if constexpr (DRV == 2) {   // p -> p_thr before the staging store (probe form)
-      const T thres = (T)drv.thres;
-#pragma unroll
-      for (int j = 0; j < XPT; ++j)
-#pragma unroll
-        for (int e = 0; e < E; ++e) src[j][e] = tabs(src[j][e]) < thres ? T(0) : src[j][e];
-    }
 #pragma unroll
     for (int j = 0; j < XPT; ++j)
       if (XFULL || xon[j]) lds_put<T, W16>(&xs[slot][xo[j]], src[j]);
@@ -1055,12 +1044,8 @@ bool launch_ax_derive(const GemmPlan& p, const T* A, const T* Xp, T* P, hipStrea
     AxDerive dd = d;
     dd.sp.pub = pub;
     dd.nd = kDrvThrBlocks;
-    // timing probe only (results are wrong): bit 0 skips the A e work, bit 1 the p_thr stores
-    dd.probe = env_int("GLX_DRV_PROBE", 0);
     const T* xs[3] = {Xp, nullptr, nullptr};
-    if (env_int("GLX_DRV_THR", 1) == 2) ax_lds_go<T, 2, 1, 1, 3, 2, 8, 2>(p, p.axb_S[1], A, xs, P, nullptr, 0, st, pub, dd);
-    else if (env_int("GLX_DRV_THR", 1) == 3) ax_lds_go<T, 2, 1, 1, 3, 2, 8, 3>(p, p.axb_S[1], A, xs, P, nullptr, 0, st, pub, dd);
-    else ax_lds_go<T, 2, 1, 1, 3, 2, 8, 1>(p, p.axb_S[1], A, xs, P, nullptr, 0, st, pub, dd);
+    ax_lds_go<T, 2, 1, 1, 3, 2, 8, 1>(p, p.axb_S[1], A, xs, P, nullptr, 0, st, pub, dd);
     return true;
   }
 }
