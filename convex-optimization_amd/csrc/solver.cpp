@@ -98,6 +98,8 @@ constexpr int kMaxGSets = kCtlMaxBatch / 2 + 2;
 // up to kMaxShardRanks ranks
 constexpr int kShardChunkMax = kShardPartOff + (6 + 4) * kMaxBlocks;
 constexpr int kMaxShardRanks = 64;
+// round 6: flagged rows from which ProxGD's split-candidate A e takes the fused form (GLX_AE_HYB_ROWS)
+constexpr double kHybRows = 1500.0;
 // the chunks' doubles: the sums of up to kMaxShardRanks ranks, plus (round 6, sderive_) every rank's
 // row masks and column bitmaps of e for its rows (n / 2 + l n / 64 doubles over all ranks)
 static int64_t shard_blk_doubles(int64_t n, int64_t l) {
@@ -646,6 +648,16 @@ class Session : public SessionBase {
     // (its publisher's reduction stretched the 33 us fused kernel by ~4 us); that opt-in form
     // (GLX_DEFER_RED=2) was removed in round 6.
     const bool dmeth = P.method == GLX_PROXGD;
+    // Round 6: ProxGD's split-candidate A e chosen per trial on one GPU under host control: the
+    // bitmap gather while few rows are flagged (its cost grows with them: 12 us at ~570 rows,
+    // ~50 us averaged over a solve), A e fused into the dense pass (launch_ax_egat, a near-constant
+    // extra) once the last accepted trial flagged at least hyb_rows_ rows. GLX_AE_HYB_ROWS: the
+    // threshold, 0 = off (the gather throughout); GLX_AE_FUSED=1 keeps the fused form throughout.
+    if (smode_ == 1 && !egat_ && gform_ == 0 && comm_ == nullptr && dc_window_ == 0 &&
+        P.method == GLX_PROXGD && P.dtype == GLX_F64 && ax_egat_ok(plan_, 8)) {
+      const char* e = std::getenv("GLX_AE_HYB_ROWS");
+      hyb_rows_ = e ? std::atof(e) : kHybRows;
+    }
     defer_ = comm_ == nullptr && dc_window_ == 0 && dmeth && spin_readback_ && attach_ok_ &&
              !env_is("GLX_DEFER_RED", "0");
     GLX_HIP(hipMemsetAsync(ticket_, 0, kTicketBytes, st_));
@@ -792,6 +804,9 @@ class Session : public SessionBase {
     s += "; split=";
     if (smode_ == 0) s += "dense";
     else if (egat_) s += "A e fused into the dense pass (k_ax_dma EG), S0=" + std::to_string(gsplit_);
+    else if (hyb_rows_ > 0.0)
+      s += "gather k_at_gather_bm, A e fused into the dense pass (k_ax_dma EG) from " +
+           std::to_string((int64_t)hyb_rows_) + " flagged rows";
     else if (rows_form_) s += "rows k_at_rows S0=" + std::to_string(gsplit_);
     else if (gform_ == 2) s += "gather k_e_lists+k_at_gather";
     else s += "gather k_at_gather_bm";
@@ -966,10 +981,10 @@ class Session : public SessionBase {
                                 rd, st_,
                                 snap_trial ? scal_ + S_TR : nullptr,
                                 snap_trial ? scal_ + S_SNAP : nullptr, snap_trial ? 6 : 0,
-                                chain ? (egat_ ? 2 : 1) : 0, gat ? gsplit_ : 0, dc_ctl_,
+                                chain ? (qeg_ ? 2 : 1) : 0, gat ? gs_of(qeg_) : 0, dc_ctl_,
                                 dmax ? ptr_.part : nullptr, dmax ? ptr_.np : 0, dmax ? ptr_.nv : 6);
     check_launch();
-    if (dfin) pfin_ = Pend{fpart_, finalize_blocks(ml_, S, gat ? gsplit_ : 0, cx ? nl_ : 0), 4, 0u, scal_ + slot};
+    if (dfin) pfin_ = Pend{fpart_, finalize_blocks(ml_, S, gat ? gs_of(qeg_) : 0, cx ? nl_ : 0), 4, 0u, scal_ + slot};
     if (defer) return;
     if (comm_) {
       comm_allreduce(comm_, scal_ + slot, nsrc, GLX_F64, st_);
@@ -1006,7 +1021,8 @@ class Session : public SessionBase {
   // itself, with the masks and bitmaps the gather reads (k_ax_lds DRV)
   void cand_ax(const T* const* xs, Pub pb = Pub{}, const AxDerive* dv = nullptr) {
     const T* xd[3] = {xs[1], nullptr, nullptr};
-    if (egat_) {   // round 6: A p and A e in one pass (S slabs each: A e at Pp_, A p behind)
+    qeg_ = dv == nullptr && egat_now();
+    if (qeg_) {   // round 6: A p and A e in one pass (S slabs each: A e at Pp_, A p behind)
       EGat eg;
       eg.E = xs[0];
       const int64_t npad = (n_ + 63) / 64 * 64;   // glx_device.h zf_npad
@@ -1014,7 +1030,7 @@ class Session : public SessionBase {
       eg.bstride = npad / 16;
       eg.Pe = Pp_;
       hipEvent_t e0 = prof_begin(0);
-      if (!launch_ax_egat<T>(plan_, A_, xs[2], Pp_ + (size_t)gsplit_ * ml_, dc_gate_, 0, st_, pb, eg))
+      if (!launch_ax_egat<T>(plan_, A_, xs[2], Pp_ + (size_t)gs_of(true) * ml_, dc_gate_, 0, st_, pb, eg))
         throw Error{GLX_E_STATE, "fused A e: the plan does not take it"};
       check_launch();
       prof_end(0, e0);
@@ -1467,6 +1483,7 @@ class Session : public SessionBase {
     stats_[1] += hs_[trs + 5];
     stats_[2] += 1;
     split_hist_.push_back(hs_[trs + 5]);
+    last_rows_ = hs_[trs + 5];
     irg_ = rpt;
     gx_ = 0.5 * hs_[S_RT + 1];
     // exact: A p from the batch; split-candidate: A p - b = (A p_thr - b) + A e; dense z
@@ -1581,7 +1598,7 @@ class Session : public SessionBase {
     launch_finalize_residual<T>(Pp_, gat ? ax_split(plan_, 1) : ax_split(plan_, nsrc), B_, nsrc, rsc,
                                 ml_, nullptr, 0, 1, cx + o, srows_ * l_, cmax, nullptr, 0.0,
                                 scal_ + S_DRN, rd, st_, nullptr, nullptr, 0,
-                                chain ? (egat_ ? 2 : 1) : 0, gat ? gsplit_ : 0, Ctl{});
+                                chain ? (qeg_ ? 2 : 1) : 0, gat ? gs_of(qeg_) : 0, Ctl{});
     check_launch();
   }
   void iter_proxgd_shard() {
@@ -2577,6 +2594,12 @@ class Session : public SessionBase {
   int gform_ = 0;              // A e: 0 bitmap gather, 1 k_at_rows, 2 lists + gather (gather_form)
   bool rows_form_ = false;     // gform_ == 1: A e by k_at_rows (round 5), gsplit_ slabs
   bool egat_ = false;          // round 6: A e inside the dense pass (launch_ax_egat), gsplit_ = its S
+  double hyb_rows_ = 0.0;      // round 6: > 0: the fused form per trial from this many flagged rows
+  double last_rows_ = 0.0;     // flagged rows of the last accepted trial
+  bool qeg_ = false;           // the queued split-candidate A@X is the fused form (its finalize reads it)
+  // the fused A e form for the next trial; its A e slabs (one per K split) in front of A p
+  bool egat_now() const { return egat_ || (hyb_rows_ > 0.0 && last_rows_ >= hyb_rows_); }
+  int gs_of(bool eg) const { return eg ? ax_split(plan_, 1) : gsplit_; }
   // entries of the gather counts the FISTA finalize sums: flagged rows per K range (row form) or
   // nonzeros per column (VALU gather)
   int gcount_n() const { return rows_form_ ? gsplit_ : (int)l_; }
