@@ -99,7 +99,7 @@ constexpr int kMaxGSets = kCtlMaxBatch / 2 + 2;
 constexpr int kShardChunkMax = kShardPartOff + (6 + 4) * kMaxBlocks;
 constexpr int kMaxShardRanks = 64;
 // round 6: flagged rows from which ProxGD's split-candidate A e takes the fused form (GLX_AE_HYB_ROWS)
-constexpr double kHybRows = 1500.0;
+constexpr double kHybRows = 2000.0;
 // the chunks' doubles: the sums of up to kMaxShardRanks ranks, plus (round 6, sderive_) every rank's
 // row masks and column bitmaps of e for its rows (n / 2 + l n / 64 doubles over all ranks)
 static int64_t shard_blk_doubles(int64_t n, int64_t l) {

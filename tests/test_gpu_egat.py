@@ -8,7 +8,7 @@ form's direct A p_thr - b (GLX_AE_FUSED=0: the transposed copy of A and k_at_gat
 forms agree to rounding (k identical, f_hist within 1e-11, x within 1e-9 of max|x|). Against the
 oracle: the north-star bar (k identical, f_hist within 1e-8, x within 1e-6 of max|x|).
 
-Round 6, the per-trial choice (GLX_AE_HYB_ROWS, default 1500 flagged rows; one GPU, host control,
+Round 6, the per-trial choice (GLX_AE_HYB_ROWS, default 2000 flagged rows; one GPU, host control,
 the NS tile): the gather while few rows are flagged, the fused form from the threshold on. Forced
 early here (100 rows) so both forms and the switch run within a short solve.
 """
