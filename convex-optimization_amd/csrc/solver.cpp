@@ -258,8 +258,9 @@ static int split_mode(const glx_problem& P, const glx_opts& O) {
 // in the window, +1.5 % over a solve (the gather grows late in a solve), but the fused pass runs
 // 210-218 µs against 174-176 µs: its A e (VALU, after the chunk's MFMAs) leaves the MFMA pipe of
 // both waves of a SIMD idle. Interleaving it into the MFMA stream (straight-line, or on opposite
-// sides of the two waves' MFMAs) spilled 16-208 VGPRs at 256. The gather stays the default;
-// the fused form also halves the session's workspace (no m x n copy of A).
+// sides of the two waves' MFMAs) spilled 16-208 VGPRs at 256. Throughout a solve it stays opt-in
+// (it also halves the session's workspace: no m x n copy of A); by default the session takes it
+// per trial once many rows are flagged (hyb_rows_, below).
 static bool egat_mode(const glx_problem& P, const GemmPlan& plan, int smode) {
   if (smode != 1 || P.method != GLX_PROXGD || P.dtype != GLX_F64) return false;
   if (gather_form() >= 0) return false;
@@ -651,8 +652,10 @@ class Session : public SessionBase {
     // Round 6: ProxGD's split-candidate A e chosen per trial on one GPU under host control: the
     // bitmap gather while few rows are flagged (its cost grows with them: 12 us at ~570 rows,
     // ~50 us averaged over a solve), A e fused into the dense pass (launch_ax_egat, a near-constant
-    // extra) once the last accepted trial flagged at least hyb_rows_ rows. GLX_AE_HYB_ROWS: the
-    // threshold, 0 = off (the gather throughout); GLX_AE_FUSED=1 keeps the fused form throughout.
+    // extra) once the last accepted trial flagged at least hyb_rows_ rows. NS whole solves 2 538-
+    // 2 541 it/s at 1 500-2 500 rows against 2 463-2 465 with the gather throughout, the 20-step
+    // window unchanged (profiles/r6_hyb/). GLX_AE_HYB_ROWS: the threshold, 0 = off (the gather
+    // throughout); GLX_AE_FUSED=1 keeps the fused form throughout.
     if (smode_ == 1 && !egat_ && gform_ == 0 && comm_ == nullptr && dc_window_ == 0 &&
         P.method == GLX_PROXGD && P.dtype == GLX_F64 && ax_egat_ok(plan_, 8)) {
       const char* e = std::getenv("GLX_AE_HYB_ROWS");
