@@ -661,17 +661,6 @@ class Session : public SessionBase {
       const char* e = std::getenv("GLX_AE_HYB_ROWS");
       hyb_rows_ = e ? std::atof(e) : kHybRows;
     }
-    // ... and FProxGD's split batch (A xc dense, A e_c = xc where thresholded, the same fused
-    // pass): the batches the gather's budget sends to the dense [xc | y_next] pass (two
-    // right-hand sides) run the fused form instead, from hyb_rows_ flagged rows on
-    // (kFistaDenseRun batches, then the gather measures the count again). GLX_FISTA_EG=0: off.
-    if (fsplit_ && comm_ == nullptr && dc_window_ == 0 && P.dtype == GLX_F64 && ax_egat_ok(plan_, 8) &&
-        !env_is("GLX_FISTA_EG", "0")) {
-      const char* e = std::getenv("GLX_AE_HYB_ROWS");
-      const double r = e ? std::atof(e) : kHybRows;
-      feg_ = r > 0.0;
-      feg_rows_ = std::min(r, nnz_budget_);
-    }
     defer_ = comm_ == nullptr && dc_window_ == 0 && dmeth && spin_readback_ && attach_ok_ &&
              !env_is("GLX_DEFER_RED", "0");
     GLX_HIP(hipMemsetAsync(ticket_, 0, kTicketBytes, st_));
@@ -1035,10 +1024,8 @@ class Session : public SessionBase {
   // itself, with the masks and bitmaps the gather reads (k_ax_lds DRV)
   void cand_ax(const T* const* xs, Pub pb = Pub{}, const AxDerive* dv = nullptr) {
     const T* xd[3] = {xs[1], nullptr, nullptr};
-    qeg_ = dv == nullptr && (egat_now() || fegb_);
+    qeg_ = dv == nullptr && egat_now();
     if (qeg_) {   // round 6: A p and A e in one pass (S slabs each: A e at Pp_, A p behind)
-      // the staged source: ProxGD's p (xs = [e | p_thr | p]), FProxGD's xc (xs = [e_c | xc])
-      const T* dsrc = P_.method == GLX_FPROXGD ? xs[1] : xs[2];
       EGat eg;
       eg.E = xs[0];
       const int64_t npad = (n_ + 63) / 64 * 64;   // glx_device.h zf_npad
@@ -1046,7 +1033,7 @@ class Session : public SessionBase {
       eg.bstride = npad / 16;
       eg.Pe = Pp_;
       hipEvent_t e0 = prof_begin(0);
-      if (!launch_ax_egat<T>(plan_, A_, dsrc, Pp_ + (size_t)gs_of(true) * ml_, dc_gate_, 0, st_, pb, eg))
+      if (!launch_ax_egat<T>(plan_, A_, xs[2], Pp_ + (size_t)gs_of(true) * ml_, dc_gate_, 0, st_, pb, eg))
         throw Error{GLX_E_STATE, "fused A e: the plan does not take it"};
       check_launch();
       prof_end(0, e0);
@@ -2057,8 +2044,7 @@ class Session : public SessionBase {
         const bool spec = want_spec(it);
         const bool merge = spec && fuse && merge_tail();
         const bool late_pub = merge || (spec && fuse && attach_ok_ && comm_ == nullptr);
-        fs_batch = fsplit_ && kslot_ >= 0 && (dense_left_ == 0 || feg_);
-        fegb_ = fs_batch && dense_left_ > 0;   // (feg_) the fused form instead of a dense batch
+        fs_batch = fsplit_ && kslot_ >= 0 && dense_left_ == 0;
         carry_ = late_pub;
         if (fs_batch) {   // A xc dense, A e_c gathered, A y_next by linearity
           fista_split_batch(R_[ryn], theta, theta_next, S_RT, X_[ic_], scal_ + S_TR + i_max,
@@ -2125,13 +2111,11 @@ class Session : public SessionBase {
     tk_ = t;
     kslot_ = (accepted && fs_batch) ? (kslot_ + 1) % 3 : -1;
     if (fsplit_ && ls) {
-      // (a fused-form batch counts no flagged rows: it stands in for a dense batch)
-      const bool counted = fs_batch && !fegb_;
-      split_hist_.push_back(counted ? hs_[S_RT + 2] : -1.0);
-      if (counted) {
+      split_hist_.push_back(fs_batch ? hs_[S_RT + 2] : -1.0);
+      if (fs_batch) {
         stats_[3] += 1;
         stats_[5] += hs_[S_RT + 2];
-        if (accepted && hs_[S_RT + 2] > (feg_ ? feg_rows_ : nnz_budget_)) dense_left_ = kFistaDenseRun;
+        if (accepted && hs_[S_RT + 2] > nnz_budget_) dense_left_ = kFistaDenseRun;
       } else {
         stats_[4] += 1;
         if (dense_left_ > 0) --dense_left_;
@@ -2447,15 +2431,14 @@ class Session : public SessionBase {
       rd.part = fpart_;
       rd.parts_only = 1;
     }
-    const int s0 = gs_of(qeg_);   // the fused form: S slabs of A e_c in front of A xc
-    launch_finalize_fista<T>(Pp_ + (size_t)s0 * ml_, ax_split(plan_, 1), Pp_, s0, B_, ry,
+    launch_finalize_fista<T>(Pp_ + (size_t)gsplit_ * ml_, ax_split(plan_, 1), Pp_, gsplit_, B_, ry,
                              SXO_[kslot_], SXO_[(kslot_ + 1) % 3], ml_, 1.0 - theta_next,
                              theta_next, theta, cx, nl_, cmax, gather_counts(glists_, n_), gcount_n(),
                              rd, st_, Ctl{}, dmax ? ptr_.part : nullptr, dmax ? ptr_.np : 0,
                              dmax ? ptr_.nv : 4);
     check_launch();
     if (dfin)
-      pfin_ = Pend{fpart_, finalize_fista_blocks(ml_, ax_split(plan_, 1), s0, cx ? nl_ : 0), 4, 0u,
+      pfin_ = Pend{fpart_, finalize_fista_blocks(ml_, ax_split(plan_, 1), gsplit_, cx ? nl_ : 0), 4, 0u,
                    scal_ + slot};
     if (defer) return;
     if (comm_) comm_allreduce(comm_, scal_ + slot, 2, GLX_F64, st_);
@@ -2617,9 +2600,6 @@ class Session : public SessionBase {
   double hyb_rows_ = 0.0;      // round 6: > 0: the fused form per trial from this many flagged rows
   double last_rows_ = 0.0;     // flagged rows of the last accepted trial
   bool qeg_ = false;           // the queued split-candidate A@X is the fused form (its finalize reads it)
-  bool feg_ = false;           // round 6: FProxGD's over-budget batches take the fused form
-  double feg_rows_ = 0.0;      // ... from this many flagged rows (the gather's count)
-  bool fegb_ = false;          // the current FProxGD split batch is the fused form
   // the fused A e form for the next trial; its A e slabs (one per K split) in front of A p
   bool egat_now() const { return egat_ || (hyb_rows_ > 0.0 && last_rows_ >= hyb_rows_); }
   int gs_of(bool eg) const { return eg ? ax_split(plan_, 1) : gsplit_; }

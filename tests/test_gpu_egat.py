@@ -88,32 +88,3 @@ def test_hybrid_form_switches_and_matches_oracle(monkeypatch):
     assert kh == kr
     assert np.max(np.abs(fh - fr) / np.abs(fr)) < 1e-8
     assert np.max(np.abs(xh - xr)) <= 1e-6 * np.max(np.abs(xr))
-
-
-def test_fista_fused_batches_match_oracle(monkeypatch):
-    """FProxGD's split batch in the fused form (A xc and A e_c in one LDS-DMA pass) where the
-    gather's count passes the threshold — forced from 50 flagged rows here, so most batches take
-    it — against the dense batches those would otherwise be (GLX_FISTA_EG=0) and the oracle
-    (gl_FProxGD_primal.py:110-151): k identical, f_hist within 1e-8, x within 1e-6 of max|x|."""
-    from oracle import numpy_ref
-    from gl_FProxGD_primal import gl_FProxGD_primal
-    m, n, l, maxit = 8192, 16384, 32, 40
-    A, b, u, x0, mu = numpy_ref.gen_data(m, n, l, 97006855)
-    opts = {"alpha0": numpy_ref.step_size_for(m, n), "maxit": maxit}
-    At, bt = torch.from_numpy(A).cuda(), torch.from_numpy(b).cuda()
-    res = {}
-    for name, env in (("eg", {"GLX_AE_HYB_ROWS": "50"}), ("dense", {"GLX_AE_HYB_ROWS": "50", "GLX_FISTA_EG": "0"})):
-        for k, v in env.items():
-            monkeypatch.setenv(k, v)
-        monkeypatch.delenv("GLX_FISTA_EG", raising=False) if name == "eg" else None
-        x, k, out = gl_FProxGD_primal(torch.from_numpy(x0).cuda(), At, bt, mu, dict(opts))
-        torch.cuda.synchronize()
-        res[name] = (x.cpu().numpy(), k, np.asarray([float(v) for v in out["f_hist"]]))
-    with warnings.catch_warnings():
-        warnings.simplefilter("ignore")
-        xr, kr, outr = numpy_ref.gl_FProxGD_primal(x0, A, b, mu, dict(opts))
-    fr = np.asarray([float(v) for v in outr["f_hist"]])
-    for name, (x, k, f) in res.items():
-        assert k == kr, (name, k, kr)
-        assert np.max(np.abs(f - fr) / np.abs(fr)) < 1e-8, name
-        assert np.max(np.abs(x - xr)) <= 1e-6 * np.max(np.abs(xr)), name
