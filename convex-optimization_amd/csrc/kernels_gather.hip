@@ -31,7 +31,7 @@ namespace glx {
 namespace {
 constexpr int kGW = 4;                  // waves per workgroup
 constexpr int kGThreads = 64 * kGW;
-constexpr int kSlabLoadsG = 8;   // k_at_gather_fin: the finalize's kSlabLoads (up to 8 of its groups: S <= 64)
+constexpr int kSlabLoadsG = 8;   // k_at_gather_fin: slab loads issued per batch (the finalize's kSlabLoads)
 }  // namespace
 
 // At = A^T through 64 x 64 LDS tiles (padded rows: conflict-free transposed reads)
@@ -384,38 +384,20 @@ __global__ __launch_bounds__(kGThreads) void k_at_gather_fin(
   T acc[RW];
   gather_bm_core<T, L, NT, 8, 256, true>(At, E, zf, m, n, counts, gx, r, c, acc);
   const int64_t ml = m * L;
-  int G = 1;   // (kernels_elem.hip finalize_groups)
-  while (G * kSlabLoadsG < S) G *= 2;
-  const int per = (S + G - 1) / G;
   double v[4] = {0.0, 0.0, 0.0, 0.0};
 #pragma unroll
   for (int j = 0; j < RW; ++j) {
     if (r + j >= m) continue;
     const int64_t idx = (r + j) * L + c;
     const T bv = B[idx];
-    // the finalize's order: G groups of per slabs each folded left (G = finalize_groups(S): its
-    // one-lane groups of up to 8 slabs), combined as its lanes' butterfly does, ((t0 + t1) +
-    // (t2 + t3)) + ..., here as a binary counter over the groups (s0, s1, s2: pending partial trees)
-    T s = T(0), s0 = T(0), s1 = T(0), s2 = T(0);
-#pragma unroll 1
-    for (int q = 0; q < G; ++q) {
-      const int k0 = q * per;
-      const int cnt = S - k0 < per ? S - k0 : per;
+    T s = T(0);
+    for (int k0 = 0; k0 < S; k0 += kSlabLoadsG) {
       T a[kSlabLoadsG];
 #pragma unroll
-      for (int k = 0; k < kSlabLoadsG; ++k) a[k] = k < cnt ? Pd[(int64_t)(k0 + k) * ml + idx] : T(0);
-      T cur = a[0];
+      for (int k = 0; k < kSlabLoadsG; ++k) a[k] = k0 + k < S ? Pd[(int64_t)(k0 + k) * ml + idx] : T(0);
 #pragma unroll
-      for (int k = 1; k < kSlabLoadsG; ++k)
-        if (k < cnt) cur = cur + a[k];
-      if ((q & 1) == 0) { s0 = cur; } else {
-        cur = s0 + cur;
-        if ((q & 2) == 0) { s1 = cur; } else {
-          cur = s1 + cur;
-          if ((q & 4) == 0) s2 = cur; else cur = s2 + cur;
-        }
-      }
-      s = cur;
+      for (int k = 0; k < kSlabLoadsG; ++k)
+        if (k0 + k < S) s = (k0 + k == 0) ? a[k] : s + a[k];
     }
     const T r1 = s - bv;
     const T r0 = r1 + acc[j];
