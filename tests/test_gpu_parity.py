@@ -299,11 +299,8 @@ def test_split_candidate_gather_waves_bit_identical(name, monkeypatch):
     """The A e gathers walk every column's ascending list in the same order whatever the form:
     round 2's lists kernel + gather (GLX_GATHER=lists, with 1 / 2 / 4-wave workgroups and its
     two-rows-per-thread variant) and round 5's bitmap gather (GLX_GATHER=bm, its loads-in-flight /
-    segment / 16-B variants) give bit-identical trajectories. (With the finalize as its own launch
-    for every form: round 6's k_at_gather_fin sums the residuals in another order, see
-    test_gather_fin_matches_two_launches.)"""
+    segment / 16-B variants) give bit-identical trajectories."""
     monkeypatch.setenv("GLX_SPLIT_CAND", "1")
-    monkeypatch.setenv("GLX_GATHER_FIN", "0")
     meta, gold = golden_case(name)
     A, b, u, x0, mu = golden_inputs(meta)
     runs = []
@@ -346,33 +343,5 @@ def test_deferred_reductions_match(monkeypatch, solver, alpha_scale):
     assert np.array_equal(x0_, x1)
     assert np.max(np.abs(f1 - f0) / np.abs(f0)) < 1e-13
     xr, kr, outr = numpy_ref.SOLVERS[solver](x0, A, b, mu, dict(opts))
-    assert k1 == kr
-    assert np.max(np.abs(f1 - np.asarray(outr["f_hist"])) / np.abs(np.asarray(outr["f_hist"]))) < 1e-8
-
-
-@pytest.mark.parametrize("alpha_scale", [1.0, 2.5])
-def test_gather_fin_matches_two_launches(monkeypatch, alpha_scale):
-    """Round 6: the bitmap gather and the split-candidate finalize in one launch (k_at_gather_fin,
-    the default on one GPU) against the two launches (GLX_GATHER_FIN=0): the same A e and residual
-    bits per element, so the same decisions and bit-identical iterates; the recorded objective moves
-    by summation order only; and the oracle's run (gl_ProxGD_primal.py:73-132) within the fp64 bar.
-    alpha0 x 2.5 adds rejected first trials."""
-    from oracle import numpy_ref
-    m, n, l = 2048, 4096, 32
-    A, b, u, x0, mu = numpy_ref.gen_data(m, n, l, 5)
-    opts = {"alpha0": alpha_scale * numpy_ref.step_size_for(m, n), "maxit": 40}
-    from gl_ProxGD_primal import gl_ProxGD_primal
-    monkeypatch.setenv("GLX_SPLIT_CAND", "1")
-    At, bt = torch.from_numpy(A).cuda(), torch.from_numpy(b).cuda()
-    runs = []
-    for gf in ("0", "1"):
-        monkeypatch.setenv("GLX_GATHER_FIN", gf)
-        x, k, out = gl_ProxGD_primal(torch.from_numpy(x0).cuda(), At, bt, mu, dict(opts))
-        runs.append((x.cpu().numpy(), k, np.asarray([float(v) for v in out["f_hist"]])))
-    (x0_, k0, f0), (x1, k1, f1) = runs
-    assert k0 == k1
-    assert np.array_equal(x0_, x1)
-    assert np.max(np.abs(f1 - f0) / np.abs(f0)) < 1e-13
-    xr, kr, outr = numpy_ref.gl_ProxGD_primal(x0, A, b, mu, dict(opts))
     assert k1 == kr
     assert np.max(np.abs(f1 - np.asarray(outr["f_hist"])) / np.abs(np.asarray(outr["f_hist"]))) < 1e-8
