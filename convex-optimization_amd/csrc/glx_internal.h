@@ -255,17 +255,6 @@ int gather_form();   // GLX_GATHER: 0 bitmaps, 1 MFMA rows, 2 k_e_lists + k_at_g
 int gather_split(int64_t m, int64_t n);
 // zf: the per-row column masks of e and, behind them, the per-column row bitmaps (glx_device.h)
 size_t zf_bytes(int64_t n);
-// Round 6: A e (k_at_gather_bm's bits) and the split-candidate finalize (k_finalize_residual's
-// chain form: R1 = A p_thr - b from the S dense slabs at Pd, sums of (R1 + A e)^2 and R1^2, the
-// count over cx; ctl: the device-controlled decision in the last workgroup) in one launch of
-// gather_fin_blocks workgroups (f64, m even, at most kMaxBlocks).
-int gather_fin_blocks(int64_t m, int64_t l);
-bool gather_fin_ok(int esize, int64_t m, int64_t n, int64_t l);
-template <typename T>
-void launch_at_gather_fin(const T* At, const T* E, const unsigned* zf, int64_t m, int64_t n, int64_t l,
-                          void* lists_ws, const T* Pd, int S, const T* B, T* R1, const T* cx, int64_t cn,
-                          const double* cmax, const double* cmp, int cmnp, int cmnv, double* fh,
-                          double fh_mu, const double* fh_rn, Red red, Ctl ctl, hipStream_t st);
 // A e from the column bitmaps behind zf (ONE slab at P; the column list lengths to gather_counts)
 template <typename T>
 void launch_at_gather_bm(const T* At, const T* E, unsigned* zf, int64_t m, int64_t n, int64_t l, T* P,

@@ -112,6 +112,36 @@ __global__ void k_ctl_seed(double* state, int* abort, double s0, double s1, doub
   }
 }
 
+// *cmax, or (cmp != NULL: the trial's sums still pending as Red::parts_only partials, cmnv values
+// per slot) the max of their column 3 over cmnp slots, by every workgroup for itself (all 256
+// threads call this; the result is order-independent)
+__device__ inline double pending_max(const double* cmax, const double* __restrict__ cmp, int cmnp, int cmnv) {
+  if (cmp == nullptr) return *cmax;
+  __shared__ double wmax[4];
+  double mv = -__builtin_inf();
+  for (int i = threadIdx.x; i < cmnp; i += 256) mv = nan_max(mv, cmp[i * cmnv + 3]);
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) mv = nan_max(mv, __shfl_xor(mv, off));
+  if ((threadIdx.x & 63) == 0) wmax[threadIdx.x >> 6] = mv;
+  __syncthreads();
+  return nan_max(nan_max(wmax[0], wmax[1]), nan_max(wmax[2], wmax[3]));
+}
+
+// count(|cx| > 1e-6 cm) over this thread's indices tid, tid + stride, ...: the first kCountAhead
+// values already in cxv (loaded ahead), the rest read here
+constexpr int kCountAhead = 2;
+template <typename T>
+__device__ inline double count_above(const T* __restrict__ cx, int64_t cn, const T (&cxv)[kCountAhead],
+                                     int64_t tid, int64_t stride, double cm) {
+  const T thr = (T)1e-6 * (T)cm;
+  double c = 0.0;
+#pragma unroll
+  for (int q = 0; q < kCountAhead; ++q)
+    if (tid + q * stride < cn) c += (tabs(cxv[q]) > thr) ? 1.0 : 0.0;
+  for (int64_t idx = tid + kCountAhead * stride; idx < cn; idx += stride) c += (tabs(cx[idx]) > thr) ? 1.0 : 0.0;
+  return c;
+}
+
 template <typename T, int NSRC, int G>
 __global__ __launch_bounds__(256) void k_finalize_residual(
     const T* __restrict__ P, int S, const T* __restrict__ B, T* __restrict__ R0, T* __restrict__ R1,

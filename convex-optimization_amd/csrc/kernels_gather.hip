@@ -31,7 +31,6 @@ namespace glx {
 namespace {
 constexpr int kGW = 4;                  // waves per workgroup
 constexpr int kGThreads = 64 * kGW;
-constexpr int kSlabLoadsG = 8;   // k_at_gather_fin: slab loads issued per batch (the finalize's kSlabLoads)
 }  // namespace
 
 // At = A^T through 64 x 64 LDS tiles (padded rows: conflict-free transposed reads)
@@ -244,26 +243,27 @@ __global__ __launch_bounds__(kGThreads) void k_at_gather2(const T* __restrict__ 
 // VEC: each thread owns E = 16 / sizeof(T) consecutive output rows and reads them with one 16-B
 // load per list entry (1 KiB per wave-instruction instead of 512 B; 8-B loads stream at ~0.54-0.70
 // of the 16-B rate, MI355X_MICROARCH.md), each row's sum in the same order (needs m % E == 0).
-// (the walk itself, shared with k_at_gather_fin: acc[j] = A e of row r + j of column c)
-template <typename T, int L, bool NT, int U, int SEGW, bool VEC>
-__device__ inline void gather_bm_core(const T* __restrict__ At, const T* __restrict__ E,
-                                      const unsigned* __restrict__ zf, int64_t m, int64_t n,
-                                      unsigned* __restrict__ counts, int gx, int64_t& r,
-                                      int& c, T (&acc)[VEC ? MF<T>::E : 1]) {
+template <typename T, int L, bool NT, int U, int SEGW, bool VEC = false>
+__global__ __launch_bounds__(kGThreads) void k_at_gather_bm(const T* __restrict__ At,
+                                                            const T* __restrict__ E,
+                                                            unsigned* __restrict__ zf, int64_t m,
+                                                            int64_t n, T* __restrict__ P,
+                                                            unsigned* __restrict__ counts, int gx,
+                                                            const int* __restrict__ skip) {
   static_assert(SEGW <= kGThreads, "one bitmap word per thread and segment");
+  if (skip != nullptr && *skip != 0) return;
   __shared__ unsigned short lst[64 * SEGW];   // one segment: SEGW words x 64 rows
   __shared__ unsigned wsum[kGW];
   const int tid = threadIdx.x;
   const int lane = tid & 63, wave = tid >> 6;
-  const int rb = (int)blockIdx.x % gx;
-  c = (int)blockIdx.x / gx;
+  const int rb = (int)blockIdx.x % gx, c = (int)blockIdx.x / gx;
   const int64_t nw = zf_npad(n) / 64;
-  const uint64_t* words = reinterpret_cast<const uint64_t*>(
-      zf_bitmaps(const_cast<unsigned*>(zf), n) + (int64_t)c * (zf_npad(n) / 16));
+  const uint64_t* words = reinterpret_cast<const uint64_t*>(zf_bitmaps(zf, n) + (int64_t)c * (zf_npad(n) / 16));
   typedef typename MF<T>::vec_t V;
   constexpr int RW = VEC ? MF<T>::E : 1;   // output rows per thread
-  r = ((int64_t)rb * kGThreads + tid) * RW;
+  const int64_t r = ((int64_t)rb * kGThreads + tid) * RW;
   const int64_t rr = r < m ? r : m - RW;
+  T acc[RW];
 #pragma unroll
   for (int j = 0; j < RW; ++j) acc[j] = T(0);
   auto ldat = [&](int64_t k, T (&a)[RW]) {
@@ -329,86 +329,10 @@ __device__ inline void gather_bm_core(const T* __restrict__ At, const T* __restr
     all += total;
     __syncthreads();   // lst and wsum are rewritten by the next segment
   }
-  if (rb == 0 && tid == 0) counts[c] = all;
-}
-
-template <typename T, int L, bool NT, int U, int SEGW, bool VEC = false>
-__global__ __launch_bounds__(kGThreads) void k_at_gather_bm(const T* __restrict__ At,
-                                                            const T* __restrict__ E,
-                                                            unsigned* __restrict__ zf, int64_t m,
-                                                            int64_t n, T* __restrict__ P,
-                                                            unsigned* __restrict__ counts, int gx,
-                                                            const int* __restrict__ skip) {
-  if (skip != nullptr && *skip != 0) return;
-  constexpr int RW = VEC ? MF<T>::E : 1;
-  int64_t r;
-  int c;
-  T acc[RW];
-  gather_bm_core<T, L, NT, U, SEGW, VEC>(At, E, zf, m, n, counts, gx, r, c, acc);
 #pragma unroll
   for (int j = 0; j < RW; ++j)
     if (r + j < m) P[(r + j) * L + c] = acc[j];
-}
-
-// Round 6: the split-candidate trial's A e gather and its residual finalize in ONE launch (one
-// GPU, host control; solver.cpp gfin_). Each workgroup gathers A e for its rows of column c
-// exactly as k_at_gather_bm (same list, order and arithmetic), then finishes those elements as
-// k_finalize_residual's chain form does: r1 = (the S dense slabs summed left to right) - b (the
-// same bits as its one-lane groups), r0 = r1 + A e; it stores r1 (the next gradient's residual)
-// and sums r0^2 and r1^2; the workgroups also split the sparsity count over cx (with the trial's
-// max |p|, pending partials included, as the finalize); then one grid reduction (or Red::
-// parts_only partials for the next packet). Replaces the finalize launch behind the gather.
-template <typename T, int L, bool NT>
-__global__ __launch_bounds__(kGThreads) void k_at_gather_fin(
-    const T* __restrict__ At, const T* __restrict__ E, const unsigned* __restrict__ zf, int64_t m,
-    int64_t n, unsigned* __restrict__ counts, int gx, const T* __restrict__ Pd, int S,
-    const T* __restrict__ B, T* __restrict__ R1, const T* __restrict__ cx, int64_t cn,
-    const double* __restrict__ cmax, const double* __restrict__ cmp, int cmnp, int cmnv,
-    double* __restrict__ fh, double fh_mu, const double* __restrict__ fh_rn, Red red, Ctl ctl) {
-  constexpr int RW = MF<T>::E;
-  // a launch of a device-controlled batch cancelled by an earlier decision: nothing is stored,
-  // no ticket touched (uniform over the grid; the finalize's rule)
-  if (red_skipped(red)) return;
-  double pre[10];
-  if (ctl.rec != nullptr && threadIdx.x == 0) {   // the decision's inputs (as the finalize)
-    for (int k = 0; k < 6; ++k) pre[k] = ctl.tr[k];
-    for (int k = 0; k < 4; ++k) pre[6 + k] = ctl.state[k];
-  }
-  const int64_t gt = (int64_t)blockIdx.x * kGThreads + threadIdx.x;
-  const int64_t gs = (int64_t)gridDim.x * kGThreads;
-  T cxv[kCountAhead];   // the count's first values, loaded ahead (as the finalize)
-#pragma unroll
-  for (int q = 0; q < kCountAhead; ++q) cxv[q] = (cx != nullptr && gt + q * gs < cn) ? cx[gt + q * gs] : T(0);
-  int64_t r;
-  int c;
-  T acc[RW];
-  gather_bm_core<T, L, NT, 8, 256, true>(At, E, zf, m, n, counts, gx, r, c, acc);
-  const int64_t ml = m * L;
-  double v[4] = {0.0, 0.0, 0.0, 0.0};
-#pragma unroll
-  for (int j = 0; j < RW; ++j) {
-    if (r + j >= m) continue;
-    const int64_t idx = (r + j) * L + c;
-    const T bv = B[idx];
-    T s = T(0);
-    for (int k0 = 0; k0 < S; k0 += kSlabLoadsG) {
-      T a[kSlabLoadsG];
-#pragma unroll
-      for (int k = 0; k < kSlabLoadsG; ++k) a[k] = k0 + k < S ? Pd[(int64_t)(k0 + k) * ml + idx] : T(0);
-#pragma unroll
-      for (int k = 0; k < kSlabLoadsG; ++k)
-        if (k0 + k < S) s = (k0 + k == 0) ? a[k] : s + a[k];
-    }
-    const T r1 = s - bv;
-    const T r0 = r1 + acc[j];
-    R1[idx] = r1;
-    v[0] += (double)(r0 * r0);
-    v[1] += (double)(r1 * r1);
-  }
-  if (cx != nullptr) v[3] = count_above(cx, cn, cxv, gt, gs, pending_max(cmax, cmp, cmnp, cmnv));
-  const bool last = grid_reduce<4, 0u>(v, red);
-  if (last && fh != nullptr && threadIdx.x == 0) *fh = 0.5 * red.out[0] + fh_mu * (*fh_rn);
-  if (last && ctl.rec != nullptr && threadIdx.x == 0) ctl_decide(ctl, red.out, pre);
+  if (rb == 0 && tid == 0) counts[c] = all;
 }
 
 // zf's column bitmaps from its n row masks (glx_flagged_rows_product's bitmap form, where no
@@ -721,39 +645,6 @@ static void at_gather_bm_go(int code, int64_t m, hipStream_t st, const T* At, co
     default: glx_launch(k_at_gather_bm<T, L, NT, 8, 256>, g, dim3(kGThreads), 0, st, At, E, zf, m, n, P, cnt, gx, skip); break;
   }
 }
-int gather_fin_blocks(int64_t m, int64_t l) {
-  return (int)((m + 2 * kGThreads - 1) / (2 * kGThreads) * l);
-}
-bool gather_fin_ok(int esize, int64_t m, int64_t n, int64_t l) {
-  return esize == 8 && gather_ok(n, l) && m % 2 == 0 && gather_fin_blocks(m, l) <= kMaxBlocks;
-}
-template <typename T>
-void launch_at_gather_fin(const T* At, const T* E, const unsigned* zf, int64_t m, int64_t n, int64_t l,
-                          void* lists_ws, const T* Pd, int S, const T* B, T* R1, const T* cx, int64_t cn,
-                          const double* cmax, const double* cmp, int cmnp, int cmnv, double* fh,
-                          double fh_mu, const double* fh_rn, Red red, Ctl ctl, hipStream_t st) {
-  if (!gather_fin_ok((int)sizeof(T), m, n, l)) throw Error{GLX_E_INVALID, "A e gather + finalize: shape"};
-  if constexpr (sizeof(T) == 8) {
-    unsigned* cnt = list_counts(lists_ws, n);
-    const int gx = (int)((m + 2 * kGThreads - 1) / (2 * kGThreads));
-    const dim3 g((unsigned)(gx * l));
-    if (l == 32)
-      glx_launch(k_at_gather_fin<T, 32, true>, g, dim3(kGThreads), 0, st, At, E, zf, m, n, cnt, gx, Pd, S, B,
-                 R1, cx, cn, cmax, cmp, cmnp, cmnv, fh, fh_mu, fh_rn, red, ctl);
-    else
-      glx_launch(k_at_gather_fin<T, 16, true>, g, dim3(kGThreads), 0, st, At, E, zf, m, n, cnt, gx, Pd, S, B,
-                 R1, cx, cn, cmax, cmp, cmnp, cmnv, fh, fh_mu, fh_rn, red, ctl);
-  }
-}
-template void launch_at_gather_fin<double>(const double*, const double*, const unsigned*, int64_t, int64_t,
-                                           int64_t, void*, const double*, int, const double*, double*,
-                                           const double*, int64_t, const double*, const double*, int, int,
-                                           double*, double, const double*, Red, Ctl, hipStream_t);
-template void launch_at_gather_fin<float>(const float*, const float*, const unsigned*, int64_t, int64_t,
-                                          int64_t, void*, const float*, int, const float*, float*,
-                                          const float*, int64_t, const double*, const double*, int, int,
-                                          double*, double, const double*, Red, Ctl, hipStream_t);
-
 template <typename T>
 void launch_at_gather_bm(const T* At, const T* E, unsigned* zf, int64_t m, int64_t n, int64_t l, T* P,
                          void* lists_ws, hipStream_t st, const int* skip) {

@@ -661,10 +661,6 @@ class Session : public SessionBase {
       const char* e = std::getenv("GLX_AE_HYB_ROWS");
       hyb_rows_ = e ? std::atof(e) : kHybRows;
     }
-    // Round 6: on one GPU the gather form's A e and its finalize run as one launch
-    // (k_at_gather_fin; host and device control alike). GLX_GATHER_FIN=0: two launches.
-    gfin_ = smode_ == 1 && gform_ == 0 && !egat_ && comm_ == nullptr && P.method == GLX_PROXGD &&
-            gather_fin_ok((int)sizeof(T), m_, n_, l_) && !env_is("GLX_GATHER_FIN", "0");
     defer_ = comm_ == nullptr && dc_window_ == 0 && dmeth && spin_readback_ && attach_ok_ &&
              !env_is("GLX_DEFER_RED", "0");
     GLX_HIP(hipMemsetAsync(ticket_, 0, kTicketBytes, st_));
@@ -966,10 +962,8 @@ class Session : public SessionBase {
                  unsigned* pub_seq = nullptr, double* defer = nullptr, bool skip_ax = false,
                  bool snap_trial = false, bool chain = false) {
     const bool gat = chain && smode_ == 1;
-    // round 6 (gfin_): the gather and this finalize as one launch where A@X is queued here
-    const bool gf = gat && gfin_ && !skip_ax && nsrc == 2 && !snap_trial && defer == nullptr;
     if (!skip_ax) {
-      if (gat) cand_ax(xs, Pub{}, nullptr, gf);
+      if (gat) cand_ax(xs);
       else spec_ax(nsrc, xs);
     }
     T* rsc[3] = {chain ? nullptr : rs[0], rs[1], rs[2]};
@@ -983,18 +977,6 @@ class Session : public SessionBase {
       flush_fin_pending();
       rd.part = fpart_;
       rd.parts_only = 1;
-    }
-    if (gf && !qeg_) {
-      hipEvent_t e2 = prof_begin(2);
-      launch_at_gather_fin<T>(At_, xs[0], zf_, m_, n_, l_, glists_, Pp_ + (size_t)gs_of(false) * ml_, S, B_,
-                              rs[1], cx, cx ? nl_ : 0, cmax, dmax ? ptr_.part : nullptr, dmax ? ptr_.np : 0,
-                              dmax ? ptr_.nv : 6, comm_ ? nullptr : fh, fh_mu, scal_ + S_DRN, rd, dc_ctl_,
-                              st_);
-      check_launch();
-      prof_end(2, e2);
-      if (dfin) pfin_ = Pend{fpart_, gather_fin_blocks(m_, l_), 4, 0u, scal_ + slot};
-      if (pub_seq != nullptr) *pub_seq = post_readback();
-      return;
     }
     launch_finalize_residual<T>(Pp_, S, B_, nsrc, rsc,
                                 ml_, nullptr, 0, 1, cx,
@@ -1040,8 +1022,7 @@ class Session : public SessionBase {
   // slabs, each workgroup compacts its K range's row flags itself), so no column lists.
   // dv (row-sharded ProxGD, sderive_): the dense pass reads p (xs[2]) and derives p_thr into xs[1]
   // itself, with the masks and bitmaps the gather reads (k_ax_lds DRV)
-  // no_gather (gfin_): the gather form's A e is left to the finalize (k_at_gather_fin)
-  void cand_ax(const T* const* xs, Pub pb = Pub{}, const AxDerive* dv = nullptr, bool no_gather = false) {
+  void cand_ax(const T* const* xs, Pub pb = Pub{}, const AxDerive* dv = nullptr) {
     const T* xd[3] = {xs[1], nullptr, nullptr};
     qeg_ = dv == nullptr && egat_now();
     if (qeg_) {   // round 6: A p and A e in one pass (S slabs each: A e at Pp_, A p behind)
@@ -1074,7 +1055,7 @@ class Session : public SessionBase {
     }
     check_launch();
     prof_end(0, e0);
-    if (dv != nullptr || no_gather) {   // A e ran inside the dense pass / runs with the finalize
+    if (dv != nullptr) {   // A e ran inside the dense pass
       ++ax_calls_;
       ax_cols_ += 1;
       return;
@@ -2619,7 +2600,6 @@ class Session : public SessionBase {
   double hyb_rows_ = 0.0;      // round 6: > 0: the fused form per trial from this many flagged rows
   double last_rows_ = 0.0;     // flagged rows of the last accepted trial
   bool qeg_ = false;           // the queued split-candidate A@X is the fused form (its finalize reads it)
-  bool gfin_ = false;          // round 6: the gather form's A e and finalize in one launch
   // the fused A e form for the next trial; its A e slabs (one per K split) in front of A p
   bool egat_now() const { return egat_ || (hyb_rows_ > 0.0 && last_rows_ >= hyb_rows_); }
   int gs_of(bool eg) const { return eg ? ax_split(plan_, 1) : gsplit_; }
