@@ -412,7 +412,6 @@ struct AxDerive {
   void* Pe = nullptr;
   const double* blk = nullptr;
   int64_t bstride = 0, moff = 0, srows = 0;
-  int unthr = 0;                 // 1: the pass computes A p (no threshold; the finalize's chain 2)
 };
 bool ax_derive_ok(const GemmPlan& p, int esize);
 // rows of A per gather workgroup of the fused dense pass (AxDerive::ggx = ceil(m / this)), and

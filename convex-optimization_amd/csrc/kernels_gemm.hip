@@ -1045,8 +1045,7 @@ bool launch_ax_derive(const GemmPlan& p, const T* A, const T* Xp, T* P, hipStrea
     dd.sp.pub = pub;
     dd.nd = kDrvThrBlocks;
     const T* xs[3] = {Xp, nullptr, nullptr};
-    if (d.unthr) ax_lds_go<T, 2, 1, 1, 3, 2, 8, 2>(p, p.axb_S[1], A, xs, P, nullptr, 0, st, pub, dd);
-    else ax_lds_go<T, 2, 1, 1, 3, 2, 8, 1>(p, p.axb_S[1], A, xs, P, nullptr, 0, st, pub, dd);
+    ax_lds_go<T, 2, 1, 1, 3, 2, 8, 1>(p, p.axb_S[1], A, xs, P, nullptr, 0, st, pub, dd);
     return true;
   }
 }

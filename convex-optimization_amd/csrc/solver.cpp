@@ -630,7 +630,6 @@ class Session : public SessionBase {
                    n_ % 64 == 0 && srows_ % 64 == 0 && n_ <= 65536 && !env_is("GLX_SHARD_DERIVE", "0");
         moff_ = schunk_;
         if (sderive_) schunk_ += srows_ / 2 + l_ * srows_ / 64;
-        drv_unthr_ = sderive_ && env_is("GLX_SHARD_DRV_AP", "1");
       } else {
         shard_model_ = false;
       }
@@ -985,7 +984,7 @@ class Session : public SessionBase {
                                 rd, st_,
                                 snap_trial ? scal_ + S_TR : nullptr,
                                 snap_trial ? scal_ + S_SNAP : nullptr, snap_trial ? 6 : 0,
-                                chain ? (qch2_ ? 2 : 1) : 0, gat ? gs_of(qeg_) : 0, dc_ctl_,
+                                chain ? (qeg_ ? 2 : 1) : 0, gat ? gs_of(qeg_) : 0, dc_ctl_,
                                 dmax ? ptr_.part : nullptr, dmax ? ptr_.np : 0, dmax ? ptr_.nv : 6);
     check_launch();
     if (dfin) pfin_ = Pend{fpart_, finalize_blocks(ml_, S, gat ? gs_of(qeg_) : 0, cx ? nl_ : 0), 4, 0u, scal_ + slot};
@@ -1026,9 +1025,6 @@ class Session : public SessionBase {
   void cand_ax(const T* const* xs, Pub pb = Pub{}, const AxDerive* dv = nullptr) {
     const T* xd[3] = {xs[1], nullptr, nullptr};
     qeg_ = dv == nullptr && egat_now();
-    // the finalize's chain 2 (its dense slabs hold A p, A p_thr = A p - A e): the fused form, or
-    // the row-sharded derive pass that reads p unthresholded
-    qch2_ = qeg_ || (dv != nullptr && dv->unthr != 0);
     if (qeg_) {   // round 6: A p and A e in one pass (S slabs each: A e at Pp_, A p behind)
       EGat eg;
       eg.E = xs[0];
@@ -1605,7 +1601,7 @@ class Session : public SessionBase {
     launch_finalize_residual<T>(Pp_, gat ? ax_split(plan_, 1) : ax_split(plan_, nsrc), B_, nsrc, rsc,
                                 ml_, nullptr, 0, 1, cx + o, srows_ * l_, cmax, nullptr, 0.0,
                                 scal_ + S_DRN, rd, st_, nullptr, nullptr, 0,
-                                chain ? (qch2_ ? 2 : 1) : 0, gat ? gs_of(qeg_) : 0, Ctl{});
+                                chain ? (qeg_ ? 2 : 1) : 0, gat ? gs_of(qeg_) : 0, Ctl{});
     check_launch();
   }
   void iter_proxgd_shard() {
@@ -1675,7 +1671,6 @@ class Session : public SessionBase {
             dv.bstride = shard_model_ ? 0 : schunk_;
             dv.moff = moff_;
             dv.srows = srows_;
-            dv.unthr = drv_unthr_ ? 1 : 0;
             cand_ax(sx, pb, &dv);
           } else if (smode_ == 1) {
             cand_ax(sx, pb);
@@ -2605,8 +2600,6 @@ class Session : public SessionBase {
   double hyb_rows_ = 0.0;      // round 6: > 0: the fused form per trial from this many flagged rows
   double last_rows_ = 0.0;     // flagged rows of the last accepted trial
   bool qeg_ = false;           // the queued split-candidate A@X is the fused form (its finalize reads it)
-  bool qch2_ = false;          // ... and its dense slabs hold A p (the finalize's chain 2)
-  bool drv_unthr_ = false;     // round 6: the row-sharded derive pass reads p unthresholded (A p)
   // the fused A e form for the next trial; its A e slabs (one per K split) in front of A p
   bool egat_now() const { return egat_ || (hyb_rows_ > 0.0 && last_rows_ >= hyb_rows_); }
   int gs_of(bool eg) const { return eg ? ax_split(plan_, 1) : gsplit_; }
