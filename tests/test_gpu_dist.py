@@ -200,8 +200,13 @@ def test_row_sharded_other_modes(tmp_path, extra_opts):
     assert "rows=sharded x2" in r0["plan"]
 
 
-@pytest.mark.parametrize("extra", [(), ("--alpha-scale", "2.5")])
-def test_row_sharded_split_candidate(tmp_path, monkeypatch, extra):
+@pytest.mark.parametrize("world,m,n,extra", [
+    (2, 512, 1024, ()),
+    (2, 512, 1024, ("--alpha-scale", "2.5")),
+    (3, 1000, 1536, ()),   # ragged rows per rank (334 / 333 / 333), three ranks' chunk bitmaps
+    (8, 1024, 1024, ()),   # 128 rows of x per rank: two bitmap words per rank and column
+])
+def test_row_sharded_split_candidate(tmp_path, monkeypatch, world, m, n, extra):
     """The split-candidate trial under the row-sharded schedule: p_thr, the masks and bitmaps of e
     are re-derived from the gathered p and the bitmap gather reads e from them. Round 6: in the
     speculative steady state the derive runs inside the next trial's dense pass (k_ax_lds DRV; its
@@ -210,14 +215,14 @@ def test_row_sharded_split_candidate(tmp_path, monkeypatch, extra):
     (those two throughout) gives the same bits. alpha0 x 2.5: rejected first trials (the
     host-path trial, then the fused form again once speculation resumes)."""
     monkeypatch.setenv("GLX_SPLIT_CAND", "1")
-    v = run_sharded(tmp_path, 2, "gl_ProxGD_primal", 512, 1024, 32, maxit=25,
-                    extra=("--shard-rows", "1") + tuple(extra))
-    r0 = _check_identical_and_oracle(v, 2)
-    assert "gather k_at_gather_bm" in r0["plan"] and "rows=sharded x2" in r0["plan"], r0["plan"]
+    v = run_sharded(tmp_path, world, "gl_ProxGD_primal", m, n, 32, maxit=25,
+                    extra=("--shard-rows", "1") + tuple(extra), timeout=150)
+    r0 = _check_identical_and_oracle(v, world)
+    assert "gather k_at_gather_bm" in r0["plan"] and ("rows=sharded x%d" % world) in r0["plan"], r0["plan"]
     assert "derive and A e in the dense pass" in r0["plan"], r0["plan"]
     monkeypatch.setenv("GLX_SHARD_DERIVE", "0")
-    w = run_sharded(tmp_path, 2, "gl_ProxGD_primal", 512, 1024, 32, maxit=25,
-                    extra=("--shard-rows", "1") + tuple(extra))
+    w = run_sharded(tmp_path, world, "gl_ProxGD_primal", m, n, 32, maxit=25,
+                    extra=("--shard-rows", "1") + tuple(extra), timeout=150)
     w0 = w["ranks"][0]
     assert "k_trial_split" in w0["plan"], w0["plan"]
     assert w0["k"] == r0["k"] and w0["x_sha"] == r0["x_sha"] and w0["f_hist"] == r0["f_hist"]
