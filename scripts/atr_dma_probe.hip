@@ -32,10 +32,8 @@ typedef float f4 __attribute__((ext_vector_type(4)));
 typedef __attribute__((address_space(1))) void g_void_t;
 typedef __attribute__((address_space(3))) void l_void_t;
 
-constexpr int WAVES = 8;
-
-// CR rows of A per chunk (8 or 16), NS ring slots per wave
-template <int CR, int NS, bool NTL>
+// CR rows of A per chunk (8 or 16), NS ring slots per wave, WAVES waves splitting the rows
+template <int CR, int NS, bool NTL, int WAVES>
 __global__ __launch_bounds__(64 * WAVES) void k_atr_dma(const float* __restrict__ A, const float* __restrict__ R,
                                                        float* __restrict__ G, int m, int n) {
   constexpr int ABYTES = CR * 64 * 4;          // A per wave and chunk
@@ -141,15 +139,15 @@ __global__ void k_ref(const float* A, const float* R, float* G, int m, int n) {
   for (int c = 0; c < 32; ++c) G[(size_t)j * 32 + c] = (float)acc[c];
 }
 
-template <int CR, int NS, bool NTL>
+template <int CR, int NS, bool NTL, int WAVES = 8>
 static double run(const float* A, const float* R, float* G, int m, int n, int reps) {
   hipEvent_t e0, e1;
   CK(hipEventCreate(&e0));
   CK(hipEventCreate(&e1));
-  hipLaunchKernelGGL((k_atr_dma<CR, NS, NTL>), dim3(n / 64), dim3(64 * WAVES), 0, 0, A, R, G, m, n);
+  hipLaunchKernelGGL((k_atr_dma<CR, NS, NTL, WAVES>), dim3(n / 64), dim3(64 * WAVES), 0, 0, A, R, G, m, n);
   CK(hipDeviceSynchronize());
   CK(hipEventRecord(e0));
-  for (int r = 0; r < reps; ++r) hipLaunchKernelGGL((k_atr_dma<CR, NS, NTL>), dim3(n / 64), dim3(64 * WAVES), 0, 0, A, R, G, m, n);
+  for (int r = 0; r < reps; ++r) hipLaunchKernelGGL((k_atr_dma<CR, NS, NTL, WAVES>), dim3(n / 64), dim3(64 * WAVES), 0, 0, A, R, G, m, n);
   CK(hipEventRecord(e1));
   CK(hipEventSynchronize(e1));
   float ms = 0.f;
@@ -186,10 +184,11 @@ int main() {
     std::printf("%s: %.1f us  %.2f TB/s  %.1f TF  max rel err %.2e\n", name, us, bytes / us / 1e6,
                 2.0 * m * n * 32 / us / 1e6, err / scale);
   };
-  check("CR16 NS3 NTL", run<16, 3, true>(A, R, G, m, n, reps));
-  check("CR16 NS3", run<16, 3, false>(A, R, G, m, n, reps));
-  check("CR8 NS5 NTL", run<8, 5, true>(A, R, G, m, n, reps));
-  check("CR8 NS6 NTL", run<8, 6, true>(A, R, G, m, n, reps));
-  check("CR8 NS6", run<8, 6, false>(A, R, G, m, n, reps));
+  check("W8 CR16 NS3 NTL", run<16, 3, true>(A, R, G, m, n, reps));
+  check("W8 CR8 NS5 NTL", run<8, 5, true>(A, R, G, m, n, reps));
+  check("W4 CR16 NS3 NTL (2 blocks/CU)", run<16, 3, true, 4>(A, R, G, m, n, reps));
+  check("W4 CR8 NS5 NTL (2 blocks/CU)", run<8, 5, true, 4>(A, R, G, m, n, reps));
+  check("W4 CR8 NS6 NTL (2 blocks/CU)", run<8, 6, true, 4>(A, R, G, m, n, reps));
+  check("W4 CR16 NS3 (2 blocks/CU)", run<16, 3, false, 4>(A, R, G, m, n, reps));
   return 0;
 }
